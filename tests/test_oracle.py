@@ -1,0 +1,101 @@
+"""The CPU oracle (oracle/bpe_oracle.c) pinned against the reference's own
+outputs (golden fixtures from oracle/_ref, the unmodified reference)."""
+import os
+
+import numpy as np
+import pytest
+
+import golden_lib as G
+import oracle_lib as O
+
+FIXTURES = [fx for fx in G.load_all() if not fx.get("error")]
+SMALL = [fx for fx in FIXTURES if G.input_size(fx) <= 300_000]
+
+
+@pytest.mark.parametrize("fx", SMALL, ids=[f["name"] for f in SMALL])
+def test_emulation_matches_reference(fx):
+    data = O.effective_bytes(G.input_bytes(fx))
+    merges, ids, st = O.train(data, fx["max_merges"], O.EMU)
+    G.check(fx, merges, ids)
+
+
+@pytest.mark.parametrize("fx", SMALL, ids=[f["name"] for f in SMALL])
+def test_fast_rule_matches_when_unambiguous(fx):
+    """The closed-form rule (max count, then min murmur bucket under B_final)
+    equals the reference on every iteration it does not flag as ambiguous."""
+    data = O.effective_bytes(G.input_bytes(fx))
+    merges, ids, st = O.train(data, fx["max_merges"], O.FAST)
+    if st.ambiguous == 0:
+        G.check(fx, merges, ids)
+    # ambiguous iterations are decided by the emulation (previous test)
+
+def test_kat_ties_are_chain_decided():
+    for name, winner in (("kat_tie_xy", [38, 63]), ("kat_tie_yx", [33, 107]),
+                         ("kat_tie_yyyxxx", [33, 107]), ("kat_tie_xxxyyy", [38, 63])):
+        fx = G.load(name)
+        assert fx["merges"] == [winner]
+        _, _, st = O.train(G.input_bytes(fx), 1, O.EMU)
+        assert st.chain_ties == 1
+
+
+def test_murmur_known_answers():
+    # collision used by the tie KATs
+    assert O.murmur_pair(33, 107) & 0xFFFF == O.murmur_pair(38, 63) & 0xFFFF
+    # murmur3_x86_32 of 8 zero bytes, seed 0x9747b28c (independent restatement)
+    def mm(a, b):
+        def rotl(x, r):
+            return ((x << r) | (x >> (32 - r))) & 0xFFFFFFFF
+        h = 0x9747B28C
+        for k in (a, b):
+            k = (k * 0xCC9E2D51) & 0xFFFFFFFF
+            k = (rotl(k, 15) * 0x1B873593) & 0xFFFFFFFF
+            h ^= k
+            h = (rotl(h, 13) * 5 + 0xE6546B64) & 0xFFFFFFFF
+        h ^= 8
+        h ^= h >> 16
+        h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+        h ^= h >> 13
+        h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+        return h ^ (h >> 16)
+    rng = np.random.default_rng(0)
+    for a, b in rng.integers(0, 1 << 20, size=(200, 2)):
+        assert O.murmur_pair(int(a), int(b)) == mm(int(a), int(b))
+
+
+def test_encode_replays_training():
+    """compress()'s final ids == the merge list replayed pass by pass."""
+    for name in ("prose", "synth_s1_4k", "aab_runs", "run_a_777_b", "binary_5k"):
+        fx = G.load(name)
+        data = O.effective_bytes(G.input_bytes(fx))
+        ids = O.encode(data, np.asarray(fx["merges"], dtype=np.uint32))
+        assert G.ids_md5(ids) == fx["ids_md5"]
+
+
+def test_decode_roundtrip():
+    for name in ("prose", "synth_s1_4k", "aab_runs", "nul_truncates", "binary_5k"):
+        fx = G.load(name)
+        data = O.effective_bytes(G.input_bytes(fx))
+        ids = O.encode(data, np.asarray(fx["merges"], dtype=np.uint32))
+        assert O.decode(ids, np.asarray(fx["merges"])) == data
+
+
+REF_FILES = {
+    "testing.txt": ("2cbb056a34a294df9ff8e80c9326c19b", "327cc96dfd8cfbbb5c69c83324c87b9f", -1),
+    "random_text.txt": ("45c9290b9dc2554bb90bca1a0dc4be9a", "9c5f6099bc1adcbd06d2afbee767f8dd", 1024),
+}
+
+
+@pytest.mark.parametrize("fname", ["testing.txt"])
+def test_reference_corpus_hashes(fname):
+    """Hashes of the reference run on its own corpora; only in
+    the build container, where /root/reference exists."""
+    path = os.path.join("/root/reference", fname)
+    if not os.path.exists(path):
+        pytest.skip("reference corpus not present")
+    import hashlib
+    m_md5, i_md5, cap = REF_FILES[fname]
+    data = O.effective_bytes(open(path, "rb").read())
+    merges, ids, _ = O.train(data, cap, O.EMU)
+    txt = "".join(f"{256 + r} {a} {b}\n" for r, (a, b) in enumerate(merges.tolist()))
+    assert hashlib.md5(txt.encode()).hexdigest() == m_md5
+    assert G.ids_md5(ids) == i_md5
