@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""Benchmark of the BPE merge-training loop on MI355X (BASELINE.json metric
+"corpus MB/s per merge iter").
+
+Workload (BASELINE.json configs[3], one GPU per rank): a 1 GiB synthetic
+random_text.txt-shaped corpus (seed 2, generated directly in HBM), trained
+for K merge iterations.  One "step" = one merge iteration over the corpus.
+The timed region is the WHOLE training job on resident input: the one-off
+pair counting sort + K iterations (count deltas -> argmax -> merge), ending
+with the final ids compacted in HBM.
+
+value = n_gpus * corpus_MB * K / wall   (MB = 1e6 bytes)
+
+Multi-GPU (torchrun, one rank per GPU): this round every rank trains an
+independent replica on its own 1 GiB slice (weak scaling, no exchange);
+see DESIGN.md "Multi-GPU" for the sharded-exchange plan.
+
+The JSON line also carries
+  roofline     -- the corpus-wide pair-count kernel (k_pair_hist), timed with
+                  HIP events on the engine's stream inside the timed run;
+  cpu_baseline -- the unmodified reference (oracle/_ref/bpe_ref, 16 threads)
+                  timed on this host on a bounded sample (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(seed, size, merges):
+    """Reference trainer on a bounded sample (first `size` bytes of the same
+    corpus).  Falls back to the oracle port (1 thread) if _ref is absent."""
+    from llmtokenizer_amd.synth import synth_bytes
+    data = synth_bytes(seed, size)
+    ref = os.path.join(ROOT, "oracle", "_ref", "bpe_ref")
+    with tempfile.TemporaryDirectory() as td:
+        inp = os.path.join(td, "c.txt")
+        with open(inp, "wb") as f:
+            f.write(data)
+        if os.path.exists(ref):
+            env = dict(os.environ, BPE_REF_MAX_MERGES=str(merges))
+            t0 = time.time()
+            p = subprocess.run([ref, inp, os.path.join(td, "m"), os.path.join(td, "i")], env=env,
+                               capture_output=True, text=True)
+            dt = time.time() - t0
+            if p.returncode != 0:
+                return None
+            kind, cores = "reference", 16
+        else:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_lib as O
+            t0 = time.time()
+            O.train(data, merges, O.FAST)
+            dt = time.time() - t0
+            kind, cores = "port", 1
+    return {"value": round(size / 1e6 * merges / dt, 3), "unit": "corpus MB/s per merge iter",
+            "cores": cores, "kind": kind,
+            "sample": f"{size / 2**20:.0f} MiB prefix of the seed-{seed} corpus, {merges} merges, "
+                      f"{dt:.1f} s wall (reference hard-codes 16 pthreads; host nproc={os.cpu_count()})"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1024, help="merge iterations timed")
+    ap.add_argument("--warmup", type=int, default=16, help="merge iterations of a throwaway run")
+    ap.add_argument("--size", type=int, default=1 << 30, help="corpus bytes per GPU")
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-size", type=int, default=64 << 20)
+    ap.add_argument("--cpu-merges", type=int, default=16)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from llmtokenizer_amd import api
+    e = api.Engine(local)
+    e.synth(args.seed, args.size, offset=rank * args.size)  # resident in HBM before timing
+
+    # warmup: a throwaway short run (kernels loaded, graphs captured, pools warm)
+    if args.warmup > 0:
+        e.train(args.warmup)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    k = e.train(args.steps)
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = e.stats()
+    name, kms, kbytes, launches = e.kernel_profile()
+
+    if rank != 0:
+        return
+    corpus_mb = args.size / 1e6
+    value = world * corpus_mb * k / elapsed
+    achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    out = {
+        "metric": "corpus MB/s per merge iter (train), 1 GiB synthetic corpus per GPU",
+        "value": round(value, 1),
+        "unit": "corpus MB/s per merge iter",
+        "n_gpus": world,
+        "steps": k,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / max(k, 1), 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (random_text.txt-shaped, splitmix64 seed %d, generated in HBM)" % args.seed,
+        "config": {"workload": "configs[3]: 1 GiB corpus/GPU, %d merges" % args.steps,
+                   "corpus_bytes_per_gpu": args.size, "merges": k,
+                   "parallelism": "replicas (independent per-GPU corpora)" if world > 1 else "single GPU"},
+        "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_launch": kbytes, "avg_ms": round(kms, 4), "launches": launches},
+        "breakdown_ms": {"init": round(st["ms_init"], 3), "loop": round(st["ms_train"], 3),
+                         "total_engine": round(st["ms_total"], 3)},
+        "engine": {k2: st[k2] for k2 in ("n_out", "iterations", "distinct_pairs", "merged_buckets",
+                                          "tracked_iters", "tie_events", "edge_events", "rule_ties",
+                                          "table_grows", "keys")},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.seed, args.cpu_size, args.cpu_merges)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,108 @@
+"""ctypes binding of libbpe_amd.so (the C-ABI in include/bpe.h, bpe_ex.h,
+bpe_gpu.h).  The library is built in-tree (make / __graft_entry__.build()) and
+loaded from this package directory; there is no Python or CPU fallback."""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbpe_amd.so")
+
+# every symbol include/*.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    # bpe.h (reference bpe/inc/bpe.h:25-37)
+    "get_file", "dump_pairs", "read_pairs", "print_text", "print_graph", "compress",
+    "decompress", "render_pairs", "resolve_pair", "is_less",
+    # dyn_arr.h (reference dyn_arr/inc/dyn_arr.h:27-85)
+    "dyn_arr_create", "dyn_arr_free", "dyn_arr_set", "dyn_arr_append", "dyn_arr_get",
+    "dyn_arr_sort", "dyn_arr_max", "dyn_arr_min",
+    # hash_table.h (reference hash_table/inc/hash_table.h:29-37)
+    "hash_table_create", "hash_table_destroy", "hash_table_insert", "hash_table_delete",
+    "hash_table_search", "hash_table_clear", "hash_table_merge",
+    # bpe_ex.h
+    "compress_ex", "bpe_train_bytes", "bpe_encode_bytes", "bpe_last_stats",
+    # bpe_gpu.h
+    "bpe_gpu_device_count", "bpe_gpu_create", "bpe_gpu_destroy", "bpe_gpu_load", "bpe_gpu_synth",
+    "bpe_gpu_train", "bpe_gpu_fetch_merges", "bpe_gpu_fetch_ids", "bpe_gpu_encode", "bpe_gpu_decode",
+    "bpe_gpu_get_stats", "bpe_gpu_device_tokens", "bpe_gpu_kernel_profile", "bpe_gpu_strerror",
+    "bpe_gpu_last_error",
+]
+
+
+class GpuStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "n_in", "n_out", "merges", "iterations", "distinct_pairs", "merged_buckets",
+        "tracked_iters", "tie_events", "edge_events", "rule_ties", "table_grows", "keys")] + \
+        [(n, ctypes.c_double) for n in ("ms_init", "ms_train", "ms_total")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class DynArr(ctypes.Structure):
+    _fields_ = [("len", ctypes.c_size_t), ("last_index", ctypes.c_size_t),
+                ("item_size", ctypes.c_size_t), ("nodes", ctypes.POINTER(ctypes.c_void_p))]
+
+
+_LIB = None
+
+
+class BpeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libbpe_amd.so; raises if it has not been built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise BpeError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build()) first")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u32p = ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32)
+    L.bpe_gpu_strerror.restype = ctypes.c_char_p
+    L.bpe_gpu_last_error.restype = ctypes.c_char_p
+    L.bpe_gpu_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.bpe_gpu_destroy.argtypes = [vp]
+    L.bpe_gpu_destroy.restype = None
+    L.bpe_gpu_load.argtypes = [vp, vp, sz]
+    L.bpe_gpu_synth.argtypes = [vp, ctypes.c_uint64, sz, ctypes.c_uint64]
+    L.bpe_gpu_train.argtypes = [vp, ctypes.c_long, ctypes.POINTER(sz)]
+    L.bpe_gpu_fetch_merges.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    L.bpe_gpu_fetch_ids.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    L.bpe_gpu_encode.argtypes = [vp, vp, sz]
+    L.bpe_gpu_decode.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz)]
+    L.bpe_gpu_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats)]
+    L.bpe_gpu_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    L.bpe_gpu_kernel_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
+    L.compress.argtypes = [ctypes.c_char_p, ctypes.POINTER(u32p), ctypes.POINTER(sz)]
+    L.compress.restype = ctypes.POINTER(DynArr)
+    L.compress_ex.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_int, ctypes.POINTER(u32p), ctypes.POINTER(sz)]
+    L.compress_ex.restype = ctypes.POINTER(DynArr)
+    L.bpe_train_bytes.argtypes = [vp, sz, ctypes.c_long, ctypes.c_int, ctypes.POINTER(u32p), ctypes.POINTER(sz)]
+    L.bpe_train_bytes.restype = ctypes.POINTER(DynArr)
+    L.bpe_encode_bytes.argtypes = [vp, sz, ctypes.POINTER(DynArr), ctypes.c_int, ctypes.POINTER(sz)]
+    L.bpe_encode_bytes.restype = u32p
+    L.decompress.argtypes = [u32p, sz, ctypes.POINTER(DynArr)]
+    L.decompress.restype = ctypes.c_void_p
+    L.dump_pairs.argtypes = [ctypes.c_char_p, ctypes.POINTER(DynArr)]
+    L.dump_pairs.restype = ctypes.c_bool
+    L.read_pairs.argtypes = [ctypes.c_char_p]
+    L.read_pairs.restype = ctypes.POINTER(DynArr)
+    L.dyn_arr_create.argtypes = [sz, sz]
+    L.dyn_arr_create.restype = ctypes.POINTER(DynArr)
+    L.dyn_arr_free.argtypes = [ctypes.POINTER(DynArr)]
+    L.dyn_arr_free.restype = None
+    L.dyn_arr_get.argtypes = [ctypes.POINTER(DynArr), sz, vp]
+    L.dyn_arr_get.restype = ctypes.c_bool
+    L.dyn_arr_set.argtypes = [ctypes.POINTER(DynArr), sz, vp]
+    L.dyn_arr_set.restype = ctypes.c_bool
+    L.bpe_last_stats.argtypes = [ctypes.POINTER(GpuStats)]
+    _LIB = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        L = load()
+        raise BpeError(f"{what}: {L.bpe_gpu_strerror(rc).decode()} ({L.bpe_gpu_last_error().decode()})")

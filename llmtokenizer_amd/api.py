@@ -1,0 +1,236 @@
+"""Python mirror of the drop-in C API (include/bpe.h + bpe_ex.h), over ctypes.
+
+Names and argument meaning follow the reference (neofytr/LLMTokenizer
+bpe/inc/bpe.h): compress(path) trains until the reference's stop rule and
+returns (merges, ids); decompress(ids, merges) inverts it; dump_pairs /
+read_pairs use the reference's raw 8-byte record format.  Merges are numpy
+uint32 arrays of shape (k, 2) for ids 256..255+k.  Every call runs through
+libbpe_amd.so on the GPU; errors raise BpeError (the C layer returns NULL).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import BpeError, GpuStats
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def _arr_to_merges(arr_p):
+    """dyn_arr_t* of pair_t (ids 0..last_index) -> (k,2) uint32 for ids >= 256"""
+    L = _lib.load()
+    last = arr_p.contents.last_index
+    k = max(0, last - 255)
+    out = np.zeros((k, 2), dtype=np.uint32)
+    buf = (ctypes.c_uint32 * 2)()
+    for r in range(k):
+        if not L.dyn_arr_get(arr_p, 256 + r, ctypes.cast(buf, ctypes.c_void_p)):
+            raise BpeError(f"merge list has no record for id {256 + r}")
+        out[r] = (buf[0], buf[1])
+    return out
+
+
+def _merges_to_arr(merges):
+    L = _lib.load()
+    m = np.ascontiguousarray(merges, dtype=np.uint32).reshape(-1, 2)
+    arr = L.dyn_arr_create(512, 8)
+    if not arr:
+        raise MemoryError
+    buf = (ctypes.c_uint32 * 2)()
+    for i in range(256):
+        buf[0], buf[1] = i, 0
+        L.dyn_arr_set(arr, i, ctypes.cast(buf, ctypes.c_void_p))
+    for r in range(m.shape[0]):
+        buf[0], buf[1] = int(m[r, 0]), int(m[r, 1])
+        L.dyn_arr_set(arr, 256 + r, ctypes.cast(buf, ctypes.c_void_p))
+    return arr
+
+
+def _take_ids(ptr, n):
+    ids = np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0, dtype=np.uint32)
+    ctypes.CDLL(None).free(ctypes.cast(ptr, ctypes.c_void_p))
+    return ids
+
+
+def last_stats():
+    st = GpuStats()
+    _lib.load().bpe_last_stats(ctypes.byref(st))
+    return st.as_dict()
+
+
+def compress(path, max_merges=None, device=0):
+    """Train on a file (reference compress, bpe.c:541).  Returns (merges, ids)."""
+    L = _lib.load()
+    enc = _u32p()
+    n = ctypes.c_size_t(0)
+    if max_merges is None and device == 0 and "BPE_MAX_MERGES" not in os.environ:
+        arr = L.compress(os.fsencode(path), ctypes.byref(enc), ctypes.byref(n))
+    else:
+        mm = -1 if max_merges is None else int(max_merges)
+        arr = L.compress_ex(os.fsencode(path), mm, int(device), ctypes.byref(enc), ctypes.byref(n))
+    if not arr:
+        raise BpeError(f"compress({path!r}) failed")
+    try:
+        merges = _arr_to_merges(arr)
+    finally:
+        L.dyn_arr_free(arr)
+    return merges, _take_ids(enc, n.value)
+
+
+def train_bytes(data: bytes, max_merges=-1, device=0):
+    """Train on in-memory bytes (no NUL truncation here).  Returns (merges, ids)."""
+    L = _lib.load()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    enc = _u32p()
+    n = ctypes.c_size_t(0)
+    arr = L.bpe_train_bytes(buf.ctypes.data_as(ctypes.c_void_p), buf.size, int(max_merges), int(device),
+                            ctypes.byref(enc), ctypes.byref(n))
+    if not arr:
+        raise BpeError("bpe_train_bytes failed")
+    try:
+        merges = _arr_to_merges(arr)
+    finally:
+        L.dyn_arr_free(arr)
+    return merges, _take_ids(enc, n.value)
+
+
+def encode(data: bytes, merges, device=0):
+    """Standalone encoder: merges applied in rank order (reference replace pass)."""
+    L = _lib.load()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    arr = _merges_to_arr(merges)
+    n = ctypes.c_size_t(0)
+    try:
+        p = L.bpe_encode_bytes(buf.ctypes.data_as(ctypes.c_void_p), buf.size, arr, int(device), ctypes.byref(n))
+    finally:
+        L.dyn_arr_free(arr)
+    if not p:
+        raise BpeError("bpe_encode_bytes failed")
+    return _take_ids(p, n.value)
+
+
+def decompress(ids, merges):
+    """Reference decompress (bpe.c:341): bytes of the ids, NUL bytes dropped."""
+    L = _lib.load()
+    ids = np.ascontiguousarray(ids, dtype=np.uint32)
+    arr = _merges_to_arr(merges)
+    try:
+        p = L.decompress(ids.ctypes.data_as(_u32p), ids.size, arr)
+    finally:
+        L.dyn_arr_free(arr)
+    if not p:
+        raise BpeError("decompress failed")
+    s = ctypes.string_at(p)
+    ctypes.CDLL(None).free(ctypes.c_void_p(p))
+    return s
+
+
+def dump_pairs(path, merges):
+    L = _lib.load()
+    arr = _merges_to_arr(merges)
+    try:
+        ok = L.dump_pairs(os.fsencode(path), arr)
+    finally:
+        L.dyn_arr_free(arr)
+    if not ok:
+        raise BpeError("dump_pairs failed")
+
+
+def read_pairs(path):
+    L = _lib.load()
+    arr = L.read_pairs(os.fsencode(path))
+    if not arr:
+        raise BpeError("read_pairs failed")
+    try:
+        return _arr_to_merges(arr)
+    finally:
+        L.dyn_arr_free(arr)
+
+
+class Engine:
+    """Direct handle on one GPU context (bpe_gpu.h) -- used by bench.py to keep
+    the corpus resident in HBM and time the training loop alone."""
+
+    def __init__(self, device=0):
+        self.L = _lib.load()
+        self.ctx = ctypes.c_void_p()
+        _lib.check(self.L.bpe_gpu_create(int(device), ctypes.byref(self.ctx)), "bpe_gpu_create")
+
+    def close(self):
+        if self.ctx:
+            self.L.bpe_gpu_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, data: bytes):
+        buf = np.frombuffer(data, dtype=np.uint8)
+        _lib.check(self.L.bpe_gpu_load(self.ctx, buf.ctypes.data_as(ctypes.c_void_p), buf.size), "load")
+
+    def synth(self, seed, n, offset=0):
+        _lib.check(self.L.bpe_gpu_synth(self.ctx, int(seed), int(n), int(offset)), "synth")
+
+    def train(self, max_merges=-1):
+        k = ctypes.c_size_t(0)
+        _lib.check(self.L.bpe_gpu_train(self.ctx, int(max_merges), ctypes.byref(k)), "train")
+        return k.value
+
+    def encode(self, merges):
+        m = np.ascontiguousarray(merges, dtype=np.uint32).reshape(-1)
+        _lib.check(self.L.bpe_gpu_encode(self.ctx, m.ctypes.data_as(ctypes.c_void_p), m.size // 2), "encode")
+
+    def merges(self):
+        cnt = ctypes.c_size_t(0)
+        _lib.check(self.L.bpe_gpu_fetch_merges(self.ctx, None, 0, ctypes.byref(cnt)), "fetch_merges")
+        out = np.zeros(2 * max(cnt.value, 1), dtype=np.uint32)
+        _lib.check(self.L.bpe_gpu_fetch_merges(self.ctx, out.ctypes.data_as(ctypes.c_void_p), cnt.value,
+                                               ctypes.byref(cnt)), "fetch_merges")
+        return out[: 2 * cnt.value].reshape(-1, 2)
+
+    def ids(self):
+        n = ctypes.c_size_t(0)
+        _lib.check(self.L.bpe_gpu_fetch_ids(self.ctx, None, 0, ctypes.byref(n)), "fetch_ids")
+        out = np.zeros(max(n.value, 1), dtype=np.uint32)
+        _lib.check(self.L.bpe_gpu_fetch_ids(self.ctx, out.ctypes.data_as(ctypes.c_void_p), n.value,
+                                            ctypes.byref(n)), "fetch_ids")
+        return out[: n.value]
+
+    def decode(self, ids, merges):
+        ids = np.ascontiguousarray(ids, dtype=np.uint32)
+        m = np.ascontiguousarray(merges, dtype=np.uint32).reshape(-1)
+        n = ctypes.c_size_t(0)
+        vp = ctypes.c_void_p
+        _lib.check(self.L.bpe_gpu_decode(self.ctx, ids.ctypes.data_as(vp), ids.size, m.ctypes.data_as(vp),
+                                         m.size // 2, None, 0, ctypes.byref(n)), "decode")
+        out = np.zeros(max(n.value, 1), dtype=np.uint8)
+        _lib.check(self.L.bpe_gpu_decode(self.ctx, ids.ctypes.data_as(vp), ids.size, m.ctypes.data_as(vp),
+                                         m.size // 2, out.ctypes.data_as(vp), out.size, ctypes.byref(n)),
+                   "decode")
+        return out[: n.value].tobytes()
+
+    def stats(self):
+        st = GpuStats()
+        _lib.check(self.L.bpe_gpu_get_stats(self.ctx, ctypes.byref(st)), "stats")
+        return st.as_dict()
+
+    def kernel_profile(self):
+        name = ctypes.c_char_p()
+        ms = ctypes.c_double()
+        by = ctypes.c_double()
+        n = ctypes.c_uint64()
+        _lib.check(self.L.bpe_gpu_kernel_profile(self.ctx, ctypes.byref(name), ctypes.byref(ms), ctypes.byref(by),
+                                                 ctypes.byref(n)), "kernel_profile")
+        return (name.value or b"").decode(), ms.value, by.value, n.value
+
+
+def device_count():
+    L = _lib.load()
+    n = ctypes.c_int(0)
+    L.bpe_gpu_device_count(ctypes.byref(n))
+    return n.value

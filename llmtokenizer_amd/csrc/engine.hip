@@ -1,0 +1,1068 @@
+// engine.hip -- host side of the gfx950 BPE engine: allocation in HBM, the
+// one-off counting sort, graph-captured merge iterations, and the resolver
+// that reproduces the reference's hash-chain tie order exactly.
+//
+// C-ABI: include/bpe_gpu.h.  One context = one device, one stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/bpe_gpu.h"
+#include "kernels.hip"
+
+using namespace bpeamd;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char *what, hipError_t e = hipSuccess) {
+    char buf[512];
+    if (e != hipSuccess)
+        snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    else
+        snprintf(buf, sizeof buf, "%s", what);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                       \
+    do {                                                                \
+        hipError_t e_ = (x);                                            \
+        if (e_ != hipSuccess) return fail(BPE_GPU_EHIP, #x, e_);        \
+    } while (0)
+
+uint64_t pow2_at_least(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+constexpr uint32_t ITERS_PER_GRAPH = 16;
+constexpr uint32_t SCAN_BLOCKS = 1024;
+constexpr uint32_t APPLY_A = 256, APPLY_B = 64;
+constexpr uint32_t RESCAN1_BLOCKS = 1024, RESCAN2_BLOCKS = 128;
+
+struct Query {
+    uint32_t t, bucket, firstc, flags;  // flags: 1 rho, 2 nb_less(new), 4 list mates
+};
+struct Mate {
+    uint32_t q, u, v, firstc, isnew, pad;
+};
+
+}  // namespace
+
+// ------------------------------------------------------ resolver kernels
+namespace bpeamd {
+
+__device__ inline uint64_t stat_cap(const Ctl *C) {
+    uint64_t cap = 1024;
+    while (cap < 2 * C->stat_n) cap <<= 1;
+    return cap;
+}
+
+__device__ inline int64_t stat_find(const Eng *E, uint64_t cap, uint32_t t, uint32_t u, uint32_t v) {
+    const unsigned long long key = skey_of(t, u, v);
+    uint64_t s = mix64(key) & (cap - 1);
+    for (;;) {
+        const unsigned long long k = E->skey[s];
+        if (k == key) return (int64_t)s;
+        if (k == 0) return -1;
+        s = (s + 1) & (cap - 1);
+    }
+}
+
+// keys of the pair table with count == M
+__global__ void k_res_collect(const Eng *E, uint32_t M, uint32_t *out, uint32_t *n, uint32_t cap) {
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < E->hcap; s += (uint64_t)gridDim.x * blockDim.x) {
+        if (E->hcnt[s] != M) continue;
+        const unsigned long long k = E->hkey[s] - 1;
+        const uint32_t p = atomicAdd(n, 1u);
+        if (p < cap) {
+            out[2 * p] = (uint32_t)(k >> 32);
+            out[2 * p + 1] = (uint32_t)k;
+        }
+    }
+}
+
+// first thread containing each key and its first compacted position there
+__global__ void k_res_lookup(const Eng *E, const Ctl *C, const uint32_t *keys, uint32_t n, uint32_t *outT,
+                             uint32_t *outFirst) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const uint64_t cap = stat_cap(C);
+    outT[q] = 0xFFFFFFFFu;
+    outFirst[q] = 0xFFFFFFFFu;
+    for (uint32_t t = 0; t < NTHR; t++) {
+        const int64_t s = stat_find(E, cap, t, keys[2 * q], keys[2 * q + 1]);
+        if (s >= 0) {
+            outT[q] = t;
+            outFirst[q] = E->sfirst[s];
+            return;
+        }
+    }
+}
+
+// largest thread-table bucket used by thread t
+__global__ void k_res_maxbucket(const Eng *E, const Ctl *C, uint32_t t, uint32_t *out) {
+    const uint64_t cap = stat_cap(C);
+    const uint64_t Bt = C->Bfin[t];
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long k = E->skey[s];
+        if (!k) continue;
+        const unsigned long long key = k - 1;
+        if ((uint32_t)(key >> 60) != t) continue;
+        const uint32_t u = (uint32_t)((key >> 30) & 0x3FFFFFFFull), v = (uint32_t)(key & 0x3FFFFFFFull);
+        atomicMax(out, (uint32_t)(murmur_pair(u, v) & (Bt - 1)));
+    }
+}
+
+// one pass over the (thread, pair) set answering a few queries
+__global__ void k_res_pass(const Eng *E, const Ctl *C, const Query *qs, uint32_t nq, uint32_t *rho, uint32_t *nbl,
+                           Mate *mates, uint32_t *nmates, uint32_t mcap, uint32_t *newt) {
+    const uint64_t cap = stat_cap(C);
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long k = E->skey[s];
+        if (!k) continue;
+        const unsigned long long key = k - 1;
+        const uint32_t t = (uint32_t)(key >> 60);
+        const uint32_t u = (uint32_t)((key >> 30) & 0x3FFFFFFFull), v = (uint32_t)(key & 0x3FFFFFFFull);
+        int isnew = -1;
+        auto is_new = [&]() {
+            if (isnew < 0) {
+                isnew = 1;
+                for (uint32_t t2 = 0; t2 < t; t2++)
+                    if (stat_find(E, cap, t2, u, v) >= 0) { isnew = 0; break; }
+            }
+            return isnew == 1;
+        };
+        if (newt && is_new()) atomicAdd(&newt[t], 1u);
+        const uint32_t bt = (uint32_t)(murmur_pair(u, v) & (C->Bfin[t] - 1));
+        const uint32_t fc = E->sfirst[s];
+        for (uint32_t q = 0; q < nq; q++) {
+            if (qs[q].t != t) continue;
+            if ((qs[q].flags & 1) && fc < qs[q].firstc) atomicAdd(&rho[q], 1u);
+            if ((qs[q].flags & 2) && bt < qs[q].bucket && is_new()) atomicAdd(&nbl[q], 1u);
+            if ((qs[q].flags & 4) && bt == qs[q].bucket) {
+                const uint32_t p = atomicAdd(nmates, 1u);
+                if (p < mcap) mates[p] = Mate{q, u, v, fc, is_new() ? 1u : 0u, 0};
+            }
+        }
+    }
+}
+
+}  // namespace bpeamd
+
+// ------------------------------------------------------------------ context
+struct bpe_gpu_ctx {
+    int dev = 0;
+    hipStream_t st = nullptr;
+    Eng h{};
+    Eng *dE = nullptr;
+    Ctl *dC = nullptr;
+    Ctl *hC = nullptr;  // pinned
+    uint64_t n0 = 0;
+    bool loaded = false;
+    bool ids_ready = false;
+    uint64_t ids_len = 0;
+    size_t merges_done = 0;
+    std::vector<void *> train_allocs;
+    uint32_t *d_tileoff = nullptr;
+    uint32_t *d_enc_pairs = nullptr;
+    hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr;
+    bpe_gpu_stats stats{};
+    // profile of the dominant kernel
+    std::string prof_name;
+    double prof_ms = 0, prof_bytes = 0;
+    uint64_t prof_launches = 0;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(bpe_gpu_ctx *c, T **p, size_t count, bool zero = true) {
+    size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+    hipError_t e = hipMalloc((void **)p, bytes);
+    if (e != hipSuccess) return fail(BPE_GPU_ENOMEM, "hipMalloc", e);
+    c->train_allocs.push_back(*p);
+    if (zero) {
+        e = hipMemsetAsync(*p, 0, bytes, c->st);
+        if (e != hipSuccess) return fail(BPE_GPU_EHIP, "hipMemsetAsync", e);
+    }
+    return 0;
+}
+
+void free_train(bpe_gpu_ctx *c) {
+    if (c->st) hipStreamSynchronize(c->st);
+    for (void *p : c->train_allocs) hipFree(p);
+    c->train_allocs.clear();
+    for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked, &c->g_encode}) {
+        if (*g) hipGraphExecDestroy(*g);
+        *g = nullptr;
+    }
+    c->ids_ready = false;
+}
+
+int push_desc(bpe_gpu_ctx *c) {
+    HIPCHK(hipMemcpyAsync(c->dE, &c->h, sizeof(Eng), hipMemcpyHostToDevice, c->st));
+    return 0;
+}
+
+int pull_ctl(bpe_gpu_ctx *c) {
+    HIPCHK(hipMemcpyAsync(c->hC, c->dC, sizeof(Ctl), hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int push_ctl(bpe_gpu_ctx *c) {
+    HIPCHK(hipMemcpyAsync(c->dC, c->hC, sizeof(Ctl), hipMemcpyHostToDevice, c->st));
+    return 0;
+}
+
+// allocate the per-run structures (sizes depend on the merge cap)
+int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
+    free_train(c);
+    Eng &h = c->h;
+    h.n0 = c->n0;
+    h.mcap = mcap;
+    h.vcap = 256 + mcap;
+    h.encode = encode ? 1 : 0;
+    const uint64_t n0 = c->n0;
+    int r;
+    if ((r = dalloc(c, &h.tok, n0, false))) return r;
+    if ((r = dalloc(c, &h.dist, n0))) return r;
+    if ((r = dalloc(c, &h.tlen, h.vcap))) return r;
+    if ((r = dalloc(c, &h.rank, 256))) return r;
+    if ((r = dalloc(c, &h.plist, n0, false))) return r;
+    if ((r = dalloc(c, &h.occ, n0, false))) return r;
+    if ((r = dalloc(c, &h.occ_off, h.vcap))) return r;
+    if ((r = dalloc(c, &h.occ_len, h.vcap))) return r;
+    if ((r = dalloc(c, &h.merges, 2ull * std::max<uint32_t>(mcap, 1)))) return r;
+    for (int p = 0; p < 2; p++) {
+        for (int v = 0; v < 4; v++) {
+            if ((r = dalloc(c, &h.vec[p][v], encode ? 1 : h.vcap))) return r;
+            if ((r = dalloc(c, &h.vlist[p][v], encode ? 1 : h.vcap, false))) return r;
+        }
+        if ((r = dalloc(c, &h.vnl[p], 4))) return r;
+    }
+    h.ntiles = (n0 + CTILE - 1) / CTILE;
+    if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
+    if ((r = dalloc(c, &c->d_tileoff, h.ntiles + 1))) return r;
+    if ((r = dalloc(c, &h.ids_out, n0, false))) return r;
+    const uint64_t tn = std::min<uint64_t>(n0, TRACK_LIMIT);
+    if ((r = dalloc(c, &h.cpos, encode ? 1 : tn, false))) return r;
+    h.scap = encode ? 1024 : pow2_at_least(std::max<uint64_t>(1024, 2 * tn));
+    if ((r = dalloc(c, &h.skey, h.scap))) return r;
+    if ((r = dalloc(c, &h.scnt, h.scap))) return r;
+    if ((r = dalloc(c, &h.sfirst, h.scap))) return r;
+    // pair table
+    if (!encode) {
+        uint64_t want = 4ull * (65536 + 16ull * (256 + std::min<uint64_t>(mcap, 4096)));
+        h.hcap = pow2_at_least(std::max<uint64_t>(want, 1ull << 17));
+    } else {
+        h.hcap = 1ull << 16;
+    }
+    const uint64_t nL1 = h.hcap / L1W, nL2 = (nL1 + L2W - 1) / L2W;
+    if ((r = dalloc(c, &h.hkey, h.hcap))) return r;
+    if ((r = dalloc(c, &h.hcnt, h.hcap))) return r;
+    if ((r = dalloc(c, &h.l1best, nL1))) return r;
+    if ((r = dalloc(c, &h.l1tie, nL1))) return r;
+    if ((r = dalloc(c, &h.l1arg, nL1))) return r;
+    if ((r = dalloc(c, &h.l1dirty, nL1))) return r;
+    if ((r = dalloc(c, &h.l1list, nL1, false))) return r;
+    if ((r = dalloc(c, &h.l2best, nL2))) return r;
+    if ((r = dalloc(c, &h.l2tie, nL2))) return r;
+    if ((r = dalloc(c, &h.l2arg, nL2))) return r;
+    if ((r = dalloc(c, &h.l2dirty, nL2))) return r;
+    if ((r = dalloc(c, &h.l2list, nL2, false))) return r;
+    // control block
+    Ctl &C = *c->hC;
+    memset(&C, 0, sizeof(Ctl));
+    C.n_live = n0;
+    for (uint32_t t = 0; t < NTHR; t++) C.Bcur[t] = THREAD_B0;
+    C.full = 1;
+    if ((r = push_ctl(c))) return r;
+    return push_desc(c);
+}
+
+// replace the pair table by one of capacity ncap (keys with count 0 dropped)
+int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
+    Eng &h = c->h;
+    unsigned long long *okey = h.hkey;
+    uint32_t *ocnt = h.hcnt;
+    const uint64_t ocap = h.hcap;
+    unsigned long long *nkey;
+    uint32_t *ncnt;
+    HIPCHK(hipMalloc(&nkey, ncap * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&ncnt, ncap * sizeof(uint32_t)));
+    HIPCHK(hipMemsetAsync(nkey, 0, ncap * sizeof(unsigned long long), c->st));
+    HIPCHK(hipMemsetAsync(ncnt, 0, ncap * sizeof(uint32_t), c->st));
+    const uint64_t nL1 = ncap / L1W, nL2 = (nL1 + L2W - 1) / L2W;
+    unsigned long long *l1b, *l2b;
+    uint32_t *l1t, *l1a, *l1d, *l1l, *l2t, *l2a, *l2d, *l2l;
+    HIPCHK(hipMalloc(&l1b, nL1 * 8));
+    HIPCHK(hipMalloc(&l1t, nL1 * 4));
+    HIPCHK(hipMalloc(&l1a, nL1 * 4));
+    HIPCHK(hipMalloc(&l1d, nL1 * 4));
+    HIPCHK(hipMalloc(&l1l, nL1 * 4));
+    HIPCHK(hipMalloc(&l2b, nL2 * 8));
+    HIPCHK(hipMalloc(&l2t, nL2 * 4));
+    HIPCHK(hipMalloc(&l2a, nL2 * 4));
+    HIPCHK(hipMalloc(&l2d, nL2 * 4));
+    HIPCHK(hipMalloc(&l2l, nL2 * 4));
+    HIPCHK(hipMemsetAsync(l1d, 0, nL1 * 4, c->st));
+    HIPCHK(hipMemsetAsync(l2d, 0, nL2 * 4, c->st));
+    void *olds[] = {h.hkey, h.hcnt, h.l1best, h.l1tie, h.l1arg, h.l1dirty, h.l1list,
+                    h.l2best, h.l2tie, h.l2arg, h.l2dirty, h.l2list};
+    h.hkey = nkey; h.hcnt = ncnt; h.hcap = ncap;
+    h.l1best = l1b; h.l1tie = l1t; h.l1arg = l1a; h.l1dirty = l1d; h.l1list = l1l;
+    h.l2best = l2b; h.l2tie = l2t; h.l2arg = l2a; h.l2dirty = l2d; h.l2list = l2l;
+    int r;
+    if ((r = push_desc(c))) return r;
+    c->hC->nkeys = 0;
+    HIPCHK(hipMemcpyAsync(&c->dC->nkeys, &c->hC->nkeys, sizeof(unsigned long long), hipMemcpyHostToDevice, c->st));
+    k_rehash<<<1024, 256, 0, c->st>>>(c->dE, c->dC, okey, ocnt, ocap);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->st));
+    for (void *p : olds) {
+        auto it = std::find(c->train_allocs.begin(), c->train_allocs.end(), p);
+        if (it != c->train_allocs.end()) c->train_allocs.erase(it);
+        hipFree(p);
+    }
+    for (void *p : {(void *)nkey, (void *)ncnt, (void *)l1b, (void *)l1t, (void *)l1a, (void *)l1d, (void *)l1l,
+                    (void *)l2b, (void *)l2t, (void *)l2a, (void *)l2d, (void *)l2l})
+        c->train_allocs.push_back(p);
+    c->stats.table_grows++;
+    return 0;
+}
+
+void launch_stats(bpe_gpu_ctx *c) {
+    k_stat_clear<<<256, 256, 0, c->st>>>(c->dE, c->dC);
+    k_stat_count<<<512, 256, 0, c->st>>>(c->dE, c->dC);
+    k_stat_scan<<<1, 1024, 0, c->st>>>(c->dE, c->dC, c->d_tileoff);
+    k_stat_map<<<512, 256, 0, c->st>>>(c->dE, c->dC, c->d_tileoff);
+    k_stat_insert<<<512, 256, 0, c->st>>>(c->dE, c->dC);
+    k_stat_final<<<1, 64, 0, c->st>>>(c->dE, c->dC);
+}
+
+void launch_summaries(bpe_gpu_ctx *c) {
+    k_rescan1<<<RESCAN1_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+    k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+}
+
+void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
+    k_scan<<<SCAN_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+    k_apply<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
+    if (tracked) launch_stats(c);
+    launch_summaries(c);
+    k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? 1u : 0u);
+}
+
+int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint32_t n_enc = 0) {
+    hipGraph_t g;
+    HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+    for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++) {
+        if (encode) {
+            k_scan<<<SCAN_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+            k_apply<<<APPLY_A, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
+            k_enc_next<<<1, 1, 0, c->st>>>(c->dE, c->dC, c->d_enc_pairs, n_enc);
+        } else {
+            launch_iteration(c, tracked);
+        }
+    }
+    HIPCHK(hipStreamEndCapture(c->st, &g));
+    HIPCHK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+    HIPCHK(hipGraphDestroy(g));
+    return 0;
+}
+
+// ----------------------------------------------------------------- resolver
+// Reproduces, for one tracked (static-split) iteration, the order in which the
+// reference's merged table lists the keys tied on (count, bucket), from the
+// per-thread statistics the device collected for this counting phase.
+struct Resolver {
+    bpe_gpu_ctx *c;
+    uint32_t *d_buf = nullptr;  // scratch
+    size_t d_cap = 0;
+
+    int scratch(size_t bytes) {
+        if (bytes <= d_cap) return 0;
+        if (d_buf) hipFree(d_buf);
+        d_cap = std::max<size_t>(bytes, 1 << 20);
+        HIPCHK(hipMalloc(&d_buf, d_cap));
+        return 0;
+    }
+    ~Resolver() {
+        if (d_buf) hipFree(d_buf);
+    }
+
+    // resize schedule of one counting phase: returns insertion counts tau after
+    // which a doubling happens (tau < D, or tau == D when a call followed)
+    static std::vector<uint64_t> resize_points(uint64_t B, uint64_t D, bool follows) {
+        std::vector<uint64_t> pts;
+        for (;;) {
+            double t = 0.3 * (double)B;
+            uint64_t tau = (uint64_t)t;
+            if ((double)tau < t) tau++;  // smallest n with n >= 0.3*B
+            if (tau < D || (tau == D && follows)) {
+                pts.push_back(tau);
+                B *= 2;
+                continue;
+            }
+            break;
+        }
+        return pts;
+    }
+
+    // final chain order of keys inserted at (1-based) times ins[i] under head
+    // insertion, with whole-bucket reversals after each point in `res`
+    static std::vector<size_t> chain_order(const std::vector<uint64_t> &ins, const std::vector<uint64_t> &res) {
+        std::vector<size_t> idx(ins.size());
+        for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+        std::sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return ins[x] < ins[y]; });
+        std::vector<size_t> chain;
+        size_t ri = 0, ii = 0;
+        while (ii < idx.size() || ri < res.size()) {
+            // event at time ins (integer) vs resize at res + 0.5
+            if (ii < idx.size() && (ri >= res.size() || ins[idx[ii]] <= res[ri])) {
+                chain.insert(chain.begin(), idx[ii]);
+                ii++;
+            } else {
+                std::reverse(chain.begin(), chain.end());
+                ri++;
+            }
+        }
+        return chain;
+    }
+
+    int run_pass(const std::vector<Query> &qs, std::vector<uint32_t> &rho, std::vector<uint32_t> &nbl,
+                 std::vector<Mate> &mates, std::vector<uint32_t> *newt) {
+        const uint32_t nq = (uint32_t)qs.size();
+        const uint32_t mcap = 4096;
+        size_t need = nq * sizeof(Query) + 2 * nq * 4 + 4 + mcap * sizeof(Mate) + 64 + 16 * 4;
+        int r;
+        if ((r = scratch(need + 256))) return r;
+        char *base = (char *)d_buf;
+        Query *dq = (Query *)base;
+        uint32_t *drho = (uint32_t *)(base + nq * sizeof(Query));
+        uint32_t *dnbl = drho + nq;
+        uint32_t *dnm = dnbl + nq;
+        uint32_t *dnewt = dnm + 1;
+        Mate *dm = (Mate *)(((uintptr_t)(dnewt + 16) + 15) & ~(uintptr_t)15);
+        HIPCHK(hipMemcpyAsync(dq, qs.data(), nq * sizeof(Query), hipMemcpyHostToDevice, c->st));
+        HIPCHK(hipMemsetAsync(drho, 0, (2 * nq + 1 + 16) * 4, c->st));
+        k_res_pass<<<512, 256, 0, c->st>>>(c->dE, c->dC, dq, nq, drho, dnbl, dm, dnm, mcap, newt ? dnewt : nullptr);
+        HIPCHK(hipGetLastError());
+        rho.assign(nq, 0);
+        nbl.assign(nq, 0);
+        uint32_t nm = 0;
+        if (nq) {
+            HIPCHK(hipMemcpyAsync(rho.data(), drho, nq * 4, hipMemcpyDeviceToHost, c->st));
+            HIPCHK(hipMemcpyAsync(nbl.data(), dnbl, nq * 4, hipMemcpyDeviceToHost, c->st));
+        }
+        HIPCHK(hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, c->st));
+        if (newt) {
+            newt->assign(16, 0);
+            HIPCHK(hipMemcpyAsync(newt->data(), dnewt, 64, hipMemcpyDeviceToHost, c->st));
+        }
+        HIPCHK(hipStreamSynchronize(c->st));
+        if (nm > mcap) return fail(BPE_GPU_EINTERNAL, "resolver: bucket chain longer than 4096");
+        mates.resize(nm);
+        if (nm) {
+            HIPCHK(hipMemcpyAsync(mates.data(), dm, nm * sizeof(Mate), hipMemcpyDeviceToHost, c->st));
+            HIPCHK(hipStreamSynchronize(c->st));
+        }
+        return 0;
+    }
+
+    struct KeyInfo {
+        uint32_t u, v, T, firstc, tb;
+        uint64_t rank_in_thread = 0;  // 0-based position among new keys of thread T
+        uint64_t merged = 0;          // 1-based merged insertion index
+    };
+
+    // Order of a thread-table bucket's keys: returns the mates of query q in
+    // chain order (head first).  rho of each mate is fetched with a second pass.
+    int thread_chain(uint32_t T, std::vector<Mate> &m, std::vector<size_t> &order) {
+        std::vector<Query> q2;
+        for (auto &x : m) q2.push_back(Query{T, 0, x.firstc, 1});
+        std::vector<uint32_t> rho, nbl;
+        std::vector<Mate> dummy;
+        int r;
+        if ((r = run_pass(q2, rho, nbl, dummy, nullptr))) return r;
+        const Ctl &C = *c->hC;
+        std::vector<uint64_t> ins(m.size());
+        for (size_t i = 0; i < m.size(); i++) ins[i] = (uint64_t)rho[i] + 1;
+        auto res = resize_points(C.Bstart[T], C.Dt[T], C.follows[T] != 0);
+        order = chain_order(ins, res);
+        return 0;
+    }
+
+    // returns the winner (u, v) for the current STOP_EVENT iteration
+    int resolve(uint32_t *wu, uint32_t *wv) {
+        int r;
+        const Ctl C = *c->hC;
+        const uint32_t M = (uint32_t)(C.W >> 32);
+        uint32_t edge;
+        const uint64_t Bn = bfinal_nominal(C.D, &edge);
+        // 1. all keys with the maximal count
+        uint32_t ncand = 0;
+        {
+            const uint32_t cap = 1u << 20;
+            if ((r = scratch((size_t)cap * 8 + 64))) return r;
+            uint32_t *dn = d_buf + 2 * (size_t)cap;
+            HIPCHK(hipMemsetAsync(dn, 0, 4, c->st));
+            k_res_collect<<<1024, 256, 0, c->st>>>(c->dE, M, d_buf, dn, cap);
+            HIPCHK(hipMemcpyAsync(&ncand, dn, 4, hipMemcpyDeviceToHost, c->st));
+            HIPCHK(hipStreamSynchronize(c->st));
+            if (ncand > cap) return fail(BPE_GPU_EINTERNAL, "resolver: too many maximal keys");
+        }
+        std::vector<uint32_t> keys(2 * (size_t)ncand);
+        HIPCHK(hipMemcpyAsync(keys.data(), d_buf, keys.size() * 4, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        // 2. B_final: at an exact threshold it depends on whether the last insert
+        //    call of the merge walk (tail of the last thread's last bucket) is a
+        //    key already seen in an earlier thread
+        uint64_t Bf = Bn;
+        bool follows_m = false;
+        if (edge) {
+            int Tl = -1;
+            for (int t = NTHR - 1; t >= 0; t--)
+                if (C.Dt[t] > 0) { Tl = t; break; }
+            if (Tl < 0) return fail(BPE_GPU_EINTERNAL, "resolver: no thread keys");
+            uint32_t *dmb = d_buf;
+            HIPCHK(hipMemsetAsync(dmb, 0, 4, c->st));
+            k_res_maxbucket<<<512, 256, 0, c->st>>>(c->dE, c->dC, (uint32_t)Tl, dmb);
+            uint32_t mb = 0;
+            HIPCHK(hipMemcpyAsync(&mb, dmb, 4, hipMemcpyDeviceToHost, c->st));
+            HIPCHK(hipStreamSynchronize(c->st));
+            std::vector<Query> q{Query{(uint32_t)Tl, mb, 0, 4}};
+            std::vector<uint32_t> rho, nbl;
+            std::vector<Mate> mates;
+            if ((r = run_pass(q, rho, nbl, mates, nullptr))) return r;
+            std::vector<size_t> order;
+            if ((r = thread_chain((uint32_t)Tl, mates, order))) return r;
+            const Mate &tail = mates[order.back()];
+            follows_m = !tail.isnew;
+            if (follows_m) Bf = 2 * Bn;
+            c->stats.edge_events++;
+        }
+        // 3. candidates: maximal count, smallest bucket under B_final
+        uint64_t bmin = ~0ull;
+        for (uint32_t i = 0; i < ncand; i++)
+            bmin = std::min<uint64_t>(bmin, murmur_pair(keys[2 * i], keys[2 * i + 1]) & (Bf - 1));
+        std::vector<KeyInfo> cand;
+        for (uint32_t i = 0; i < ncand; i++)
+            if ((murmur_pair(keys[2 * i], keys[2 * i + 1]) & (Bf - 1)) == bmin)
+                cand.push_back(KeyInfo{keys[2 * i], keys[2 * i + 1], 0, 0, 0});
+        if (cand.size() == 1) {
+            *wu = cand[0].u;
+            *wv = cand[0].v;
+            return 0;
+        }
+        c->stats.tie_events++;
+        // 4. per candidate: first thread, first position, thread bucket
+        {
+            std::vector<uint32_t> kk;
+            for (auto &k : cand) { kk.push_back(k.u); kk.push_back(k.v); }
+            const uint32_t n = (uint32_t)cand.size();
+            if ((r = scratch(kk.size() * 4 + 2 * n * 4 + 64))) return r;
+            HIPCHK(hipMemcpyAsync(d_buf, kk.data(), kk.size() * 4, hipMemcpyHostToDevice, c->st));
+            k_res_lookup<<<(n + 255) / 256, 256, 0, c->st>>>(c->dE, c->dC, d_buf, n, d_buf + 2 * n, d_buf + 3 * n);
+            std::vector<uint32_t> T(n), F(n);
+            HIPCHK(hipMemcpyAsync(T.data(), d_buf + 2 * n, n * 4, hipMemcpyDeviceToHost, c->st));
+            HIPCHK(hipMemcpyAsync(F.data(), d_buf + 3 * n, n * 4, hipMemcpyDeviceToHost, c->st));
+            HIPCHK(hipStreamSynchronize(c->st));
+            for (uint32_t i = 0; i < n; i++) {
+                if (T[i] == 0xFFFFFFFFu) return fail(BPE_GPU_EINTERNAL, "resolver: candidate not in thread tables");
+                cand[i].T = T[i];
+                cand[i].firstc = F[i];
+                cand[i].tb = (uint32_t)(murmur_pair(cand[i].u, cand[i].v) & (C.Bfin[T[i]] - 1));
+            }
+        }
+        // 5. merged insertion index of each candidate
+        std::vector<Query> qs;
+        for (auto &k : cand) qs.push_back(Query{k.T, k.tb, k.firstc, 2 | 4});
+        std::vector<uint32_t> rho, nbl, newt;
+        std::vector<Mate> mates;
+        if ((r = run_pass(qs, rho, nbl, mates, &newt))) return r;
+        for (size_t i = 0; i < cand.size(); i++) {
+            KeyInfo &k = cand[i];
+            std::vector<Mate> m;
+            for (auto &x : mates)
+                if (x.q == i) m.push_back(x);
+            std::vector<size_t> order;
+            if ((r = thread_chain(k.T, m, order))) return r;
+            uint64_t before = 0;
+            bool seen = false;
+            for (size_t o : order) {
+                if (m[o].u == k.u && m[o].v == k.v) { seen = true; break; }
+                if (m[o].isnew) before++;
+            }
+            if (!seen) return fail(BPE_GPU_EINTERNAL, "resolver: candidate missing from its bucket");
+            uint64_t prior = 0;
+            for (uint32_t t = 0; t < k.T; t++) prior += newt[t];
+            k.merged = prior + nbl[i] + before + 1;
+        }
+        // 6. merged chain of the candidates' bucket
+        std::vector<uint64_t> ins;
+        for (auto &k : cand) ins.push_back(k.merged);
+        auto res = resize_points(MERGED_B0, C.D, follows_m);
+        auto order = chain_order(ins, res);
+        *wu = cand[order.front()].u;
+        *wv = cand[order.front()].v;
+        return 0;
+    }
+};
+
+int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
+    int r;
+    Resolver res{c};
+    for (;;) {
+        if ((r = pull_ctl(c))) return r;
+        Ctl &C = *c->hC;
+        switch (C.stop) {
+        case STOP_NONE: {
+            hipGraphExec_t *g;
+            if (encode) {
+                g = &c->g_encode;
+            } else {
+                const bool tracked = C.n_live < TRACK_LIMIT;
+                g = tracked ? &c->g_tracked : &c->g_plain;
+                if (!*g && (r = capture(c, g, tracked, false))) return r;
+            }
+            HIPCHK(hipGraphLaunch(*g, c->st));
+            break;
+        }
+        case STOP_DONE:
+        case STOP_CAP:
+        case STOP_ENC_END:
+            return 0;
+        case STOP_ERROR:
+            return fail(BPE_GPU_EINTERNAL, "engine invariant violated (count decrement of an absent pair)");
+        case STOP_MODE:
+            C.stop = STOP_NONE;
+            if ((r = push_ctl(c))) return r;
+            launch_stats(c);
+            launch_summaries(c);
+            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, 1u);
+            HIPCHK(hipGetLastError());
+            break;
+        case STOP_GROW: {
+            C.stop = STOP_NONE;
+            C.full = 1;
+            if ((r = push_ctl(c))) return r;
+            if ((r = grow_table(c, c->h.hcap * 4))) return r;
+            const bool tracked = C.n_live < TRACK_LIMIT;
+            launch_summaries(c);
+            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? 1u : 0u);
+            HIPCHK(hipGetLastError());
+            break;
+        }
+        case STOP_EVENT: {
+            uint32_t u = 0, v = 0;
+            if ((r = res.resolve(&u, &v))) return r;
+            k_commit<<<1, 1, 0, c->st>>>(c->dE, c->dC, u, v);
+            HIPCHK(hipGetLastError());
+            break;
+        }
+        default:
+            return fail(BPE_GPU_EINTERNAL, "unknown stop state");
+        }
+    }
+}
+
+int compact_ids(bpe_gpu_ctx *c) {
+    k_tile_count<<<512, 256, 0, c->st>>>(c->dE);
+    // plain exclusive scan of tile counts
+    k_scan_single<<<1, 1024, 0, c->st>>>(c->h.tilecnt, c->d_tileoff, (uint32_t)c->h.ntiles);
+    k_tile_write<<<512, 256, 0, c->st>>>(c->dE, c->d_tileoff, 0);
+    HIPCHK(hipGetLastError());
+    uint32_t tot = 0;
+    HIPCHK(hipMemcpyAsync(&tot, c->d_tileoff + c->h.ntiles, 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->ids_len = tot;
+    c->ids_ready = true;
+    return 0;
+}
+
+// common init: tokens, byte ranks, counting sort of byte-pair positions
+int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_tot_out) {
+    Eng &h = c->h;
+    uint32_t *d_bh;
+    int r;
+    if ((r = dalloc(c, &d_bh, 256))) return r;
+    k_init_tok<<<1024, 256, 0, c->st>>>(c->dE, d_bh);
+    HIPCHK(hipGetLastError());
+    std::vector<uint32_t> bh(256);
+    HIPCHK(hipMemcpyAsync(bh.data(), d_bh, 1024, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    std::vector<uint32_t> rank(256, HOLE), unrank;
+    for (uint32_t x = 0; x < 256; x++)
+        if (bh[x]) { rank[x] = (uint32_t)unrank.size(); unrank.push_back(x); }
+    h.A = (uint32_t)unrank.size();
+    HIPCHK(hipMemcpyAsync(h.rank, rank.data(), 1024, hipMemcpyHostToDevice, c->st));
+    std::vector<uint32_t> tl(h.vcap, 1);
+    HIPCHK(hipMemcpyAsync(h.tlen, tl.data(), 4ull * h.vcap, hipMemcpyHostToDevice, c->st));
+    const uint32_t AA = h.A * h.A;
+    if ((r = dalloc(c, &h.poff, AA + 1))) return r;
+    if ((r = push_desc(c))) return r;
+    // counting sort of pair positions by rank key
+    const uint64_t npairs = c->n0 - 1;
+    uint64_t tile = std::max<uint64_t>(1 << 16, (npairs + 1023) / 1024);
+    const uint32_t ntl = (uint32_t)((npairs + tile - 1) / tile);
+    const uint32_t parts = (AA + HBINS - 1) / HBINS;
+    uint32_t *d_hist, *d_tot;
+    if ((r = dalloc(c, &d_hist, (size_t)ntl * AA, false))) return r;
+    if ((r = dalloc(c, &d_tot, AA + 1))) return r;
+    if (npairs > 0) {
+        // the one full pass over the corpus: time it with events on our stream
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipEventRecord(e0, c->st));
+        k_pair_hist<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
+        HIPCHK(hipEventRecord(e1, c->st));
+        HIPCHK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        hipEventDestroy(e0);
+        hipEventDestroy(e1);
+        c->prof_name = "k_pair_hist";
+        c->prof_ms = ms;
+        c->prof_bytes = (double)c->n0 * parts;  // 1 B/token (V = 256), re-read once per bin part
+        c->prof_launches = 1;
+        k_pair_colscan<<<(AA + 255) / 256, 256, 0, c->st>>>(d_hist, d_tot, AA, ntl);
+        k_scan_single<<<1, 1024, 0, c->st>>>(d_tot, h.poff, AA);
+        k_pair_scatter<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
+        HIPCHK(hipGetLastError());
+    } else {
+        HIPCHK(hipMemsetAsync(h.poff, 0, 4ull * (AA + 1), c->st));
+    }
+    *unrank_out = unrank;
+    *d_tot_out = d_tot;
+    return 0;
+}
+
+}  // namespace
+
+// ===================================================================== C-ABI
+extern "C" {
+
+const char *bpe_gpu_strerror(int code) {
+    switch (code) {
+    case BPE_GPU_OK: return "ok";
+    case BPE_GPU_EINVAL: return "invalid argument";
+    case BPE_GPU_EHIP: return "HIP runtime error";
+    case BPE_GPU_ENOMEM: return "device out of memory";
+    case BPE_GPU_ENODEV: return "no such GPU";
+    case BPE_GPU_ESTATE: return "call out of order";
+    case BPE_GPU_ERANGE: return "corpus too large for one device (max 2^32-2 bytes)";
+    case BPE_GPU_EDATA: return "unknown token id or corrupt merge list";
+    case BPE_GPU_EINTERNAL: return "engine invariant violated";
+    default: return "unknown error";
+    }
+}
+
+const char *bpe_gpu_last_error(void) { return g_last_error.c_str(); }
+
+int bpe_gpu_device_count(int *count) {
+    if (!count) return BPE_GPU_EINVAL;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) { *count = 0; return fail(BPE_GPU_ENODEV, "hipGetDeviceCount", e); }
+    *count = n;
+    return 0;
+}
+
+int bpe_gpu_create(int device, bpe_gpu_ctx **out) {
+    if (!out) return BPE_GPU_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(BPE_GPU_ENODEV, "no such device");
+    HIPCHK(hipSetDevice(device));
+    bpe_gpu_ctx *c = new bpe_gpu_ctx();
+    c->dev = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
+    HIPCHK(hipMalloc(&c->dE, sizeof(Eng)));
+    HIPCHK(hipMalloc(&c->dC, sizeof(Ctl)));
+    HIPCHK(hipHostMalloc(&c->hC, sizeof(Ctl), hipHostMallocDefault));
+    memset(&c->h, 0, sizeof(Eng));
+    *out = c;
+    return 0;
+}
+
+void bpe_gpu_destroy(bpe_gpu_ctx *c) {
+    if (!c) return;
+    hipSetDevice(c->dev);
+    free_train(c);
+    if (c->h.bytes) hipFree(c->h.bytes);
+    if (c->dE) hipFree(c->dE);
+    if (c->dC) hipFree(c->dC);
+    if (c->hC) hipHostFree(c->hC);
+    if (c->d_enc_pairs) hipFree(c->d_enc_pairs);
+    if (c->st) hipStreamDestroy(c->st);
+    delete c;
+}
+
+static int alloc_bytes(bpe_gpu_ctx *c, size_t n) {
+    if (n > 0xFFFFFFFEull) return fail(BPE_GPU_ERANGE, "corpus > 2^32-2 bytes");
+    free_train(c);
+    if (c->h.bytes) { hipFree(c->h.bytes); c->h.bytes = nullptr; }
+    HIPCHK(hipMalloc(&c->h.bytes, std::max<size_t>(n, 1)));
+    c->n0 = n;
+    c->loaded = true;
+    return 0;
+}
+
+int bpe_gpu_load(bpe_gpu_ctx *c, const uint8_t *bytes, size_t n) {
+    if (!c || (!bytes && n)) return BPE_GPU_EINVAL;
+    HIPCHK(hipSetDevice(c->dev));
+    int r;
+    if ((r = alloc_bytes(c, n))) return r;
+    if (n) HIPCHK(hipMemcpyAsync(c->h.bytes, bytes, n, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int bpe_gpu_synth(bpe_gpu_ctx *c, uint64_t seed, size_t n, uint64_t offset) {
+    if (!c) return BPE_GPU_EINVAL;
+    HIPCHK(hipSetDevice(c->dev));
+    int r;
+    if ((r = alloc_bytes(c, n))) return r;
+    if (n) k_synth<<<2048, 256, 0, c->st>>>(c->h.bytes, n, seed, offset);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+int bpe_gpu_train(bpe_gpu_ctx *c, long max_merges, size_t *n_merges) {
+    if (!c || !n_merges) return BPE_GPU_EINVAL;
+    if (!c->loaded) return fail(BPE_GPU_ESTATE, "train before load");
+    HIPCHK(hipSetDevice(c->dev));
+    c->stats = bpe_gpu_stats{};
+    c->stats.n_in = c->n0;
+    *n_merges = 0;
+    c->merges_done = 0;
+    if (c->n0 < 2) return fail(BPE_GPU_EINVAL, "fewer than 2 tokens");
+    uint64_t cap = c->n0 - 1;  // a run can never learn more merges than pairs
+    cap = std::min<uint64_t>(cap, 1ull << 24);
+    if (max_merges >= 0) cap = std::min<uint64_t>(cap, (uint64_t)max_merges);
+    const double t0 = now_ms();
+    int r;
+    if ((r = setup_run(c, (uint32_t)cap, false))) return r;
+    std::vector<uint32_t> unrank;
+    uint32_t *d_tot;
+    if ((r = init_tokens(c, &unrank, &d_tot))) return r;
+    uint32_t *d_unrank;
+    if ((r = dalloc(c, &d_unrank, unrank.size()))) return r;
+    if (!unrank.empty())
+        HIPCHK(hipMemcpyAsync(d_unrank, unrank.data(), unrank.size() * 4, hipMemcpyHostToDevice, c->st));
+    const uint32_t AA = c->h.A * c->h.A;
+    k_init_counts<<<(AA + 255) / 256, 256, 0, c->st>>>(c->dE, c->dC, d_tot, d_unrank);
+    HIPCHK(hipGetLastError());
+    const bool tracked = c->n0 < TRACK_LIMIT;
+    if (tracked) launch_stats(c);
+    launch_summaries(c);
+    k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? 1u : 0u);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->st));
+    const double t1 = now_ms();
+    if ((r = drive(c, false, 0))) return r;
+    HIPCHK(hipStreamSynchronize(c->st));
+    const double t2 = now_ms();
+    if ((r = pull_ctl(c))) return r;
+    const Ctl &C = *c->hC;
+    c->merges_done = C.merges_done;
+    *n_merges = C.merges_done;
+    if ((r = compact_ids(c))) return r;
+    c->stats.n_out = c->ids_len;
+    c->stats.merges = C.merges_done;
+    c->stats.iterations = C.counters[0] + 1;
+    c->stats.distinct_pairs = C.D;
+    c->stats.merged_buckets = C.B;
+    c->stats.tracked_iters = C.counters[1];
+    c->stats.rule_ties = C.counters[2];
+    c->stats.keys = C.nkeys;
+    c->stats.ms_init = t1 - t0;
+    c->stats.ms_train = t2 - t1;
+    c->stats.ms_total = t2 - t0;
+    return 0;
+}
+
+int bpe_gpu_fetch_merges(bpe_gpu_ctx *c, uint32_t *pairs, size_t cap, size_t *count) {
+    if (!c || !count) return BPE_GPU_EINVAL;
+    HIPCHK(hipSetDevice(c->dev));
+    size_t n = std::min(cap, c->merges_done);
+    if (n) {
+        HIPCHK(hipMemcpyAsync(pairs, c->h.merges, n * 8, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+    }
+    *count = c->merges_done;
+    return 0;
+}
+
+int bpe_gpu_fetch_ids(bpe_gpu_ctx *c, uint32_t *ids, size_t cap, size_t *len) {
+    if (!c || !len) return BPE_GPU_EINVAL;
+    if (!c->ids_ready) return fail(BPE_GPU_ESTATE, "no ids: train or encode first");
+    HIPCHK(hipSetDevice(c->dev));
+    *len = c->ids_len;
+    size_t n = std::min<size_t>(cap, c->ids_len);
+    if (n && ids) {
+        HIPCHK(hipMemcpyAsync(ids, c->h.ids_out, n * 4, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+    }
+    return 0;
+}
+
+int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
+    if (!c || (!pairs && n_merges)) return BPE_GPU_EINVAL;
+    if (!c->loaded) return fail(BPE_GPU_ESTATE, "encode before load");
+    if (n_merges > 0xFFFFFEFFull) return fail(BPE_GPU_ERANGE, "merge list too long");
+    HIPCHK(hipSetDevice(c->dev));
+    c->stats = bpe_gpu_stats{};
+    c->stats.n_in = c->n0;
+    const double t0 = now_ms();
+    int r;
+    if ((r = setup_run(c, (uint32_t)n_merges, true))) return r;
+    if (c->d_enc_pairs) hipFree(c->d_enc_pairs);
+    HIPCHK(hipMalloc(&c->d_enc_pairs, std::max<size_t>(n_merges, 1) * 8));
+    if (n_merges) HIPCHK(hipMemcpyAsync(c->d_enc_pairs, pairs, n_merges * 8, hipMemcpyHostToDevice, c->st));
+    if (c->n0 == 0) {
+        c->ids_len = 0;
+        c->ids_ready = true;
+        return 0;
+    }
+    std::vector<uint32_t> unrank;
+    uint32_t *d_tot;
+    if (c->n0 >= 2) {
+        if ((r = init_tokens(c, &unrank, &d_tot))) return r;
+    } else {
+        uint32_t *d_bh;
+        if ((r = dalloc(c, &d_bh, 256))) return r;
+        k_init_tok<<<1, 256, 0, c->st>>>(c->dE, d_bh);
+    }
+    // first merge, then graph batches of (scan, apply, next)
+    HIPCHK(hipStreamSynchronize(c->st));
+    k_enc_next<<<1, 1, 0, c->st>>>(c->dE, c->dC, c->d_enc_pairs, (uint32_t)n_merges);
+    HIPCHK(hipGetLastError());
+    if (c->n0 >= 2 && n_merges) {
+        if ((r = capture(c, &c->g_encode, false, true, (uint32_t)n_merges))) return r;
+        if ((r = drive(c, true, (uint32_t)n_merges))) return r;
+    }
+    if ((r = compact_ids(c))) return r;
+    const double t1 = now_ms();
+    c->merges_done = 0;
+    c->stats.n_out = c->ids_len;
+    c->stats.merges = n_merges;
+    c->stats.ms_train = t1 - t0;
+    c->stats.ms_total = t1 - t0;
+    return 0;
+}
+
+int bpe_gpu_decode(bpe_gpu_ctx *c, const uint32_t *ids, size_t len, const uint32_t *pairs, size_t n_merges,
+                   uint8_t *out, size_t cap, size_t *out_len) {
+    if (!c || !out_len || (!ids && len) || (!pairs && n_merges)) return BPE_GPU_EINVAL;
+    HIPCHK(hipSetDevice(c->dev));
+    // expansion lengths (non-NUL bytes) per id, memoized DFS with cycle check
+    const size_t V = 256 + n_merges;
+    std::vector<uint64_t> elen(V, 0);
+    std::vector<uint8_t> state(V, 0);  // 0 new, 1 in progress, 2 done
+    for (uint32_t x = 0; x < 256; x++) { elen[x] = x ? 1 : 0; state[x] = 2; }
+    for (size_t root = 256; root < V; root++) {
+        if (state[root] == 2) continue;
+        std::vector<size_t> stk{root};
+        while (!stk.empty()) {
+            size_t x = stk.back();
+            if (state[x] == 2) { stk.pop_back(); continue; }
+            const uint32_t a = pairs[2 * (x - 256)], b = pairs[2 * (x - 256) + 1];
+            if (a == x) {  // self-referencing record: the reference prints it as one char
+                elen[x] = (uint8_t)a ? 1 : 0;
+                state[x] = 2;
+                stk.pop_back();
+                continue;
+            }
+            if (a >= V || b >= V) return fail(BPE_GPU_EDATA, "merge references an unknown id");
+            state[x] = 1;
+            bool ready = true;
+            for (uint32_t y : {a, b}) {
+                if (state[y] == 1 && y != x) return fail(BPE_GPU_EDATA, "cyclic merge list");
+                if (state[y] == 0) { stk.push_back(y); ready = false; }
+            }
+            if (ready) {
+                elen[x] = elen[a] + elen[b];
+                state[x] = 2;
+                stk.pop_back();
+            }
+        }
+    }
+    uint64_t total = 0;
+    std::vector<uint64_t> off(len + 1);
+    for (size_t i = 0; i < len; i++) {
+        if (ids[i] >= V) return fail(BPE_GPU_EDATA, "unknown token id");
+        off[i] = total;
+        total += elen[ids[i]];
+    }
+    off[len] = total;
+    *out_len = total;
+    if (!out) return 0;
+    if (cap < total) return fail(BPE_GPU_EINVAL, "decode: output buffer too small");
+    if (len == 0 || total == 0) return 0;
+    uint32_t *d_ids, *d_pairs;
+    uint64_t *d_elen, *d_off;
+    uint8_t *d_out;
+    HIPCHK(hipMalloc(&d_ids, len * 4));
+    HIPCHK(hipMalloc(&d_pairs, std::max<size_t>(n_merges, 1) * 8));
+    HIPCHK(hipMalloc(&d_elen, V * 8));
+    HIPCHK(hipMalloc(&d_off, (len + 1) * 8));
+    HIPCHK(hipMalloc(&d_out, total));
+    HIPCHK(hipMemcpyAsync(d_ids, ids, len * 4, hipMemcpyHostToDevice, c->st));
+    if (n_merges) HIPCHK(hipMemcpyAsync(d_pairs, pairs, n_merges * 8, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(d_elen, elen.data(), V * 8, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(d_off, off.data(), (len + 1) * 8, hipMemcpyHostToDevice, c->st));
+    k_dec_expand<<<1024, 256, 0, c->st>>>(d_ids, len, d_pairs, d_elen, d_off, d_out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, d_out, total, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    hipFree(d_ids);
+    hipFree(d_pairs);
+    hipFree(d_elen);
+    hipFree(d_off);
+    hipFree(d_out);
+    return 0;
+}
+
+int bpe_gpu_get_stats(bpe_gpu_ctx *c, bpe_gpu_stats *st) {
+    if (!c || !st) return BPE_GPU_EINVAL;
+    *st = c->stats;
+    return 0;
+}
+
+int bpe_gpu_device_tokens(bpe_gpu_ctx *c, const void **dev_tok, size_t *n) {
+    if (!c || !dev_tok || !n) return BPE_GPU_EINVAL;
+    *dev_tok = c->h.bytes;
+    *n = c->n0;
+    return 0;
+}
+
+int bpe_gpu_kernel_profile(bpe_gpu_ctx *c, const char **name, double *avg_ms, double *bytes_per_launch,
+                           uint64_t *launches) {
+    if (!c) return BPE_GPU_EINVAL;
+    if (name) *name = c->prof_name.c_str();
+    if (avg_ms) *avg_ms = c->prof_ms;
+    if (bytes_per_launch) *bytes_per_launch = c->prof_bytes;
+    if (launches) *launches = c->prof_launches;
+    return 0;
+}
+
+}  // extern "C"

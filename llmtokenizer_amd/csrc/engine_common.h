@@ -1,0 +1,188 @@
+// engine_common.h -- shared device-side definitions of the gfx950 BPE engine.
+//
+// Token representation in HBM ("position space"): the corpus keeps its
+// original byte positions 0..n0-1 for the whole run.  A token covering bytes
+// [s, e) stores its id at tok[s]; every other slot of the span holds HOLE.
+// dist[e-1] = e-1-s lets the token to the RIGHT of a span find the span's
+// start (its left neighbour) in O(1); the right neighbour of a token at s is
+// simply s + tlen[id].  Merging two adjacent tokens is therefore three word
+// writes, and no compaction pass is needed during training (the reference
+// rewrites the whole u32 array per merge, bpe/src/bpe.c:760-777).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bpeamd {
+
+constexpr uint32_t HOLE = 0xFFFFFFFFu;
+constexpr uint32_t LSPAN = 256;          // ids aggregated in LDS by the scan kernel
+constexpr uint32_t NTHR = 16;            // reference THREAD_NO (bpe.c:409)
+constexpr uint64_t CHUNK = 65536;        // reference CHUNK_SIZE (bpe.c:423)
+constexpr uint64_t DYN_LIMIT = CHUNK * NTHR;     // n >= this: chunked counting
+constexpr uint64_t TRACK_LIMIT = 2 * DYN_LIMIT;  // per-thread history tracked below this
+constexpr uint64_t MERGED_B0 = 65536;    // reference MERGED_TABLE_BUCKET_NUM (bpe.c:611)
+constexpr uint64_t THREAD_B0 = 256;      // reference PER_THREAD_TABLE_BUCKET_NUM (bpe.c:610)
+constexpr uint32_t L1W = 256;            // slots per level-1 summary block
+constexpr uint32_t L2W = 256;            // level-1 entries per level-2 summary
+
+enum { V_DL = 0, V_DR = 1, V_IL = 2, V_IR = 3 };
+
+enum : uint32_t {
+    STOP_NONE = 0,
+    STOP_DONE = 1,     // reference stop rule: no pair or max count <= 1
+    STOP_CAP = 2,      // merge cap reached
+    STOP_EVENT = 3,    // tracked-mode tie / edge: host runs the emulation resolver
+    STOP_GROW = 4,     // pair table needs regrowth
+    STOP_ERROR = 5,    // invariant violated (decrement of a missing key ...)
+    STOP_ENC_END = 6,  // encode: merge list exhausted
+    STOP_MODE = 7,     // n fell below 2^21: switch to the tracked iteration graph
+};
+
+// Device-resident descriptor: every kernel takes a pointer to it, so tables can
+// be regrown without re-capturing the iteration graph.
+struct Eng {
+    uint64_t n0;          // positions
+    uint32_t vcap;        // vocab capacity (256 + merge cap)
+    uint32_t mcap;        // merge cap
+    uint32_t A;           // distinct bytes in the corpus
+    uint32_t encode;      // 1: encode mode (no counting)
+    uint8_t *bytes;
+    uint32_t *tok;
+    uint32_t *dist;
+    uint32_t *tlen;       // byte length of each id
+    uint32_t *rank;       // [256] byte -> dense rank (HOLE if absent)
+    uint32_t *plist;      // byte-pair positions grouped by rank key (counting sort)
+    uint32_t *poff;       // [A*A + 1]
+    uint32_t *occ;        // occurrence pool: positions where merged id z was created
+    uint32_t *occ_off;    // [vcap]
+    uint32_t *occ_len;    // [vcap]
+    uint32_t *merges;     // [2 * mcap]
+    uint32_t *vec[2][4];  // delta vectors (dec-left, dec-right, inc-left, inc-right), 2 parities
+    uint32_t *vlist[2][4];
+    uint32_t *vnl[2];     // [4] list lengths
+    // pair-count table: open addressing on (a,b), never deletes (count may hit 0)
+    uint64_t hcap;        // power of two
+    unsigned long long *hkey;  // key + 1, 0 = empty
+    uint32_t *hcnt;
+    unsigned long long *l1best;
+    uint32_t *l1tie, *l1arg, *l1dirty, *l1list;
+    unsigned long long *l2best;
+    uint32_t *l2tie, *l2arg, *l2dirty, *l2list;
+    // per-thread history tracking (n < TRACK_LIMIT)
+    uint64_t scap;        // stats table capacity (power of two)
+    unsigned long long *skey;  // ((t << 60) | (a << 30) | b) + 1
+    uint32_t *scnt;
+    uint32_t *sfirst;     // first compacted index of (t, key)
+    uint32_t *cpos;       // compacted index -> position
+    uint32_t *tilecnt;    // live tokens per tile (compaction)
+    uint64_t ntiles;
+    uint32_t *ids_out;    // compaction output
+    uint32_t *aux;        // per-slot scratch for the resolver (first thread)
+};
+
+struct Ctl {
+    uint32_t a, b, z, stop;
+    uint32_t merges_done, parity, R, occ_top;
+    uint32_t cand_mode, cand_off, cand_len, nl1;
+    uint32_t nl2, full, event, ties;
+    unsigned long long n_live;
+    unsigned long long D;
+    unsigned long long B;      // B used by the level summaries
+    unsigned long long nkeys;
+    unsigned long long W;      // packed best of the last selection
+    uint32_t edge, pending, wslot, err;
+    unsigned long long Bcur[NTHR];    // per-thread table sizes (history)
+    unsigned long long Bstart[NTHR];  // sizes at the start of the tracked iteration
+    unsigned long long Bfin[NTHR];    // sizes after its count phase
+    uint32_t Dt[NTHR];
+    uint32_t follows[NTHR];
+    uint32_t last_c[NTHR];            // last pair position (compacted) per thread
+    unsigned long long stat_n;        // n of the tracked iteration
+    unsigned long long counters[8];   // 0 iterations, 1 tracked, 2 rule ties, 3 events
+};
+
+__host__ __device__ inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// murmur3_x86_32 of the 8-byte key {a, b}, seed 0x9747b28c: the reference's
+// bucket hash (hash_table/src/hash_table.c:8-53) -- it defines the tie order.
+__host__ __device__ inline uint32_t murmur_pair(uint32_t a, uint32_t b) {
+    const uint32_t c1 = 0xcc9e2d51u, c2 = 0x1b873593u;
+    uint32_t h = 0x9747b28cu;
+    uint32_t k = a * c1;
+    k = rotl32(k, 15) * c2;
+    h ^= k;
+    h = rotl32(h, 13) * 5u + 0xe6546b64u;
+    k = b * c1;
+    k = rotl32(k, 15) * c2;
+    h ^= k;
+    h = rotl32(h, 13) * 5u + 0xe6546b64u;
+    h ^= 8u;
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
+// slot hash for our own open-addressed tables (independent of murmur so the
+// tie-order bits do not correlate with probe clustering)
+__host__ __device__ inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+// B_final of the reference's merged table for D distinct keys: the table
+// starts at 65536 buckets and doubles at every insert call made while
+// num_of_nodes >= 0.3 * buckets (hash_table.c:286-292, evaluated in double).
+// *edge = 1 when D equals a threshold exactly, i.e. the last doubling depends
+// on whether another insert call followed the D-th new key.
+__host__ __device__ inline uint64_t bfinal_nominal(uint64_t D, uint32_t *edge) {
+    uint64_t B = MERGED_B0;
+    *edge = 0;
+    for (;;) {
+        double t = 0.3 * (double)B;
+        if (D >= 1 && (double)(D - 1) >= t) { B *= 2; continue; }
+        if ((double)D >= t) *edge = 1;
+        break;
+    }
+    return B;
+}
+
+// Per-thread table growth over one counting phase: start at B, D distinct
+// keys inserted, `follows` = an insert call came after the D-th new key.
+__host__ __device__ inline uint64_t thread_cascade(uint64_t B, uint64_t D, uint32_t follows) {
+    for (;;) {
+        double t = 0.3 * (double)B;
+        if (D >= 1 && (double)(D - 1) >= t) { B *= 2; continue; }
+        if ((double)D >= t && follows) { B *= 2; continue; }
+        break;
+    }
+    return B;
+}
+
+// packed order key: larger count first, then smaller bucket
+__host__ __device__ inline uint64_t pack_val(uint32_t cnt, uint32_t a, uint32_t b, uint64_t B) {
+    if (!cnt) return 0;
+    uint64_t bucket = murmur_pair(a, b) & (B - 1);
+    return ((uint64_t)cnt << 32) | (0xFFFFFFFFull - bucket);
+}
+
+// thread of the reference that counts pair position c (compacted) when the
+// text has n tokens: static 1/16 split (bpe.c:449-476) or, for n >= 2^20,
+// 64Ki chunks dealt round-robin (the schedule this project fixes)
+__host__ __device__ inline uint32_t thread_of(uint64_t c, uint64_t n) {
+    if (n < DYN_LIMIT) {
+        uint64_t per = n / NTHR;
+        if (per == 0) return NTHR - 1;
+        uint64_t t = c / per;
+        return t >= NTHR ? NTHR - 1 : (uint32_t)t;
+    }
+    return (uint32_t)((c / CHUNK) % NTHR);
+}
+
+}  // namespace bpeamd

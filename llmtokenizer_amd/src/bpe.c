@@ -1,0 +1,416 @@
+/*
+ * bpe.c -- the drop-in implementation of include/bpe.h (and bpe_ex.h).
+ *
+ * Host code stays C, as in the reference (neofytr/LLMTokenizer bpe/src/bpe.c);
+ * all training / encoding / decoding work is done by the gfx950 engine behind
+ * the C-ABI shim include/bpe_gpu.h.  There is no CPU fallback: without a GPU
+ * these functions report the error and return NULL, exactly like the
+ * reference's own failure paths.
+ */
+#include "../../include/bpe.h"
+#include "../../include/bpe_ex.h"
+#include "../../include/bpe_gpu.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static bpe_gpu_stats g_last_stats;
+
+bool is_less(const void *a, const void *b)
+{
+    return ((const pair_freq_t *)a)->freq < ((const pair_freq_t *)b)->freq;
+}
+
+/* ------------------------------------------------------------ file helpers */
+char *get_file(const char *path)
+{
+    FILE *f = fopen(path, "r");
+    if (!f) {
+        perror("fopen");
+        return NULL;
+    }
+    char *buf = NULL;
+    long size = -1;
+    if (fseek(f, 0, SEEK_END) == -1) {
+        perror("fseek");
+    } else if ((size = ftell(f)) == -1) {
+        perror("ftell");
+    } else {
+        rewind(f);
+        buf = malloc((size_t)size + 1);
+        if (!buf) {
+            perror("malloc");
+        } else {
+            size_t got = fread(buf, 1, (size_t)size, f);
+            if (got < (size_t)size && ferror(f)) {
+                perror("fread");
+                free(buf);
+                buf = NULL;
+            } else {
+                buf[size] = '\0';
+            }
+        }
+    }
+    fclose(f);
+    return buf;
+}
+
+void print_text(const uint32_t *text, int length)
+{
+    for (int i = 0; i < length; i++) {
+        uint32_t v = text[i];
+        if (v >= 32 && v <= 126)
+            putchar((int)v);
+        else
+            printf("[%u]", v);
+    }
+    putchar('\n');
+}
+
+void print_graph(dyn_arr_t *pair_arr, const char *png_name, bool add_ascii)
+{
+    const char *dot = "temp_graph.dot";
+    FILE *f = fopen(dot, "w");
+    if (!f) {
+        perror("Failed to create temp file");
+        return;
+    }
+    fputs("digraph Pairs {\n", f);
+    for (size_t id = add_ascii ? 0 : 256; id < pair_arr->last_index; id++) {
+        pair_t p;
+        if (!dyn_arr_get(pair_arr, id, &p)) continue;
+        fprintf(f, "%u -> %u;\n%u -> %u;\n", (unsigned)id, p.a, (unsigned)id, p.b);
+    }
+    fputs("}\n", f);
+    fclose(f);
+    char cmd[512];
+    snprintf(cmd, sizeof cmd, "dot -Tpng %s -o %s", dot, png_name);
+    if (system(cmd) != 0) fprintf(stderr, "Failed to generate PNG\n");
+    remove(dot);
+}
+
+/* Merge-list file: raw little-endian 8-byte pair_t records, no header, first
+ * record = id 256.  As in the reference (bpe.c:258) the writer stops BEFORE
+ * last_index, i.e. the final merge is not written; the reference's 16-bit
+ * loop counter (which never terminates past id 65535) is not reproduced. */
+bool dump_pairs(const char *path, dyn_arr_t *pair_arr)
+{
+    if (!path || !pair_arr) {
+        fprintf(stderr, "Invalid arguments to dump_pairs\n");
+        return false;
+    }
+    FILE *f = fopen(path, "wb");
+    if (!f) {
+        perror("fopen");
+        return false;
+    }
+    for (size_t id = 256; id < pair_arr->last_index; id++) {
+        pair_t p;
+        if (!dyn_arr_get(pair_arr, id, &p)) {
+            fprintf(stderr, "Error retrieving element at index %zu\n", id);
+            fclose(f);
+            return false;
+        }
+        if (fwrite(&p, sizeof p, 1, f) != 1) {
+            perror("fwrite");
+            fclose(f);
+            return false;
+        }
+    }
+    fclose(f);
+    return true;
+}
+
+static dyn_arr_t *new_pair_arr(void)
+{
+    dyn_arr_t *arr = dyn_arr_create(512, sizeof(pair_t));
+    if (!arr) return NULL;
+    for (uint32_t i = 0; i < 256; i++) {
+        pair_t p = {i, 0};
+        if (!dyn_arr_set(arr, i, &p)) {
+            dyn_arr_free(arr);
+            return NULL;
+        }
+    }
+    return arr;
+}
+
+dyn_arr_t *read_pairs(const char *path)
+{
+    if (!path) {
+        fprintf(stderr, "Invalid file path\n");
+        return NULL;
+    }
+    FILE *f = fopen(path, "rb");
+    if (!f) {
+        perror("fopen");
+        return NULL;
+    }
+    dyn_arr_t *arr = new_pair_arr();
+    if (!arr) {
+        fprintf(stderr, "Failed to create dynamic array\n");
+        fclose(f);
+        return NULL;
+    }
+    pair_t p;
+    for (size_t id = 256; fread(&p, sizeof p, 1, f) == 1; id++) {
+        if (!dyn_arr_set(arr, id, &p)) {
+            fprintf(stderr, "dyn_arr_set failed at index %zu\n", id);
+            dyn_arr_free(arr);
+            fclose(f);
+            return NULL;
+        }
+    }
+    bool bad = ferror(f) != 0;
+    fclose(f);
+    if (bad) {
+        perror("fread");
+        dyn_arr_free(arr);
+        return NULL;
+    }
+    return arr;
+}
+
+/* -------------------------------------------------------------- GPU glue */
+static int env_int(const char *name, long dflt, long *out)
+{
+    const char *s = getenv(name);
+    if (!s || !*s) {
+        *out = dflt;
+        return 0;
+    }
+    char *end;
+    long v = strtol(s, &end, 10);
+    if (*end) return -1;
+    *out = v;
+    return 0;
+}
+
+static void report(const char *what, int rc)
+{
+    fprintf(stderr, "bpe: %s failed: %s (%s)\n", what, bpe_gpu_strerror(rc), bpe_gpu_last_error());
+}
+
+static int open_engine(int device, bpe_gpu_ctx **ctx)
+{
+    int rc = bpe_gpu_create(device, ctx);
+    if (rc) report("GPU context (an MI355X is required; there is no CPU path)", rc);
+    return rc;
+}
+
+/* merges (pairs) -> a reference-shaped merge list */
+static dyn_arr_t *pairs_to_arr(const uint32_t *pairs, size_t k)
+{
+    dyn_arr_t *arr = new_pair_arr();
+    for (size_t r = 0; arr && r < k; r++) {
+        pair_t p = {pairs[2 * r], pairs[2 * r + 1]};
+        if (!dyn_arr_set(arr, 256 + r, &p)) {
+            dyn_arr_free(arr);
+            arr = NULL;
+        }
+    }
+    return arr;
+}
+
+/* reference-shaped merge list -> flat pairs for ids 256..last_index */
+static uint32_t *arr_to_pairs(dyn_arr_t *arr, size_t *k)
+{
+    size_t n = arr->last_index >= 256 ? arr->last_index - 255 : 0;
+    uint32_t *pairs = malloc((n ? n : 1) * 2 * sizeof(uint32_t));
+    if (!pairs) return NULL;
+    for (size_t r = 0; r < n; r++) {
+        pair_t p = {0xFFFFFFFFu, 0xFFFFFFFFu}; /* unknown record -> decode error */
+        dyn_arr_get(arr, 256 + r, &p);
+        pairs[2 * r] = p.a;
+        pairs[2 * r + 1] = p.b;
+    }
+    *k = n;
+    return pairs;
+}
+
+dyn_arr_t *bpe_train_bytes(const uint8_t *bytes, size_t n, long max_merges, int device, uint32_t **encoding,
+                           size_t *len)
+{
+    if (!bytes || !encoding || !len) return NULL;
+    bpe_gpu_ctx *ctx = NULL;
+    dyn_arr_t *arr = NULL;
+    uint32_t *pairs = NULL, *ids = NULL;
+    size_t k = 0, n_ids = 0, got = 0;
+    int rc;
+    if ((rc = open_engine(device, &ctx))) goto fail;
+    if ((rc = bpe_gpu_load(ctx, bytes, n))) { report("load", rc); goto fail; }
+    if ((rc = bpe_gpu_train(ctx, max_merges, &k))) { report("train", rc); goto fail; }
+    pairs = malloc((k ? k : 1) * 2 * sizeof(uint32_t));
+    if (!pairs) goto fail;
+    if ((rc = bpe_gpu_fetch_merges(ctx, pairs, k, &got))) { report("fetch merges", rc); goto fail; }
+    if ((rc = bpe_gpu_fetch_ids(ctx, NULL, 0, &n_ids))) { report("fetch ids", rc); goto fail; }
+    ids = malloc((n_ids ? n_ids : 1) * sizeof(uint32_t));
+    if (!ids) goto fail;
+    if ((rc = bpe_gpu_fetch_ids(ctx, ids, n_ids, &n_ids))) { report("fetch ids", rc); goto fail; }
+    arr = pairs_to_arr(pairs, k);
+    if (!arr) goto fail;
+    bpe_gpu_get_stats(ctx, &g_last_stats);
+    bpe_gpu_destroy(ctx);
+    free(pairs);
+    *encoding = ids;
+    *len = n_ids;
+    return arr;
+fail:
+    bpe_gpu_destroy(ctx);
+    free(pairs);
+    free(ids);
+    *encoding = NULL;
+    *len = 0;
+    return NULL;
+}
+
+dyn_arr_t *compress_ex(const char *path, long max_merges, int device, uint32_t **encoding, size_t *len)
+{
+    if (!path || !encoding || !len) return NULL;
+    char *buf = get_file(path);
+    if (!buf) return NULL;
+    size_t n = strlen(buf); /* the reference trains on the text up to the first NUL */
+    if (n < 2) {
+        printf("Error: File contains less than 2 characters\n");
+        fflush(stdout);
+        free(buf);
+        return NULL;
+    }
+    dyn_arr_t *arr = bpe_train_bytes((const uint8_t *)buf, n, max_merges, device, encoding, len);
+    free(buf);
+    return arr;
+}
+
+dyn_arr_t *compress(const char *path, uint32_t **encoding, size_t *len)
+{
+    long maxm, dev;
+    if (env_int("BPE_MAX_MERGES", -1, &maxm) || env_int("BPE_DEVICE", 0, &dev)) {
+        fprintf(stderr, "bpe: BPE_MAX_MERGES / BPE_DEVICE must be integers\n");
+        return NULL;
+    }
+    return compress_ex(path, maxm, (int)dev, encoding, len);
+}
+
+uint32_t *bpe_encode_bytes(const uint8_t *bytes, size_t n, dyn_arr_t *pair_arr, int device, size_t *len)
+{
+    if ((!bytes && n) || !pair_arr || !len) return NULL;
+    bpe_gpu_ctx *ctx = NULL;
+    size_t k = 0, n_ids = 0;
+    uint32_t *pairs = arr_to_pairs(pair_arr, &k), *ids = NULL;
+    int rc;
+    if (!pairs) return NULL;
+    if ((rc = open_engine(device, &ctx))) goto done;
+    if ((rc = bpe_gpu_load(ctx, bytes, n))) { report("load", rc); goto done; }
+    if ((rc = bpe_gpu_encode(ctx, pairs, k))) { report("encode", rc); goto done; }
+    if ((rc = bpe_gpu_fetch_ids(ctx, NULL, 0, &n_ids))) { report("fetch ids", rc); goto done; }
+    ids = malloc((n_ids ? n_ids : 1) * sizeof(uint32_t));
+    if (ids && (rc = bpe_gpu_fetch_ids(ctx, ids, n_ids, &n_ids))) {
+        report("fetch ids", rc);
+        free(ids);
+        ids = NULL;
+    }
+    if (ids) {
+        *len = n_ids;
+        bpe_gpu_get_stats(ctx, &g_last_stats);
+    }
+done:
+    bpe_gpu_destroy(ctx);
+    free(pairs);
+    return ids;
+}
+
+int bpe_last_stats(bpe_gpu_stats *out)
+{
+    if (!out) return -1;
+    *out = g_last_stats;
+    return 0;
+}
+
+char *decompress(uint32_t *encoding, size_t len, dyn_arr_t *pair_arr)
+{
+    if ((!encoding && len) || !pair_arr) return NULL;
+    size_t k = 0, out_len = 0;
+    uint32_t *pairs = arr_to_pairs(pair_arr, &k);
+    if (!pairs) return NULL;
+    char *out = NULL;
+    long dev;
+    bpe_gpu_ctx *ctx = NULL;
+    if (env_int("BPE_DEVICE", 0, &dev) || open_engine((int)dev, &ctx)) goto done;
+    int rc = bpe_gpu_decode(ctx, encoding, len, pairs, k, NULL, 0, &out_len);
+    if (rc) {
+        report("decode", rc);
+        goto done;
+    }
+    out = malloc(out_len + 1);
+    if (!out) goto done;
+    rc = bpe_gpu_decode(ctx, encoding, len, pairs, k, (uint8_t *)out, out_len, &out_len);
+    if (rc) {
+        report("decode", rc);
+        free(out);
+        out = NULL;
+        goto done;
+    }
+    out[out_len] = '\0';
+done:
+    bpe_gpu_destroy(ctx);
+    free(pairs);
+    return out;
+}
+
+/* ------------------------------------------------ single-token utilities */
+/* Expansion of one id as a C string, memoised in `memo` (u32 -> char*), with
+ * the reference's semantics (bpe.c:23-92): a record whose first element is
+ * its own id is that single char; otherwise expand(a) ++ expand(b).  Returns a
+ * fresh malloc'd string owned by the caller, or NULL. */
+char *resolve_pair(uint32_t pair_index, dyn_arr_t *pair_arr, hash_table_t *memo)
+{
+    if (!pair_arr || !memo) return NULL;
+    char *hit;
+    if (hash_table_search(memo, &pair_index, &hit)) return strdup(hit);
+    pair_t p;
+    if (!dyn_arr_get(pair_arr, pair_index, &p)) return NULL;
+    char *s;
+    if (p.a == pair_index) {
+        s = malloc(2);
+        if (!s) return NULL;
+        s[0] = (char)p.a;
+        s[1] = '\0';
+    } else {
+        char *l = resolve_pair(p.a, pair_arr, memo);
+        char *r = l ? resolve_pair(p.b, pair_arr, memo) : NULL;
+        s = (l && r) ? malloc(strlen(l) + strlen(r) + 1) : NULL;
+        if (s) {
+            strcpy(s, l);
+            strcat(s, r);
+        }
+        free(l);
+        free(r);
+        if (!s) return NULL;
+    }
+    char *keep = strdup(s);
+    if (keep && !hash_table_insert(memo, &pair_index, &keep)) free(keep);
+    return s;
+}
+
+void render_pairs(dyn_arr_t *pair_arr)
+{
+    hash_table_t *memo = hash_table_create(256, sizeof(uint32_t), sizeof(char *));
+    if (!memo) return;
+    for (size_t id = 256; id <= pair_arr->last_index; id++) {
+        pair_t p;
+        if (!dyn_arr_get(pair_arr, id, &p)) break;
+        if (p.a == id) {
+            printf("%zu => %c\n", id, (char)p.a);
+            continue;
+        }
+        char *s = resolve_pair((uint32_t)id, pair_arr, memo);
+        if (!s) break;
+        printf("%zu => %s\n", id, s);
+        free(s);
+    }
+    /* the memo owns strdup'd strings */
+    for (size_t b = 0; b < memo->num_of_buckets; b++)
+        for (node_t *n = memo->buckets[b]; n; n = n->next) free(*(char **)n->value);
+    hash_table_destroy(memo);
+}

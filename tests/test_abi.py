@@ -1,0 +1,152 @@
+"""CPU-side checks of the drop-in C-ABI library (no GPU compute calls):
+the library loads, exports every symbol include/*.h declares, and the
+host-only parts of the reference API behave like the reference."""
+import ctypes
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from llmtokenizer_amd import _lib
+from llmtokenizer_amd import api
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    names = set()
+    for h in ("bpe.h", "dyn_arr.h", "hash_table.h", "bpe_ex.h", "bpe_gpu.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\([^;{]*\)\s*;", txt, flags=re.M):
+            if not m.group(0).startswith("typedef"):
+                names.add(m.group(1))
+    return names
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    L = _lib.load()
+    declared = _declared_functions()
+    assert {"compress", "decompress", "dyn_arr_free", "hash_table_merge", "bpe_gpu_train"} <= declared
+    missing = [n for n in sorted(declared) if not hasattr(L, n)]
+    assert not missing, missing
+    assert declared <= set(_lib.EXPORTS) | declared  # EXPORTS documents the same set
+    assert set(_lib.EXPORTS) == declared
+
+
+def test_compress_without_gpu_fails_loudly(tmp_path):
+    """No CPU fallback: with no GPU the library reports and returns NULL."""
+    L = _lib.load()
+    n = ctypes.c_int(0)
+    L.bpe_gpu_device_count(ctypes.byref(n))
+    if n.value > 0:
+        pytest.skip("a GPU is present")
+    p = tmp_path / "t.txt"
+    p.write_bytes(b"hello hello hello")
+    with pytest.raises(api.BpeError):
+        api.compress(str(p))
+
+
+def test_short_file_message(tmp_path, capfd):
+    """Reference bpe.c:558-563: fewer than 2 chars -> stdout message, NULL."""
+    p = tmp_path / "one.txt"
+    p.write_bytes(b"x\x00yz")  # strlen == 1
+    with pytest.raises(api.BpeError):
+        api.compress(str(p))
+    out = capfd.readouterr().out
+    assert "Error: File contains less than 2 characters" in out
+
+
+def test_dump_read_pairs_format(tmp_path):
+    """Raw 8-byte LE records from id 256; the final merge is NOT written
+    (reference bpe.c:258 stops before last_index); read_pairs rebuilds 0..255."""
+    merges = np.array([[32, 116], [101, 114], [115, 32], [256, 258]], dtype=np.uint32)
+    p = tmp_path / "m.bin"
+    api.dump_pairs(str(p), merges)
+    raw = p.read_bytes()
+    assert len(raw) == 8 * 3
+    assert np.frombuffer(raw, dtype="<u4").reshape(-1, 2).tolist() == merges[:3].tolist()
+    back = api.read_pairs(str(p))
+    assert back.tolist() == merges[:3].tolist()
+
+
+def test_hash_table_order_matches_reference_model():
+    """Host hash_table: murmur buckets, head insertion, 0.3 doubling -- the
+    iteration order a caller walking table->buckets would observe."""
+    L = _lib.load()
+
+    class Node(ctypes.Structure):
+        pass
+    Node._fields_ = [("key", ctypes.c_void_p), ("value", ctypes.c_void_p), ("is_free", ctypes.c_bool),
+                     ("next", ctypes.POINTER(Node))]
+
+    class Table(ctypes.Structure):
+        _fields_ = [("num_of_buckets", ctypes.c_size_t), ("key_size", ctypes.c_size_t),
+                    ("value_size", ctypes.c_size_t), ("buckets", ctypes.POINTER(ctypes.POINTER(Node))),
+                    ("free_nodes", ctypes.POINTER(Node)), ("num_of_nodes", ctypes.c_size_t)]
+    L.hash_table_create.restype = ctypes.POINTER(Table)
+    L.hash_table_create.argtypes = [ctypes.c_size_t] * 3
+    L.hash_table_insert.argtypes = [ctypes.POINTER(Table), ctypes.c_void_p, ctypes.c_void_p]
+    L.hash_table_insert.restype = ctypes.c_bool
+    L.hash_table_destroy.argtypes = [ctypes.POINTER(Table)]
+    t = L.hash_table_create(4, 8, 8)
+    keys = [(i * 7 + 3, i % 5) for i in range(40)]
+    import oracle_lib as O  # murmur reference restatement (test infrastructure)
+    # python model of the reference structure
+    B, chains, n = 4, {b: [] for b in range(4)}, 0
+    for (a, b) in keys:
+        if n >= 0.3 * B:
+            nb = 2 * B
+            new = {x: [] for x in range(nb)}
+            for bk in range(B):
+                for key in chains[bk]:
+                    new[O.murmur_pair(*key) % nb].insert(0, key)
+            B, chains = nb, new
+        chains[O.murmur_pair(a, b) % B].insert(0, (a, b))
+        n += 1
+        k = (ctypes.c_uint32 * 2)(a, b)
+        v = ctypes.c_uint64(1)
+        assert L.hash_table_insert(t, k, ctypes.byref(v))
+    assert t.contents.num_of_buckets == B
+    walked = []
+    for bk in range(B):
+        node = t.contents.buckets[bk]
+        while node:
+            kk = ctypes.cast(node.contents.key, ctypes.POINTER(ctypes.c_uint32))
+            walked.append((kk[0], kk[1]))
+            node = node.contents.next
+    expect = [key for bk in range(B) for key in chains[bk]]
+    assert walked == expect
+    L.hash_table_destroy(t)
+
+
+def test_dyn_arr_max_first_strict_max():
+    L = _lib.load()
+    arr = L.dyn_arr_create(0, 12)
+    vals = [(1, 2, 5), (3, 4, 9), (5, 6, 9), (7, 8, 1)]
+    for i, (a, b, f) in enumerate(vals):
+        rec = (ctypes.c_uint32 * 3)(a, b, f)
+        L.dyn_arr_set(arr, i, ctypes.cast(rec, ctypes.c_void_p))
+    out = (ctypes.c_uint32 * 3)()
+    L.dyn_arr_max.argtypes = [ctypes.POINTER(_lib.DynArr), ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                              ctypes.c_void_p]
+    L.dyn_arr_max.restype = ctypes.c_bool
+    assert L.dyn_arr_max(arr, 0, 3, ctypes.cast(L.is_less, ctypes.c_void_p), ctypes.cast(out, ctypes.c_void_p))
+    assert list(out) == [3, 4, 9]  # first of the two 9s, as dyn_arr.c:256 keeps
+    assert arr.contents.last_index == 3
+    L.dyn_arr_free(arr)
+
+
+def test_reference_main_links_against_library(tmp_path):
+    """Drop-in check: the reference's own main.c (read in place, not copied)
+    compiles and links against libbpe_amd.so unchanged."""
+    main = "/root/reference/main.c"
+    if not os.path.exists(main) or not shutil.which("gcc"):
+        pytest.skip("reference sources not present")
+    exe = tmp_path / "ref_main"
+    subprocess.check_call(["gcc", "-O1", main, "-o", str(exe), "-L" + os.path.dirname(_lib.LIB_PATH),
+                           "-lbpe_amd", "-Wl,-rpath," + os.path.dirname(_lib.LIB_PATH)])
+    assert exe.exists()
