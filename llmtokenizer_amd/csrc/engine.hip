@@ -74,12 +74,13 @@ __device__ inline uint64_t stat_cap(const Ctl *C) {
 __device__ inline int64_t stat_find(const Eng *E, uint64_t cap, uint32_t t, uint32_t u, uint32_t v) {
     const unsigned long long key = skey_of(t, u, v);
     uint64_t s = mix64(key) & (cap - 1);
-    for (;;) {
+    for (uint64_t p = 0; p < cap; p++) {
         const unsigned long long k = E->skey[s];
         if (k == key) return (int64_t)s;
         if (k == 0) return -1;
         s = (s + 1) & (cap - 1);
     }
+    return -1;
 }
 
 // keys of the pair table with count == M
@@ -649,7 +650,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
         case STOP_ENC_END:
             return 0;
         case STOP_ERROR:
-            return fail(BPE_GPU_EINTERNAL, "engine invariant violated (count decrement of an absent pair)");
+            return fail(BPE_GPU_EINTERNAL, C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : "thread-stat table full");
         case STOP_MODE:
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;

@@ -162,19 +162,20 @@ __device__ inline uint64_t hfind(const Eng *E, uint32_t u, uint32_t v) {
     const unsigned long long key = (((unsigned long long)u << 32) | v) + 1ull;
     const uint64_t m = E->hcap - 1;
     uint64_t s = mix64(key) & m;
-    for (;;) {
+    for (uint64_t p = 0; p <= m; p++) {
         const unsigned long long k = E->hkey[s];
         if (k == key) return s;
         if (k == 0) return ~0ull;
         s = (s + 1) & m;
     }
+    return ~0ull;
 }
 
 __device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v) {
     const unsigned long long key = (((unsigned long long)u << 32) | v) + 1ull;
     const uint64_t m = E->hcap - 1;
     uint64_t s = mix64(key) & m;
-    for (;;) {
+    for (uint64_t p = 0; p <= m; p++) {
         unsigned long long k = __hip_atomic_load(&E->hkey[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == key) return s;
         if (k == 0) {
@@ -187,6 +188,7 @@ __device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v)
         }
         s = (s + 1) & m;
     }
+    return ~0ull;  // table full: callers flag STOP_ERROR
 }
 
 __device__ inline void mark_l1(const Eng *E, Ctl *C, uint64_t slot) {
@@ -260,6 +262,7 @@ __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *_
         uint64_t slot;
         if (d > 0) {
             slot = hinsert(E, C, u, v);
+            if (slot == ~0ull) { C->err = 2; C->stop = STOP_ERROR; continue; }
         } else {
             slot = hfind(E, u, v);
             if (slot == ~0ull) { C->err = 1; C->stop = STOP_ERROR; continue; }
@@ -623,6 +626,7 @@ __global__ void k_init_counts(const Eng *__restrict__ E, Ctl *__restrict__ C, co
     if (!c) return;
     const uint32_t u = unrank[k / E->A], v = unrank[k % E->A];
     const uint64_t slot = hinsert(E, C, u, v);
+    if (slot == ~0ull) { C->err = 2; C->stop = STOP_ERROR; return; }
     E->hcnt[slot] = c;
     atomicAdd(&C->D, 1ull);
 }
@@ -635,6 +639,7 @@ __global__ void k_rehash(const Eng *__restrict__ E, Ctl *__restrict__ C, const u
         if (!k) continue;
         if (!ocnt[s]) continue;  // zero-count keys are dropped on regrowth
         const uint64_t slot = hinsert(E, C, (uint32_t)((k - 1) >> 32), (uint32_t)(k - 1));
+        if (slot == ~0ull) { C->err = 2; C->stop = STOP_ERROR; return; }
         E->hcnt[slot] = ocnt[s];
     }
 }
@@ -797,7 +802,8 @@ __global__ __launch_bounds__(256) void k_stat_insert(const Eng *__restrict__ E, 
         const uint32_t t = thread_of(c, n);
         const unsigned long long key = skey_of(t, u, v);
         uint64_t s = mix64(key) & (cap - 1);
-        for (;;) {
+        for (uint64_t p = 0;; p++) {
+            if (p >= cap) { C->err = 4; C->stop = STOP_ERROR; return; }
             unsigned long long k = __hip_atomic_load(&E->skey[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (k == key) break;
             if (k == 0) {
@@ -851,7 +857,9 @@ __global__ void k_stat_final(const Eng *__restrict__ E, Ctl *__restrict__ C) {
         const uint32_t v = E->tok[i + E->tlen[u]];
         const unsigned long long key = skey_of(t, u, v);
         uint64_t s = mix64(key) & (cap - 1);
-        while (E->skey[s] != key) s = (s + 1) & (cap - 1);
+        uint64_t probes = 0;
+        while (E->skey[s] != key && ++probes < cap) s = (s + 1) & (cap - 1);
+        if (probes >= cap) { C->err = 3; C->stop = STOP_ERROR; return; }
         follows = E->scnt[s] != 1;  // key of the last call seen before => a call followed the last new key
     }
     C->last_c[t] = last >= 0 ? (uint32_t)last : 0xFFFFFFFFu;
