@@ -177,7 +177,8 @@ struct bpe_gpu_ctx {
     bool ids_ready = false;
     uint64_t ids_len = 0;
     size_t merges_done = 0;
-    std::vector<void *> train_allocs;
+    std::vector<std::pair<void *, size_t>> train_allocs;  // live buffers of the current run
+    std::vector<std::pair<void *, size_t>> pool;          // released buffers, reused by size
     uint32_t *d_tileoff = nullptr;
     uint32_t *d_enc_pairs = nullptr;
     hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr;
@@ -190,25 +191,50 @@ struct bpe_gpu_ctx {
 
 namespace {
 
+// Device buffers are pooled per context: a second train()/encode() on the
+// same context reuses the previous run's allocations of equal size instead of
+// paying hipMalloc/hipFree for ~20 GB again (allocation is not part of the
+// algorithm; the corpus upload is not either).
 template <typename T>
 int dalloc(bpe_gpu_ctx *c, T **p, size_t count, bool zero = true) {
     size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
-    hipError_t e = hipMalloc((void **)p, bytes);
-    if (e != hipSuccess) return fail(BPE_GPU_ENOMEM, "hipMalloc", e);
-    c->train_allocs.push_back(*p);
+    bytes = (bytes + 255) & ~(size_t)255;
+    *p = nullptr;
+    for (size_t k = 0; k < c->pool.size(); k++) {
+        if (c->pool[k].second == bytes) {
+            *p = (T *)c->pool[k].first;
+            c->pool.erase(c->pool.begin() + k);
+            break;
+        }
+    }
+    if (!*p) {
+        hipError_t e = hipMalloc((void **)p, bytes);
+        if (e != hipSuccess) {
+            // return cached memory to the device and retry once
+            for (auto &q : c->pool) hipFree(q.first);
+            c->pool.clear();
+            e = hipMalloc((void **)p, bytes);
+            if (e != hipSuccess) return fail(BPE_GPU_ENOMEM, "hipMalloc", e);
+        }
+    }
+    c->train_allocs.push_back({(void *)*p, bytes});
     if (zero) {
-        e = hipMemsetAsync(*p, 0, bytes, c->st);
+        hipError_t e = hipMemsetAsync(*p, 0, bytes, c->st);
         if (e != hipSuccess) return fail(BPE_GPU_EHIP, "hipMemsetAsync", e);
     }
     return 0;
 }
 
-void free_train(bpe_gpu_ctx *c) {
-    if (c->st) hipStreamSynchronize(c->st);
-    for (void *p : c->train_allocs) hipFree(p);
+void free_train(bpe_gpu_ctx *c, bool release = false) {
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    for (auto &q : c->train_allocs) c->pool.push_back(q);
     c->train_allocs.clear();
+    if (release) {
+        for (auto &q : c->pool) (void)hipFree(q.first);
+        c->pool.clear();
+    }
     for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked, &c->g_encode}) {
-        if (*g) hipGraphExecDestroy(*g);
+        if (*g) (void)hipGraphExecDestroy(*g);
         *g = nullptr;
     }
     c->ids_ready = false;
@@ -241,7 +267,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     const uint64_t n0 = c->n0;
     int r;
     if ((r = dalloc(c, &h.tok, n0, false))) return r;
-    if ((r = dalloc(c, &h.dist, n0))) return r;
+    if ((r = dalloc(c, &h.dist, n0, false))) return r;  // read only where written (left_start)
     if ((r = dalloc(c, &h.tlen, h.vcap))) return r;
     if ((r = dalloc(c, &h.rank, 256))) return r;
     if ((r = dalloc(c, &h.plist, n0, false))) return r;
@@ -251,11 +277,12 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.merges, 2ull * std::max<uint32_t>(mcap, 1)))) return r;
     for (int p = 0; p < 2; p++) {
         for (int v = 0; v < 4; v++) {
-            if ((r = dalloc(c, &h.vec[p][v], encode ? 1 : h.vcap))) return r;
+            if ((r = dalloc(c, &h.vec[p][v], encode ? 1 : std::max<uint32_t>(h.vcap, DENSE)))) return r;
             if ((r = dalloc(c, &h.vlist[p][v], encode ? 1 : h.vcap, false))) return r;
         }
         if ((r = dalloc(c, &h.vnl[p], 4))) return r;
     }
+    if ((r = dalloc(c, &h.vecd, encode ? 1 : (size_t)REPL * 4 * DENSE))) return r;
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
     if ((r = dalloc(c, &c->d_tileoff, h.ntiles + 1))) return r;
@@ -277,15 +304,13 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.hkey, h.hcap))) return r;
     if ((r = dalloc(c, &h.hcnt, h.hcap))) return r;
     if ((r = dalloc(c, &h.l1best, nL1))) return r;
+    if ((r = dalloc(c, &h.l1key, nL1))) return r;
     if ((r = dalloc(c, &h.l1tie, nL1))) return r;
-    if ((r = dalloc(c, &h.l1arg, nL1))) return r;
-    if ((r = dalloc(c, &h.l1dirty, nL1))) return r;
-    if ((r = dalloc(c, &h.l1list, nL1, false))) return r;
+    if ((r = dalloc(c, &h.l1list, nL1 + 4ull * DENSE + 4ull * h.vcap + 64, false))) return r;
     if ((r = dalloc(c, &h.l2best, nL2))) return r;
+    if ((r = dalloc(c, &h.l2key, nL2))) return r;
     if ((r = dalloc(c, &h.l2tie, nL2))) return r;
-    if ((r = dalloc(c, &h.l2arg, nL2))) return r;
-    if ((r = dalloc(c, &h.l2dirty, nL2))) return r;
-    if ((r = dalloc(c, &h.l2list, nL2, false))) return r;
+    if ((r = dalloc(c, &h.l2list, nL1 + 4ull * DENSE + 4ull * h.vcap + 64, false))) return r;
     // control block
     Ctl &C = *c->hC;
     memset(&C, 0, sizeof(Ctl));
@@ -309,25 +334,21 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
     HIPCHK(hipMemsetAsync(nkey, 0, ncap * sizeof(unsigned long long), c->st));
     HIPCHK(hipMemsetAsync(ncnt, 0, ncap * sizeof(uint32_t), c->st));
     const uint64_t nL1 = ncap / L1W, nL2 = (nL1 + L2W - 1) / L2W;
-    unsigned long long *l1b, *l2b;
-    uint32_t *l1t, *l1a, *l1d, *l1l, *l2t, *l2a, *l2d, *l2l;
+    const uint64_t nlist = nL1 + 4ull * DENSE + 4ull * h.vcap + 64;
+    unsigned long long *l1b, *l1k, *l2b, *l2k;
+    uint32_t *l1t, *l1l, *l2t, *l2l;
     HIPCHK(hipMalloc(&l1b, nL1 * 8));
+    HIPCHK(hipMalloc(&l1k, nL1 * 8));
     HIPCHK(hipMalloc(&l1t, nL1 * 4));
-    HIPCHK(hipMalloc(&l1a, nL1 * 4));
-    HIPCHK(hipMalloc(&l1d, nL1 * 4));
-    HIPCHK(hipMalloc(&l1l, nL1 * 4));
+    HIPCHK(hipMalloc(&l1l, nlist * 4));
     HIPCHK(hipMalloc(&l2b, nL2 * 8));
+    HIPCHK(hipMalloc(&l2k, nL2 * 8));
     HIPCHK(hipMalloc(&l2t, nL2 * 4));
-    HIPCHK(hipMalloc(&l2a, nL2 * 4));
-    HIPCHK(hipMalloc(&l2d, nL2 * 4));
-    HIPCHK(hipMalloc(&l2l, nL2 * 4));
-    HIPCHK(hipMemsetAsync(l1d, 0, nL1 * 4, c->st));
-    HIPCHK(hipMemsetAsync(l2d, 0, nL2 * 4, c->st));
-    void *olds[] = {h.hkey, h.hcnt, h.l1best, h.l1tie, h.l1arg, h.l1dirty, h.l1list,
-                    h.l2best, h.l2tie, h.l2arg, h.l2dirty, h.l2list};
+    HIPCHK(hipMalloc(&l2l, nlist * 4));
+    void *olds[] = {h.hkey, h.hcnt, h.l1best, h.l1key, h.l1tie, h.l1list, h.l2best, h.l2key, h.l2tie, h.l2list};
     h.hkey = nkey; h.hcnt = ncnt; h.hcap = ncap;
-    h.l1best = l1b; h.l1tie = l1t; h.l1arg = l1a; h.l1dirty = l1d; h.l1list = l1l;
-    h.l2best = l2b; h.l2tie = l2t; h.l2arg = l2a; h.l2dirty = l2d; h.l2list = l2l;
+    h.l1best = l1b; h.l1key = l1k; h.l1tie = l1t; h.l1list = l1l;
+    h.l2best = l2b; h.l2key = l2k; h.l2tie = l2t; h.l2list = l2l;
     int r;
     if ((r = push_desc(c))) return r;
     c->hC->nkeys = 0;
@@ -336,33 +357,41 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));
     for (void *p : olds) {
-        auto it = std::find(c->train_allocs.begin(), c->train_allocs.end(), p);
-        if (it != c->train_allocs.end()) c->train_allocs.erase(it);
-        hipFree(p);
+        for (size_t k = 0; k < c->train_allocs.size(); k++)
+            if (c->train_allocs[k].first == p) {
+                c->train_allocs.erase(c->train_allocs.begin() + k);
+                break;
+            }
+        (void)hipFree(p);
     }
-    for (void *p : {(void *)nkey, (void *)ncnt, (void *)l1b, (void *)l1t, (void *)l1a, (void *)l1d, (void *)l1l,
-                    (void *)l2b, (void *)l2t, (void *)l2a, (void *)l2d, (void *)l2l})
-        c->train_allocs.push_back(p);
+    const size_t sizes[] = {ncap * 8, ncap * 4, nL1 * 8, nL1 * 8, nL1 * 4, nlist * 4, nL2 * 8, nL2 * 8, nL2 * 4, nlist * 4};
+    void *news[] = {nkey, ncnt, l1b, l1k, l1t, l1l, l2b, l2k, l2t, l2l};
+    for (int k = 0; k < 10; k++) c->train_allocs.push_back({news[k], sizes[k]});
     c->stats.table_grows++;
+    // iteration graphs depend on the table size (level-2 summaries): recapture
+    for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked}) {
+        if (*g) (void)hipGraphExecDestroy(*g);
+        *g = nullptr;
+    }
     return 0;
 }
 
 void launch_stats(bpe_gpu_ctx *c) {
     k_stat_clear<<<256, 256, 0, c->st>>>(c->dE, c->dC);
-    k_stat_count<<<512, 256, 0, c->st>>>(c->dE, c->dC);
-    k_stat_scan<<<1, 1024, 0, c->st>>>(c->dE, c->dC, c->d_tileoff);
-    k_stat_map<<<512, 256, 0, c->st>>>(c->dE, c->dC, c->d_tileoff);
+    k_live_count<<<1024, 256, 0, c->st>>>(c->dE, c->dC, 1);
+    k_live_scan<<<1, 1024, 0, c->st>>>(c->dE, c->dC, 1, c->d_tileoff);
+    k_live_write<<<1024, 256, 0, c->st>>>(c->dE, c->dC, 1, c->d_tileoff, 1);
     k_stat_insert<<<512, 256, 0, c->st>>>(c->dE, c->dC);
     k_stat_final<<<1, 64, 0, c->st>>>(c->dE, c->dC);
 }
 
 void launch_summaries(bpe_gpu_ctx *c) {
     k_rescan1<<<RESCAN1_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
-    k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+    if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
 }
 
 void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
-    k_scan<<<SCAN_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+    k_scan<<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
     k_apply<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
     if (tracked) launch_stats(c);
     launch_summaries(c);
@@ -374,7 +403,7 @@ int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
     for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++) {
         if (encode) {
-            k_scan<<<SCAN_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+            k_scan<<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
             k_apply<<<APPLY_A, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
             k_enc_next<<<1, 1, 0, c->st>>>(c->dE, c->dC, c->d_enc_pairs, n_enc);
         } else {
@@ -684,10 +713,9 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
 }
 
 int compact_ids(bpe_gpu_ctx *c) {
-    k_tile_count<<<512, 256, 0, c->st>>>(c->dE);
-    // plain exclusive scan of tile counts
-    k_scan_single<<<1, 1024, 0, c->st>>>(c->h.tilecnt, c->d_tileoff, (uint32_t)c->h.ntiles);
-    k_tile_write<<<512, 256, 0, c->st>>>(c->dE, c->d_tileoff, 0);
+    k_live_count<<<1024, 256, 0, c->st>>>(c->dE, c->dC, 0);
+    k_live_scan<<<1, 1024, 0, c->st>>>(c->dE, c->dC, 0, c->d_tileoff);
+    k_live_write<<<1024, 256, 0, c->st>>>(c->dE, c->dC, 0, c->d_tileoff, 0);
     HIPCHK(hipGetLastError());
     uint32_t tot = 0;
     HIPCHK(hipMemcpyAsync(&tot, c->d_tileoff + c->h.ntiles, 4, hipMemcpyDeviceToHost, c->st));
@@ -721,6 +749,7 @@ int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_
     // counting sort of pair positions by rank key
     const uint64_t npairs = c->n0 - 1;
     uint64_t tile = std::max<uint64_t>(1 << 16, (npairs + 1023) / 1024);
+    tile = (tile + 15) & ~15ull;  // kernels read 16-byte groups
     const uint32_t ntl = (uint32_t)((npairs + tile - 1) / tile);
     const uint32_t parts = (AA + HBINS - 1) / HBINS;
     uint32_t *d_hist, *d_tot;
@@ -745,7 +774,10 @@ int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_
         c->prof_launches = 1;
         k_pair_colscan<<<(AA + 255) / 256, 256, 0, c->st>>>(d_hist, d_tot, AA, ntl);
         k_scan_single<<<1, 1024, 0, c->st>>>(d_tot, h.poff, AA);
-        k_pair_scatter<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
+        unsigned long long *d_tmp;
+        if ((r = dalloc(c, &d_tmp, npairs, false))) return r;
+        k_sort_a<<<ntl, SORT_T, 0, c->st>>>(c->dE, d_hist, tile, d_tmp);
+        k_sort_b<<<1024, SORT_T, 0, c->st>>>(c->dE, d_hist, d_tot, ntl, d_tmp);
         HIPCHK(hipGetLastError());
     } else {
         HIPCHK(hipMemsetAsync(h.poff, 0, 4ull * (AA + 1), c->st));
@@ -805,8 +837,8 @@ int bpe_gpu_create(int device, bpe_gpu_ctx **out) {
 
 void bpe_gpu_destroy(bpe_gpu_ctx *c) {
     if (!c) return;
-    hipSetDevice(c->dev);
-    free_train(c);
+    (void)hipSetDevice(c->dev);
+    free_train(c, true);
     if (c->h.bytes) hipFree(c->h.bytes);
     if (c->dE) hipFree(c->dE);
     if (c->dC) hipFree(c->dC);
@@ -818,9 +850,10 @@ void bpe_gpu_destroy(bpe_gpu_ctx *c) {
 
 static int alloc_bytes(bpe_gpu_ctx *c, size_t n) {
     if (n > 0xFFFFFFFEull) return fail(BPE_GPU_ERANGE, "corpus > 2^32-2 bytes");
-    free_train(c);
-    if (c->h.bytes) { hipFree(c->h.bytes); c->h.bytes = nullptr; }
-    HIPCHK(hipMalloc(&c->h.bytes, std::max<size_t>(n, 1)));
+    free_train(c, true);
+    if (c->h.bytes) { (void)hipFree(c->h.bytes); c->h.bytes = nullptr; }
+    HIPCHK(hipMalloc(&c->h.bytes, n + 64));  // kernels read whole 16-byte groups
+    HIPCHK(hipMemsetAsync(c->h.bytes, 0, n + 64, c->st));
     c->n0 = n;
     c->loaded = true;
     return 0;

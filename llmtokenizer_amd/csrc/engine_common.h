@@ -15,14 +15,15 @@
 namespace bpeamd {
 
 constexpr uint32_t HOLE = 0xFFFFFFFFu;
-constexpr uint32_t LSPAN = 256;          // ids aggregated in LDS by the scan kernel
+constexpr uint32_t DENSE = 2048;         // ids aggregated in LDS / stored densely in delta vectors
+constexpr uint32_t REPL = 8;             // replicas of the dense delta accumulators
 constexpr uint32_t NTHR = 16;            // reference THREAD_NO (bpe.c:409)
 constexpr uint64_t CHUNK = 65536;        // reference CHUNK_SIZE (bpe.c:423)
 constexpr uint64_t DYN_LIMIT = CHUNK * NTHR;     // n >= this: chunked counting
 constexpr uint64_t TRACK_LIMIT = 2 * DYN_LIMIT;  // per-thread history tracked below this
 constexpr uint64_t MERGED_B0 = 65536;    // reference MERGED_TABLE_BUCKET_NUM (bpe.c:611)
 constexpr uint64_t THREAD_B0 = 256;      // reference PER_THREAD_TABLE_BUCKET_NUM (bpe.c:610)
-constexpr uint32_t L1W = 256;            // slots per level-1 summary block
+constexpr uint32_t L1W = 1024;           // slots per level-1 summary block
 constexpr uint32_t L2W = 256;            // level-1 entries per level-2 summary
 
 enum { V_DL = 0, V_DR = 1, V_IL = 2, V_IR = 3 };
@@ -60,14 +61,17 @@ struct Eng {
     uint32_t *vec[2][4];  // delta vectors (dec-left, dec-right, inc-left, inc-right), 2 parities
     uint32_t *vlist[2][4];
     uint32_t *vnl[2];     // [4] list lengths
+    uint32_t *vecd;       // [REPL][4][DENSE] replicated dense accumulators (ids < DENSE)
     // pair-count table: open addressing on (a,b), never deletes (count may hit 0)
     uint64_t hcap;        // power of two
     unsigned long long *hkey;  // key + 1, 0 = empty
     uint32_t *hcnt;
-    unsigned long long *l1best;
-    uint32_t *l1tie, *l1arg, *l1dirty, *l1list;
-    unsigned long long *l2best;
-    uint32_t *l2tie, *l2arg, *l2dirty, *l2list;
+    // max summaries: level 1 = 256 slots, level 2 = 256 level-1 entries;
+    // best packed value, number of keys holding it, smallest such key
+    unsigned long long *l1best, *l1key;
+    uint32_t *l1tie, *l1list;
+    unsigned long long *l2best, *l2key;
+    uint32_t *l2tie, *l2list;
     // per-thread history tracking (n < TRACK_LIMIT)
     uint64_t scap;        // stats table capacity (power of two)
     unsigned long long *skey;  // ((t << 60) | (a << 30) | b) + 1

@@ -35,8 +35,20 @@ __device__ inline uint32_t wave_append(bool pred, uint32_t *counter) {
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
-__device__ inline void vadd(uint32_t (*s)[LSPAN], const Eng *E, uint32_t P, int v, uint32_t x) {
-    if (x < LSPAN) {
+// Delta vectors: ids < DENSE are aggregated in LDS and flushed with
+// fire-and-forget atomics (k_apply enumerates them densely); rarer ids >= DENSE
+// go straight to global memory and are listed on first touch.
+// value of delta vector v at id x (dense ids: sum of the REPL replicas)
+__device__ inline uint32_t dval(const Eng *E, uint32_t P, int v, uint32_t x) {
+    if (x >= DENSE) return E->vec[P][v][x];
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < REPL; r++) sum += E->vecd[(r * 4 + v) * DENSE + x];
+    return sum;
+}
+
+__device__ inline void vadd(uint32_t (*s)[DENSE], const Eng *E, uint32_t P, int v, uint32_t x) {
+    if (x < DENSE) {
         atomicAdd(&s[v][x], 1u);
     } else {
         uint32_t old = atomicAdd(&E->vec[P][v][x], 1u);
@@ -48,10 +60,36 @@ __device__ inline void vadd(uint32_t (*s)[LSPAN], const Eng *E, uint32_t P, int 
 }
 
 // ---------------------------------------------------------------- k_scan
-__global__ __launch_bounds__(256) void k_scan(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+// Start of the token that ends at position i-1 (the left neighbour of the
+// token starting at i).  A single-byte token is its own end slot (tok != HOLE
+// there); a longer one stored its start distance in dist[end] when it was
+// created -- so dist never needs initialising.
+__device__ inline uint64_t left_start(const uint32_t *__restrict__ tok, const uint32_t *__restrict__ dist,
+                                      uint64_t i) {
+    const uint64_t e = i - 1;
+    return tok[e] != HOLE ? e : e - dist[e];
+}
+
+constexpr uint32_t SCAN_T = 1024;  // threads per k_scan block = candidates per round
+
+// append the block's staged occurrence positions to the new id's list
+__device__ inline void flush_list(uint32_t *list, uint32_t *lcount, uint32_t *gbase, uint32_t *R, uint32_t *occz) {
+    __syncthreads();
+    const uint32_t n = min(*lcount, SCAN_T);
+    if (threadIdx.x == 0) *gbase = n ? atomicAdd(R, n) : 0;
+    __syncthreads();
+    if (threadIdx.x < n) occz[*gbase + threadIdx.x] = list[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) *lcount = 0;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (C->stop) return;
+    const uint32_t len = C->cand_len;
+    if (blockIdx.x * SCAN_T >= len) return;  // block-uniform
     const uint32_t a = C->a, b = C->b, z = C->z;
-    const uint32_t mode = C->cand_mode, off = C->cand_off, len = C->cand_len;
+    const uint32_t mode = C->cand_mode, off = C->cand_off;
     const uint32_t P = C->parity;
     const uint64_t n0 = E->n0;
     const uint32_t *__restrict__ tok = E->tok;
@@ -60,20 +98,23 @@ __global__ __launch_bounds__(256) void k_scan(const Eng *__restrict__ E, Ctl *__
     const bool count = !E->encode;
     uint32_t *occz = E->occ + C->occ_top;
 
-    __shared__ uint32_t s[4][LSPAN];
-    for (uint32_t i = threadIdx.x; i < 4 * LSPAN; i += blockDim.x) (&s[0][0])[i] = 0;
+    __shared__ uint32_t s[4][DENSE];
+    __shared__ uint32_t list[SCAN_T];
+    __shared__ uint32_t lcount, gbase;
+    if (count)
+        for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) (&s[0][0])[x] = 0;
+    if (threadIdx.x == 0) lcount = 0;
     __syncthreads();
 
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t e0 = blockIdx.x * blockDim.x; e0 < len; e0 += stride) {
+    for (uint32_t e0 = blockIdx.x * SCAN_T; e0 < len; e0 += gridDim.x * SCAN_T) {
         const uint32_t e = e0 + threadIdx.x;
         bool ok = false;
         uint64_t i = 0, j = 0;
         if (e < len) {
             if (mode == 2) {
                 j = E->occ[off + e];
-                if (tok[j] == b && j > 0) {
-                    i = j - 1 - dist[j - 1];
+                if (j > 0 && tok[j] == b) {
+                    i = left_start(tok, dist, j);
                     ok = tok[i] == a;
                 }
             } else {
@@ -85,16 +126,16 @@ __global__ __launch_bounds__(256) void k_scan(const Eng *__restrict__ E, Ctl *__
             }
         }
         if (a != b) {
-            uint32_t slot = wave_append(ok, &C->R);
+            const uint32_t slot = wave_append(ok, &lcount);  // LDS counter
             if (ok) {
-                occz[slot] = (uint32_t)i;
+                list[slot] = (uint32_t)i;
                 if (count) {
                     const uint64_t k = j + lb;
                     if (i > 0) {
-                        const uint64_t ps = i - 1 - dist[i - 1];
+                        const uint64_t ps = left_start(tok, dist, i);
                         const uint32_t p = tok[ps];
                         bool cov = false;
-                        if (p == b && ps > 0) cov = tok[ps - 1 - dist[ps - 1]] == a;
+                        if (p == b && ps > 0) cov = tok[left_start(tok, dist, ps)] == a;
                         if (!cov) {
                             vadd(s, E, P, V_DL, p);
                             vadd(s, E, P, V_IL, p);
@@ -112,18 +153,19 @@ __global__ __launch_bounds__(256) void k_scan(const Eng *__restrict__ E, Ctl *__
             // a == b: only the thread holding a run's first token walks it,
             // pairing tokens 0-1, 2-3, ... (greedy left-to-right)
             uint32_t p = HOLE;
+            bool start = true;
             if (i > 0) {
-                const uint64_t ps = i - 1 - dist[i - 1];
-                p = tok[ps];
-                if (p == a) continue;  // not a run start
+                p = tok[left_start(tok, dist, i)];
+                start = p != a;
             }
             uint64_t pos = i;
-            for (uint32_t m = 0;; m++) {
+            for (uint32_t m = 0; start; m++) {
                 const uint64_t jj = pos + la;
                 if (jj >= n0 || tok[jj] != a) break;
                 const uint64_t k = jj + la;
-                const uint32_t slot = atomicAdd(&C->R, 1u);
-                occz[slot] = (uint32_t)pos;
+                const uint32_t slot = atomicAdd(&lcount, 1u);
+                if (slot < SCAN_T) list[slot] = (uint32_t)pos;
+                else occz[atomicAdd(&C->R, 1u)] = (uint32_t)pos;  // overflow: straight out
                 const bool knext = k < n0 && tok[k] == a;
                 if (count) {
                     if (m == 0 && p != HOLE) {
@@ -141,19 +183,14 @@ __global__ __launch_bounds__(256) void k_scan(const Eng *__restrict__ E, Ctl *__
                 pos = k;
             }
         }
+        flush_list(list, &lcount, &gbase, &C->R, occz);
     }
     if (!count) return;
-    __syncthreads();
-    for (uint32_t x = threadIdx.x; x < 4 * LSPAN; x += blockDim.x) {
-        const uint32_t v = x / LSPAN, id = x % LSPAN;
-        const uint32_t c = s[v][id];
-        if (c) {
-            uint32_t old = atomicAdd(&E->vec[P][v][id], c);
-            if (old == 0) {
-                uint32_t q = atomicAdd(&E->vnl[P][v], 1u);
-                E->vlist[P][v][q] = id;
-            }
-        }
+    // flush into replica (block % REPL): ~REPL x fewer same-address atomics
+    uint32_t *rep = E->vecd + (uint64_t)(blockIdx.x % REPL) * 4 * DENSE;
+    for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) {
+        const uint32_t c = (&s[0][0])[x];
+        if (c) atomicAdd(&rep[x], c);  // result unused: no-return atomic
     }
 }
 
@@ -191,15 +228,9 @@ __device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v)
     return ~0ull;  // table full: callers flag STOP_ERROR
 }
 
-__device__ inline void mark_l1(const Eng *E, Ctl *C, uint64_t slot) {
-    const uint32_t blk = (uint32_t)(slot / L1W);
-    if (atomicExch(&E->l1dirty[blk], 1u) == 0) {
-        uint32_t p = atomicAdd(&C->nl1, 1u);
-        E->l1list[p] = blk;
-    }
-}
-
 // ---------------------------------------------------------------- k_apply
+constexpr uint32_t MARK_CAP = 1024;
+
 __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *__restrict__ C,
                                                 uint32_t roleA_blocks) {
     if (C->stop) return;
@@ -214,7 +245,7 @@ __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *_
             const uint64_t j = i + la, k = j + lb;
             tok[i] = z;
             tok[j] = HOLE;
-            dist[k - 1] = (uint32_t)(k - 1 - i);
+            dist[k - 1] = (uint32_t)(k - 1 - i);  // k-1 >= j: never a token start now
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             E->occ_off[z] = C->occ_top;
@@ -224,60 +255,89 @@ __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *_
         return;
     }
     if (E->encode) return;
-    // role B: one owner thread per distinct touched key
+    // role B: one owner thread per distinct touched key.  Enumeration:
+    //   [0]                 (a,b)
+    //   [1, 1+4*DENSE)      dense ids of DR (b,x), DL (x,a), IR (z,x), IL (x,z)
+    //   then the listed ids >= DENSE of DR, DL, IR, IL
     const uint32_t nB = gridDim.x - roleA_blocks;
-    const uint32_t tid = (blockIdx.x - roleA_blocks) * blockDim.x + threadIdx.x;
     const uint32_t stride = nB * blockDim.x;
-    uint32_t *const *vec = E->vec[P];
     uint32_t *const *lst = E->vlist[P];
-    const uint32_t n_dl = E->vnl[P][V_DL], n_dr = E->vnl[P][V_DR];
-    const uint32_t n_il = E->vnl[P][V_IL], n_ir = E->vnl[P][V_IR];
-    const uint32_t total = 1 + n_dr + n_dl + n_ir + n_il;
+    uint32_t nl[4];
+    for (int v = 0; v < 4; v++) nl[v] = E->vnl[P][v];
+    const uint32_t dense_end = 1 + 4 * DENSE;
+    const uint32_t total = dense_end + nl[0] + nl[1] + nl[2] + nl[3];
+    __shared__ uint32_t marks[MARK_CAP];
+    __shared__ uint32_t nmark, mbase;
+    if (threadIdx.x == 0) nmark = 0;
+    __syncthreads();
     long long dD = 0;
-    for (uint32_t t = tid; t < total; t += stride) {
-        uint32_t u, v;
-        bool owner = true;
+    const uint32_t base0 = (blockIdx.x - roleA_blocks) * blockDim.x;
+    for (uint32_t t0 = base0; t0 < total; t0 += stride) {  // uniform trip count per block
+        const uint32_t t = t0 + threadIdx.x;
+        bool mark = false;
+        uint32_t blk = 0;
+        uint32_t u = 0, v = 0;
+        int cat = -1;  // category of this entry
+        uint32_t x = 0;
         if (t == 0) {
-            if (R == 0) continue;
-            u = a; v = b;
-        } else if (t < 1 + n_dr) {
-            u = b; v = lst[V_DR][t - 1];
-            owner = !(u == a && v == b);
-        } else if (t < 1 + n_dr + n_dl) {
-            u = lst[V_DL][t - 1 - n_dr]; v = a;
-            owner = !(u == a && v == b) && !(u == b && vec[V_DR][v] != 0);
-        } else if (t < 1 + n_dr + n_dl + n_ir) {
-            u = z; v = lst[V_IR][t - 1 - n_dr - n_dl];
-        } else {
-            u = lst[V_IL][t - 1 - n_dr - n_dl - n_ir]; v = z;
+            cat = 4; u = a; v = b;
+        } else if (t < dense_end) {
+            cat = (t - 1) / DENSE;
+            x = (t - 1) % DENSE;
+        } else if (t < total) {
+            uint32_t q = t - dense_end;
+            for (cat = 0; cat < 4 && q >= nl[cat]; cat++) q -= nl[cat];
+            x = lst[cat][q];
         }
-        if (!owner) continue;
-        long long d = 0;
-        if (u == a && v == b) d -= R;
-        if (u == b) d -= vec[V_DR][v];
-        if (v == a) d -= vec[V_DL][u];
-        if (u == z) d += vec[V_IR][v];
-        if (v == z) d += vec[V_IL][u];
-        if (d == 0) continue;
-        uint64_t slot;
-        if (d > 0) {
-            slot = hinsert(E, C, u, v);
-            if (slot == ~0ull) { C->err = 2; C->stop = STOP_ERROR; continue; }
-        } else {
-            slot = hfind(E, u, v);
-            if (slot == ~0ull) { C->err = 1; C->stop = STOP_ERROR; continue; }
+        if (cat >= 0 && cat < 4) {
+            if (cat == V_DL) { u = x; v = a; }
+            else if (cat == V_DR) { u = b; v = x; }
+            else if (cat == V_IL) { u = x; v = z; }
+            else { u = z; v = x; }
         }
-        const uint32_t old = E->hcnt[slot];
-        const uint32_t nw = (uint32_t)((long long)old + d);
-        E->hcnt[slot] = nw;
-        dD += (long long)(nw != 0) - (long long)(old != 0);
-        mark_l1(E, C, slot);
-    }
-    // zero the other parity's vectors (used by the previous iteration)
-    const uint32_t Q = P ^ 1;
-    for (int v = 0; v < 4; v++) {
-        const uint32_t nq = E->vnl[Q][v];
-        for (uint32_t t = tid; t < nq; t += stride) E->vec[Q][v][E->vlist[Q][v][t]] = 0;
+        // the four delta values that can touch key (u, v), loaded together
+        uint32_t vdr = 0, vdl = 0, vir = 0, vil = 0;
+        if (cat >= 0) {
+            vdr = u == b ? dval(E, P, V_DR, v) : 0;
+            vdl = v == a ? dval(E, P, V_DL, u) : 0;
+            vir = u == z ? dval(E, P, V_IR, v) : 0;
+            vil = v == z ? dval(E, P, V_IL, u) : 0;
+        }
+        bool owner = cat >= 0;
+        if (owner && cat == 4) owner = R != 0;
+        if (owner && cat == V_DR) owner = vdr != 0 && !(u == a && v == b);
+        if (owner && cat == V_DL) owner = vdl != 0 && !(u == a && v == b) && !(u == b && vdr != 0);
+        if (owner && cat == V_IR) owner = vir != 0;
+        if (owner && cat == V_IL) owner = vil != 0;
+        if (owner) {
+            long long d = -(long long)vdr - (long long)vdl + (long long)vir + (long long)vil;
+            if (u == a && v == b) d -= R;
+            if (d != 0) {
+                const uint64_t slot = d > 0 ? hinsert(E, C, u, v) : hfind(E, u, v);
+                if (slot == ~0ull) {
+                    C->err = d > 0 ? 2 : 1;
+                    C->stop = STOP_ERROR;
+                } else {
+                    const uint32_t old = E->hcnt[slot];
+                    const uint32_t nw = (uint32_t)((long long)old + d);
+                    E->hcnt[slot] = nw;
+                    dD += (long long)(nw != 0) - (long long)(old != 0);
+                    blk = (uint32_t)(slot / L1W);
+                    mark = true;
+                }
+            }
+        }
+        const uint32_t p = wave_append(mark, &nmark);
+        if (mark) marks[p] = blk;
+        __syncthreads();
+        if (nmark > MARK_CAP - blockDim.x || t0 + stride >= total) {
+            if (threadIdx.x == 0) mbase = nmark ? atomicAdd(&C->nl1, nmark) : 0;
+            __syncthreads();
+            for (uint32_t k = threadIdx.x; k < nmark; k += blockDim.x) E->l1list[mbase + k] = marks[k];
+            __syncthreads();
+            if (threadIdx.x == 0) nmark = 0;
+            __syncthreads();
+        }
     }
     // block-reduce dD
     __shared__ long long sd[256];
@@ -300,97 +360,104 @@ __device__ inline uint64_t summary_B(uint64_t D) {
     return edge ? 2 * B : B;
 }
 
+// best packed value; tie = number of keys holding it; key = smallest such key
 struct Best {
     unsigned long long v;
-    uint32_t tie, arg;
+    uint32_t tie;
+    unsigned long long key;
 };
 
 __device__ inline Best best_merge(Best x, Best y) {
     if (y.v > x.v) return y;
     if (y.v < x.v) return x;
-    Best r = x;
-    r.tie = x.tie + y.tie;
-    r.arg = x.arg < y.arg ? x.arg : y.arg;
-    return r;
+    return Best{x.v, x.tie + y.tie, x.key < y.key ? x.key : y.key};
 }
 
-__device__ inline Best block_best(Best mine) {
-    __shared__ unsigned long long sv[1024 / 64];
-    __shared__ uint32_t st[1024 / 64], sa[1024 / 64];
-    // wave reduce
+__device__ inline Best wave_best(Best m) {
     for (int o = 32; o > 0; o >>= 1) {
         Best y;
-        y.v = __shfl_down(mine.v, o);
-        y.tie = __shfl_down(mine.tie, o);
-        y.arg = __shfl_down(mine.arg, o);
-        mine = best_merge(mine, y);
+        y.v = __shfl_xor(m.v, o);
+        y.tie = __shfl_xor(m.tie, o);
+        y.key = __shfl_xor(m.key, o);
+        m = best_merge(m, y);
     }
-    const uint32_t w = threadIdx.x / 64, nw = (blockDim.x + 63) / 64;
-    if (lane_id() == 0) { sv[w] = mine.v; st[w] = mine.tie; sa[w] = mine.arg; }
-    __syncthreads();
-    Best r{0, 0, 0xFFFFFFFFu};
-    if (threadIdx.x == 0) {
-        r.v = sv[0]; r.tie = st[0]; r.arg = sa[0];
-        for (uint32_t k = 1; k < nw; k++) r = best_merge(r, Best{sv[k], st[k], sa[k]});
-    }
-    __syncthreads();
-    return r;  // valid in thread 0
+    return m;  // identical in every lane
 }
 
+constexpr uint64_t SELECT_L1_MAX = 16384;  // k_select reduces level 1 directly up to this
+
+// one wave per dirty level-1 block (256 slots, 4 per lane)
 __global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (C->stop) return;
+    {   // k_apply has consumed this iteration's delta vectors: clear them
+        const uint32_t P = C->parity;
+        const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+        for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride) E->vecd[x] = 0;
+        for (int vv = 0; vv < 4; vv++) {
+            const uint32_t nq = E->vnl[P][vv];
+            for (uint32_t t = tid; t < nq; t += stride) E->vec[P][vv][E->vlist[P][vv][t]] = 0;
+        }
+    }
     const uint64_t B = summary_B(C->D);
     const bool full = C->full || B != C->B;
     const uint64_t nL1 = E->hcap / L1W;
     const uint64_t nwork = full ? nL1 : C->nl1;
-    for (uint64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t w = wid; w < nwork; w += nwaves) {
         const uint32_t blk = full ? (uint32_t)w : E->l1list[w];
-        const uint64_t slot = (uint64_t)blk * L1W + threadIdx.x;
-        Best mine{0, 0, (uint32_t)slot};
-        const uint32_t c = E->hcnt[slot];
-        if (c) {
-            const unsigned long long k = E->hkey[slot] - 1;
-            mine.v = pack_val(c, (uint32_t)(k >> 32), (uint32_t)k, B);
-            mine.tie = 1;
+        Best mine{0, 0, ~0ull};
+        uint32_t cnt[L1W / 64];
+        unsigned long long key[L1W / 64];
+#pragma unroll
+        for (uint32_t q = 0; q < L1W / 64; q++) {  // all loads first: one round trip
+            const uint64_t slot = (uint64_t)blk * L1W + q * 64 + lane;
+            cnt[q] = E->hcnt[slot];
+            key[q] = E->hkey[slot];
         }
-        Best r = block_best(mine);
-        if (threadIdx.x == 0) {
+#pragma unroll
+        for (uint32_t q = 0; q < L1W / 64; q++) {
+            if (cnt[q]) {
+                const unsigned long long k = key[q] - 1;
+                mine = best_merge(mine, Best{pack_val(cnt[q], (uint32_t)(k >> 32), (uint32_t)k, B), 1, k});
+            }
+        }
+        const Best r = wave_best(mine);
+        if (lane == 0) {
             E->l1best[blk] = r.v;
             E->l1tie[blk] = r.v ? r.tie : 0;
-            E->l1arg[blk] = r.arg;
-            E->l1dirty[blk] = 0;
-            if (!full) {
-                const uint32_t b2 = blk / L2W;
-                if (atomicExch(&E->l2dirty[b2], 1u) == 0) {
-                    uint32_t p = atomicAdd(&C->nl2, 1u);
-                    E->l2list[p] = b2;
-                }
-            }
+            E->l1key[blk] = r.key;
+            if (!full) E->l2list[w] = blk / L2W;  // duplicates are harmless
         }
     }
 }
 
+// one wave per dirty level-2 entry (256 level-1 entries, 4 per lane); only
+// for tables too large for k_select to reduce level 1 directly
 __global__ __launch_bounds__(256) void k_rescan2(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (C->stop) return;
+    const uint64_t nL1 = E->hcap / L1W;
+    if (nL1 <= SELECT_L1_MAX) return;
     const uint64_t B = summary_B(C->D);
     const bool full = C->full || B != C->B;
-    const uint64_t nL1 = E->hcap / L1W;
     const uint64_t nL2 = (nL1 + L2W - 1) / L2W;
-    const uint64_t nwork = full ? nL2 : C->nl2;
-    for (uint64_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+    const uint64_t nwork = full ? nL2 : C->nl1;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t w = wid; w < nwork; w += nwaves) {
         const uint32_t b2 = full ? (uint32_t)w : E->l2list[w];
-        const uint64_t i1 = (uint64_t)b2 * L2W + threadIdx.x;
-        Best mine{0, 0, (uint32_t)i1};
-        if (i1 < nL1) {
-            mine.v = E->l1best[i1];
-            mine.tie = E->l1tie[i1];
+        Best mine{0, 0, ~0ull};
+        for (uint32_t q = 0; q < L2W / 64; q++) {
+            const uint64_t i1 = (uint64_t)b2 * L2W + q * 64 + lane;
+            if (i1 < nL1 && E->l1best[i1]) mine = best_merge(mine, Best{E->l1best[i1], E->l1tie[i1], E->l1key[i1]});
         }
-        Best r = block_best(mine);
-        if (threadIdx.x == 0) {
+        const Best r = wave_best(mine);
+        if (lane == 0) {
             E->l2best[b2] = r.v;
             E->l2tie[b2] = r.v ? r.tie : 0;
-            E->l2arg[b2] = r.arg;
-            E->l2dirty[b2] = 0;
+            E->l2key[b2] = r.key;
         }
     }
 }
@@ -443,9 +510,7 @@ __device__ inline void finish_iteration(const Eng *E, Ctl *C) {
     C->R = 0;
     C->nl1 = 0;
     C->nl2 = 0;
-    const uint32_t Q = C->parity ^ 1;
-    for (int v = 0; v < 4; v++) E->vnl[Q][v] = 0;
-    C->parity = Q;
+    for (int v = 0; v < 4; v++) E->vnl[C->parity][v] = 0;  // entries zeroed by k_rescan1
     C->counters[0]++;
 }
 
@@ -453,12 +518,23 @@ __device__ inline void finish_iteration(const Eng *E, Ctl *C) {
 __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t tracked_graph) {
     if (C->stop) return;
     const uint64_t nL1 = E->hcap / L1W;
-    const uint64_t nL2 = (nL1 + L2W - 1) / L2W;
-    Best mine{0, 0, 0xFFFFFFFFu};
-    for (uint64_t i = threadIdx.x; i < nL2; i += blockDim.x)
-        mine = best_merge(mine, Best{E->l2best[i], E->l2tie[i], (uint32_t)i});
-    Best r = block_best(mine);
+    Best mine{0, 0, ~0ull};
+    if (nL1 <= SELECT_L1_MAX) {
+#pragma unroll 4
+        for (uint64_t i = threadIdx.x; i < nL1; i += blockDim.x)
+            if (E->l1best[i]) mine = best_merge(mine, Best{E->l1best[i], E->l1tie[i], E->l1key[i]});
+    } else {
+        const uint64_t nL2 = (nL1 + L2W - 1) / L2W;
+        for (uint64_t i = threadIdx.x; i < nL2; i += blockDim.x)
+            if (E->l2best[i]) mine = best_merge(mine, Best{E->l2best[i], E->l2tie[i], E->l2key[i]});
+    }
+    mine = wave_best(mine);
+    __shared__ Best sw[16];
+    if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = mine;
+    __syncthreads();
     if (threadIdx.x != 0) return;
+    Best r = sw[0];
+    for (uint32_t k = 1; k < blockDim.x / 64; k++) r = best_merge(r, sw[k]);
     finish_iteration(E, C);
     if (!tracked_graph && C->n_live < TRACK_LIMIT) { C->stop = STOP_MODE; return; }
     const uint64_t D = C->D;
@@ -475,32 +551,10 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
     if (C->nkeys + 4ull * (256ull + C->merges_done + 2) >= E->hcap / 2) { C->stop = STOP_GROW; return; }
     const bool tracked = C->n_live < DYN_LIMIT;   // deterministic (static) reference iteration
     if (tracked && (edge || r.tie > 1)) { C->stop = STOP_EVENT; return; }
-    // descend to the slot
-    const uint32_t i1 = E->l2arg[r.arg];
-    uint32_t slot = E->l1arg[i1];
-    if (r.tie > 1) {
-        // schedule-dependent tie (n >= 2^20): project rule = smallest (a,b)
-        unsigned long long bestk = ~0ull;
-        for (uint64_t i2 = 0; i2 < nL2; i2++) {
-            if (E->l2best[i2] != r.v) continue;
-            for (uint64_t j1 = i2 * L2W; j1 < (i2 + 1) * L2W && j1 < nL1; j1++) {
-                if (E->l1best[j1] != r.v) continue;
-                for (uint64_t s = j1 * L1W; s < (j1 + 1) * L1W; s++) {
-                    const uint32_t c = E->hcnt[s];
-                    if (!c) continue;
-                    const unsigned long long k = E->hkey[s] - 1;
-                    if (pack_val(c, (uint32_t)(k >> 32), (uint32_t)k, C->B) == r.v && k < bestk) {
-                        bestk = k;
-                        slot = (uint32_t)s;
-                    }
-                }
-            }
-        }
-        C->counters[2]++;
-    }
-    C->wslot = slot;
-    const unsigned long long key = E->hkey[slot] - 1;
-    commit_merge(E, C, (uint32_t)(key >> 32), (uint32_t)key);
+    // untracked tie (n >= 2^20, schedule-dependent in the reference): the
+    // project rule is the smallest (a,b) -- r.key already is that key
+    if (r.tie > 1) C->counters[2]++;
+    commit_merge(E, C, (uint32_t)(r.key >> 32), (uint32_t)r.key);
 }
 
 // commit a merge chosen by the host resolver (after STOP_EVENT)
@@ -521,38 +575,71 @@ __global__ void k_enc_next(const Eng *__restrict__ E, Ctl *__restrict__ C, const
 }
 
 // ------------------------------------------------------------- init kernels
-__global__ void k_init_tok(const Eng *__restrict__ E, uint32_t *__restrict__ bhist) {
-    __shared__ uint32_t h[256];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) h[i] = 0;
+// tok[i] = byte i (16 bytes per thread, uint4 in / 4 x uint4 out) and the set
+// of byte values present (only presence is needed to rank them)
+__global__ __launch_bounds__(256) void k_init_tok(const Eng *__restrict__ E, uint32_t *__restrict__ present) {
+    __shared__ uint32_t seen[256];
+    for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x) seen[x] = 0;
     __syncthreads();
-    const uint64_t n0 = E->n0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n0; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t x = E->bytes[i];
-        E->tok[i] = x;
-        atomicAdd(&h[x], 1u);
+    const uint64_t n0 = E->n0, nv = n0 / 16;
+    const uint4 *src = reinterpret_cast<const uint4 *>(E->bytes);
+    uint4 *dst = reinterpret_cast<uint4 *>(E->tok);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nv; c += stride) {
+        const uint4 v = src[c];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t b0 = w[q] & 0xFF, b1 = (w[q] >> 8) & 0xFF, b2 = (w[q] >> 16) & 0xFF, b3 = w[q] >> 24;
+            dst[4 * c + q] = make_uint4(b0, b1, b2, b3);
+            seen[b0] = 1; seen[b1] = 1; seen[b2] = 1; seen[b3] = 1;  // benign same-value races
+        }
     }
+    if (blockIdx.x == 0)
+        for (uint64_t k = nv * 16 + threadIdx.x; k < n0; k += blockDim.x) {
+            E->tok[k] = E->bytes[k];
+            seen[E->bytes[k]] = 1;
+        }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x)
-        if (h[i]) atomicAdd(&bhist[i], h[i]);
+    for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x)
+        if (seen[x] && !present[x]) atomicOr(&present[x], 1u);
 }
 
-// per-(tile, part) histogram of byte-pair rank keys; LDS u32 bins
+// per-(tile, part) histogram of byte-pair rank keys; LDS u32 bins.
+// 16 pair positions per thread from one uint4 load (+1 byte of the next).
 constexpr uint32_t HBINS = 16384;
+
+__device__ inline uint32_t byte_at(const uint4 &v, uint32_t k) {
+    const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+    return (w >> (8 * (k & 3))) & 0xFF;
+}
 
 __global__ __launch_bounds__(1024) void k_pair_hist(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
                                                     uint64_t tile, uint32_t parts) {
     __shared__ uint32_t h[HBINS];
-    const uint32_t AA = E->A * E->A;
+    __shared__ uint32_t rk[256];
+    const uint32_t A = E->A, AA = A * A;
     const uint32_t tl = blockIdx.x / parts, part = blockIdx.x % parts;
     const uint32_t lo = part * HBINS, hi = min(AA, lo + HBINS);
     for (uint32_t i = threadIdx.x; i < HBINS; i += blockDim.x) h[i] = 0;
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) rk[i] = E->rank[i];
     __syncthreads();
     const uint64_t n0 = E->n0;
-    const uint64_t s = (uint64_t)tl * tile, e = min(n0 - 1, s + tile);  // pair positions i < n0-1
-    const uint32_t A = E->A;
-    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-        const uint32_t k = E->rank[E->bytes[i]] * A + E->rank[E->bytes[i + 1]];
-        if (k >= lo && k < hi) atomicAdd(&h[k - lo], 1u);
+    const uint64_t s = (uint64_t)tl * tile, e = min(n0 - 1, s + tile);  // pair positions [s, e), tile % 16 == 0
+    const uint4 *src = reinterpret_cast<const uint4 *>(E->bytes);
+    for (uint64_t c = s / 16 + threadIdx.x; c * 16 < e; c += blockDim.x) {
+        const uint64_t p0 = c * 16;
+        const uint4 v = src[c];
+        const uint32_t nxt = p0 + 16 < n0 ? E->bytes[p0 + 16] : 0;
+        const uint32_t lim = (uint32_t)min<uint64_t>(16, e - p0);
+        uint32_t prev = rk[byte_at(v, 0)];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+            const uint32_t cur = k + 1 < 16 ? rk[byte_at(v, k + 1)] : rk[nxt];
+            const uint32_t key = prev * A + cur;
+            if (k < lim && key >= lo && key < hi) atomicAdd(&h[key - lo], 1u);
+            prev = cur;
+        }
     }
     __syncthreads();
     for (uint32_t k = lo + threadIdx.x; k < hi; k += blockDim.x) hist[(uint64_t)tl * AA + k] = h[k - lo];
@@ -571,47 +658,178 @@ __global__ void k_pair_colscan(uint32_t *__restrict__ hist, uint32_t *__restrict
     tot[k] = run;
 }
 
-// exclusive scan of tot[0..AA) into poff[0..AA], single block
-__global__ __launch_bounds__(1024) void k_scan_single(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
-                                                      uint32_t n) {
-    __shared__ uint32_t sh[1024];
-    uint32_t carry = 0;
-    for (uint32_t base = 0; base < n; base += 1024) {
-        const uint32_t i = base + threadIdx.x;
-        const uint32_t x = i < n ? in[i] : 0;
-        sh[threadIdx.x] = x;
-        __syncthreads();
-        for (uint32_t o = 1; o < 1024; o <<= 1) {
-            uint32_t y = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-            __syncthreads();
-            sh[threadIdx.x] += y;
-            __syncthreads();
-        }
-        if (i < n) out[i] = carry + sh[threadIdx.x] - x;
-        const uint32_t tot = sh[1023];
-        __syncthreads();
-        carry += tot;
+// exclusive scan of in[0..n) into out[0..n], out[n] = total; one block of
+// 1024 threads, each owning a contiguous chunk (shuffle scan of the partials)
+__device__ inline uint32_t block_excl_scan1024(uint32_t x, uint32_t *total) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = x;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += y;
     }
-    if (threadIdx.x == 0) out[n] = carry;
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t r = 0;
+        for (uint32_t k = 0; k < blockDim.x / 64; k++) { const uint32_t t = wsum[k]; wsum[k] = r; r += t; }
+        *total = r;
+    }
+    __syncthreads();
+    const uint32_t ex = wsum[w] + incl - x;
+    __syncthreads();
+    return ex;
 }
 
-__global__ __launch_bounds__(1024) void k_pair_scatter(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
-                                                       uint64_t tile, uint32_t parts) {
-    __shared__ uint32_t cur[HBINS];
-    const uint32_t AA = E->A * E->A;
-    const uint32_t tl = blockIdx.x / parts, part = blockIdx.x % parts;
-    const uint32_t lo = part * HBINS, hi = min(AA, lo + HBINS);
-    for (uint32_t k = lo + threadIdx.x; k < hi; k += blockDim.x)
-        cur[k - lo] = E->poff[k] + hist[(uint64_t)tl * AA + k];
+__global__ __launch_bounds__(1024) void k_scan_single(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                      uint32_t n) {
+    __shared__ uint32_t tot;
+    const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
+    const uint32_t lo = threadIdx.x * per, hi = min(n, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; i++) sum += in[i];
+    uint32_t run = block_excl_scan1024(sum, &tot);
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint32_t x = in[i];
+        out[i] = run;
+        run += x;
+    }
+    if (threadIdx.x == 0) out[n] = tot;
+}
+
+// Counting sort of pair positions by rank key (k1, k2) = (first, second byte
+// rank) in two MSD passes.  A single pass writes 1G positions into A^2 (9025
+// for printable text) interleaved streams per block and every 4-byte store
+// ends up as its own memory transaction (13.6 ms for 1 GiB); two passes keep
+// only A (<= 256) streams per block open, so stores combine in L2.
+// hist[t][key] holds, after k_pair_colscan, the number of pair positions with
+// `key` in tiles < t; tot[key] the total; poff the key offsets.
+__device__ inline uint32_t tile_count(const uint32_t *hist, const uint32_t *tot, uint32_t t, uint32_t ntl,
+                                      uint32_t AA, uint32_t key) {
+    const uint32_t here = hist[(uint64_t)t * AA + key];
+    const uint32_t next = t + 1 < ntl ? hist[(uint64_t)(t + 1) * AA + key] : tot[key];
+    return next - here;
+}
+
+// Both passes sort CH-element chunks inside LDS first (local counting sort),
+// then copy each bin's run out contiguously: consecutive lanes store to
+// consecutive addresses.
+constexpr uint32_t SORT_T = 1024, SORT_PER = 8, SORT_CH = SORT_T * SORT_PER;
+
+struct SortLds {
+    unsigned long long ent[SORT_CH];  // staged entries in local bin order
+    uint8_t bin[SORT_CH];             // their bins
+    uint32_t cnt[256], lstart[256], gcur[256], gstart[256];
+};
+
+// local counting sort of this thread's SORT_PER (bin, entry) pairs, then a
+// coalesced copy of every bin's run to out[gcur[bin] ...]; gcur advances
+__device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const unsigned long long *vals, uint32_t nb,
+                                     void *out, bool out64) {
+    for (uint32_t x = threadIdx.x; x < nb; x += SORT_T) L.cnt[x] = 0;
+    __syncthreads();
+    uint32_t rank[SORT_PER];
+#pragma unroll
+    for (uint32_t k = 0; k < SORT_PER; k++) rank[k] = bins[k] < nb ? atomicAdd(&L.cnt[bins[k]], 1u) : 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t r = 0;
+        for (uint32_t x = 0; x < nb; x++) {
+            L.lstart[x] = r;
+            L.gstart[x] = L.gcur[x];
+            L.gcur[x] += L.cnt[x];
+            r += L.cnt[x];
+        }
+        L.cnt[0] = r;  // total staged (cnt[] no longer needed)
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < SORT_PER; k++)
+        if (bins[k] < nb) {
+            const uint32_t s = L.lstart[bins[k]] + rank[k];
+            L.ent[s] = vals[k];
+            L.bin[s] = (uint8_t)bins[k];
+        }
+    __syncthreads();
+    const uint32_t total = L.cnt[0];
+    for (uint32_t s = threadIdx.x; s < total; s += SORT_T) {
+        const uint32_t bn = L.bin[s];
+        const uint32_t d = L.gstart[bn] + (s - L.lstart[bn]);
+        if (out64) reinterpret_cast<unsigned long long *>(out)[d] = L.ent[s];
+        else reinterpret_cast<uint32_t *>(out)[d] = (uint32_t)L.ent[s];
+    }
+    __syncthreads();
+}
+
+// pass A: tile t -> entries (k2 << 32 | position) grouped by k1, in the same
+// slot range plist will use for that tile's k1 group
+__global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
+                                                   uint64_t tile, unsigned long long *__restrict__ tmp) {
+    __shared__ SortLds L;
+    __shared__ uint32_t rk[256];
+    const uint32_t A = E->A, AA = A * A;
+    const uint32_t t = blockIdx.x;
+    for (uint32_t x = threadIdx.x; x < 256; x += SORT_T) rk[x] = E->rank[x];
+    if (threadIdx.x < A) {
+        uint32_t s0 = E->poff[threadIdx.x * A];
+        for (uint32_t k2 = 0; k2 < A; k2++) s0 += hist[(uint64_t)t * AA + threadIdx.x * A + k2];
+        L.gcur[threadIdx.x] = s0;
+    }
     __syncthreads();
     const uint64_t n0 = E->n0;
-    const uint64_t s = (uint64_t)tl * tile, e = min(n0 - 1, s + tile);
-    const uint32_t A = E->A;
-    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-        const uint32_t k = E->rank[E->bytes[i]] * A + E->rank[E->bytes[i + 1]];
-        if (k >= lo && k < hi) {
-            const uint32_t p = atomicAdd(&cur[k - lo], 1u);
-            E->plist[p] = (uint32_t)i;
+    const uint64_t s = (uint64_t)t * tile, e = min(n0 - 1, s + tile);
+    // each thread takes SORT_PER = 8 consecutive positions per round (uint2 load + 1 byte)
+    for (uint64_t p0 = s + threadIdx.x * SORT_PER; p0 - threadIdx.x * SORT_PER < e; p0 += SORT_CH) {
+        uint32_t bins[SORT_PER];
+        unsigned long long vals[SORT_PER];
+        uint32_t by[SORT_PER + 1] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (p0 < e) {
+            const uint2 w = *reinterpret_cast<const uint2 *>(E->bytes + p0);
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) { by[k] = (w.x >> (8 * k)) & 0xFF; by[4 + k] = (w.y >> (8 * k)) & 0xFF; }
+            by[SORT_PER] = p0 + SORT_PER < n0 ? E->bytes[p0 + SORT_PER] : 0;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < SORT_PER; k++) {
+            const bool in = p0 + k < e;
+            bins[k] = in ? rk[by[k]] : 256u;
+            vals[k] = in ? (((unsigned long long)rk[by[k + 1]] << 32) | (uint32_t)(p0 + k)) : 0ull;
+        }
+        lds_sort_emit(L, bins, vals, A, tmp, true);
+    }
+}
+
+// pass B: unit (tile t, first rank k1) -> plist by second rank
+__global__ __launch_bounds__(SORT_T) void k_sort_b(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
+                                                   const uint32_t *__restrict__ tot, uint32_t ntl,
+                                                   const unsigned long long *__restrict__ tmp) {
+    __shared__ SortLds L;
+    __shared__ uint32_t range[2];
+    const uint32_t A = E->A, AA = A * A;
+    for (uint32_t u = blockIdx.x; u < ntl * A; u += gridDim.x) {
+        const uint32_t t = u / A, k1 = u % A;
+        __syncthreads();
+        if (threadIdx.x == 0) { range[0] = E->poff[k1 * A]; range[1] = 0; }
+        __syncthreads();
+        for (uint32_t k2 = threadIdx.x; k2 < A; k2 += SORT_T) {
+            const uint32_t before = hist[(uint64_t)t * AA + k1 * A + k2];
+            L.gcur[k2] = E->poff[k1 * A + k2] + before;
+            atomicAdd(&range[0], before);
+            atomicAdd(&range[1], tile_count(hist, tot, t, ntl, AA, k1 * A + k2));
+        }
+        __syncthreads();
+        const uint32_t lo = range[0], n = range[1];
+        for (uint32_t q0 = 0; q0 < n; q0 += SORT_CH) {
+            uint32_t bins[SORT_PER];
+            unsigned long long vals[SORT_PER];
+#pragma unroll
+            for (uint32_t k = 0; k < SORT_PER; k++) {
+                const uint32_t q = q0 + k * SORT_T + threadIdx.x;  // coalesced reads
+                const unsigned long long w = q < n ? tmp[lo + q] : 0ull;
+                bins[k] = q < n ? (uint32_t)(w >> 32) : 256u;
+                vals[k] = (uint32_t)w;
+            }
+            lds_sort_emit(L, bins, vals, A, E->plist, false);
         }
     }
 }
@@ -645,52 +863,90 @@ __global__ void k_rehash(const Eng *__restrict__ E, Ctl *__restrict__ C, const u
 }
 
 // ------------------------------------------------------------- compaction
-constexpr uint32_t CTILE = 2048;
+// Live tokens (tok != HOLE) in position order -> ids (mode 0) or the
+// compacted-index -> position map used by the tracked statistics (mode 1).
+// Tiles of CTILE positions; 256 threads read one uint4 (4 positions) each per
+// round, so loads and the order-preserving writes are both contiguous.
+constexpr uint32_t CTILE = 16384;
 
-__global__ __launch_bounds__(256) void k_tile_count(const Eng *__restrict__ E) {
+__device__ inline bool tracking_on(const Ctl *C) { return C->n_live - C->R < TRACK_LIMIT; }
+
+__device__ inline uint32_t live4(const uint32_t *tok, uint64_t p, uint64_t n0, uint4 *out) {
+    if (p + 4 <= n0) {
+        *out = *reinterpret_cast<const uint4 *>(tok + p);
+    } else {
+        out->x = p < n0 ? tok[p] : HOLE;
+        out->y = p + 1 < n0 ? tok[p + 1] : HOLE;
+        out->z = p + 2 < n0 ? tok[p + 2] : HOLE;
+        out->w = HOLE;
+    }
+    return (out->x != HOLE) + (out->y != HOLE) + (out->z != HOLE) + (out->w != HOLE);
+}
+
+__global__ __launch_bounds__(256) void k_live_count(const Eng *__restrict__ E, const Ctl *__restrict__ C, int guard) {
+    if (guard && (C->stop || !tracking_on(C))) return;
     const uint64_t n0 = E->n0;
+    __shared__ uint32_t ws[4];
     for (uint64_t t = blockIdx.x; t < E->ntiles; t += gridDim.x) {
         uint32_t c = 0;
-        for (uint64_t i = t * CTILE + threadIdx.x; i < min(n0, (t + 1) * CTILE); i += blockDim.x)
-            c += E->tok[i] != HOLE;
-        __shared__ uint32_t sh[256];
-        sh[threadIdx.x] = c;
-        __syncthreads();
-        for (uint32_t w = 128; w > 0; w >>= 1) {
-            if (threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-            __syncthreads();
+        for (uint32_t r = 0; r < CTILE / 1024; r++) {
+            uint4 v;
+            c += live4(E->tok, t * CTILE + r * 1024 + threadIdx.x * 4, n0, &v);
         }
-        if (threadIdx.x == 0) E->tilecnt[t] = sh[0];
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) E->tilecnt[t] = ws[0] + ws[1] + ws[2] + ws[3];
         __syncthreads();
     }
 }
 
-// write ids (mode 0) or the compacted-index -> position map (mode 1)
-__global__ __launch_bounds__(256) void k_tile_write(const Eng *__restrict__ E, const uint32_t *__restrict__ tileoff,
-                                                    int mode) {
+__global__ __launch_bounds__(1024) void k_live_scan(const Eng *__restrict__ E, const Ctl *__restrict__ C, int guard,
+                                                    uint32_t *__restrict__ tileoff) {
+    if (guard && (C->stop || !tracking_on(C))) return;
+    __shared__ uint32_t tot;
+    const uint32_t n = (uint32_t)E->ntiles;
+    const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
+    const uint32_t lo = threadIdx.x * per, hi = min(n, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; i++) sum += E->tilecnt[i];
+    uint32_t run = block_excl_scan1024(sum, &tot);
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint32_t x = E->tilecnt[i];
+        tileoff[i] = run;
+        run += x;
+    }
+    if (threadIdx.x == 0) tileoff[n] = tot;
+}
+
+__global__ __launch_bounds__(256) void k_live_write(const Eng *__restrict__ E, const Ctl *__restrict__ C, int guard,
+                                                    const uint32_t *__restrict__ tileoff, int mode) {
+    if (guard && (C->stop || !tracking_on(C))) return;
     const uint64_t n0 = E->n0;
-    __shared__ uint32_t sh[256];
+    __shared__ uint32_t ws[4];
+    uint32_t *out = mode == 0 ? E->ids_out : E->cpos;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (uint64_t t = blockIdx.x; t < E->ntiles; t += gridDim.x) {
         uint32_t base = tileoff[t];
-        for (uint64_t c0 = t * CTILE; c0 < min(n0, (t + 1) * CTILE); c0 += 256) {
-            const uint64_t i = c0 + threadIdx.x;
-            const uint32_t x = i < n0 ? E->tok[i] : HOLE;
-            const uint32_t f = x != HOLE;
-            sh[threadIdx.x] = f;
+        for (uint32_t r = 0; r < CTILE / 1024; r++) {
+            const uint64_t p = t * CTILE + r * 1024 + threadIdx.x * 4;
+            uint4 v;
+            const uint32_t c = live4(E->tok, p, n0, &v);
+            uint32_t incl = c;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if ((int)lane >= o) incl += y;
+            }
+            if (lane == 63) ws[w] = incl;
             __syncthreads();
-            for (uint32_t o = 1; o < 256; o <<= 1) {
-                uint32_t y = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-                __syncthreads();
-                sh[threadIdx.x] += y;
-                __syncthreads();
-            }
-            const uint32_t incl = sh[threadIdx.x];
-            const uint32_t tot = sh[255];
-            if (f) {
-                if (mode == 0) E->ids_out[base + incl - 1] = x;
-                else E->cpos[base + incl - 1] = (uint32_t)i;
-            }
-            base += tot;
+            uint32_t pre = 0;
+            for (uint32_t k = 0; k < w; k++) pre += ws[k];
+            uint32_t o = base + pre + incl - c;
+            const uint32_t x4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (x4[q] != HOLE) out[o++] = mode == 0 ? x4[q] : (uint32_t)(p + q);
+            base += ws[0] + ws[1] + ws[2] + ws[3];
             __syncthreads();
         }
     }
@@ -700,8 +956,6 @@ __global__ __launch_bounds__(256) void k_tile_write(const Eng *__restrict__ E, c
 // Runs on the token array of the NEXT counting phase (after k_apply), only
 // when that phase has n < 2^21 tokens.  Builds the (thread, pair) set with
 // counts and first positions and each thread's distinct count D_t.
-__device__ inline bool tracking_on(const Ctl *C) { return C->n_live - C->R < TRACK_LIMIT; }
-
 __global__ void k_stat_clear(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (C->stop || !tracking_on(C)) return;
     const uint64_t n = C->n_live - C->R;
@@ -713,74 +967,6 @@ __global__ void k_stat_clear(const Eng *__restrict__ E, Ctl *__restrict__ C) {
         E->sfirst[s] = 0xFFFFFFFFu;
     }
     if (blockIdx.x == 0 && threadIdx.x < NTHR) C->Dt[threadIdx.x] = 0;
-}
-
-__global__ __launch_bounds__(256) void k_stat_count(const Eng *__restrict__ E, Ctl *__restrict__ C) {
-    if (C->stop || !tracking_on(C)) return;
-    const uint64_t n0 = E->n0;
-    for (uint64_t t = blockIdx.x; t < E->ntiles; t += gridDim.x) {
-        uint32_t c = 0;
-        for (uint64_t i = t * CTILE + threadIdx.x; i < min(n0, (t + 1) * CTILE); i += blockDim.x)
-            c += E->tok[i] != HOLE;
-        __shared__ uint32_t sh[256];
-        sh[threadIdx.x] = c;
-        __syncthreads();
-        for (uint32_t w = 128; w > 0; w >>= 1) {
-            if (threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) E->tilecnt[t] = sh[0];
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(1024) void k_stat_scan(const Eng *__restrict__ E, Ctl *__restrict__ C,
-                                                    uint32_t *__restrict__ tileoff) {
-    if (C->stop || !tracking_on(C)) return;
-    __shared__ uint32_t sh[1024];
-    uint32_t carry = 0;
-    const uint64_t n = E->ntiles;
-    for (uint64_t base = 0; base < n; base += 1024) {
-        const uint64_t i = base + threadIdx.x;
-        const uint32_t x = i < n ? E->tilecnt[i] : 0;
-        sh[threadIdx.x] = x;
-        __syncthreads();
-        for (uint32_t o = 1; o < 1024; o <<= 1) {
-            uint32_t y = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-            __syncthreads();
-            sh[threadIdx.x] += y;
-            __syncthreads();
-        }
-        if (i < n) tileoff[i] = carry + sh[threadIdx.x] - x;
-        const uint32_t tot = sh[1023];
-        __syncthreads();
-        carry += tot;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_stat_map(const Eng *__restrict__ E, Ctl *__restrict__ C,
-                                                  const uint32_t *__restrict__ tileoff) {
-    if (C->stop || !tracking_on(C)) return;
-    const uint64_t n0 = E->n0;
-    __shared__ uint32_t sh[256];
-    for (uint64_t t = blockIdx.x; t < E->ntiles; t += gridDim.x) {
-        uint32_t base = tileoff[t];
-        for (uint64_t c0 = t * CTILE; c0 < min(n0, (t + 1) * CTILE); c0 += 256) {
-            const uint64_t i = c0 + threadIdx.x;
-            const uint32_t f = i < n0 && E->tok[i] != HOLE;
-            sh[threadIdx.x] = f;
-            __syncthreads();
-            for (uint32_t o = 1; o < 256; o <<= 1) {
-                uint32_t y = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
-                __syncthreads();
-                sh[threadIdx.x] += y;
-                __syncthreads();
-            }
-            if (f) E->cpos[base + sh[threadIdx.x] - 1] = (uint32_t)i;
-            base += sh[255];
-            __syncthreads();
-        }
-    }
 }
 
 __device__ inline unsigned long long skey_of(uint32_t t, uint32_t u, uint32_t v) {
