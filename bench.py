@@ -16,8 +16,12 @@ independent replica on its own 1 GiB slice (weak scaling, no exchange);
 see DESIGN.md "Multi-GPU" for the sharded-exchange plan.
 
 The JSON line also carries
-  roofline     -- the corpus-wide pair-count kernel (k_pair_hist), timed with
-                  HIP events on the engine's stream inside the timed run;
+  roofline     -- the dominant kernel of the loop (k_scan), its average span
+                  from the device wall clock inside the timed run, corroborated
+                  by HIP event nodes in a second run; algorithmic bytes =
+                  8 B/candidate + 20 B/occurrence (DESIGN.md section 4);
+  roofline_count_pass -- the one corpus-wide streaming pass (k_pair_hist),
+                  timed with HIP events on the engine's stream;
   cpu_baseline -- the unmodified reference (oracle/_ref/bpe_ref, 16 threads)
                   timed on this host on a bounded sample (rank 0, N=1 only).
 """
@@ -115,13 +119,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = e.stats()
-    name, kms, kbytes, launches = e.kernel_profile()
+    name, kms, kbytes, launches = e.kernel_profile()  # live, in-kernel wall clock
+    # corroboration with HIP events: event-record nodes spliced around every
+    # k_scan node of a second, shorter run (they add latency, so not in the timed run)
+    e.set_profile(True)
+    e.train(min(args.steps, 256))
+    ev_ms, ev_n = e.event_profile()
+    e.set_profile(False)
 
     if rank != 0:
         return
     corpus_mb = args.size / 1e6
     value = world * corpus_mb * k / elapsed
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    cp_ms = st["ms_count_pass"]
+    cp_achieved = args.size / (cp_ms * 1e-3) / 1e9 if cp_ms > 0 else 0.0
     out = {
         "metric": "corpus MB/s per merge iter (train), 1 GiB synthetic corpus per GPU",
         "value": round(value, 1),
@@ -138,15 +150,38 @@ def main():
         "config": {"workload": "configs[3]: 1 GiB corpus/GPU, %d merges" % args.steps,
                    "corpus_bytes_per_gpu": args.size, "merges": k,
                    "parallelism": "replicas (independent per-GPU corpora)" if world > 1 else "single GPU"},
+        # dominant kernel of the timed run: k_scan (latency-bound random gathers);
+        # algorithmic bytes per launch = 8 B/candidate + 20 B/occurrence
         "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "bytes_per_launch": kbytes, "avg_ms": round(kms, 4), "launches": launches},
+                     "bytes_per_launch": round(kbytes), "avg_ms": round(kms, 5), "launches": launches,
+                     "avg_ms_source": "device wall clock inside the timed run (block-0 entry to last block exit)",
+                     "avg_ms_hip_events": round(ev_ms, 5), "hip_event_launches": ev_n,
+                     "note": "per-merge kernel is bound by dependent-load latency, not bandwidth; "
+                             "event nodes add their own latency to the measured span"},
+        # the one corpus-wide streaming pass (pair count over 1 B/token, V = 256)
+        "roofline_count_pass": {"kernel": "k_pair_hist", "bound": "hbm", "achieved": round(cp_achieved, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(cp_achieved / HBM_PEAK_GBS, 4),
+                                "bytes_per_launch": args.size, "avg_ms": round(cp_ms, 4)},
         "breakdown_ms": {"init": round(st["ms_init"], 3), "loop": round(st["ms_train"], 3),
                          "total_engine": round(st["ms_total"], 3)},
         "engine": {k2: st[k2] for k2 in ("n_out", "iterations", "distinct_pairs", "merged_buckets",
                                           "tracked_iters", "tie_events", "edge_events", "rule_ties",
                                           "table_grows", "keys")},
     }
+    # HBM traffic per launch from the committed rocprofv3 PMC passes
+    # (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE in separate runs)
+    pmc = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            tr = json.load(f)
+        if name in tr:
+            out["roofline"]["traffic"] = tr[name]["traffic_bytes_per_launch"]
+            out["roofline"]["traffic_source"] = ("profiles/r1_pmc_traffic.json (FETCH_SIZE raw, uncalibrated for "
+                                                 "4-byte gathers, + WRITE_SIZE; 256-merge run)")
+        if "k_pair_hist" in tr:
+            out["roofline_count_pass"]["traffic"] = tr["k_pair_hist"]["traffic_bytes_per_launch"]
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.cpu_size, args.cpu_merges)
     print(json.dumps(out), flush=True)

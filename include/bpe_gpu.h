@@ -58,6 +58,7 @@ typedef struct {
     double ms_init;           /* device-side setup (counting sort, table)      */
     double ms_train;          /* merge loop                                    */
     double ms_total;          /* init + loop (what bench.py times end to end)  */
+    double ms_count_pass;     /* the one corpus-wide pair-count pass (k_pair_hist) */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */
@@ -100,11 +101,21 @@ int bpe_gpu_get_stats(bpe_gpu_ctx *ctx, bpe_gpu_stats *st);
 /* device pointer of the loaded corpus bytes / ids (for in-HBM benchmarking) */
 int bpe_gpu_device_tokens(bpe_gpu_ctx *ctx, const void **dev_tok, size_t *n);
 
-/* Average duration (ms) of the engine's dominant kernel over the last train
- * or encode call, measured with HIP events on the engine's stream, and the
- * algorithmic bytes it moved (for bench.py's roofline object). */
+/* Record HIP events around every k_scan node of the iteration graphs (the
+ * dominant kernel of the merge loop) during the next train() calls. */
+int bpe_gpu_set_profile(bpe_gpu_ctx *ctx, int on);
+
+/* Average duration (ms) of the engine's dominant kernel (k_scan) over the
+ * last train call, measured live with the device wall clock (block 0 entry to
+ * the last block's exit; no effect on the run), and its algorithmic bytes per
+ * launch (bench.py's roofline object). */
 int bpe_gpu_kernel_profile(bpe_gpu_ctx *ctx, const char **name, double *avg_ms,
                            double *bytes_per_launch, uint64_t *launches);
+
+/* Average k_scan duration from HIP event-record nodes spliced around every
+ * k_scan node of the iteration graphs (only when bpe_gpu_set_profile(1) was
+ * set for the last train call; the event nodes slow the loop down). */
+int bpe_gpu_event_profile(bpe_gpu_ctx *ctx, double *avg_ms, uint64_t *launches);
 
 const char *bpe_gpu_strerror(int code);
 const char *bpe_gpu_last_error(void);

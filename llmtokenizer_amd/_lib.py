@@ -23,7 +23,8 @@ EXPORTS = [
     # bpe_gpu.h
     "bpe_gpu_device_count", "bpe_gpu_create", "bpe_gpu_destroy", "bpe_gpu_load", "bpe_gpu_synth",
     "bpe_gpu_train", "bpe_gpu_fetch_merges", "bpe_gpu_fetch_ids", "bpe_gpu_encode", "bpe_gpu_decode",
-    "bpe_gpu_get_stats", "bpe_gpu_device_tokens", "bpe_gpu_kernel_profile", "bpe_gpu_strerror",
+    "bpe_gpu_get_stats", "bpe_gpu_device_tokens", "bpe_gpu_kernel_profile", "bpe_gpu_set_profile", "bpe_gpu_event_profile",
+    "bpe_gpu_strerror",
     "bpe_gpu_last_error",
 ]
 
@@ -32,7 +33,7 @@ class GpuStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "n_in", "n_out", "merges", "iterations", "distinct_pairs", "merged_buckets",
         "tracked_iters", "tie_events", "edge_events", "rule_ties", "table_grows", "keys")] + \
-        [(n, ctypes.c_double) for n in ("ms_init", "ms_train", "ms_total")]
+        [(n, ctypes.c_double) for n in ("ms_init", "ms_train", "ms_total", "ms_count_pass")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -72,6 +73,8 @@ def load():
     L.bpe_gpu_encode.argtypes = [vp, vp, sz]
     L.bpe_gpu_decode.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats)]
+    L.bpe_gpu_set_profile.argtypes = [vp, ctypes.c_int]
+    L.bpe_gpu_event_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
     L.bpe_gpu_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
     L.bpe_gpu_kernel_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]

@@ -219,6 +219,15 @@ class Engine:
         _lib.check(self.L.bpe_gpu_get_stats(self.ctx, ctypes.byref(st)), "stats")
         return st.as_dict()
 
+    def set_profile(self, on=True):
+        _lib.check(self.L.bpe_gpu_set_profile(self.ctx, 1 if on else 0), "set_profile")
+
+    def event_profile(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        _lib.check(self.L.bpe_gpu_event_profile(self.ctx, ctypes.byref(ms), ctypes.byref(n)), "event_profile")
+        return ms.value, n.value
+
     def kernel_profile(self):
         name = ctypes.c_char_p()
         ms = ctypes.c_double()

@@ -49,7 +49,7 @@ double now_ms() {
 }
 
 constexpr uint32_t ITERS_PER_GRAPH = 16;
-constexpr uint32_t SCAN_BLOCKS = 1024;
+constexpr uint32_t SCAN_BLOCKS = 1024;  // == k_select's block size (it reduces the exit stamps)
 constexpr uint32_t APPLY_A = 256, APPLY_B = 64;
 constexpr uint32_t RESCAN1_BLOCKS = 1024, RESCAN2_BLOCKS = 128;
 
@@ -183,7 +183,12 @@ struct bpe_gpu_ctx {
     uint32_t *d_enc_pairs = nullptr;
     hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr;
     bpe_gpu_stats stats{};
-    // profile of the dominant kernel
+    // profile of the dominant kernel: HIP events captured around every k_scan
+    // node of the iteration graphs (bpe_gpu_set_profile)
+    bool profile = false;
+    hipEvent_t ev[2][ITERS_PER_GRAPH][2] = {};  // [graph tracked?][iteration][start/end]
+    double scan_ms = 0, event_ms = 0;
+    uint64_t scan_n = 0, event_n = 0;
     std::string prof_name;
     double prof_ms = 0, prof_bytes = 0;
     uint64_t prof_launches = 0;
@@ -283,6 +288,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         if ((r = dalloc(c, &h.vnl[p], 4))) return r;
     }
     if ((r = dalloc(c, &h.vecd, encode ? 1 : (size_t)REPL * 4 * DENSE))) return r;
+    if ((r = dalloc(c, &h.scan_tend, SCAN_BLOCKS))) return r;
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
     if ((r = dalloc(c, &c->d_tileoff, h.ntiles + 1))) return r;
@@ -398,8 +404,63 @@ void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
     k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? 1u : 0u);
 }
 
+// Splice event-record nodes around every k_scan node of a captured (linear)
+// iteration graph.  ROCm 7.2: events recorded on a capturing stream do not
+// give elapsed times, explicitly added event-record nodes do.
+int add_scan_events(bpe_gpu_ctx *c, hipGraph_t g, bool tracked) {
+    size_t n = 0;
+    HIPCHK(hipGraphGetNodes(g, nullptr, &n));
+    std::vector<hipGraphNode_t> nodes(n);
+    HIPCHK(hipGraphGetNodes(g, nodes.data(), &n));
+    // walk the chain from its root
+    hipGraphNode_t cur = nullptr;
+    for (auto nd : nodes) {
+        size_t np = 0;
+        HIPCHK(hipGraphNodeGetDependencies(nd, nullptr, &np));
+        if (np == 0) { cur = nd; break; }
+    }
+    uint32_t k = 0;
+    while (cur && k < ITERS_PER_GRAPH) {
+        size_t ns = 0;
+        HIPCHK(hipGraphNodeGetDependentNodes(cur, nullptr, &ns));
+        hipGraphNode_t next = nullptr;
+        if (ns == 1) HIPCHK(hipGraphNodeGetDependentNodes(cur, &next, &ns));
+        hipGraphNodeType ty;
+        HIPCHK(hipGraphNodeGetType(cur, &ty));
+        if (ty == hipGraphNodeTypeKernel) {
+            hipKernelNodeParams kp{};
+            HIPCHK(hipGraphKernelNodeGetParams(cur, &kp));
+            if (kp.func == (void *)k_scan) {
+                size_t np = 0;
+                hipGraphNode_t pred = nullptr;
+                HIPCHK(hipGraphNodeGetDependencies(cur, nullptr, &np));
+                if (np == 1) HIPCHK(hipGraphNodeGetDependencies(cur, &pred, &np));
+                hipGraphNode_t e0, e1;
+                if (pred) {
+                    HIPCHK(hipGraphRemoveDependencies(g, &pred, &cur, 1));
+                    HIPCHK(hipGraphAddEventRecordNode(&e0, g, &pred, 1, c->ev[tracked][k][0]));
+                } else {
+                    HIPCHK(hipGraphAddEventRecordNode(&e0, g, nullptr, 0, c->ev[tracked][k][0]));
+                }
+                HIPCHK(hipGraphAddDependencies(g, &e0, &cur, 1));
+                if (next) HIPCHK(hipGraphRemoveDependencies(g, &cur, &next, 1));
+                HIPCHK(hipGraphAddEventRecordNode(&e1, g, &cur, 1, c->ev[tracked][k][1]));
+                if (next) HIPCHK(hipGraphAddDependencies(g, &e1, &next, 1));
+                k++;
+            }
+        }
+        cur = next;
+    }
+    return 0;
+}
+
 int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint32_t n_enc = 0) {
     hipGraph_t g;
+    const bool prof = c->profile && !encode;
+    if (prof)
+        for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++)
+            for (int q = 0; q < 2; q++)
+                if (!c->ev[tracked][k][q]) HIPCHK(hipEventCreate(&c->ev[tracked][k][q]));
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
     for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++) {
         if (encode) {
@@ -411,6 +472,8 @@ int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint
         }
     }
     HIPCHK(hipStreamEndCapture(c->st, &g));
+    int r;
+    if (prof && (r = add_scan_events(c, g, tracked))) return r;
     HIPCHK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(g));
     return 0;
@@ -658,9 +721,26 @@ struct Resolver {
 int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
     int r;
     Resolver res{c};
+    int last_graph = -1;             // graph replayed last (0 plain, 1 tracked)
+    uint64_t iters_before = 0;
     for (;;) {
         if ((r = pull_ctl(c))) return r;
         Ctl &C = *c->hC;
+        if (last_graph >= 0 && c->profile) {
+            // iterations of the last replay that did real work (the rest early-exited)
+            const uint64_t done = std::min<uint64_t>(C.counters[0] - iters_before, ITERS_PER_GRAPH);
+            for (uint64_t k = 0; k < done; k++) {
+                float ms = 0;
+                if (hipEventElapsedTime(&ms, c->ev[last_graph][k][0], c->ev[last_graph][k][1]) == hipSuccess) {
+                    c->scan_ms += ms;
+                    c->scan_n++;
+                } else {
+                    (void)hipGetLastError();  // do not leave a sticky error behind
+                }
+            }
+        }
+        last_graph = -1;
+        iters_before = C.counters[0];
         switch (C.stop) {
         case STOP_NONE: {
             hipGraphExec_t *g;
@@ -670,6 +750,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
                 const bool tracked = C.n_live < TRACK_LIMIT;
                 g = tracked ? &c->g_tracked : &c->g_plain;
                 if (!*g && (r = capture(c, g, tracked, false))) return r;
+                last_graph = tracked ? 1 : 0;
             }
             HIPCHK(hipGraphLaunch(*g, c->st));
             break;
@@ -769,6 +850,7 @@ int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_
         hipEventDestroy(e0);
         hipEventDestroy(e1);
         c->prof_name = "k_pair_hist";
+        c->stats.ms_count_pass = ms;
         c->prof_ms = ms;
         c->prof_bytes = (double)c->n0 * parts;  // 1 B/token (V = 256), re-read once per bin part
         c->prof_launches = 1;
@@ -844,7 +926,11 @@ void bpe_gpu_destroy(bpe_gpu_ctx *c) {
     if (c->dC) hipFree(c->dC);
     if (c->hC) hipHostFree(c->hC);
     if (c->d_enc_pairs) hipFree(c->d_enc_pairs);
-    if (c->st) hipStreamDestroy(c->st);
+    for (auto &a : c->ev)
+        for (auto &b : a)
+            for (auto &e : b)
+                if (e) (void)hipEventDestroy(e);
+    if (c->st) (void)hipStreamDestroy(c->st);
     delete c;
 }
 
@@ -886,6 +972,8 @@ int bpe_gpu_train(bpe_gpu_ctx *c, long max_merges, size_t *n_merges) {
     HIPCHK(hipSetDevice(c->dev));
     c->stats = bpe_gpu_stats{};
     c->stats.n_in = c->n0;
+    c->scan_ms = 0;
+    c->scan_n = 0;
     *n_merges = 0;
     c->merges_done = 0;
     if (c->n0 < 2) return fail(BPE_GPU_EINVAL, "fewer than 2 tokens");
@@ -931,6 +1019,19 @@ int bpe_gpu_train(bpe_gpu_ctx *c, long max_merges, size_t *n_merges) {
     c->stats.ms_init = t1 - t0;
     c->stats.ms_train = t2 - t1;
     c->stats.ms_total = t2 - t0;
+    // k_scan touches, per candidate, its 4-byte position and the token word it
+    // validates; per replaced occurrence the partner, both neighbours and the
+    // occurrence-list entry: 8 B + 20 B
+    if (C.scan_launches) {
+        int khz = 0;
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
+        c->prof_name = "k_scan";
+        c->prof_ms = khz > 0 ? (double)C.scan_ticks / C.scan_launches / khz : 0;
+        c->prof_bytes = (8.0 * C.counters[4] + 20.0 * C.counters[5]) / std::max<double>(1.0, C.counters[0]);
+        c->prof_launches = C.scan_launches;
+    }
+    c->event_ms = c->scan_n ? c->scan_ms / c->scan_n : 0;
+    c->event_n = c->scan_n;
     return 0;
 }
 
@@ -1073,6 +1174,25 @@ int bpe_gpu_decode(bpe_gpu_ctx *c, const uint32_t *ids, size_t len, const uint32
     hipFree(d_elen);
     hipFree(d_off);
     hipFree(d_out);
+    return 0;
+}
+
+int bpe_gpu_set_profile(bpe_gpu_ctx *c, int on) {
+    if (!c) return BPE_GPU_EINVAL;
+    if (c->profile != (on != 0)) {
+        for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked}) {
+            if (*g) (void)hipGraphExecDestroy(*g);
+            *g = nullptr;
+        }
+    }
+    c->profile = on != 0;
+    return 0;
+}
+
+int bpe_gpu_event_profile(bpe_gpu_ctx *c, double *avg_ms, uint64_t *launches) {
+    if (!c || !avg_ms || !launches) return BPE_GPU_EINVAL;
+    *avg_ms = c->event_ms;
+    *launches = c->event_n;
     return 0;
 }
 

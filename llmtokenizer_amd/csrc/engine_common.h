@@ -82,6 +82,7 @@ struct Eng {
     uint64_t ntiles;
     uint32_t *ids_out;    // compaction output
     uint32_t *aux;        // per-slot scratch for the resolver (first thread)
+    unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
 };
 
 struct Ctl {
@@ -102,7 +103,11 @@ struct Ctl {
     uint32_t follows[NTHR];
     uint32_t last_c[NTHR];            // last pair position (compacted) per thread
     unsigned long long stat_n;        // n of the tracked iteration
-    unsigned long long counters[8];   // 0 iterations, 1 tracked, 2 rule ties, 3 events
+    unsigned long long counters[8];   // 0 iterations, 1 tracked, 2 rule ties, 3 events,
+                                      // 4 candidates scanned, 5 occurrences replaced
+    unsigned long long scan_t0;       // wall clock at k_scan block 0 entry
+    unsigned long long scan_ticks;    // sum over merges of k_scan spans (wall-clock ticks)
+    unsigned long long scan_launches;
 };
 
 __host__ __device__ inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }

@@ -84,10 +84,20 @@ __device__ inline void flush_list(uint32_t *list, uint32_t *lcount, uint32_t *gb
     __syncthreads();
 }
 
+// in-kernel timing (bench.py's roofline): block 0 stamps the entry, every
+// block stamps its exit; k_select folds max(exit) - entry into Ctl
+__device__ inline void scan_exit_stamp(const Eng *E) {
+    if (threadIdx.x == 0) E->scan_tend[blockIdx.x] = wall_clock64();
+}
+
 __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) C->scan_t0 = wall_clock64();
     if (C->stop) return;
     const uint32_t len = C->cand_len;
-    if (blockIdx.x * SCAN_T >= len) return;  // block-uniform
+    if (blockIdx.x * SCAN_T >= len) {  // block-uniform
+        scan_exit_stamp(E);
+        return;
+    }
     const uint32_t a = C->a, b = C->b, z = C->z;
     const uint32_t mode = C->cand_mode, off = C->cand_off;
     const uint32_t P = C->parity;
@@ -185,13 +195,16 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
         }
         flush_list(list, &lcount, &gbase, &C->R, occz);
     }
-    if (!count) return;
-    // flush into replica (block % REPL): ~REPL x fewer same-address atomics
-    uint32_t *rep = E->vecd + (uint64_t)(blockIdx.x % REPL) * 4 * DENSE;
-    for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) {
-        const uint32_t c = (&s[0][0])[x];
-        if (c) atomicAdd(&rep[x], c);  // result unused: no-return atomic
+    if (count) {
+        // flush into replica (block % REPL): ~REPL x fewer same-address atomics
+        uint32_t *rep = E->vecd + (uint64_t)(blockIdx.x % REPL) * 4 * DENSE;
+        for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) {
+            const uint32_t c = (&s[0][0])[x];
+            if (c) atomicAdd(&rep[x], c);  // result unused: no-return atomic
+        }
+        __syncthreads();
     }
+    scan_exit_stamp(E);
 }
 
 // --------------------------------------------------------------- pair table
@@ -505,6 +518,8 @@ __device__ inline void commit_merge(const Eng *E, Ctl *C, uint32_t u, uint32_t v
 __device__ inline void finish_iteration(const Eng *E, Ctl *C) {
     if (!C->pending) return;
     C->pending = 0;
+    C->counters[4] += C->cand_len;  // candidates examined by k_scan (profiling)
+    C->counters[5] += C->R;         // occurrences replaced
     C->occ_top += C->R;
     C->n_live -= C->R;
     C->R = 0;
@@ -529,12 +544,26 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
             if (E->l2best[i]) mine = best_merge(mine, Best{E->l2best[i], E->l2tie[i], E->l2key[i]});
     }
     mine = wave_best(mine);
+    // k_scan's last block exit (blockDim == SCAN_BLOCKS == 1024 stamps)
+    unsigned long long tend = E->scan_tend[threadIdx.x];
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(tend, o);
+        tend = y > tend ? y : tend;
+    }
     __shared__ Best sw[16];
-    if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = mine;
+    __shared__ unsigned long long st[16];
+    if ((threadIdx.x & 63) == 0) { sw[threadIdx.x >> 6] = mine; st[threadIdx.x >> 6] = tend; }
     __syncthreads();
     if (threadIdx.x != 0) return;
     Best r = sw[0];
     for (uint32_t k = 1; k < blockDim.x / 64; k++) r = best_merge(r, sw[k]);
+    if (C->pending) {  // a merge ran: account its k_scan span
+        for (uint32_t k = 0; k < blockDim.x / 64; k++) tend = st[k] > tend ? st[k] : tend;
+        if (tend > C->scan_t0) {
+            C->scan_ticks += tend - C->scan_t0;
+            C->scan_launches++;
+        }
+    }
     finish_iteration(E, C);
     if (!tracked_graph && C->n_live < TRACK_LIMIT) { C->stop = STOP_MODE; return; }
     const uint64_t D = C->D;
