@@ -80,6 +80,14 @@ int bpe_gpu_synth(bpe_gpu_ctx *ctx, uint64_t seed, size_t n, uint64_t offset);
  * max_merges (< 0 = unbounded).  *n_merges receives the merge count. */
 int bpe_gpu_train(bpe_gpu_ctx *ctx, long max_merges, size_t *n_merges);
 
+/* Train flags.  BPE_GPU_FAST: decide every tie by the schedule-free rule
+ * (smallest (a, b) among the keys with the maximal count and bucket) instead
+ * of emulating the reference's static 16-thread schedule below 2^20 tokens.
+ * For corpora of >= 2^20 tokens both are the same (the reference itself is
+ * schedule-dependent there); sharded training always uses it. */
+enum { BPE_GPU_FAST = 1 };
+int bpe_gpu_train_ex(bpe_gpu_ctx *ctx, long max_merges, unsigned flags, size_t *n_merges);
+
 /* merges as (a, b) pairs, ids 256.. in order; cap in pairs */
 int bpe_gpu_fetch_merges(bpe_gpu_ctx *ctx, uint32_t *pairs, size_t cap, size_t *count);
 
@@ -116,6 +124,42 @@ int bpe_gpu_kernel_profile(bpe_gpu_ctx *ctx, const char **name, double *avg_ms,
  * k_scan node of the iteration graphs (only when bpe_gpu_set_profile(1) was
  * set for the last train call; the event nodes slow the loop down). */
 int bpe_gpu_event_profile(bpe_gpu_ctx *ctx, double *avg_ms, uint64_t *launches);
+
+/* ------------------------------------------------------------------------
+ * Sharded training.  The corpus is cut into contiguous
+ * shards in order; shard s holds bytes [off_s, off_s + n_s).  Every shard
+ * keeps the replicated pair-count table; per merge the shards allreduce the
+ * count deltas and allgather 16-word edge records (pairs across an edge
+ * belong to the left shard).  Merges are identical on every shard; the
+ * global ids are the concatenation of the shards' ids.
+ *
+ * Two kinds of group:
+ *   comm_id == NULL: `local_shards` shards on one device (nranks must be 1);
+ *   comm_id != NULL: one shard per rank, ranks exchange over RCCL (xGMI);
+ *                    comm_id = the 128-byte id rank 0 got from
+ *                    bpe_gpu_comm_id(), passed to every rank.
+ * ---------------------------------------------------------------------- */
+typedef struct bpe_gpu_group bpe_gpu_group;
+
+int bpe_gpu_comm_id(uint8_t *id, size_t cap);
+int bpe_gpu_group_create(int device, int local_shards, int nranks, int rank, const uint8_t *comm_id,
+                         bpe_gpu_group **out);
+void bpe_gpu_group_destroy(bpe_gpu_group *g);
+int bpe_gpu_group_shards(bpe_gpu_group *g, int *local_shards, int *nshards, int *first_shard);
+/* shard k (local index) of the group */
+int bpe_gpu_group_load(bpe_gpu_group *g, int k, const uint8_t *bytes, size_t n);
+int bpe_gpu_group_synth(bpe_gpu_group *g, int k, uint64_t seed, size_t n, uint64_t offset);
+int bpe_gpu_group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges);
+int bpe_gpu_group_fetch_merges(bpe_gpu_group *g, uint32_t *pairs, size_t cap, size_t *count);
+int bpe_gpu_group_fetch_ids(bpe_gpu_group *g, int k, uint32_t *ids, size_t cap, size_t *len);
+int bpe_gpu_group_get_stats(bpe_gpu_group *g, bpe_gpu_stats *st);
+/* 1 when the per-merge exchange runs inside captured HIP graphs */
+int bpe_gpu_group_exchange_mode(bpe_gpu_group *g, int *graph_captured);
+
+/* The halo shard `me` derives from all edge records for a merge (a, b):
+ * out8 = {HL[0..2], HR[0..2], hlrun, myidx} (pure function, no GPU; exported
+ * for the host-side protocol tests). */
+int bpe_gpu_shard_halo(const uint32_t *records, uint32_t nshards, uint32_t me, uint32_t a, uint32_t *out8);
 
 const char *bpe_gpu_strerror(int code);
 const char *bpe_gpu_last_error(void);

@@ -25,7 +25,11 @@ EXPORTS = [
     "bpe_gpu_train", "bpe_gpu_fetch_merges", "bpe_gpu_fetch_ids", "bpe_gpu_encode", "bpe_gpu_decode",
     "bpe_gpu_get_stats", "bpe_gpu_device_tokens", "bpe_gpu_kernel_profile", "bpe_gpu_set_profile", "bpe_gpu_event_profile",
     "bpe_gpu_strerror",
-    "bpe_gpu_last_error",
+    "bpe_gpu_last_error", "bpe_gpu_train_ex",
+    # bpe_gpu.h: sharded training
+    "bpe_gpu_comm_id", "bpe_gpu_group_create", "bpe_gpu_group_destroy", "bpe_gpu_group_shards",
+    "bpe_gpu_group_load", "bpe_gpu_group_synth", "bpe_gpu_group_train", "bpe_gpu_group_fetch_merges",
+    "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo",
 ]
 
 
@@ -68,6 +72,21 @@ def load():
     L.bpe_gpu_load.argtypes = [vp, vp, sz]
     L.bpe_gpu_synth.argtypes = [vp, ctypes.c_uint64, sz, ctypes.c_uint64]
     L.bpe_gpu_train.argtypes = [vp, ctypes.c_long, ctypes.POINTER(sz)]
+    L.bpe_gpu_train_ex.argtypes = [vp, ctypes.c_long, ctypes.c_uint, ctypes.POINTER(sz)]
+    ip = ctypes.POINTER(ctypes.c_int)
+    L.bpe_gpu_comm_id.argtypes = [vp, sz]
+    L.bpe_gpu_group_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
+    L.bpe_gpu_group_destroy.argtypes = [vp]
+    L.bpe_gpu_group_destroy.restype = None
+    L.bpe_gpu_group_shards.argtypes = [vp, ip, ip, ip]
+    L.bpe_gpu_group_load.argtypes = [vp, ctypes.c_int, vp, sz]
+    L.bpe_gpu_group_synth.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, sz, ctypes.c_uint64]
+    L.bpe_gpu_group_train.argtypes = [vp, ctypes.c_long, ctypes.POINTER(sz)]
+    L.bpe_gpu_group_fetch_merges.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    L.bpe_gpu_group_fetch_ids.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.POINTER(sz)]
+    L.bpe_gpu_group_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats)]
+    L.bpe_gpu_group_exchange_mode.argtypes = [vp, ip]
+    L.bpe_gpu_shard_halo.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp]
     L.bpe_gpu_fetch_merges.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_fetch_ids.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_encode.argtypes = [vp, vp, sz]

@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 from . import _lib
-from ._lib import BpeError, GpuStats
+from ._lib import BpeError, GpuStats  # noqa: F401
 
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 
@@ -176,9 +176,10 @@ class Engine:
     def synth(self, seed, n, offset=0):
         _lib.check(self.L.bpe_gpu_synth(self.ctx, int(seed), int(n), int(offset)), "synth")
 
-    def train(self, max_merges=-1):
+    def train(self, max_merges=-1, fast=False):
+        """fast=True: schedule-free tie rule everywhere (bpe_gpu.h BPE_GPU_FAST)"""
         k = ctypes.c_size_t(0)
-        _lib.check(self.L.bpe_gpu_train(self.ctx, int(max_merges), ctypes.byref(k)), "train")
+        _lib.check(self.L.bpe_gpu_train_ex(self.ctx, int(max_merges), 1 if fast else 0, ctypes.byref(k)), "train")
         return k.value
 
     def encode(self, merges):
@@ -236,6 +237,103 @@ class Engine:
         _lib.check(self.L.bpe_gpu_kernel_profile(self.ctx, ctypes.byref(name), ctypes.byref(ms), ctypes.byref(by),
                                                  ctypes.byref(n)), "kernel_profile")
         return (name.value or b"").decode(), ms.value, by.value, n.value
+
+
+class ShardGroup:
+    """Corpus-sharded training (bpe_gpu.h group API).
+
+    ShardGroup(device, local_shards=K)           K shards on one device
+    ShardGroup(device, nranks=N, rank=r, comm_id=id)  one shard per rank, RCCL
+    Shards hold contiguous slices of the corpus in order; merges are the same
+    on every shard and the corpus ids are the shards' ids concatenated."""
+
+    def __init__(self, device=0, local_shards=1, nranks=1, rank=0, comm_id=None):
+        self.L = _lib.load()
+        self.g = ctypes.c_void_p()
+        cid = None
+        if comm_id is not None:
+            cid = ctypes.create_string_buffer(bytes(comm_id), len(comm_id))
+        _lib.check(self.L.bpe_gpu_group_create(int(device), int(local_shards), int(nranks), int(rank),
+                                               cid, ctypes.byref(self.g)), "group_create")
+        k, n, f = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.L.bpe_gpu_group_shards(self.g, ctypes.byref(k), ctypes.byref(n), ctypes.byref(f)), "shards")
+        self.local_shards, self.nshards, self.first_shard = k.value, n.value, f.value
+
+    def close(self):
+        if self.g:
+            self.L.bpe_gpu_group_destroy(self.g)
+            self.g = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, k, data: bytes):
+        buf = np.frombuffer(data, dtype=np.uint8)
+        _lib.check(self.L.bpe_gpu_group_load(self.g, int(k), buf.ctypes.data_as(ctypes.c_void_p), buf.size), "load")
+
+    def load_split(self, data: bytes, cuts):
+        """local mode: shard k gets data[cuts[k]:cuts[k+1]]"""
+        for k in range(self.local_shards):
+            self.load(k, data[cuts[k]:cuts[k + 1]])
+
+    def synth(self, k, seed, n, offset=0):
+        _lib.check(self.L.bpe_gpu_group_synth(self.g, int(k), int(seed), int(n), int(offset)), "synth")
+
+    def train(self, max_merges=-1):
+        m = ctypes.c_size_t(0)
+        _lib.check(self.L.bpe_gpu_group_train(self.g, int(max_merges), ctypes.byref(m)), "group_train")
+        return m.value
+
+    def merges(self):
+        cnt = ctypes.c_size_t(0)
+        _lib.check(self.L.bpe_gpu_group_fetch_merges(self.g, None, 0, ctypes.byref(cnt)), "fetch_merges")
+        out = np.zeros(2 * max(cnt.value, 1), dtype=np.uint32)
+        _lib.check(self.L.bpe_gpu_group_fetch_merges(self.g, out.ctypes.data_as(ctypes.c_void_p), cnt.value,
+                                                     ctypes.byref(cnt)), "fetch_merges")
+        return out[: 2 * cnt.value].reshape(-1, 2)
+
+    def ids(self, k):
+        n = ctypes.c_size_t(0)
+        _lib.check(self.L.bpe_gpu_group_fetch_ids(self.g, int(k), None, 0, ctypes.byref(n)), "fetch_ids")
+        out = np.zeros(max(n.value, 1), dtype=np.uint32)
+        _lib.check(self.L.bpe_gpu_group_fetch_ids(self.g, int(k), out.ctypes.data_as(ctypes.c_void_p), n.value,
+                                                  ctypes.byref(n)), "fetch_ids")
+        return out[: n.value]
+
+    def all_ids(self):
+        return np.concatenate([self.ids(k) for k in range(self.local_shards)])
+
+    def stats(self):
+        st = GpuStats()
+        _lib.check(self.L.bpe_gpu_group_get_stats(self.g, ctypes.byref(st)), "stats")
+        return st.as_dict()
+
+    def graph_captured(self):
+        v = ctypes.c_int()
+        _lib.check(self.L.bpe_gpu_group_exchange_mode(self.g, ctypes.byref(v)), "exchange_mode")
+        return bool(v.value)
+
+
+def comm_id():
+    """RCCL unique id (rank 0), to be passed to every rank's ShardGroup"""
+    L = _lib.load()
+    buf = ctypes.create_string_buffer(128)
+    _lib.check(L.bpe_gpu_comm_id(buf, 128), "comm_id")
+    return buf.raw
+
+
+def shard_halo(records, me, a):
+    """halo of shard `me` from the (nshards, 16) uint32 edge records (pure host function)"""
+    L = _lib.load()
+    rec = np.ascontiguousarray(records, dtype=np.uint32).reshape(-1, 16)
+    out = np.zeros(8, dtype=np.uint32)
+    _lib.check(L.bpe_gpu_shard_halo(rec.ctypes.data_as(ctypes.c_void_p), rec.shape[0], int(me), int(a),
+                                    out.ctypes.data_as(ctypes.c_void_p)), "shard_halo")
+    return {"HL": [int(x) for x in out[0:3]], "HR": [int(x) for x in out[3:6]], "hlrun": int(out[6]),
+            "myidx": int(out[7])}
 
 
 def device_count():

@@ -168,6 +168,10 @@ __global__ void k_res_pass(const Eng *E, const Ctl *C, const Query *qs, uint32_t
 struct bpe_gpu_ctx {
     int dev = 0;
     hipStream_t st = nullptr;
+    bool own_stream = true;
+    // run configuration (set before setup_run)
+    uint32_t fast = 0;                     // schedule-free tie rule everywhere
+    uint32_t sharded = 0, shard = 0, nshards = 1;
     Eng h{};
     Eng *dE = nullptr;
     Ctl *dC = nullptr;
@@ -269,6 +273,10 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.mcap = mcap;
     h.vcap = 256 + mcap;
     h.encode = encode ? 1 : 0;
+    h.fast = c->fast || c->sharded;
+    h.sharded = c->sharded;
+    h.shard = c->shard;
+    h.nshards = c->nshards;
     const uint64_t n0 = c->n0;
     int r;
     if ((r = dalloc(c, &h.tok, n0, false))) return r;
@@ -276,7 +284,16 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.tlen, h.vcap))) return r;
     if ((r = dalloc(c, &h.rank, 256))) return r;
     if ((r = dalloc(c, &h.plist, n0, false))) return r;
-    if ((r = dalloc(c, &h.occ, n0, false))) return r;
+    // occurrences: at most one per retired token start, plus (sharded) one
+    // crossing pair at the right edge per merge
+    if ((r = dalloc(c, &h.occ, n0 + (c->sharded ? (uint64_t)mcap + 64 : 0), false))) return r;
+    if (c->sharded) {
+        if ((r = dalloc(c, &h.xbuf, 4ull * h.vcap + 2))) return r;
+        if ((r = dalloc(c, &h.myrec, EDGE_WORDS))) return r;
+        if ((r = dalloc(c, &h.erec, (size_t)EDGE_WORDS * c->nshards))) return r;
+    } else {
+        h.xbuf = h.myrec = h.erec = nullptr;
+    }
     if ((r = dalloc(c, &h.occ_off, h.vcap))) return r;
     if ((r = dalloc(c, &h.occ_len, h.vcap))) return r;
     if ((r = dalloc(c, &h.merges, 2ull * std::max<uint32_t>(mcap, 1)))) return r;
@@ -323,6 +340,11 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     C.n_live = n0;
     for (uint32_t t = 0; t < NTHR; t++) C.Bcur[t] = THREAD_B0;
     C.full = 1;
+    for (int m = 0; m < 3; m++) C.HL[m] = C.HR[m] = HOLE;
+    C.F1 = 0;
+    C.L1 = n0 ? (uint32_t)(n0 - 1) : 0;
+    C.L1new = HOLE;
+    C.xleft = HOLE;
     if ((r = push_ctl(c))) return r;
     return push_desc(c);
 }
@@ -747,7 +769,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             if (encode) {
                 g = &c->g_encode;
             } else {
-                const bool tracked = C.n_live < TRACK_LIMIT;
+                const bool tracked = !c->h.fast && C.n_live < TRACK_LIMIT;
                 g = tracked ? &c->g_tracked : &c->g_plain;
                 if (!*g && (r = capture(c, g, tracked, false))) return r;
                 last_graph = tracked ? 1 : 0;
@@ -774,7 +796,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             C.full = 1;
             if ((r = push_ctl(c))) return r;
             if ((r = grow_table(c, c->h.hcap * 4))) return r;
-            const bool tracked = C.n_live < TRACK_LIMIT;
+            const bool tracked = !c->h.fast && C.n_live < TRACK_LIMIT;
             launch_summaries(c);
             k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? 1u : 0u);
             HIPCHK(hipGetLastError());
@@ -806,17 +828,21 @@ int compact_ids(bpe_gpu_ctx *c) {
     return 0;
 }
 
-// common init: tokens, byte ranks, counting sort of byte-pair positions
-int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_tot_out) {
-    Eng &h = c->h;
-    uint32_t *d_bh;
+// init phase 1: tok[] = bytes and the set of byte values present
+int init_presence(bpe_gpu_ctx *c, uint32_t **d_bh) {
     int r;
-    if ((r = dalloc(c, &d_bh, 256))) return r;
-    k_init_tok<<<1024, 256, 0, c->st>>>(c->dE, d_bh);
+    if ((r = dalloc(c, d_bh, 256))) return r;
+    k_init_tok<<<1024, 256, 0, c->st>>>(c->dE, *d_bh);
     HIPCHK(hipGetLastError());
-    std::vector<uint32_t> bh(256);
-    HIPCHK(hipMemcpyAsync(bh.data(), d_bh, 1024, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    return 0;
+}
+
+// init phase 2: byte ranks (from the presence vector `bh`, nonzero = present),
+// token lengths, counting sort of byte-pair positions by rank key
+int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint32_t> *unrank_out,
+              uint32_t **d_tot_out) {
+    Eng &h = c->h;
+    int r;
     std::vector<uint32_t> rank(256, HOLE), unrank;
     for (uint32_t x = 0; x < 256; x++)
         if (bh[x]) { rank[x] = (uint32_t)unrank.size(); unrank.push_back(x); }
@@ -869,6 +895,36 @@ int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_
     return 0;
 }
 
+// common init of a one-context run
+int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_tot_out) {
+    uint32_t *d_bh;
+    int r;
+    if ((r = init_presence(c, &d_bh))) return r;
+    std::vector<uint32_t> bh(256);
+    HIPCHK(hipMemcpyAsync(bh.data(), d_bh, 1024, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    return init_sort(c, bh, unrank_out, d_tot_out);
+}
+
+// a context on `device`; shared == nullptr creates its own stream
+int ctx_new(int device, hipStream_t shared, bpe_gpu_ctx **out) {
+    bpe_gpu_ctx *c = new bpe_gpu_ctx();
+    c->dev = device;
+    if (shared) {
+        c->st = shared;
+        c->own_stream = false;
+    } else {
+        hipError_t e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
+        if (e != hipSuccess) { delete c; return fail(BPE_GPU_EHIP, "hipStreamCreate", e); }
+    }
+    HIPCHK(hipMalloc(&c->dE, sizeof(Eng)));
+    HIPCHK(hipMalloc(&c->dC, sizeof(Ctl)));
+    HIPCHK(hipHostMalloc(&c->hC, sizeof(Ctl), hipHostMallocDefault));
+    memset(&c->h, 0, sizeof(Eng));
+    *out = c;
+    return 0;
+}
+
 }  // namespace
 
 // ===================================================================== C-ABI
@@ -906,15 +962,7 @@ int bpe_gpu_create(int device, bpe_gpu_ctx **out) {
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
         return fail(BPE_GPU_ENODEV, "no such device");
     HIPCHK(hipSetDevice(device));
-    bpe_gpu_ctx *c = new bpe_gpu_ctx();
-    c->dev = device;
-    HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking));
-    HIPCHK(hipMalloc(&c->dE, sizeof(Eng)));
-    HIPCHK(hipMalloc(&c->dC, sizeof(Ctl)));
-    HIPCHK(hipHostMalloc(&c->hC, sizeof(Ctl), hipHostMallocDefault));
-    memset(&c->h, 0, sizeof(Eng));
-    *out = c;
-    return 0;
+    return ctx_new(device, nullptr, out);
 }
 
 void bpe_gpu_destroy(bpe_gpu_ctx *c) {
@@ -930,7 +978,7 @@ void bpe_gpu_destroy(bpe_gpu_ctx *c) {
         for (auto &b : a)
             for (auto &e : b)
                 if (e) (void)hipEventDestroy(e);
-    if (c->st) (void)hipStreamDestroy(c->st);
+    if (c->st && c->own_stream) (void)hipStreamDestroy(c->st);
     delete c;
 }
 
@@ -967,9 +1015,18 @@ int bpe_gpu_synth(bpe_gpu_ctx *c, uint64_t seed, size_t n, uint64_t offset) {
 }
 
 int bpe_gpu_train(bpe_gpu_ctx *c, long max_merges, size_t *n_merges) {
+    return bpe_gpu_train_ex(c, max_merges, 0, n_merges);
+}
+
+int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_merges) {
     if (!c || !n_merges) return BPE_GPU_EINVAL;
     if (!c->loaded) return fail(BPE_GPU_ESTATE, "train before load");
+    if (flags & ~(unsigned)BPE_GPU_FAST) return fail(BPE_GPU_EINVAL, "unknown train flag");
     HIPCHK(hipSetDevice(c->dev));
+    c->fast = (flags & BPE_GPU_FAST) ? 1 : 0;
+    c->sharded = 0;
+    c->shard = 0;
+    c->nshards = 1;
     c->stats = bpe_gpu_stats{};
     c->stats.n_in = c->n0;
     c->scan_ms = 0;
@@ -993,7 +1050,7 @@ int bpe_gpu_train(bpe_gpu_ctx *c, long max_merges, size_t *n_merges) {
     const uint32_t AA = c->h.A * c->h.A;
     k_init_counts<<<(AA + 255) / 256, 256, 0, c->st>>>(c->dE, c->dC, d_tot, d_unrank);
     HIPCHK(hipGetLastError());
-    const bool tracked = c->n0 < TRACK_LIMIT;
+    const bool tracked = !c->fast && c->n0 < TRACK_LIMIT;
     if (tracked) launch_stats(c);
     launch_summaries(c);
     k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? 1u : 0u);
@@ -1067,6 +1124,10 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
     HIPCHK(hipSetDevice(c->dev));
     c->stats = bpe_gpu_stats{};
     c->stats.n_in = c->n0;
+    c->fast = 0;
+    c->sharded = 0;
+    c->shard = 0;
+    c->nshards = 1;
     const double t0 = now_ms();
     int r;
     if ((r = setup_run(c, (uint32_t)n_merges, true))) return r;
@@ -1220,3 +1281,4 @@ int bpe_gpu_kernel_profile(bpe_gpu_ctx *c, const char **name, double *avg_ms, do
 }
 
 }  // extern "C"
+#include "shard.hip"

@@ -25,6 +25,8 @@ constexpr uint64_t MERGED_B0 = 65536;    // reference MERGED_TABLE_BUCKET_NUM (b
 constexpr uint64_t THREAD_B0 = 256;      // reference PER_THREAD_TABLE_BUCKET_NUM (bpe.c:610)
 constexpr uint32_t L1W = 1024;           // slots per level-1 summary block
 constexpr uint32_t L2W = 256;            // level-1 entries per level-2 summary
+constexpr uint32_t MARK = 0xFFFFFFFFu;   // dist[] of an end slot whose token starts in an earlier shard
+constexpr uint32_t EDGE_WORDS = 16;      // words per shard edge record
 
 enum { V_DL = 0, V_DR = 1, V_IL = 2, V_IR = 3 };
 
@@ -83,6 +85,12 @@ struct Eng {
     uint32_t *ids_out;    // compaction output
     uint32_t *aux;        // per-slot scratch for the resolver (first thread)
     unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
+    uint32_t fast;        // 1: schedule-free tie rule everywhere (no tracking)
+    // corpus sharding (one shard per context; nshards == 1 -> no halo traffic)
+    uint32_t sharded, shard, nshards;
+    uint32_t *xbuf;       // [4*vcap + 2] per-merge exchange: dense deltas | R | flags (allreduced)
+    uint32_t *myrec;      // [EDGE_WORDS] this shard's edge record
+    uint32_t *erec;       // [nshards * EDGE_WORDS] all edge records (allgathered)
 };
 
 struct Ctl {
@@ -108,7 +116,53 @@ struct Ctl {
     unsigned long long scan_t0;       // wall clock at k_scan block 0 entry
     unsigned long long scan_ticks;    // sum over merges of k_scan spans (wall-clock ticks)
     unsigned long long scan_launches;
+    // sharding: tokens around this shard's edges (for the current merge)
+    uint32_t HL[3];                   // ids before the first token start (HL[0] adjacent)
+    uint32_t HR[3];                   // ids after the last token (HR[0] adjacent)
+    uint32_t hlrun;                   // consecutive a's immediately left of the first token
+    uint32_t myidx;                   // run index of the last token (when it is an a)
+    uint32_t F1, L1, L1new, xleft;    // first / last token start, pending last, consumed first
 };
+
+// Edge record of a shard: its first and last three token ids, the run of the
+// last id at its end, and whether the whole shard is that run.  The halo a
+// shard needs for one merge is a pure function of all records (and a), so it
+// is computed redundantly on every shard instead of being exchanged.
+enum { ER_CNT = 0, ER_F = 1, ER_L = 4, ER_TRAIL = 7, ER_ALL = 8, ER_NLO = 9, ER_NHI = 10 };
+
+struct Halo {
+    uint32_t HL[3], HR[3], hlrun, myidx;
+};
+
+__host__ __device__ inline void shard_halo(const uint32_t *rec, uint32_t nshards, uint32_t me, uint32_t a, Halo *h) {
+    for (int m = 0; m < 3; m++) h->HL[m] = h->HR[m] = 0xFFFFFFFFu;
+    uint32_t m = 0;
+    for (int s = (int)me - 1; s >= 0 && m < 3; s--) {
+        const uint32_t *r = rec + (uint64_t)s * EDGE_WORDS;
+        const uint32_t c = r[ER_CNT] < 3 ? r[ER_CNT] : 3;
+        for (uint32_t t = 0; t < c && m < 3; t++) h->HL[m++] = r[ER_L + t];
+    }
+    m = 0;
+    for (uint32_t s = me + 1; s < nshards && m < 3; s++) {
+        const uint32_t *r = rec + (uint64_t)s * EDGE_WORDS;
+        const uint32_t c = r[ER_CNT] < 3 ? r[ER_CNT] : 3;
+        for (uint32_t t = 0; t < c && m < 3; t++) h->HR[m++] = r[ER_F + t];
+    }
+    // a==b runs that cross shard edges: how many a's precede my first token
+    uint64_t run = 0;
+    for (int s = (int)me - 1; s >= 0; s--) {
+        const uint32_t *r = rec + (uint64_t)s * EDGE_WORDS;
+        if (r[ER_CNT] == 0) continue;
+        if (r[ER_L] != a) break;
+        run += r[ER_TRAIL];
+        if (!r[ER_ALL]) break;
+    }
+    h->hlrun = run > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)run;
+    const uint32_t *r = rec + (uint64_t)me * EDGE_WORDS;
+    uint64_t idx = 0;
+    if (r[ER_CNT] && r[ER_L] == a) idx = (uint64_t)r[ER_TRAIL] - 1 + (r[ER_ALL] ? run : 0);
+    h->myidx = idx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)idx;
+}
 
 __host__ __device__ inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 

@@ -60,14 +60,38 @@ __device__ inline void vadd(uint32_t (*s)[DENSE], const Eng *E, uint32_t P, int 
 }
 
 // ---------------------------------------------------------------- k_scan
-// Start of the token that ends at position i-1 (the left neighbour of the
-// token starting at i).  A single-byte token is its own end slot (tok != HOLE
-// there); a longer one stored its start distance in dist[end] when it was
-// created -- so dist never needs initialising.
-__device__ inline uint64_t left_start(const uint32_t *__restrict__ tok, const uint32_t *__restrict__ dist,
-                                      uint64_t i) {
-    const uint64_t e = i - 1;
-    return tok[e] != HOLE ? e : e - dist[e];
+// Neighbour lookups.  Positions are int64: 0..n-1 are this shard's slots,
+// -1-m is HL[m] (m-th token left of the shard's first token start) and n+m is
+// HR[m] (m-th token after its last token), both from the halo the merge
+// step derived from the shards' edge records.  With one shard the halo is
+// all HOLE, which is exactly "no neighbour".
+struct Halo6 {
+    uint32_t HL[3], HR[3];
+};
+
+__device__ inline uint32_t id_at(const uint32_t *__restrict__ tok, const Halo6 &h, int64_t p, int64_t n) {
+    if (p < 0) return p >= -3 ? h.HL[-1 - p] : HOLE;
+    if (p >= n) return p - n < 3 ? h.HR[p - n] : HOLE;
+    return tok[p];
+}
+
+// start of the token left of the token starting at p.  A single-slot token is
+// its own end slot (tok != HOLE there); a longer one stored its start distance
+// in dist[end] when it was created, or MARK when it starts in an earlier
+// shard -- so dist never needs initialising.
+__device__ inline int64_t v_left(const uint32_t *__restrict__ tok, const uint32_t *__restrict__ dist, int64_t p) {
+    if (p <= 0) return p - 1;
+    const int64_t e = p - 1;
+    if (tok[e] != HOLE) return e;
+    const uint32_t d = dist[e];
+    return (int64_t)d > e ? -1 : e - (int64_t)d;
+}
+
+// start of the token after the token of length len starting at p (p >= 0)
+__device__ inline int64_t v_right(int64_t p, uint32_t len, int64_t n) {
+    if (p >= n) return p + 1;
+    const int64_t q = p + len;
+    return q >= n ? n : q;
 }
 
 constexpr uint32_t SCAN_T = 1024;  // threads per k_scan block = candidates per round
@@ -90,23 +114,35 @@ __device__ inline void scan_exit_stamp(const Eng *E) {
     if (threadIdx.x == 0) E->scan_tend[blockIdx.x] = wall_clock64();
 }
 
+// stage one occurrence position (single-thread path: walker / shard edge)
+__device__ inline void stage_one(uint32_t *list, uint32_t *lcount, uint32_t *R, uint32_t *occz, uint32_t pos) {
+    const uint32_t slot = atomicAdd(lcount, 1u);
+    if (slot < SCAN_T) list[slot] = pos;
+    else occz[atomicAdd(R, 1u)] = pos;  // overflow: straight out
+}
+
 __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (blockIdx.x == 0 && threadIdx.x == 0) C->scan_t0 = wall_clock64();
     if (C->stop) return;
     const uint32_t len = C->cand_len;
-    if (blockIdx.x * SCAN_T >= len) {  // block-uniform
+    const bool edge_block = E->sharded && blockIdx.x == 0;
+    if (blockIdx.x * SCAN_T >= len && !edge_block) {  // block-uniform
         scan_exit_stamp(E);
         return;
     }
     const uint32_t a = C->a, b = C->b, z = C->z;
     const uint32_t mode = C->cand_mode, off = C->cand_off;
     const uint32_t P = C->parity;
-    const uint64_t n0 = E->n0;
+    const int64_t n = (int64_t)E->n0;
     const uint32_t *__restrict__ tok = E->tok;
     const uint32_t *__restrict__ dist = E->dist;
     const uint32_t la = E->tlen[a], lb = E->tlen[b];
     const bool count = !E->encode;
     uint32_t *occz = E->occ + C->occ_top;
+    Halo6 h;
+#pragma unroll
+    for (int m = 0; m < 3; m++) { h.HL[m] = C->HL[m]; h.HR[m] = C->HR[m]; }
+    const uint32_t hlrun = C->hlrun;
 
     __shared__ uint32_t s[4][DENSE];
     __shared__ uint32_t list[SCAN_T];
@@ -119,19 +155,19 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
     for (uint32_t e0 = blockIdx.x * SCAN_T; e0 < len; e0 += gridDim.x * SCAN_T) {
         const uint32_t e = e0 + threadIdx.x;
         bool ok = false;
-        uint64_t i = 0, j = 0;
+        int64_t i = 0, j = 0;
         if (e < len) {
             if (mode == 2) {
                 j = E->occ[off + e];
-                if (j > 0 && tok[j] == b) {
-                    i = left_start(tok, dist, j);
-                    ok = tok[i] == a;
+                if (tok[j] == b) {
+                    i = v_left(tok, dist, j);
+                    ok = i >= 0 && tok[i] == a;  // i < 0: the pair is the left shard's
                 }
             } else {
                 i = (mode == 0) ? E->plist[off + e] : E->occ[off + e];
                 if (tok[i] == a) {
                     j = i + la;
-                    ok = j < n0 && tok[j] == b;
+                    ok = j < n && tok[j] == b;  // j >= n: crossing pair, handled below
                 }
             }
         }
@@ -140,58 +176,92 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             if (ok) {
                 list[slot] = (uint32_t)i;
                 if (count) {
-                    const uint64_t k = j + lb;
-                    if (i > 0) {
-                        const uint64_t ps = left_start(tok, dist, i);
-                        const uint32_t p = tok[ps];
+                    const int64_t ps = v_left(tok, dist, i);
+                    const uint32_t p = id_at(tok, h, ps, n);
+                    if (p != HOLE) {
                         bool cov = false;
-                        if (p == b && ps > 0) cov = tok[left_start(tok, dist, ps)] == a;
+                        if (p == b) cov = id_at(tok, h, v_left(tok, dist, ps), n) == a;
                         if (!cov) {
                             vadd(s, E, P, V_DL, p);
                             vadd(s, E, P, V_IL, p);
                         }
                     }
-                    if (k < n0) {
-                        const uint32_t q = tok[k];
+                    const int64_t k = v_right(j, lb, n);
+                    const uint32_t q = id_at(tok, h, k, n);
+                    if (q != HOLE) {
                         vadd(s, E, P, V_DR, q);
-                        const bool nocc = q == a && k + la < n0 && tok[k + la] == b;
+                        const bool nocc = q == a && id_at(tok, h, v_right(k, la, n), n) == b;
                         vadd(s, E, P, V_IR, nocc ? z : q);
                     }
                 }
             }
         } else if (ok) {
             // a == b: only the thread holding a run's first token walks it,
-            // pairing tokens 0-1, 2-3, ... (greedy left-to-right)
-            uint32_t p = HOLE;
-            bool start = true;
-            if (i > 0) {
-                p = tok[left_start(tok, dist, i)];
-                start = p != a;
+            // pairing tokens 0-1, 2-3, ... (greedy left-to-right).  A run that
+            // enters from the left shard continues its parity (hlrun a's precede).
+            const int64_t ps = v_left(tok, dist, i);
+            const uint32_t p = id_at(tok, h, ps, n);
+            bool start = true, left = p != HOLE;
+            int64_t pos = i;
+            if (p == a) {
+                start = ps < 0;
+                left = false;
+                if (hlrun & 1) pos = j;  // i pairs with HL[0] (the left shard's pair)
             }
-            uint64_t pos = i;
             for (uint32_t m = 0; start; m++) {
-                const uint64_t jj = pos + la;
-                if (jj >= n0 || tok[jj] != a) break;
-                const uint64_t k = jj + la;
-                const uint32_t slot = atomicAdd(&lcount, 1u);
-                if (slot < SCAN_T) list[slot] = (uint32_t)pos;
-                else occz[atomicAdd(&C->R, 1u)] = (uint32_t)pos;  // overflow: straight out
-                const bool knext = k < n0 && tok[k] == a;
+                const int64_t jj = pos + la;
+                if (jj >= n || tok[jj] != a) break;  // crossing pair: the shard-edge step
+                const int64_t k = v_right(jj, la, n);
+                stage_one(list, &lcount, &C->R, occz, (uint32_t)pos);
+                const uint32_t q = id_at(tok, h, k, n);
+                const bool knext = q == a;
                 if (count) {
-                    if (m == 0 && p != HOLE) {
+                    if (m == 0 && left) {
                         vadd(s, E, P, V_DL, p);
                         vadd(s, E, P, V_IL, p);
                     }
-                    if (k < n0) {
-                        const uint32_t q = tok[k];
+                    if (q != HOLE) {
                         vadd(s, E, P, V_DR, q);
-                        const bool nocc = knext && k + la < n0 && tok[k + la] == a;
+                        const bool nocc = knext && id_at(tok, h, v_right(k, la, n), n) == a;
                         vadd(s, E, P, V_IR, nocc ? z : q);
                     }
                 }
-                if (!knext) break;
+                if (!knext || k >= n) break;
                 pos = k;
             }
+        }
+        flush_list(list, &lcount, &gbase, &C->R, occz);
+    }
+    if (edge_block) {
+        // Shard edges.  Right: my last token and the first token after it form
+        // a pair I own.  Left: my first token is the b of a pair an earlier
+        // shard owns -- k_apply retires it (xleft).
+        if (threadIdx.x == 0) {
+            uint32_t xl = HOLE;
+            const int64_t F1 = C->F1;
+            if (F1 < n) {
+                if (h.HL[0] == a && tok[F1] == b && (a != b || (hlrun & 1))) xl = (uint32_t)F1;
+                const int64_t i = C->L1;
+                if (tok[i] == a && h.HR[0] == b && (a != b || !(C->myidx & 1))) {
+                    stage_one(list, &lcount, &C->R, occz, (uint32_t)i);
+                    if (count) {
+                        const int64_t ps = v_left(tok, dist, i);
+                        const uint32_t p = id_at(tok, h, ps, n);
+                        bool cov = p == HOLE;
+                        if (!cov) cov = a != b ? (p == b && id_at(tok, h, v_left(tok, dist, ps), n) == a) : p == a;
+                        if (!cov) {
+                            vadd(s, E, P, V_DL, p);
+                            vadd(s, E, P, V_IL, p);
+                        }
+                        const uint32_t q = h.HR[1];
+                        if (q != HOLE) {
+                            vadd(s, E, P, V_DR, q);
+                            vadd(s, E, P, V_IR, (q == a && h.HR[2] == b) ? z : q);
+                        }
+                    }
+                }
+            }
+            C->xleft = xl;
         }
         flush_list(list, &lcount, &gbase, &C->R, occz);
     }
@@ -253,17 +323,30 @@ __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *_
         const uint32_t *occz = E->occ + C->occ_top;
         uint32_t *tok = E->tok;
         uint32_t *dist = E->dist;
+        const uint64_t n = E->n0;
+        const bool sh = E->sharded;
+        const uint64_t L1 = C->L1;
         for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < R; e += roleA_blocks * blockDim.x) {
             const uint64_t i = occz[e];
             const uint64_t j = i + la, k = j + lb;
             tok[i] = z;
-            tok[j] = HOLE;
-            dist[k - 1] = (uint32_t)(k - 1 - i);  // k-1 >= j: never a token start now
+            if (j < n) {  // else: b starts in a later shard, which retires it
+                tok[j] = HOLE;
+                if (k - 1 < n) dist[k - 1] = (uint32_t)(k - 1 - i);  // k-1 >= j: never a token start now
+                if (sh && j == L1) C->L1new = (uint32_t)i;
+            }
         }
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             E->occ_off[z] = C->occ_top;
             E->occ_len[z] = R;
             C->pending = 1;
+            const uint32_t xl = sh ? C->xleft : HOLE;
+            if (xl != HOLE) {  // my first token is the b of the left shard's pair
+                tok[xl] = HOLE;
+                const uint64_t end = (uint64_t)xl + lb;
+                if (end - 1 < n) dist[end - 1] = MARK;
+                C->F1 = (uint32_t)(end < n ? end : n);
+            }
         }
         return;
     }
@@ -272,13 +355,17 @@ __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *_
     //   [0]                 (a,b)
     //   [1, 1+4*DENSE)      dense ids of DR (b,x), DL (x,a), IR (z,x), IL (x,z)
     //   then the listed ids >= DENSE of DR, DL, IR, IL
+    //   sharded: [1, 1+4*vcap) the allreduced dense vectors in xbuf, no lists
     const uint32_t nB = gridDim.x - roleA_blocks;
     const uint32_t stride = nB * blockDim.x;
     uint32_t *const *lst = E->vlist[P];
+    const bool sh = E->sharded;
+    const uint32_t W = sh ? E->vcap : DENSE;
     uint32_t nl[4];
-    for (int v = 0; v < 4; v++) nl[v] = E->vnl[P][v];
-    const uint32_t dense_end = 1 + 4 * DENSE;
+    for (int v = 0; v < 4; v++) nl[v] = sh ? 0 : E->vnl[P][v];
+    const uint32_t dense_end = 1 + 4 * W;
     const uint32_t total = dense_end + nl[0] + nl[1] + nl[2] + nl[3];
+    const uint32_t Rg = sh ? E->xbuf[4 * E->vcap] : R;  // occurrences over all shards
     __shared__ uint32_t marks[MARK_CAP];
     __shared__ uint32_t nmark, mbase;
     if (threadIdx.x == 0) nmark = 0;
@@ -295,8 +382,8 @@ __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *_
         if (t == 0) {
             cat = 4; u = a; v = b;
         } else if (t < dense_end) {
-            cat = (t - 1) / DENSE;
-            x = (t - 1) % DENSE;
+            cat = (t - 1) / W;
+            x = (t - 1) % W;
         } else if (t < total) {
             uint32_t q = t - dense_end;
             for (cat = 0; cat < 4 && q >= nl[cat]; cat++) q -= nl[cat];
@@ -310,21 +397,27 @@ __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *_
         }
         // the four delta values that can touch key (u, v), loaded together
         uint32_t vdr = 0, vdl = 0, vir = 0, vil = 0;
-        if (cat >= 0) {
+        if (cat >= 0 && sh) {
+            const uint32_t *xb = E->xbuf, vc = E->vcap;
+            vdr = u == b && v < vc ? xb[V_DR * vc + v] : 0;
+            vdl = v == a && u < vc ? xb[V_DL * vc + u] : 0;
+            vir = u == z && v < vc ? xb[V_IR * vc + v] : 0;
+            vil = v == z && u < vc ? xb[V_IL * vc + u] : 0;
+        } else if (cat >= 0) {
             vdr = u == b ? dval(E, P, V_DR, v) : 0;
             vdl = v == a ? dval(E, P, V_DL, u) : 0;
             vir = u == z ? dval(E, P, V_IR, v) : 0;
             vil = v == z ? dval(E, P, V_IL, u) : 0;
         }
         bool owner = cat >= 0;
-        if (owner && cat == 4) owner = R != 0;
+        if (owner && cat == 4) owner = Rg != 0;
         if (owner && cat == V_DR) owner = vdr != 0 && !(u == a && v == b);
         if (owner && cat == V_DL) owner = vdl != 0 && !(u == a && v == b) && !(u == b && vdr != 0);
         if (owner && cat == V_IR) owner = vir != 0;
         if (owner && cat == V_IL) owner = vil != 0;
         if (owner) {
             long long d = -(long long)vdr - (long long)vdl + (long long)vir + (long long)vil;
-            if (u == a && v == b) d -= R;
+            if (u == a && v == b) d -= Rg;
             if (d != 0) {
                 const uint64_t slot = d > 0 ? hinsert(E, C, u, v) : hfind(E, u, v);
                 if (slot == ~0ull) {
@@ -521,7 +614,7 @@ __device__ inline void finish_iteration(const Eng *E, Ctl *C) {
     C->counters[4] += C->cand_len;  // candidates examined by k_scan (profiling)
     C->counters[5] += C->R;         // occurrences replaced
     C->occ_top += C->R;
-    C->n_live -= C->R;
+    C->n_live -= E->sharded ? E->xbuf[4 * E->vcap] : C->R;
     C->R = 0;
     C->nl1 = 0;
     C->nl2 = 0;
@@ -565,7 +658,7 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
         }
     }
     finish_iteration(E, C);
-    if (!tracked_graph && C->n_live < TRACK_LIMIT) { C->stop = STOP_MODE; return; }
+    if (!tracked_graph && !E->fast && C->n_live < TRACK_LIMIT) { C->stop = STOP_MODE; return; }
     const uint64_t D = C->D;
     uint32_t edge;
     const uint64_t Bn = bfinal_nominal(D, &edge);
@@ -578,12 +671,104 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
     if (C->merges_done >= E->mcap) { C->stop = STOP_CAP; return; }
     if (r.v == 0 || cnt <= 1) { C->stop = STOP_DONE; return; }
     if (C->nkeys + 4ull * (256ull + C->merges_done + 2) >= E->hcap / 2) { C->stop = STOP_GROW; return; }
-    const bool tracked = C->n_live < DYN_LIMIT;   // deterministic (static) reference iteration
+    const bool tracked = !E->fast && C->n_live < DYN_LIMIT;  // deterministic (static) reference iteration
     if (tracked && (edge || r.tie > 1)) { C->stop = STOP_EVENT; return; }
     // untracked tie (n >= 2^20, schedule-dependent in the reference): the
     // project rule is the smallest (a,b) -- r.key already is that key
     if (r.tie > 1) C->counters[2]++;
     commit_merge(E, C, (uint32_t)(r.key >> 32), (uint32_t)r.key);
+    if (E->sharded) {  // halo of this shard for the merge just chosen
+        Halo hl;
+        shard_halo(E->erec, E->nshards, E->shard, C->a, &hl);
+        for (int m = 0; m < 3; m++) { C->HL[m] = hl.HL[m]; C->HR[m] = hl.HR[m]; }
+        C->hlrun = hl.hlrun;
+        C->myidx = hl.myidx;
+    }
+}
+
+// ------------------------------------------------------------ shard exchange
+// dense copy of this shard's delta vectors (replicas summed) + its R, the
+// buffer every shard allreduces before k_apply
+__global__ __launch_bounds__(256) void k_pack(const Eng *__restrict__ E, const Ctl *__restrict__ C) {
+    const uint32_t vc = E->vcap, P = C->parity;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < 4 * vc) {
+        const uint32_t v = t / vc, x = t % vc;
+        E->xbuf[t] = C->stop ? 0 : dval(E, P, v, x);
+    } else if (t == 4 * vc) {
+        E->xbuf[t] = C->stop ? 0 : C->R;
+    } else if (t == 4 * vc + 1) {
+        E->xbuf[t] = C->stop;
+    }
+}
+
+// this shard's edge record after k_apply (one thread; walks at most a few
+// tokens, plus the run of its last id)
+__global__ void k_edges(const Eng *__restrict__ E, Ctl *__restrict__ C, int force) {
+    if (threadIdx.x != 0 || (C->stop && !force)) return;
+    if (C->L1new != HOLE) { C->L1 = C->L1new; C->L1new = HOLE; }
+    const int64_t n = (int64_t)E->n0;
+    const uint32_t *tok = E->tok, *dist = E->dist, *tlen = E->tlen;
+    uint32_t r[EDGE_WORDS];
+    for (uint32_t w = 0; w < EDGE_WORDS; w++) r[w] = 0;
+    for (int m = 0; m < 3; m++) r[ER_F + m] = r[ER_L + m] = HOLE;
+    const int64_t F1 = C->F1, L1 = C->L1;
+    if (F1 < n) {
+        uint32_t c = 0;
+        for (int64_t p = F1; p <= L1 && c < 7; c++) {
+            const uint32_t id = tok[p];
+            if (c < 3) r[ER_F + c] = id;
+            p += tlen[id];
+        }
+        r[ER_CNT] = c;
+        int64_t p = L1;
+        for (int m = 0; m < 3 && p >= 0; m++) {
+            r[ER_L + m] = tok[p];
+            p = v_left(tok, dist, p);
+        }
+        const uint32_t last = r[ER_L];
+        uint64_t trail = 0;
+        p = L1;
+        while (p >= 0 && tok[p] == last) {
+            trail++;
+            p = v_left(tok, dist, p);
+        }
+        r[ER_TRAIL] = trail > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)trail;
+        r[ER_ALL] = p < 0;
+    }
+    r[ER_NLO] = (uint32_t)E->n0;
+    r[ER_NHI] = (uint32_t)(E->n0 >> 32);
+    for (uint32_t w = 0; w < EDGE_WORDS; w++) E->myrec[w] = r[w];
+}
+
+// one-device shard groups: the exchange is a sum / gather over the shards'
+// buffers (pointer tables in device memory)
+__global__ __launch_bounds__(256) void k_xsum(uint32_t *const *__restrict__ bufs, uint32_t nb, uint32_t count) {
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += gridDim.x * blockDim.x) {
+        uint32_t sum = 0;
+        for (uint32_t q = 0; q < nb; q++) sum += bufs[q][t];
+        for (uint32_t q = 0; q < nb; q++) bufs[q][t] = sum;
+    }
+}
+
+__global__ void k_xgather(uint32_t *const *__restrict__ src, uint32_t *const *__restrict__ dst, uint32_t nb,
+                          uint32_t words) {
+    for (uint32_t t = threadIdx.x; t < nb * words; t += blockDim.x)
+        for (uint32_t q = 0; q < nb; q++) dst[q][t] = src[t / words][t % words];
+}
+
+// initial counts: the byte pair across this shard's right edge
+__global__ void k_init_cross(const Eng *__restrict__ E, uint32_t *__restrict__ tot) {
+    const uint32_t me = E->shard;
+    const uint32_t *my = E->erec + (uint64_t)me * EDGE_WORDS;
+    if (threadIdx.x != 0 || my[ER_CNT] == 0) return;
+    for (uint32_t s = me + 1; s < E->nshards; s++) {
+        const uint32_t *r = E->erec + (uint64_t)s * EDGE_WORDS;
+        if (r[ER_CNT] == 0) continue;
+        const uint32_t u = E->rank[my[ER_L]], v = E->rank[r[ER_F]];
+        if (u != HOLE && v != HOLE) tot[u * E->A + v] += 1;
+        return;
+    }
 }
 
 // commit a merge chosen by the host resolver (after STOP_EVENT)

@@ -1,0 +1,483 @@
+// shard.hip -- corpus-sharded training; included by engine.hip.
+//
+// The corpus is cut into contiguous shards, one engine context each (one per
+// GPU across ranks, or several on one device for testing).  Every context
+// keeps the full replicated pair-count table and its own shard's position
+// space; per merge the shards exchange exactly two things:
+//   1. allreduce of the dense count-delta vectors + occurrence count (k_pack
+//      -> xbuf), so every replica applies the same update and the argmax
+//      stays identical everywhere;
+//   2. allgather of 16-word edge records (k_edges), from which every shard
+//      derives the tokens just outside its edges for the next merge
+//      (shard_halo): pairs across an edge belong to the left shard, runs of
+//      a==b continue their pairing parity across edges.
+// Across GPUs the exchange is RCCL over xGMI (librccl, loaded at run time);
+// within one device it is a sum / gather kernel over the shards' buffers.
+// Ties are decided by the schedule-free rule (smallest (a,b) among the
+// maximal (count, bucket) keys) in every iteration: for corpora of >= 2^20
+// tokens this is the single-GPU engine's rule as well, so 1 GPU == N GPUs.
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+namespace {
+
+struct RcclApi {
+    void *lib = nullptr;
+    ncclResult_t (*getUniqueId)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*commInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*allReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                              hipStream_t) = nullptr;
+    ncclResult_t (*allGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    const char *(*errStr)(ncclResult_t) = nullptr;
+};
+
+// librccl is loaded on first use (a process that already loaded it, e.g.
+// through torch, shares that copy: same soname)
+int rccl_api(RcclApi **out) {
+    static RcclApi api;
+    if (!api.lib) {
+        void *l = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!l) l = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!l) return fail(BPE_GPU_ENODEV, "librccl.so.1 not loadable");
+        api.getUniqueId = (decltype(api.getUniqueId))dlsym(l, "ncclGetUniqueId");
+        api.commInitRank = (decltype(api.commInitRank))dlsym(l, "ncclCommInitRank");
+        api.allReduce = (decltype(api.allReduce))dlsym(l, "ncclAllReduce");
+        api.allGather = (decltype(api.allGather))dlsym(l, "ncclAllGather");
+        api.commDestroy = (decltype(api.commDestroy))dlsym(l, "ncclCommDestroy");
+        api.errStr = (decltype(api.errStr))dlsym(l, "ncclGetErrorString");
+        if (!api.getUniqueId || !api.commInitRank || !api.allReduce || !api.allGather || !api.commDestroy ||
+            !api.errStr)
+            return fail(BPE_GPU_ENODEV, "librccl.so.1 lacks the nccl entry points");
+        api.lib = l;
+    }
+    *out = &api;
+    return 0;
+}
+
+int rccl_fail(RcclApi *api, const char *what, ncclResult_t e) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s", what, api->errStr(e));
+    g_last_error = buf;
+    return BPE_GPU_EHIP;
+}
+
+}  // namespace
+
+struct bpe_gpu_group {
+    int dev = 0;
+    hipStream_t st = nullptr;
+    std::vector<bpe_gpu_ctx *> cs;  // local shards, in corpus order
+    uint32_t nshards = 1, shard0 = 0;
+    RcclApi *rccl = nullptr;
+    ncclComm_t comm = nullptr;
+    uint32_t **d_ptrs = nullptr;      // local mode: [xbuf | myrec | erec] pointer tables
+    uint32_t **d_ptrs_tmp = nullptr;  // local mode: init-time tables
+    hipGraphExec_t graph = nullptr;
+    bool eager = false;               // collectives could not be graph-captured
+    size_t merges_done = 0;
+    bpe_gpu_stats stats{};
+};
+
+namespace {
+
+int group_free_graph(bpe_gpu_group *g) {
+    if (g->graph) (void)hipGraphExecDestroy(g->graph);
+    g->graph = nullptr;
+    return 0;
+}
+
+// sum-allreduce of `count` u32 at bufs[k] (one per local shard), in place
+int ex_allreduce(bpe_gpu_group *g, uint32_t **d_tab, const std::vector<uint32_t *> &bufs, size_t count) {
+    if (g->rccl) {
+        ncclResult_t e = g->rccl->allReduce(bufs[0], bufs[0], count, ncclUint32, ncclSum, g->comm, g->st);
+        if (e != ncclSuccess) return rccl_fail(g->rccl, "ncclAllReduce", e);
+        return 0;
+    }
+    if (bufs.size() == 1) return 0;
+    const uint32_t blocks = (uint32_t)std::min<size_t>(1024, (count + 255) / 256);
+    k_xsum<<<std::max<uint32_t>(blocks, 1), 256, 0, g->st>>>(d_tab, (uint32_t)bufs.size(), (uint32_t)count);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// allgather of the edge records: erec[s] = shard s's myrec, on every shard
+int ex_records(bpe_gpu_group *g, uint32_t **d_tab) {
+    bpe_gpu_ctx *c0 = g->cs[0];
+    if (g->rccl) {
+        ncclResult_t e = g->rccl->allGather(c0->h.myrec, c0->h.erec, EDGE_WORDS, ncclUint32, g->comm, g->st);
+        if (e != ncclSuccess) return rccl_fail(g->rccl, "ncclAllGather", e);
+        return 0;
+    }
+    const uint32_t K = (uint32_t)g->cs.size();
+    k_xgather<<<1, 256, 0, g->st>>>(d_tab + K, d_tab + 2 * K, K, EDGE_WORDS);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int upload_table(bpe_gpu_group *g, uint32_t **d_tab, const std::vector<uint32_t *> &ptrs) {
+    HIPCHK(hipMemcpyAsync(d_tab, ptrs.data(), ptrs.size() * sizeof(uint32_t *), hipMemcpyHostToDevice, g->st));
+    return 0;
+}
+
+int launch_group_iteration(bpe_gpu_group *g) {
+    int r;
+    std::vector<uint32_t *> xb;
+    for (bpe_gpu_ctx *c : g->cs) {
+        k_scan<<<SCAN_BLOCKS, SCAN_T, 0, g->st>>>(c->dE, c->dC);
+        const uint32_t nx = 4 * c->h.vcap + 2;
+        k_pack<<<(nx + 255) / 256, 256, 0, g->st>>>(c->dE, c->dC);
+        xb.push_back(c->h.xbuf);
+    }
+    if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
+    for (bpe_gpu_ctx *c : g->cs) {
+        k_apply<<<APPLY_A + APPLY_B, 256, 0, g->st>>>(c->dE, c->dC, APPLY_A);
+        k_edges<<<1, 64, 0, g->st>>>(c->dE, c->dC, 0);
+    }
+    if ((r = ex_records(g, g->d_ptrs))) return r;
+    for (bpe_gpu_ctx *c : g->cs) {
+        launch_summaries(c);
+        k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int capture_group(bpe_gpu_group *g) {
+    hipGraph_t gr;
+    HIPCHK(hipStreamBeginCapture(g->st, hipStreamCaptureModeThreadLocal));
+    int r = 0;
+    for (uint32_t k = 0; k < ITERS_PER_GRAPH && !r; k++) r = launch_group_iteration(g);
+    hipError_t e = hipStreamEndCapture(g->st, &gr);
+    if (r || e != hipSuccess) {
+        (void)hipGetLastError();
+        if (e == hipSuccess) (void)hipGraphDestroy(gr);
+        return r ? r : fail(BPE_GPU_EHIP, "hipStreamEndCapture", e);
+    }
+    e = hipGraphInstantiate(&g->graph, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    if (e != hipSuccess) {
+        g->graph = nullptr;
+        return fail(BPE_GPU_EHIP, "hipGraphInstantiate", e);
+    }
+    return 0;
+}
+
+int drive_group(bpe_gpu_group *g) {
+    int r;
+    for (;;) {
+        for (bpe_gpu_ctx *c : g->cs)
+            if ((r = pull_ctl(c))) return r;
+        const Ctl &C0 = *g->cs[0]->hC;
+        for (bpe_gpu_ctx *c : g->cs)
+            if (c->hC->stop != C0.stop || c->hC->merges_done != C0.merges_done || c->hC->D != C0.D)
+                return fail(BPE_GPU_EINTERNAL, "shards diverged");
+        switch (C0.stop) {
+        case STOP_NONE:
+            if (!g->graph && !g->eager && capture_group(g)) {
+                // collectives that refuse stream capture: launch eagerly
+                g->eager = true;
+                (void)hipGetLastError();
+            }
+            if (g->graph) {
+                HIPCHK(hipGraphLaunch(g->graph, g->st));
+            } else {
+                for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++)
+                    if ((r = launch_group_iteration(g))) return r;
+            }
+            break;
+        case STOP_DONE:
+        case STOP_CAP:
+            return 0;
+        case STOP_ERROR:
+            return fail(BPE_GPU_EINTERNAL, C0.err == 1 ? "engine invariant violated (count decrement of an absent pair)"
+                                                       : "pair table full");
+        case STOP_GROW:
+            group_free_graph(g);
+            for (bpe_gpu_ctx *c : g->cs) {
+                c->hC->stop = STOP_NONE;
+                c->hC->full = 1;
+                if ((r = push_ctl(c))) return r;
+                if ((r = grow_table(c, c->h.hcap * 4))) return r;
+            }
+            for (bpe_gpu_ctx *c : g->cs) {
+                launch_summaries(c);
+                k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
+            }
+            HIPCHK(hipGetLastError());
+            break;
+        default:
+            return fail(BPE_GPU_EINTERNAL, "unexpected stop state in sharded training");
+        }
+    }
+}
+
+// total positions over all shards (u64 sum across ranks)
+int group_total(bpe_gpu_group *g, uint64_t *tot) {
+    uint64_t local = 0;
+    for (bpe_gpu_ctx *c : g->cs) local += c->n0;
+    if (!g->rccl) {
+        *tot = local;
+        return 0;
+    }
+    uint64_t *d;
+    HIPCHK(hipMalloc(&d, 8));
+    HIPCHK(hipMemcpyAsync(d, &local, 8, hipMemcpyHostToDevice, g->st));
+    ncclResult_t e = g->rccl->allReduce(d, d, 1, ncclUint64, ncclSum, g->comm, g->st);
+    if (e != ncclSuccess) { hipFree(d); return rccl_fail(g->rccl, "ncclAllReduce", e); }
+    HIPCHK(hipMemcpyAsync(tot, d, 8, hipMemcpyDeviceToHost, g->st));
+    HIPCHK(hipStreamSynchronize(g->st));
+    hipFree(d);
+    return 0;
+}
+
+int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
+    int r;
+    const uint32_t K = (uint32_t)g->cs.size();
+    for (bpe_gpu_ctx *c : g->cs)
+        if (!c->loaded || c->n0 < 1) return fail(BPE_GPU_ESTATE, "every shard needs at least one byte");
+    group_free_graph(g);
+    g->stats = bpe_gpu_stats{};
+    g->merges_done = 0;
+    *n_merges = 0;
+    const double t0 = now_ms();
+    uint64_t ntot;
+    if ((r = group_total(g, &ntot))) return r;
+    g->stats.n_in = ntot;
+    if (ntot < 2) return fail(BPE_GPU_EINVAL, "fewer than 2 tokens");
+    uint64_t cap = std::min<uint64_t>(ntot - 1, 1ull << 24);
+    if (max_merges >= 0) cap = std::min<uint64_t>(cap, (uint64_t)max_merges);
+    for (uint32_t k = 0; k < K; k++) {
+        bpe_gpu_ctx *c = g->cs[k];
+        c->stats = bpe_gpu_stats{};
+        c->scan_ms = 0;
+        c->scan_n = 0;
+        c->merges_done = 0;
+        c->fast = 1;
+        c->sharded = 1;
+        c->shard = g->shard0 + k;
+        c->nshards = g->nshards;
+        if ((r = setup_run(c, (uint32_t)cap, false))) return r;
+        c->hC->n_live = ntot;  // global token count (the tracking thresholds are global)
+        if ((r = push_ctl(c))) return r;
+    }
+    // pointer tables for the one-device exchange
+    if (!g->rccl) {
+        if (!g->d_ptrs) {
+            HIPCHK(hipMalloc(&g->d_ptrs, 3ull * K * sizeof(uint32_t *)));
+            HIPCHK(hipMalloc(&g->d_ptrs_tmp, (size_t)K * sizeof(uint32_t *)));
+        }
+        std::vector<uint32_t *> t;
+        for (auto *c : g->cs) t.push_back(c->h.xbuf);
+        for (auto *c : g->cs) t.push_back(c->h.myrec);
+        for (auto *c : g->cs) t.push_back(c->h.erec);
+        if ((r = upload_table(g, g->d_ptrs, t))) return r;
+    }
+    // 1. global byte alphabet
+    std::vector<uint32_t *> bh(K);
+    for (uint32_t k = 0; k < K; k++)
+        if ((r = init_presence(g->cs[k], &bh[k]))) return r;
+    if (!g->rccl && (r = upload_table(g, g->d_ptrs_tmp, bh))) return r;
+    if ((r = ex_allreduce(g, g->d_ptrs_tmp, bh, 256))) return r;
+    std::vector<uint32_t> pres(256);
+    HIPCHK(hipMemcpyAsync(pres.data(), bh[0], 1024, hipMemcpyDeviceToHost, g->st));
+    HIPCHK(hipStreamSynchronize(g->st));
+    // 2. local counting sorts under the global ranks
+    std::vector<uint32_t> unrank;
+    std::vector<uint32_t *> tot(K), d_unrank(K);
+    for (uint32_t k = 0; k < K; k++)
+        if ((r = init_sort(g->cs[k], pres, &unrank, &tot[k]))) return r;
+    // 3. edge records, the byte pairs across edges, global byte-pair counts
+    for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 64, 0, g->st>>>(c->dE, c->dC, 1);
+    if ((r = ex_records(g, g->d_ptrs))) return r;
+    for (uint32_t k = 0; k < K; k++) k_init_cross<<<1, 64, 0, g->st>>>(g->cs[k]->dE, tot[k]);
+    const uint32_t A = g->cs[0]->h.A, AA = A * A;
+    if (!g->rccl && (r = upload_table(g, g->d_ptrs_tmp, tot))) return r;
+    if (AA && (r = ex_allreduce(g, g->d_ptrs_tmp, tot, AA))) return r;
+    for (uint32_t k = 0; k < K; k++) {
+        bpe_gpu_ctx *c = g->cs[k];
+        if ((r = dalloc(c, &d_unrank[k], unrank.size()))) return r;
+        if (!unrank.empty())
+            HIPCHK(hipMemcpyAsync(d_unrank[k], unrank.data(), unrank.size() * 4, hipMemcpyHostToDevice, g->st));
+        if (AA) k_init_counts<<<(AA + 255) / 256, 256, 0, g->st>>>(c->dE, c->dC, tot[k], d_unrank[k]);
+    }
+    // warm the per-merge collective once outside any graph (lazy connection setup)
+    {
+        std::vector<uint32_t *> xb;
+        for (auto *c : g->cs) xb.push_back(c->h.xbuf);
+        if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
+        for (auto *c : g->cs) HIPCHK(hipMemsetAsync(c->h.xbuf, 0, (4ull * c->h.vcap + 2) * 4, g->st));
+    }
+    for (bpe_gpu_ctx *c : g->cs) {
+        launch_summaries(c);
+        k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(g->st));
+    const double t1 = now_ms();
+    if ((r = drive_group(g))) return r;
+    HIPCHK(hipStreamSynchronize(g->st));
+    const double t2 = now_ms();
+    uint64_t nout = 0;
+    for (bpe_gpu_ctx *c : g->cs) {
+        if ((r = pull_ctl(c))) return r;
+        if ((r = compact_ids(c))) return r;
+        c->merges_done = c->hC->merges_done;
+        nout += c->ids_len;
+    }
+    const Ctl &C = *g->cs[0]->hC;
+    g->merges_done = C.merges_done;
+    *n_merges = C.merges_done;
+    g->stats.n_out = nout;
+    g->stats.merges = C.merges_done;
+    g->stats.iterations = C.counters[0] + 1;
+    g->stats.distinct_pairs = C.D;
+    g->stats.merged_buckets = C.B;
+    g->stats.rule_ties = C.counters[2];
+    g->stats.keys = C.nkeys;
+    g->stats.table_grows = g->cs[0]->stats.table_grows;
+    g->stats.ms_init = t1 - t0;
+    g->stats.ms_train = t2 - t1;
+    g->stats.ms_total = t2 - t0;
+    g->stats.ms_count_pass = g->cs[0]->stats.ms_count_pass;
+    return 0;
+}
+
+bpe_gpu_ctx *group_shard(bpe_gpu_group *g, int k) {
+    if (!g || k < 0 || (size_t)k >= g->cs.size()) return nullptr;
+    return g->cs[k];
+}
+
+}  // namespace
+
+extern "C" {
+
+int bpe_gpu_comm_id(uint8_t *id, size_t cap) {
+    if (!id || cap < sizeof(ncclUniqueId)) return BPE_GPU_EINVAL;
+    RcclApi *api;
+    int r;
+    if ((r = rccl_api(&api))) return r;
+    ncclUniqueId u;
+    ncclResult_t e = api->getUniqueId(&u);
+    if (e != ncclSuccess) return rccl_fail(api, "ncclGetUniqueId", e);
+    memcpy(id, &u, sizeof u);
+    return 0;
+}
+
+int bpe_gpu_group_create(int device, int local_shards, int nranks, int rank, const uint8_t *comm_id,
+                         bpe_gpu_group **out) {
+    if (!out || local_shards < 1 || nranks < 1 || rank < 0 || rank >= nranks) return BPE_GPU_EINVAL;
+    if (comm_id && local_shards != 1) return fail(BPE_GPU_EINVAL, "an RCCL group has one shard per rank");
+    if (!comm_id && nranks != 1) return fail(BPE_GPU_EINVAL, "nranks > 1 needs an RCCL id");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return fail(BPE_GPU_ENODEV, "no such device");
+    HIPCHK(hipSetDevice(device));
+    bpe_gpu_group *g = new bpe_gpu_group();
+    g->dev = device;
+    int r;
+    hipError_t e = hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete g; return fail(BPE_GPU_EHIP, "hipStreamCreate", e); }
+    if (comm_id) {
+        if ((r = rccl_api(&g->rccl))) { bpe_gpu_group_destroy(g); return r; }
+        ncclUniqueId u;
+        memcpy(&u, comm_id, sizeof u);
+        ncclResult_t ne = g->rccl->commInitRank(&g->comm, nranks, u, rank);
+        if (ne != ncclSuccess) {
+            r = rccl_fail(g->rccl, "ncclCommInitRank", ne);
+            g->comm = nullptr;
+            bpe_gpu_group_destroy(g);
+            return r;
+        }
+        g->nshards = (uint32_t)nranks;
+        g->shard0 = (uint32_t)rank;
+    } else {
+        g->nshards = (uint32_t)local_shards;
+        g->shard0 = 0;
+    }
+    for (int k = 0; k < local_shards; k++) {
+        bpe_gpu_ctx *c;
+        if ((r = ctx_new(device, g->st, &c))) { bpe_gpu_group_destroy(g); return r; }
+        g->cs.push_back(c);
+    }
+    *out = g;
+    return 0;
+}
+
+void bpe_gpu_group_destroy(bpe_gpu_group *g) {
+    if (!g) return;
+    (void)hipSetDevice(g->dev);
+    if (g->st) (void)hipStreamSynchronize(g->st);
+    group_free_graph(g);
+    for (bpe_gpu_ctx *c : g->cs) bpe_gpu_destroy(c);
+    if (g->d_ptrs) hipFree(g->d_ptrs);
+    if (g->d_ptrs_tmp) hipFree(g->d_ptrs_tmp);
+    if (g->comm) (void)g->rccl->commDestroy(g->comm);
+    if (g->st) (void)hipStreamDestroy(g->st);
+    delete g;
+}
+
+int bpe_gpu_group_shards(bpe_gpu_group *g, int *local_shards, int *nshards, int *first_shard) {
+    if (!g) return BPE_GPU_EINVAL;
+    if (local_shards) *local_shards = (int)g->cs.size();
+    if (nshards) *nshards = (int)g->nshards;
+    if (first_shard) *first_shard = (int)g->shard0;
+    return 0;
+}
+
+int bpe_gpu_group_load(bpe_gpu_group *g, int k, const uint8_t *bytes, size_t n) {
+    bpe_gpu_ctx *c = group_shard(g, k);
+    if (!c) return BPE_GPU_EINVAL;
+    group_free_graph(g);
+    return bpe_gpu_load(c, bytes, n);
+}
+
+int bpe_gpu_group_synth(bpe_gpu_group *g, int k, uint64_t seed, size_t n, uint64_t offset) {
+    bpe_gpu_ctx *c = group_shard(g, k);
+    if (!c) return BPE_GPU_EINVAL;
+    group_free_graph(g);
+    return bpe_gpu_synth(c, seed, n, offset);
+}
+
+int bpe_gpu_group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
+    if (!g || !n_merges) return BPE_GPU_EINVAL;
+    HIPCHK(hipSetDevice(g->dev));
+    return group_train(g, max_merges, n_merges);
+}
+
+int bpe_gpu_group_fetch_merges(bpe_gpu_group *g, uint32_t *pairs, size_t cap, size_t *count) {
+    if (!g) return BPE_GPU_EINVAL;
+    return bpe_gpu_fetch_merges(g->cs[0], pairs, cap, count);
+}
+
+int bpe_gpu_group_fetch_ids(bpe_gpu_group *g, int k, uint32_t *ids, size_t cap, size_t *len) {
+    bpe_gpu_ctx *c = group_shard(g, k);
+    if (!c) return BPE_GPU_EINVAL;
+    return bpe_gpu_fetch_ids(c, ids, cap, len);
+}
+
+int bpe_gpu_group_get_stats(bpe_gpu_group *g, bpe_gpu_stats *st) {
+    if (!g || !st) return BPE_GPU_EINVAL;
+    *st = g->stats;
+    return 0;
+}
+
+int bpe_gpu_group_exchange_mode(bpe_gpu_group *g, int *graph_captured) {
+    if (!g || !graph_captured) return BPE_GPU_EINVAL;
+    *graph_captured = g->eager ? 0 : 1;
+    return 0;
+}
+
+int bpe_gpu_shard_halo(const uint32_t *records, uint32_t nshards, uint32_t me, uint32_t a, uint32_t *out8) {
+    if (!records || !out8 || me >= nshards) return BPE_GPU_EINVAL;
+    Halo h;
+    shard_halo(records, nshards, me, a, &h);
+    for (int m = 0; m < 3; m++) {
+        out8[m] = h.HL[m];
+        out8[3 + m] = h.HR[m];
+    }
+    out8[6] = h.hlrun;
+    out8[7] = h.myidx;
+    return 0;
+}
+
+}  // extern "C"

@@ -15,6 +15,7 @@ _LIB = None
 
 EMU = 0
 FAST = 1
+RULE = 2  # schedule-free tie rule at every size (sharded training, BPE_GPU_FAST)
 
 
 class OracleStats(ctypes.Structure):

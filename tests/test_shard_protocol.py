@@ -1,0 +1,169 @@
+"""Sharded training protocol on CPU.
+
+* the library's shard_halo (the same __host__ __device__ function k_select
+  runs) against a brute-force reading of the global token sequence;
+* the per-shard step (tests/shard_sim.py mirrors k_scan / k_apply / k_edges)
+  against the oracle's RULE mode on the whole corpus, in one process and
+  across two processes exchanging over torch.distributed (gloo).
+"""
+import os
+import random
+import socket
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import shard_sim as S
+from llmtokenizer_amd import api
+
+HOLE = 0xFFFFFFFF
+
+
+def _records(shard_tokens):
+    recs = []
+    for toks in shard_tokens:
+        r = [0] * 16
+        for m in range(3):
+            r[1 + m] = r[4 + m] = HOLE
+        c = len(toks)
+        if c:
+            r[0] = min(c, 7)
+            for m in range(min(c, 3)):
+                r[1 + m] = toks[m]
+                r[4 + m] = toks[c - 1 - m]
+            t = 0
+            while t < c and toks[c - 1 - t] == toks[-1]:
+                t += 1
+            r[7] = t
+            r[8] = 1 if t == c else 0
+        recs.append(r)
+    return np.array(recs, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_halo_matches_global_sequence(seed):
+    rng = random.Random(seed)
+    for _ in range(200):
+        ntok = rng.randint(0, 30)
+        ids = [rng.choice([1, 1, 2, 3]) for _ in range(ntok)]
+        nsh = rng.randint(1, 8)
+        # assign tokens to shards in order, empty shards allowed
+        owners = sorted(rng.randrange(nsh) for _ in range(ntok))
+        shard_tokens = [[ids[g] for g in range(ntok) if owners[g] == s] for s in range(nsh)]
+        recs = _records(shard_tokens)
+        for s in range(nsh):
+            if not shard_tokens[s]:
+                continue
+            gi = owners.index(s)
+            gl = len(owners) - 1 - owners[::-1].index(s)
+            for a in (1, 2, 3):
+                h = api.shard_halo(recs, s, a)
+                HL = [ids[gi - 1 - m] if gi - 1 - m >= 0 else HOLE for m in range(3)]
+                HR = [ids[gl + 1 + m] if gl + 1 + m < ntok else HOLE for m in range(3)]
+                run = 0
+                while gi - 1 - run >= 0 and ids[gi - 1 - run] == a:
+                    run += 1
+                idx = 0
+                if ids[gl] == a:
+                    while gl - 1 - idx >= 0 and ids[gl - 1 - idx] == a:
+                        idx += 1
+                assert h["HL"] == HL and h["HR"] == HR, (ids, owners, s)
+                assert h["hlrun"] == run and h["myidx"] == idx, (ids, owners, s, a)
+
+
+def _cases(seed, count, nmax=160, kmax=10):
+    rng = random.Random(seed)
+    out = []
+    for _ in range(count):
+        n = rng.randint(2, nmax)
+        alpha = rng.choice([b"a", b"ab", b"aab", b"aaab", b"abc", b"a b", bytes(range(32, 127))])
+        data = bytes(rng.choice(alpha) for _ in range(n))
+        if rng.random() < 0.3:
+            data = b"a" * rng.randint(1, 60) + data
+        n = len(data)
+        k = rng.randint(1, min(n, kmax))
+        cuts = [0] + sorted(rng.sample(range(1, n), k - 1)) + [n]
+        out.append((data, cuts, rng.choice([-1, -1, 20])))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_sharded_step_equals_oracle_rule(seed):
+    sc, ga = S.local_exchange()
+    for data, cuts, mm in _cases(seed, 120):
+        parts = [data[cuts[k]:cuts[k + 1]] for k in range(len(cuts) - 1)]
+        m, ids = S.train_sharded(parts, mm, sc, ga, 0, len(parts))
+        om, oi, _ = O.train(data, mm, O.RULE)
+        assert [tuple(x) for x in om.tolist()] == m, (data, cuts)
+        assert list(oi) == [x for l in ids for x in l], (data, cuts)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, cases, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from collections import Counter
+        results = []
+        for data, cuts, mm, per in cases:
+            nsh = len(cuts) - 1
+            mine = list(range(rank * per, min(nsh, (rank + 1) * per)))
+            parts = [data[cuts[k]:cuts[k + 1]] for k in mine]
+
+            def sum_counters(cs):
+                allc = [None] * world
+                dist.all_gather_object(allc, cs)
+                out = [Counter() for _ in cs]
+                for other in allc:
+                    for v, c in enumerate(other):
+                        out[v].update(c)
+                return out
+
+            def gather(recs):
+                allr = [None] * world
+                dist.all_gather_object(allr, recs)
+                return [r for rr in allr for r in rr]
+
+            m, ids = S.train_sharded(parts, mm, sum_counters, gather, mine[0] if mine else 0, nsh)
+            allids = [None] * world
+            dist.all_gather_object(allids, ids)
+            results.append((m, [x for per_rank in allids for l in per_rank for x in l]))
+        if rank == 0:
+            q.put(results)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_step_two_processes_gloo():
+    """world_size 2: each process holds half of the shards and exchanges the
+    count deltas and edge records over gloo"""
+    import torch.multiprocessing as mp
+    cases = []
+    for data, cuts, mm in _cases(11, 12, nmax=120, kmax=8):
+        nsh = len(cuts) - 1
+        if nsh < 2:
+            continue
+        cases.append((data, cuts, mm, (nsh + 1) // 2))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, cases, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(results) == len(cases)
+    for (data, cuts, mm, _), (m, ids) in zip(cases, results):
+        om, oi, _ = O.train(data, mm, O.RULE)
+        assert [tuple(x) for x in om.tolist()] == m, (data, cuts)
+        assert list(oi) == ids, (data, cuts)
