@@ -11,9 +11,12 @@ with the final ids compacted in HBM.
 
 value = n_gpus * corpus_MB * K / wall   (MB = 1e6 bytes)
 
-Multi-GPU (torchrun, one rank per GPU): this round every rank trains an
-independent replica on its own 1 GiB slice (weak scaling, no exchange);
-see DESIGN.md "Multi-GPU" for the sharded-exchange plan.
+Multi-GPU (torchrun, one rank per GPU): ONE training job over an N GiB
+corpus cut into N contiguous 1 GiB shards (weak scaling).  Every merge
+allreduces the shards' count deltas and allgathers their 16-word edge records
+over RCCL (libbpe_amd.so's own communicator; torch.distributed/gloo only
+carries the RCCL id, the barrier and the max over ranks).  The merges are
+checked identical on every rank.  value = N * 1073.7 MB * K / wall.
 
 The JSON line also carries
   roofline     -- the dominant kernel of the loop (k_scan), its average span
@@ -81,21 +84,31 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=64 << 20)
     ap.add_argument("--cpu-merges", type=int, default=16)
+    ap.add_argument("--sharded", action="store_true",
+                    help="use the sharded (RCCL) path even with one rank")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    sharded = world > 1 or args.sharded
     dist = None
-    if world > 1:
+    if sharded:
         import torch
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from llmtokenizer_amd import api
-    e = api.Engine(local)
-    e.synth(args.seed, args.size, offset=rank * args.size)  # resident in HBM before timing
+    if sharded:
+        from llmtokenizer_amd import dist as bdist
+        e = bdist.rccl_group(local)
+        e.synth(0, args.seed, args.size, offset=rank * args.size)  # resident in HBM before timing
+    else:
+        e = api.Engine(local)
+        e.synth(args.seed, args.size)
 
     # warmup: a throwaway short run (kernels loaded, graphs captured, pools warm)
     if args.warmup > 0:
@@ -113,19 +126,28 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
+    same = True
     if dist is not None:
+        import hashlib
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        digests = [None] * world
+        dist.all_gather_object(digests, hashlib.md5(e.merges().tobytes()).hexdigest())
+        same = len(set(digests)) == 1
     st = e.stats()
     name, kms, kbytes, launches = e.kernel_profile()  # live, in-kernel wall clock
-    # corroboration with HIP events: event-record nodes spliced around every
-    # k_scan node of a second, shorter run (they add latency, so not in the timed run)
-    e.set_profile(True)
-    e.train(min(args.steps, 256))
-    ev_ms, ev_n = e.event_profile()
-    e.set_profile(False)
+    ev_ms, ev_n = 0.0, 0
+    if not sharded:
+        # corroboration with HIP events: event-record nodes spliced around every
+        # k_scan node of a second, shorter run (they add latency, so not in the timed run)
+        e.set_profile(True)
+        e.train(min(args.steps, 256))
+        ev_ms, ev_n = e.event_profile()
+        e.set_profile(False)
+    if dist is not None:
+        dist.barrier()
 
     if rank != 0:
         return
@@ -148,15 +170,18 @@ def main():
         "dtype": "u32",
         "data": "synthetic (random_text.txt-shaped, splitmix64 seed %d, generated in HBM)" % args.seed,
         "config": {"workload": "configs[3]: 1 GiB corpus/GPU, %d merges" % args.steps,
-                   "corpus_bytes_per_gpu": args.size, "merges": k,
-                   "parallelism": "replicas (independent per-GPU corpora)" if world > 1 else "single GPU"},
+                   "corpus_bytes_per_gpu": args.size, "corpus_bytes_total": args.size * world, "merges": k,
+                   "parallelism": ("dp%d: one training job, %d contiguous corpus shards, per merge RCCL allreduce "
+                                   "of count deltas + allgather of edge records" % (world, world)) if sharded
+                   else "single GPU",
+                   "merges_identical_across_ranks": same},
         # dominant kernel of the timed run: k_scan (latency-bound random gathers);
         # algorithmic bytes per launch = 8 B/candidate + 20 B/occurrence
         "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "bytes_per_launch": round(kbytes), "avg_ms": round(kms, 5), "launches": launches,
                      "avg_ms_source": "device wall clock inside the timed run (block-0 entry to last block exit)",
-                     "avg_ms_hip_events": round(ev_ms, 5), "hip_event_launches": ev_n,
+                     "avg_ms_hip_events": round(ev_ms, 5) if ev_n else None, "hip_event_launches": ev_n,
                      "note": "per-merge kernel is bound by dependent-load latency, not bandwidth; "
                              "event nodes add their own latency to the measured span"},
         # the one corpus-wide streaming pass (pair count over 1 B/token, V = 256)

@@ -153,6 +153,9 @@ int bpe_gpu_group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges);
 int bpe_gpu_group_fetch_merges(bpe_gpu_group *g, uint32_t *pairs, size_t cap, size_t *count);
 int bpe_gpu_group_fetch_ids(bpe_gpu_group *g, int k, uint32_t *ids, size_t cap, size_t *len);
 int bpe_gpu_group_get_stats(bpe_gpu_group *g, bpe_gpu_stats *st);
+/* bpe_gpu_kernel_profile of local shard k after a group train */
+int bpe_gpu_group_kernel_profile(bpe_gpu_group *g, int k, const char **name, double *avg_ms,
+                                 double *bytes_per_launch, uint64_t *launches);
 /* 1 when the per-merge exchange runs inside captured HIP graphs */
 int bpe_gpu_group_exchange_mode(bpe_gpu_group *g, int *graph_captured);
 

@@ -29,7 +29,7 @@ EXPORTS = [
     # bpe_gpu.h: sharded training
     "bpe_gpu_comm_id", "bpe_gpu_group_create", "bpe_gpu_group_destroy", "bpe_gpu_group_shards",
     "bpe_gpu_group_load", "bpe_gpu_group_synth", "bpe_gpu_group_train", "bpe_gpu_group_fetch_merges",
-    "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo",
+    "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo", "bpe_gpu_group_kernel_profile",
 ]
 
 
@@ -86,6 +86,9 @@ def load():
     L.bpe_gpu_group_fetch_ids.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_group_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats)]
     L.bpe_gpu_group_exchange_mode.argtypes = [vp, ip]
+    L.bpe_gpu_group_kernel_profile.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                               ctypes.POINTER(ctypes.c_uint64)]
     L.bpe_gpu_shard_halo.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp]
     L.bpe_gpu_fetch_merges.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_fetch_ids.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]

@@ -311,6 +311,15 @@ class ShardGroup:
         _lib.check(self.L.bpe_gpu_group_get_stats(self.g, ctypes.byref(st)), "stats")
         return st.as_dict()
 
+    def kernel_profile(self, k=0):
+        name = ctypes.c_char_p()
+        ms = ctypes.c_double()
+        by = ctypes.c_double()
+        n = ctypes.c_uint64()
+        _lib.check(self.L.bpe_gpu_group_kernel_profile(self.g, int(k), ctypes.byref(name), ctypes.byref(ms),
+                                                       ctypes.byref(by), ctypes.byref(n)), "kernel_profile")
+        return (name.value or b"").decode(), ms.value, by.value, n.value
+
     def graph_captured(self):
         v = ctypes.c_int()
         _lib.check(self.L.bpe_gpu_group_exchange_mode(self.g, ctypes.byref(v)), "exchange_mode")

@@ -419,7 +419,7 @@ void launch_summaries(bpe_gpu_ctx *c) {
 }
 
 void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
-    k_scan<<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
+    k_scan<false><<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
     k_apply<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
     if (tracked) launch_stats(c);
     launch_summaries(c);
@@ -452,7 +452,7 @@ int add_scan_events(bpe_gpu_ctx *c, hipGraph_t g, bool tracked) {
         if (ty == hipGraphNodeTypeKernel) {
             hipKernelNodeParams kp{};
             HIPCHK(hipGraphKernelNodeGetParams(cur, &kp));
-            if (kp.func == (void *)k_scan) {
+            if (kp.func == (void *)k_scan<false>) {
                 size_t np = 0;
                 hipGraphNode_t pred = nullptr;
                 HIPCHK(hipGraphNodeGetDependencies(cur, nullptr, &np));
@@ -486,7 +486,7 @@ int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
     for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++) {
         if (encode) {
-            k_scan<<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
+            k_scan<false><<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
             k_apply<<<APPLY_A, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
             k_enc_next<<<1, 1, 0, c->st>>>(c->dE, c->dC, c->d_enc_pairs, n_enc);
         } else {
@@ -906,6 +906,23 @@ int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_
     return init_sort(c, bh, unrank_out, d_tot_out);
 }
 
+// k_scan touches, per candidate, its 4-byte position and the token word it
+// validates; per replaced occurrence the partner, both neighbours and the
+// occurrence-list entry: 8 B + 20 B
+void fill_profile(bpe_gpu_ctx *c) {
+    const Ctl &C = *c->hC;
+    if (C.scan_launches) {
+        int khz = 0;
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
+        c->prof_name = "k_scan";
+        c->prof_ms = khz > 0 ? (double)C.scan_ticks / C.scan_launches / khz : 0;
+        c->prof_bytes = (8.0 * C.counters[4] + 20.0 * C.counters[5]) / std::max<double>(1.0, C.counters[0]);
+        c->prof_launches = C.scan_launches;
+    }
+    c->event_ms = c->scan_n ? c->scan_ms / c->scan_n : 0;
+    c->event_n = c->scan_n;
+}
+
 // a context on `device`; shared == nullptr creates its own stream
 int ctx_new(int device, hipStream_t shared, bpe_gpu_ctx **out) {
     bpe_gpu_ctx *c = new bpe_gpu_ctx();
@@ -1076,19 +1093,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.ms_init = t1 - t0;
     c->stats.ms_train = t2 - t1;
     c->stats.ms_total = t2 - t0;
-    // k_scan touches, per candidate, its 4-byte position and the token word it
-    // validates; per replaced occurrence the partner, both neighbours and the
-    // occurrence-list entry: 8 B + 20 B
-    if (C.scan_launches) {
-        int khz = 0;
-        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
-        c->prof_name = "k_scan";
-        c->prof_ms = khz > 0 ? (double)C.scan_ticks / C.scan_launches / khz : 0;
-        c->prof_bytes = (8.0 * C.counters[4] + 20.0 * C.counters[5]) / std::max<double>(1.0, C.counters[0]);
-        c->prof_launches = C.scan_launches;
-    }
-    c->event_ms = c->scan_n ? c->scan_ms / c->scan_n : 0;
-    c->event_n = c->scan_n;
+    fill_profile(c);
     return 0;
 }
 

@@ -69,9 +69,10 @@ struct Halo6 {
     uint32_t HL[3], HR[3];
 };
 
+template <bool SH>
 __device__ inline uint32_t id_at(const uint32_t *__restrict__ tok, const Halo6 &h, int64_t p, int64_t n) {
-    if (p < 0) return p >= -3 ? h.HL[-1 - p] : HOLE;
-    if (p >= n) return p - n < 3 ? h.HR[p - n] : HOLE;
+    if (p < 0) return SH && p >= -3 ? h.HL[-1 - p] : HOLE;
+    if (p >= n) return SH && p - n < 3 ? h.HR[p - n] : HOLE;
     return tok[p];
 }
 
@@ -79,11 +80,13 @@ __device__ inline uint32_t id_at(const uint32_t *__restrict__ tok, const Halo6 &
 // its own end slot (tok != HOLE there); a longer one stored its start distance
 // in dist[end] when it was created, or MARK when it starts in an earlier
 // shard -- so dist never needs initialising.
+template <bool SH = true>
 __device__ inline int64_t v_left(const uint32_t *__restrict__ tok, const uint32_t *__restrict__ dist, int64_t p) {
     if (p <= 0) return p - 1;
     const int64_t e = p - 1;
     if (tok[e] != HOLE) return e;
     const uint32_t d = dist[e];
+    if (!SH) return e - (int64_t)d;  // one shard: every dist[] is a real distance
     return (int64_t)d > e ? -1 : e - (int64_t)d;
 }
 
@@ -121,11 +124,14 @@ __device__ inline void stage_one(uint32_t *list, uint32_t *lcount, uint32_t *R, 
     else occz[atomicAdd(R, 1u)] = pos;  // overflow: straight out
 }
 
+// SH: sharded corpus (halo lookups, shard-edge step); the one-shard instance
+// compiles to the plain position-space scan
+template <bool SH>
 __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (blockIdx.x == 0 && threadIdx.x == 0) C->scan_t0 = wall_clock64();
     if (C->stop) return;
     const uint32_t len = C->cand_len;
-    const bool edge_block = E->sharded && blockIdx.x == 0;
+    const bool edge_block = SH && blockIdx.x == 0;
     if (blockIdx.x * SCAN_T >= len && !edge_block) {  // block-uniform
         scan_exit_stamp(E);
         return;
@@ -141,8 +147,11 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
     uint32_t *occz = E->occ + C->occ_top;
     Halo6 h;
 #pragma unroll
-    for (int m = 0; m < 3; m++) { h.HL[m] = C->HL[m]; h.HR[m] = C->HR[m]; }
-    const uint32_t hlrun = C->hlrun;
+    for (int m = 0; m < 3; m++) {
+        h.HL[m] = SH ? C->HL[m] : HOLE;
+        h.HR[m] = SH ? C->HR[m] : HOLE;
+    }
+    const uint32_t hlrun = SH ? C->hlrun : 0;
 
     __shared__ uint32_t s[4][DENSE];
     __shared__ uint32_t list[SCAN_T];
@@ -160,7 +169,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             if (mode == 2) {
                 j = E->occ[off + e];
                 if (tok[j] == b) {
-                    i = v_left(tok, dist, j);
+                    i = v_left<SH>(tok, dist, j);
                     ok = i >= 0 && tok[i] == a;  // i < 0: the pair is the left shard's
                 }
             } else {
@@ -176,21 +185,21 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             if (ok) {
                 list[slot] = (uint32_t)i;
                 if (count) {
-                    const int64_t ps = v_left(tok, dist, i);
-                    const uint32_t p = id_at(tok, h, ps, n);
+                    const int64_t ps = v_left<SH>(tok, dist, i);
+                    const uint32_t p = id_at<SH>(tok, h, ps, n);
                     if (p != HOLE) {
                         bool cov = false;
-                        if (p == b) cov = id_at(tok, h, v_left(tok, dist, ps), n) == a;
+                        if (p == b) cov = id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a;
                         if (!cov) {
                             vadd(s, E, P, V_DL, p);
                             vadd(s, E, P, V_IL, p);
                         }
                     }
                     const int64_t k = v_right(j, lb, n);
-                    const uint32_t q = id_at(tok, h, k, n);
+                    const uint32_t q = id_at<SH>(tok, h, k, n);
                     if (q != HOLE) {
                         vadd(s, E, P, V_DR, q);
-                        const bool nocc = q == a && id_at(tok, h, v_right(k, la, n), n) == b;
+                        const bool nocc = q == a && id_at<SH>(tok, h, v_right(k, la, n), n) == b;
                         vadd(s, E, P, V_IR, nocc ? z : q);
                     }
                 }
@@ -199,8 +208,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             // a == b: only the thread holding a run's first token walks it,
             // pairing tokens 0-1, 2-3, ... (greedy left-to-right).  A run that
             // enters from the left shard continues its parity (hlrun a's precede).
-            const int64_t ps = v_left(tok, dist, i);
-            const uint32_t p = id_at(tok, h, ps, n);
+            const int64_t ps = v_left<SH>(tok, dist, i);
+            const uint32_t p = id_at<SH>(tok, h, ps, n);
             bool start = true, left = p != HOLE;
             int64_t pos = i;
             if (p == a) {
@@ -213,7 +222,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 if (jj >= n || tok[jj] != a) break;  // crossing pair: the shard-edge step
                 const int64_t k = v_right(jj, la, n);
                 stage_one(list, &lcount, &C->R, occz, (uint32_t)pos);
-                const uint32_t q = id_at(tok, h, k, n);
+                const uint32_t q = id_at<SH>(tok, h, k, n);
                 const bool knext = q == a;
                 if (count) {
                     if (m == 0 && left) {
@@ -222,7 +231,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                     }
                     if (q != HOLE) {
                         vadd(s, E, P, V_DR, q);
-                        const bool nocc = knext && id_at(tok, h, v_right(k, la, n), n) == a;
+                        const bool nocc = knext && id_at<SH>(tok, h, v_right(k, la, n), n) == a;
                         vadd(s, E, P, V_IR, nocc ? z : q);
                     }
                 }
@@ -245,10 +254,10 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 if (tok[i] == a && h.HR[0] == b && (a != b || !(C->myidx & 1))) {
                     stage_one(list, &lcount, &C->R, occz, (uint32_t)i);
                     if (count) {
-                        const int64_t ps = v_left(tok, dist, i);
-                        const uint32_t p = id_at(tok, h, ps, n);
+                        const int64_t ps = v_left<SH>(tok, dist, i);
+                        const uint32_t p = id_at<SH>(tok, h, ps, n);
                         bool cov = p == HOLE;
-                        if (!cov) cov = a != b ? (p == b && id_at(tok, h, v_left(tok, dist, ps), n) == a) : p == a;
+                        if (!cov) cov = a != b ? (p == b && id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a) : p == a;
                         if (!cov) {
                             vadd(s, E, P, V_DL, p);
                             vadd(s, E, P, V_IL, p);

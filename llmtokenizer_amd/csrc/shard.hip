@@ -124,7 +124,7 @@ int launch_group_iteration(bpe_gpu_group *g) {
     int r;
     std::vector<uint32_t *> xb;
     for (bpe_gpu_ctx *c : g->cs) {
-        k_scan<<<SCAN_BLOCKS, SCAN_T, 0, g->st>>>(c->dE, c->dC);
+        k_scan<true><<<SCAN_BLOCKS, SCAN_T, 0, g->st>>>(c->dE, c->dC);
         const uint32_t nx = 4 * c->h.vcap + 2;
         k_pack<<<(nx + 255) / 256, 256, 0, g->st>>>(c->dE, c->dC);
         xb.push_back(c->h.xbuf);
@@ -324,6 +324,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         if ((r = compact_ids(c))) return r;
         c->merges_done = c->hC->merges_done;
         nout += c->ids_len;
+        fill_profile(c);
     }
     const Ctl &C = *g->cs[0]->hC;
     g->merges_done = C.merges_done;
@@ -459,6 +460,13 @@ int bpe_gpu_group_get_stats(bpe_gpu_group *g, bpe_gpu_stats *st) {
     if (!g || !st) return BPE_GPU_EINVAL;
     *st = g->stats;
     return 0;
+}
+
+int bpe_gpu_group_kernel_profile(bpe_gpu_group *g, int k, const char **name, double *avg_ms,
+                                 double *bytes_per_launch, uint64_t *launches) {
+    bpe_gpu_ctx *c = group_shard(g, k);
+    if (!c) return BPE_GPU_EINVAL;
+    return bpe_gpu_kernel_profile(c, name, avg_ms, bytes_per_launch, launches);
 }
 
 int bpe_gpu_group_exchange_mode(bpe_gpu_group *g, int *graph_captured) {
