@@ -122,6 +122,7 @@ struct Ctl {
     uint32_t hlrun;                   // consecutive a's immediately left of the first token
     uint32_t myidx;                   // run index of the last token (when it is an a)
     uint32_t F1, L1, L1new, xleft;    // first / last token start, pending last, consumed first
+    uint32_t done_scan, pad_;         // k_scan blocks finished (sharded: last one packs xbuf)
 };
 
 // Edge record of a shard: its first and last three token ids, the run of the

@@ -23,6 +23,12 @@ namespace bpeamd {
 
 __device__ inline uint32_t lane_id() { return __lane_id(); }
 
+// load that bypasses the (non-coherent) vector L1: values other blocks of the
+// same kernel produced before a fence
+__device__ inline uint32_t aload(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // wave-aggregated append: every lane of the wave must call it
 __device__ inline uint32_t wave_append(bool pred, uint32_t *counter) {
     unsigned long long m = __ballot(pred);
@@ -124,6 +130,43 @@ __device__ inline void stage_one(uint32_t *list, uint32_t *lcount, uint32_t *R, 
     else occz[atomicAdd(R, 1u)] = pos;  // overflow: straight out
 }
 
+// xbuf[v*vcap + x] = delta v of id x (dense replicas summed), xbuf[4*vcap] = R.
+// All loads are issued before any sum so one block needs ~2 round trips.
+__device__ inline void pack_exchange(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t P) {
+    const uint32_t vc = E->vcap, nd = min(vc, DENSE);
+    constexpr uint32_t U = 4;
+    for (uint32_t t0 = threadIdx.x; t0 < 4 * nd; t0 += U * SCAN_T) {
+        uint32_t val[U][REPL];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t t = min(t0 + u * SCAN_T, 4 * nd - 1);
+            const uint32_t v = t / nd, x = t % nd;
+#pragma unroll
+            for (uint32_t r = 0; r < REPL; r++) val[u][r] = aload(&E->vecd[(r * 4 + v) * DENSE + x]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t t = t0 + u * SCAN_T;
+            uint32_t sum = 0;
+#pragma unroll
+            for (uint32_t r = 0; r < REPL; r++) sum += val[u][r];
+            if (t < 4 * nd) E->xbuf[(t / nd) * vc + t % nd] = sum;
+        }
+    }
+    if (vc > DENSE) {
+        const uint32_t w = vc - DENSE;
+        for (uint32_t t = threadIdx.x; t < 4 * w; t += SCAN_T) {
+            const uint32_t v = t / w, x = DENSE + t % w;
+            E->xbuf[v * vc + x] = aload(&E->vec[P][v][x]);
+        }
+    }
+    if (threadIdx.x == 0) {
+        E->xbuf[4 * vc] = aload(&C->R);
+        E->xbuf[4 * vc + 1] = 0;
+        C->done_scan = 0;
+    }
+}
+
 // SH: sharded corpus (halo lookups, shard-edge step); the one-shard instance
 // compiles to the plain position-space scan
 template <bool SH>
@@ -131,7 +174,9 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
     if (blockIdx.x == 0 && threadIdx.x == 0) C->scan_t0 = wall_clock64();
     if (C->stop) return;
     const uint32_t len = C->cand_len;
-    const bool edge_block = SH && blockIdx.x == 0;
+    // the shard-edge step runs in the last block, which usually has no
+    // candidates, so its dependent loads overlap the other blocks' work
+    const bool edge_block = SH && blockIdx.x == gridDim.x - 1;
     if (blockIdx.x * SCAN_T >= len && !edge_block) {  // block-uniform
         scan_exit_stamp(E);
         return;
@@ -283,6 +328,23 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
         }
         __syncthreads();
     }
+    if (SH) {
+        // The last block to finish packs the dense exchange buffer (replicas
+        // summed, ids >= DENSE, R) that the shards allreduce next.  Everything
+        // it reads was produced by agent-scope atomics, drained before the
+        // arrival add; it reads with sc1 loads -- no fence needed (the
+        // returning-counter hand-off of MI355X_MICROARCH.md).
+        __shared__ uint32_t is_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t nact = min(gridDim.x, (len + SCAN_T - 1) / SCAN_T);
+            const uint32_t target = nact < gridDim.x ? nact + 1 : gridDim.x;  // + the edge block
+            is_last = atomicAdd(&C->done_scan, 1u) == target - 1;
+        }
+        __syncthreads();
+        if (is_last) pack_exchange(E, C, P);
+    }
     scan_exit_stamp(E);
 }
 
@@ -323,9 +385,7 @@ __device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v)
 // ---------------------------------------------------------------- k_apply
 constexpr uint32_t MARK_CAP = 1024;
 
-__global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *__restrict__ C,
-                                                uint32_t roleA_blocks) {
-    if (C->stop) return;
+__device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks) {
     const uint32_t a = C->a, b = C->b, z = C->z, R = C->R, P = C->parity;
     if (blockIdx.x < roleA_blocks) {
         const uint32_t la = E->tlen[a], lb = E->tlen[b];
@@ -463,6 +523,12 @@ __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *_
         __syncthreads();
     }
     if (threadIdx.x == 0 && sd[0] != 0) atomicAdd(&C->D, (unsigned long long)sd[0]);
+}
+
+__global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *__restrict__ C,
+                                                uint32_t roleA_blocks) {
+    if (C->stop) return;
+    apply_body(E, C, roleA_blocks);
 }
 
 // -------------------------------------------------------- summary rescans
@@ -696,58 +762,92 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
 }
 
 // ------------------------------------------------------------ shard exchange
-// dense copy of this shard's delta vectors (replicas summed) + its R, the
-// buffer every shard allreduces before k_apply
-__global__ __launch_bounds__(256) void k_pack(const Eng *__restrict__ E, const Ctl *__restrict__ C) {
-    const uint32_t vc = E->vcap, P = C->parity;
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < 4 * vc) {
-        const uint32_t v = t / vc, x = t % vc;
-        E->xbuf[t] = C->stop ? 0 : dval(E, P, v, x);
-    } else if (t == 4 * vc) {
-        E->xbuf[t] = C->stop ? 0 : C->R;
-    } else if (t == 4 * vc + 1) {
-        E->xbuf[t] = C->stop;
+// exclusive prefix of a predicate over a 256-thread block, and its total
+__device__ inline uint32_t block_prefix256(bool pred, uint32_t *total) {
+    __shared__ uint32_t wsum[4];
+    const unsigned long long m = __ballot(pred);
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t in_wave = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t k = 0; k < 4; k++) {
+        if (k < w) before += wsum[k];
+        tot += wsum[k];
     }
+    __syncthreads();
+    *total = tot;
+    return before + in_wave;
 }
 
-// this shard's edge record after k_apply (one thread; walks at most a few
-// tokens, plus the run of its last id)
-__global__ void k_edges(const Eng *__restrict__ E, Ctl *__restrict__ C, int force) {
-    if (threadIdx.x != 0 || (C->stop && !force)) return;
-    if (C->L1new != HOLE) { C->L1 = C->L1new; C->L1new = HOLE; }
-    const int64_t n = (int64_t)E->n0;
-    const uint32_t *tok = E->tok, *dist = E->dist, *tlen = E->tlen;
-    uint32_t r[EDGE_WORDS];
-    for (uint32_t w = 0; w < EDGE_WORDS; w++) r[w] = 0;
-    for (int m = 0; m < 3; m++) r[ER_F + m] = r[ER_L + m] = HOLE;
-    const int64_t F1 = C->F1, L1 = C->L1;
-    if (F1 < n) {
-        uint32_t c = 0;
-        for (int64_t p = F1; p <= L1 && c < 7; c++) {
-            const uint32_t id = tok[p];
-            if (c < 3) r[ER_F + c] = id;
-            p += tlen[id];
+// This shard's edge record (256 threads).  Token starts are exactly the
+// non-HOLE slots of [F1, L1], so the first / last tokens are found with
+// block-wide ballots over 256-slot windows (one round trip when tokens are
+// short) instead of a dependent walk.
+__device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    __shared__ uint32_t rec[EDGE_WORDS];
+    __shared__ uint32_t sF1, sL1, slast, firstdiff;
+    const uint32_t tid = threadIdx.x, T = 256;
+    const uint32_t *tok = E->tok;
+    if (tid == 0) {
+        const uint32_t l1n = aload(&C->L1new);
+        if (l1n != HOLE) {
+            C->L1 = l1n;
+            C->L1new = HOLE;
         }
-        r[ER_CNT] = c;
-        int64_t p = L1;
-        for (int m = 0; m < 3 && p >= 0; m++) {
-            r[ER_L + m] = tok[p];
-            p = v_left(tok, dist, p);
-        }
-        const uint32_t last = r[ER_L];
-        uint64_t trail = 0;
-        p = L1;
-        while (p >= 0 && tok[p] == last) {
-            trail++;
-            p = v_left(tok, dist, p);
-        }
-        r[ER_TRAIL] = trail > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)trail;
-        r[ER_ALL] = p < 0;
+        sL1 = l1n != HOLE ? l1n : aload(&C->L1);
+        sF1 = aload(&C->F1);
+        for (uint32_t w = 0; w < EDGE_WORDS; w++) rec[w] = 0;
+        for (int m = 0; m < 3; m++) rec[ER_F + m] = rec[ER_L + m] = HOLE;
+        firstdiff = HOLE;
     }
-    r[ER_NLO] = (uint32_t)E->n0;
-    r[ER_NHI] = (uint32_t)(E->n0 >> 32);
-    for (uint32_t w = 0; w < EDGE_WORDS; w++) E->myrec[w] = r[w];
+    __syncthreads();
+    const int64_t n = (int64_t)E->n0, F1 = sF1, L1 = sL1;
+    if (F1 < n) {
+        uint32_t found = 0;
+        for (int64_t base = F1; found < 7 && base <= L1; base += T) {
+            const int64_t p = base + tid;
+            const uint32_t v = p <= L1 ? aload(&tok[p]) : HOLE;
+            uint32_t tot;
+            const uint32_t r = found + block_prefix256(v != HOLE, &tot);
+            if (v != HOLE && r < 3) rec[ER_F + r] = v;
+            found += tot;
+        }
+        if (tid == 0) slast = aload(&tok[L1]);
+        __syncthreads();
+        const uint32_t last = slast;
+        uint32_t foundL = 0;
+        bool done = false;
+        for (int64_t top = L1; top >= F1 && (!done || foundL < 3); top -= T) {
+            const int64_t p = top - tid;  // rank from the end grows with tid
+            const uint32_t v = p >= F1 ? aload(&tok[p]) : HOLE;
+            uint32_t tot;
+            const uint32_t r = foundL + block_prefix256(v != HOLE, &tot);
+            if (v != HOLE && r < 3) rec[ER_L + r] = v;
+            if (v != HOLE && v != last) atomicMin(&firstdiff, r);
+            __syncthreads();
+            done = firstdiff != HOLE;
+            foundL += tot;
+        }
+        if (tid == 0) {
+            rec[ER_CNT] = found < 7 ? found : 7;
+            rec[ER_TRAIL] = done ? firstdiff : foundL;
+            rec[ER_ALL] = done ? 0 : 1;
+        }
+    }
+    if (tid == 0) {
+        rec[ER_NLO] = (uint32_t)E->n0;
+        rec[ER_NHI] = (uint32_t)(E->n0 >> 32);
+    }
+    __syncthreads();
+    if (tid < EDGE_WORDS) E->myrec[tid] = rec[tid];
+}
+
+// edge record after k_apply (its span writes are visible at the kernel
+// boundary) and at set-up (force); 256 threads
+__global__ __launch_bounds__(256) void k_edges(const Eng *__restrict__ E, Ctl *__restrict__ C, int force) {
+    if (C->stop && !force) return;
+    edge_record_block(E, C);
 }
 
 // one-device shard groups: the exchange is a sum / gather over the shards'

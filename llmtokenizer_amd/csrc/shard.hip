@@ -124,15 +124,13 @@ int launch_group_iteration(bpe_gpu_group *g) {
     int r;
     std::vector<uint32_t *> xb;
     for (bpe_gpu_ctx *c : g->cs) {
-        k_scan<true><<<SCAN_BLOCKS, SCAN_T, 0, g->st>>>(c->dE, c->dC);
-        const uint32_t nx = 4 * c->h.vcap + 2;
-        k_pack<<<(nx + 255) / 256, 256, 0, g->st>>>(c->dE, c->dC);
+        k_scan<true><<<SCAN_BLOCKS, SCAN_T, 0, g->st>>>(c->dE, c->dC);  // + packs xbuf
         xb.push_back(c->h.xbuf);
     }
     if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
     for (bpe_gpu_ctx *c : g->cs) {
         k_apply<<<APPLY_A + APPLY_B, 256, 0, g->st>>>(c->dE, c->dC, APPLY_A);
-        k_edges<<<1, 64, 0, g->st>>>(c->dE, c->dC, 0);
+        k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 0);
     }
     if ((r = ex_records(g, g->d_ptrs))) return r;
     for (bpe_gpu_ctx *c : g->cs) {
@@ -288,7 +286,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     for (uint32_t k = 0; k < K; k++)
         if ((r = init_sort(g->cs[k], pres, &unrank, &tot[k]))) return r;
     // 3. edge records, the byte pairs across edges, global byte-pair counts
-    for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 64, 0, g->st>>>(c->dE, c->dC, 1);
+    for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 1);
     if ((r = ex_records(g, g->d_ptrs))) return r;
     for (uint32_t k = 0; k < K; k++) k_init_cross<<<1, 64, 0, g->st>>>(g->cs[k]->dE, tot[k]);
     const uint32_t A = g->cs[0]->h.A, AA = A * A;
