@@ -59,6 +59,8 @@ typedef struct {
     double ms_train;          /* merge loop                                    */
     double ms_total;          /* init + loop (what bench.py times end to end)  */
     double ms_count_pass;     /* the one corpus-wide pair-count pass (k_pair_hist) */
+    uint64_t candidates;      /* candidate positions examined by the scans      */
+    uint64_t occurrences;     /* pair occurrences replaced                       */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */
@@ -150,6 +152,11 @@ int bpe_gpu_group_shards(bpe_gpu_group *g, int *local_shards, int *nshards, int 
 int bpe_gpu_group_load(bpe_gpu_group *g, int k, const uint8_t *bytes, size_t n);
 int bpe_gpu_group_synth(bpe_gpu_group *g, int k, uint64_t seed, size_t n, uint64_t offset);
 int bpe_gpu_group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges);
+/* Encode the shards' bytes with a merge list (ids 256 + r); the corpus ids are
+ * the shards' ids (bpe_gpu_group_fetch_ids) concatenated.  Exact across
+ * shard edges; a group of several shards on one device encodes corpora
+ * larger than 4 GiB. */
+int bpe_gpu_group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges);
 int bpe_gpu_group_fetch_merges(bpe_gpu_group *g, uint32_t *pairs, size_t cap, size_t *count);
 int bpe_gpu_group_fetch_ids(bpe_gpu_group *g, int k, uint32_t *ids, size_t cap, size_t *len);
 int bpe_gpu_group_get_stats(bpe_gpu_group *g, bpe_gpu_stats *st);

@@ -28,7 +28,7 @@ EXPORTS = [
     "bpe_gpu_last_error", "bpe_gpu_train_ex",
     # bpe_gpu.h: sharded training
     "bpe_gpu_comm_id", "bpe_gpu_group_create", "bpe_gpu_group_destroy", "bpe_gpu_group_shards",
-    "bpe_gpu_group_load", "bpe_gpu_group_synth", "bpe_gpu_group_train", "bpe_gpu_group_fetch_merges",
+    "bpe_gpu_group_load", "bpe_gpu_group_synth", "bpe_gpu_group_train", "bpe_gpu_group_encode", "bpe_gpu_group_fetch_merges",
     "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo", "bpe_gpu_group_kernel_profile",
 ]
 
@@ -37,7 +37,8 @@ class GpuStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "n_in", "n_out", "merges", "iterations", "distinct_pairs", "merged_buckets",
         "tracked_iters", "tie_events", "edge_events", "rule_ties", "table_grows", "keys")] + \
-        [(n, ctypes.c_double) for n in ("ms_init", "ms_train", "ms_total", "ms_count_pass")]
+        [(n, ctypes.c_double) for n in ("ms_init", "ms_train", "ms_total", "ms_count_pass")] + \
+        [(n, ctypes.c_uint64) for n in ("candidates", "occurrences")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -82,6 +83,7 @@ def load():
     L.bpe_gpu_group_load.argtypes = [vp, ctypes.c_int, vp, sz]
     L.bpe_gpu_group_synth.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, sz, ctypes.c_uint64]
     L.bpe_gpu_group_train.argtypes = [vp, ctypes.c_long, ctypes.POINTER(sz)]
+    L.bpe_gpu_group_encode.argtypes = [vp, vp, sz]
     L.bpe_gpu_group_fetch_merges.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_group_fetch_ids.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_group_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats)]

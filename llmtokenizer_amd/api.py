@@ -287,6 +287,10 @@ class ShardGroup:
         _lib.check(self.L.bpe_gpu_group_train(self.g, int(max_merges), ctypes.byref(m)), "group_train")
         return m.value
 
+    def encode(self, merges):
+        m = np.ascontiguousarray(merges, dtype=np.uint32).reshape(-1)
+        _lib.check(self.L.bpe_gpu_group_encode(self.g, m.ctypes.data_as(ctypes.c_void_p), m.size // 2), "group_encode")
+
     def merges(self):
         cnt = ctypes.c_size_t(0)
         _lib.check(self.L.bpe_gpu_group_fetch_merges(self.g, None, 0, ctypes.byref(cnt)), "fetch_merges")

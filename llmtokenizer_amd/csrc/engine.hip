@@ -15,6 +15,7 @@
 
 #include "../../include/bpe_gpu.h"
 #include "kernels.hip"
+#include "encode.hip"
 
 using namespace bpeamd;
 
@@ -52,6 +53,7 @@ constexpr uint32_t ITERS_PER_GRAPH = 16;
 constexpr uint32_t SCAN_BLOCKS = 1024;  // == k_select's block size (it reduces the exit stamps)
 constexpr uint32_t APPLY_A = 256, APPLY_B = 64;
 constexpr uint32_t RESCAN1_BLOCKS = 1024, RESCAN2_BLOCKS = 128;
+constexpr uint32_t ENC_APPLY_BLOCKS = 1024;
 
 struct Query {
     uint32_t t, bucket, firstc, flags;  // flags: 1 rho, 2 nb_less(new), 4 list mates
@@ -169,6 +171,7 @@ struct bpe_gpu_ctx {
     int dev = 0;
     hipStream_t st = nullptr;
     bool own_stream = true;
+    bool lean = false;                     // free init scratch at once (large sharded encodes)
     // run configuration (set before setup_run)
     uint32_t fast = 0;                     // schedule-free tie rule everywhere
     uint32_t sharded = 0, shard = 0, nshards = 1;
@@ -486,9 +489,8 @@ int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
     for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++) {
         if (encode) {
-            k_scan<false><<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
-            k_apply<<<APPLY_A, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
-            k_enc_next<<<1, 1, 0, c->st>>>(c->dE, c->dC, c->d_enc_pairs, n_enc);
+            k_scan_batch<false><<<SCAN_BLOCKS, ESCAN_T, 0, c->st>>>(c->dE, c->dC);
+            k_apply_batch<false><<<ENC_APPLY_BLOCKS + 1, 256, 0, c->st>>>(c->dE, c->dC);
         } else {
             launch_iteration(c, tracked);
         }
@@ -883,10 +885,18 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
         k_pair_colscan<<<(AA + 255) / 256, 256, 0, c->st>>>(d_hist, d_tot, AA, ntl);
         k_scan_single<<<1, 1024, 0, c->st>>>(d_tot, h.poff, AA);
         unsigned long long *d_tmp;
-        if ((r = dalloc(c, &d_tmp, npairs, false))) return r;
+        if (c->lean) {
+            HIPCHK(hipMalloc(&d_tmp, npairs * 8));
+        } else if ((r = dalloc(c, &d_tmp, npairs, false))) {
+            return r;
+        }
         k_sort_a<<<ntl, SORT_T, 0, c->st>>>(c->dE, d_hist, tile, d_tmp);
         k_sort_b<<<1024, SORT_T, 0, c->st>>>(c->dE, d_hist, d_tot, ntl, d_tmp);
         HIPCHK(hipGetLastError());
+        if (c->lean) {  // 8 B/byte of scratch back before the next shard sorts
+            HIPCHK(hipStreamSynchronize(c->st));
+            HIPCHK(hipFree(d_tmp));
+        }
     } else {
         HIPCHK(hipMemsetAsync(h.poff, 0, 4ull * (AA + 1), c->st));
     }
@@ -1090,6 +1100,8 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.tracked_iters = C.counters[1];
     c->stats.rule_ties = C.counters[2];
     c->stats.keys = C.nkeys;
+    c->stats.candidates = C.counters[4];
+    c->stats.occurrences = C.counters[5];
     c->stats.ms_init = t1 - t0;
     c->stats.ms_train = t2 - t1;
     c->stats.ms_total = t2 - t0;
@@ -1153,13 +1165,22 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
         if ((r = dalloc(c, &d_bh, 256))) return r;
         k_init_tok<<<1, 256, 0, c->st>>>(c->dE, d_bh);
     }
-    // first merge, then graph batches of (scan, apply, next)
-    HIPCHK(hipStreamSynchronize(c->st));
-    k_enc_next<<<1, 1, 0, c->st>>>(c->dE, c->dC, c->d_enc_pairs, (uint32_t)n_merges);
-    HIPCHK(hipGetLastError());
+    // merges in commuting batches: first batch, then graphs of (scan, apply + next batch)
+    EncBatch *d_eb;
+    if ((r = dalloc(c, &d_eb, 2))) return r;
+    c->h.eb = d_eb;
+    c->h.enc_pairs = c->d_enc_pairs;
+    c->h.n_enc = (uint32_t)n_merges;
+    if ((r = push_desc(c))) return r;
     if (c->n0 >= 2 && n_merges) {
+        k_enc_first<<<1, 256, 0, c->st>>>(c->dE, c->dC);
+        HIPCHK(hipGetLastError());
         if ((r = capture(c, &c->g_encode, false, true, (uint32_t)n_merges))) return r;
         if ((r = drive(c, true, (uint32_t)n_merges))) return r;
+        if ((r = pull_ctl(c))) return r;
+        c->stats.iterations = c->hC->counters[6];  // batches
+        c->stats.candidates = c->hC->counters[4];
+        c->stats.occurrences = c->hC->counters[5];
     }
     if ((r = compact_ids(c))) return r;
     const double t1 = now_ms();

@@ -41,6 +41,19 @@ enum : uint32_t {
     STOP_MODE = 7,     // n fell below 2^21: switch to the tracked iteration graph
 };
 
+// encode batch descriptor (encode.hip)
+constexpr uint32_t BMAX = 64;        // merges per batch
+constexpr uint32_t BSET = 512;       // LDS hash set of the batch's ids
+
+struct EncBatch {
+    uint32_t nb, total, occ_base, r0;  // nb: merges formed locally (sharded: a cut proposal)
+    uint32_t nbg;                      // merges applied (sharded: min over shards' proposals)
+    uint32_t a[BMAX], b[BMAX], z[BMAX], mode[BMAX], off[BMAX], len[BMAX], la[BMAX], lb[BMAX];
+    uint32_t seg[BMAX + 1];  // candidate segment offsets in the scratch buffer
+    uint32_t R[BMAX];        // occurrences found (atomic)
+};
+
+
 // Device-resident descriptor: every kernel takes a pointer to it, so tables can
 // be regrown without re-capturing the iteration graph.
 struct Eng {
@@ -91,6 +104,10 @@ struct Eng {
     uint32_t *xbuf;       // [4*vcap + 2] per-merge exchange: dense deltas | R | flags (allreduced)
     uint32_t *myrec;      // [EDGE_WORDS] this shard's edge record
     uint32_t *erec;       // [nshards * EDGE_WORDS] all edge records (allgathered)
+    // encode (batched replay of a merge list)
+    const uint32_t *enc_pairs;  // [2 * n_enc]
+    uint32_t n_enc;
+    EncBatch *eb;         // [2] double-buffered batch descriptors
 };
 
 struct Ctl {
@@ -122,14 +139,15 @@ struct Ctl {
     uint32_t hlrun;                   // consecutive a's immediately left of the first token
     uint32_t myidx;                   // run index of the last token (when it is an a)
     uint32_t F1, L1, L1new, xleft;    // first / last token start, pending last, consumed first
-    uint32_t done_scan, pad_;         // k_scan blocks finished (sharded: last one packs xbuf)
+    uint32_t xleft_lb;                // length of the consumed first token (encode batches)
+    uint32_t done_scan, ebp;          // k_scan blocks finished (sharded); encode batch parity
 };
 
 // Edge record of a shard: its first and last three token ids, the run of the
 // last id at its end, and whether the whole shard is that run.  The halo a
 // shard needs for one merge is a pure function of all records (and a), so it
 // is computed redundantly on every shard instead of being exchanged.
-enum { ER_CNT = 0, ER_F = 1, ER_L = 4, ER_TRAIL = 7, ER_ALL = 8, ER_NLO = 9, ER_NHI = 10 };
+enum { ER_CNT = 0, ER_F = 1, ER_L = 4, ER_TRAIL = 7, ER_ALL = 8, ER_NLO = 9, ER_NHI = 10, ER_CUT = 11 };
 
 struct Halo {
     uint32_t HL[3], HR[3], hlrun, myidx;

@@ -838,6 +838,8 @@ __device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C
     if (tid == 0) {
         rec[ER_NLO] = (uint32_t)E->n0;
         rec[ER_NHI] = (uint32_t)(E->n0 >> 32);
+        // encode: this shard's proposal for the next batch (the formed descriptor)
+        rec[ER_CUT] = E->encode ? E->eb[C->ebp].nb : 0;
     }
     __syncthreads();
     if (tid < EDGE_WORDS) E->myrec[tid] = rec[tid];

@@ -75,6 +75,7 @@ struct bpe_gpu_group {
     uint32_t **d_ptrs_tmp = nullptr;  // local mode: init-time tables
     hipGraphExec_t graph = nullptr;
     bool eager = false;               // collectives could not be graph-captured
+    bool encoding = false;            // the captured step is an encode batch
     size_t merges_done = 0;
     bpe_gpu_stats stats{};
 };
@@ -141,11 +142,22 @@ int launch_group_iteration(bpe_gpu_group *g) {
     return 0;
 }
 
+// one encode batch on every shard: scan, apply (+ next batch), edge records
+int launch_group_batch(bpe_gpu_group *g) {
+    for (bpe_gpu_ctx *c : g->cs) k_scan_batch<true><<<SCAN_BLOCKS, ESCAN_T, 0, g->st>>>(c->dE, c->dC);
+    for (bpe_gpu_ctx *c : g->cs) k_apply_batch<true><<<ENC_APPLY_BLOCKS + 1, 256, 0, g->st>>>(c->dE, c->dC);
+    for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 0);
+    HIPCHK(hipGetLastError());
+    return ex_records(g, g->d_ptrs);
+}
+
+int group_step(bpe_gpu_group *g) { return g->encoding ? launch_group_batch(g) : launch_group_iteration(g); }
+
 int capture_group(bpe_gpu_group *g) {
     hipGraph_t gr;
     HIPCHK(hipStreamBeginCapture(g->st, hipStreamCaptureModeThreadLocal));
     int r = 0;
-    for (uint32_t k = 0; k < ITERS_PER_GRAPH && !r; k++) r = launch_group_iteration(g);
+    for (uint32_t k = 0; k < ITERS_PER_GRAPH && !r; k++) r = group_step(g);
     hipError_t e = hipStreamEndCapture(g->st, &gr);
     if (r || e != hipSuccess) {
         (void)hipGetLastError();
@@ -181,11 +193,12 @@ int drive_group(bpe_gpu_group *g) {
                 HIPCHK(hipGraphLaunch(g->graph, g->st));
             } else {
                 for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++)
-                    if ((r = launch_group_iteration(g))) return r;
+                    if ((r = group_step(g))) return r;
             }
             break;
         case STOP_DONE:
         case STOP_CAP:
+        case STOP_ENC_END:
             return 0;
         case STOP_ERROR:
             return fail(BPE_GPU_EINTERNAL, C0.err == 1 ? "engine invariant violated (count decrement of an absent pair)"
@@ -235,6 +248,8 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     for (bpe_gpu_ctx *c : g->cs)
         if (!c->loaded || c->n0 < 1) return fail(BPE_GPU_ESTATE, "every shard needs at least one byte");
     group_free_graph(g);
+    g->encoding = false;
+    for (bpe_gpu_ctx *c : g->cs) c->lean = false;
     g->stats = bpe_gpu_stats{};
     g->merges_done = 0;
     *n_merges = 0;
@@ -342,6 +357,93 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     return 0;
 }
 
+// Encode every shard's bytes with a merge list: batches of commuting merges
+// (encode.hip), the same batch on every shard (cut = min of the shards'
+// proposals, carried in the edge records), pairs across edges owned by the
+// left shard as in training.
+int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
+    int r;
+    const uint32_t K = (uint32_t)g->cs.size();
+    for (bpe_gpu_ctx *c : g->cs)
+        if (!c->loaded || c->n0 < 1) return fail(BPE_GPU_ESTATE, "every shard needs at least one byte");
+    if (n_merges > 0xFFFFFEFFull) return fail(BPE_GPU_ERANGE, "merge list too long");
+    group_free_graph(g);
+    g->encoding = true;
+    g->stats = bpe_gpu_stats{};
+    const double t0 = now_ms();
+    uint64_t ntot;
+    if ((r = group_total(g, &ntot))) return r;
+    g->stats.n_in = ntot;
+    for (uint32_t k = 0; k < K; k++) {
+        bpe_gpu_ctx *c = g->cs[k];
+        c->stats = bpe_gpu_stats{};
+        c->merges_done = 0;
+        c->fast = 1;
+        c->sharded = 1;
+        c->shard = g->shard0 + k;
+        c->nshards = g->nshards;
+        c->lean = true;
+        if ((r = setup_run(c, (uint32_t)n_merges, true))) return r;
+        if (c->d_enc_pairs) hipFree(c->d_enc_pairs);
+        HIPCHK(hipMalloc(&c->d_enc_pairs, std::max<size_t>(n_merges, 1) * 8));
+        if (n_merges) HIPCHK(hipMemcpyAsync(c->d_enc_pairs, pairs, n_merges * 8, hipMemcpyHostToDevice, g->st));
+    }
+    if (!g->rccl) {
+        if (!g->d_ptrs) {
+            HIPCHK(hipMalloc(&g->d_ptrs, 3ull * K * sizeof(uint32_t *)));
+            HIPCHK(hipMalloc(&g->d_ptrs_tmp, (size_t)K * sizeof(uint32_t *)));
+        }
+        std::vector<uint32_t *> t;
+        for (auto *c : g->cs) t.push_back(c->h.xbuf);
+        for (auto *c : g->cs) t.push_back(c->h.myrec);
+        for (auto *c : g->cs) t.push_back(c->h.erec);
+        if ((r = upload_table(g, g->d_ptrs, t))) return r;
+    }
+    for (bpe_gpu_ctx *c : g->cs) {
+        uint32_t *d_bh;
+        if ((r = init_presence(c, &d_bh))) return r;
+        std::vector<uint32_t> bh(256);
+        HIPCHK(hipMemcpyAsync(bh.data(), d_bh, 1024, hipMemcpyDeviceToHost, g->st));
+        HIPCHK(hipStreamSynchronize(g->st));
+        std::vector<uint32_t> unrank;
+        uint32_t *d_tot;
+        if ((r = init_sort(c, bh, &unrank, &d_tot))) return r;
+        EncBatch *d_eb;
+        if ((r = dalloc(c, &d_eb, 2))) return r;
+        c->h.eb = d_eb;
+        c->h.enc_pairs = c->d_enc_pairs;
+        c->h.n_enc = (uint32_t)n_merges;
+        if ((r = push_desc(c))) return r;
+        k_enc_first<<<1, 256, 0, g->st>>>(c->dE, c->dC);
+    }
+    for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 1);
+    if ((r = ex_records(g, g->d_ptrs))) return r;
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(g->st));
+    const double t1 = now_ms();
+    if ((r = drive_group(g))) return r;
+    HIPCHK(hipStreamSynchronize(g->st));
+    uint64_t nout = 0;
+    for (bpe_gpu_ctx *c : g->cs) {
+        if ((r = pull_ctl(c))) return r;
+        if ((r = compact_ids(c))) return r;
+        c->merges_done = 0;
+        nout += c->ids_len;
+    }
+    const double t2 = now_ms();
+    const Ctl &C = *g->cs[0]->hC;
+    g->merges_done = 0;
+    g->stats.n_out = nout;
+    g->stats.merges = n_merges;
+    g->stats.iterations = C.counters[6];
+    g->stats.candidates = C.counters[4];
+    g->stats.occurrences = C.counters[5];
+    g->stats.ms_init = t1 - t0;
+    g->stats.ms_train = t2 - t1;
+    g->stats.ms_total = t2 - t0;
+    return 0;
+}
+
 bpe_gpu_ctx *group_shard(bpe_gpu_group *g, int k) {
     if (!g || k < 0 || (size_t)k >= g->cs.size()) return nullptr;
     return g->cs[k];
@@ -441,6 +543,12 @@ int bpe_gpu_group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     if (!g || !n_merges) return BPE_GPU_EINVAL;
     HIPCHK(hipSetDevice(g->dev));
     return group_train(g, max_merges, n_merges);
+}
+
+int bpe_gpu_group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
+    if (!g || (!pairs && n_merges)) return BPE_GPU_EINVAL;
+    HIPCHK(hipSetDevice(g->dev));
+    return group_encode(g, pairs, n_merges);
 }
 
 int bpe_gpu_group_fetch_merges(bpe_gpu_group *g, uint32_t *pairs, size_t cap, size_t *count) {

@@ -229,7 +229,7 @@ class Shard:
         return [x for x in self.tok if x != HOLE]
 
 
-def train_sharded(parts, max_merges, sum_counters, gather_records, first_shard, nshards):
+def train_sharded(parts, max_merges, sum_counters, gather_records, first_shard, nshards, forced=None):
     """Train on this process's shards `parts` (list of bytes, shard indices
     first_shard..).  sum_counters(list of 4 Counters + R) -> global; gather_records
     (list of local records) -> all records.  Returns (merges, [ids per local shard])."""
@@ -250,10 +250,21 @@ def train_sharded(parts, max_merges, sum_counters, gather_records, first_shard, 
     merges = []
     z = 256
     while max_merges < 0 or len(merges) < max_merges:
-        w = select(counts)
+        if forced is not None:  # encode: replay a given merge list
+            if len(merges) == len(forced):
+                break
+            w = forced[len(merges)]
+        else:
+            w = select(counts)
         if w is None:
             break
         a, b = w
+        if not (a < z and b < z):  # invalid record: no occurrence (tlen 1)
+            merges.append((a, b))
+            tlen[z] = 1
+            recs = gather_records([s.record(tlen) for s in shards])
+            z += 1
+            continue
         merges.append((a, b))
         tlen[z] = tlen[a] + tlen[b]
         for q, s in enumerate(shards):

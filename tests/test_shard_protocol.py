@@ -167,3 +167,24 @@ def test_sharded_step_two_processes_gloo():
         om, oi, _ = O.train(data, mm, O.RULE)
         assert [tuple(x) for x in om.tolist()] == m, (data, cuts)
         assert list(oi) == ids, (data, cuts)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_sharded_encode_replay_equals_oracle_encode(seed):
+    """the same per-shard step replaying a fixed merge list (encode)"""
+    rng = random.Random(500 + seed)
+    sc, ga = S.local_exchange()
+    for data, cuts, _ in _cases(600 + seed, 40):
+        alpha = sorted(set(data))
+        ids = list(alpha)
+        forced = []
+        for r in range(rng.randint(1, 60)):
+            u, v = rng.choice(ids), rng.choice(ids)
+            if rng.random() < 0.3:
+                v = u
+            forced.append((u, v))
+            ids.append(256 + r)
+        parts = [data[cuts[k]:cuts[k + 1]] for k in range(len(cuts) - 1)]
+        _, got = S.train_sharded(parts, -1, sc, ga, 0, len(parts), forced=forced)
+        want = O.encode(data, np.array(forced, dtype=np.uint32))
+        assert [x for l in got for x in l] == list(want), (data, cuts, forced)
