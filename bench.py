@@ -74,6 +74,81 @@ def cpu_baseline(seed, size, merges):
                       f"{dt:.1f} s wall (reference hard-codes 16 pthreads; host nproc={os.cpu_count()})"}
 
 
+def cpu_encode_baseline(merges, seed, size):
+    """Reference-structure encoder (the replace pass applied rank by rank,
+    oracle/bpe_oracle.c oracle_encode, one thread) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    from llmtokenizer_amd.synth import synth_bytes
+    data = synth_bytes(seed, size)
+    t0 = time.time()
+    O.encode(data, merges)
+    dt = time.time() - t0
+    return {"value": round(size / 1e6 / dt, 4), "unit": "MB/s", "cores": 1, "kind": "port",
+            "sample": f"{size >> 10} KiB prefix of the seed-{seed} stream, all {len(merges)} merges as "
+                      f"sequential replace passes, {dt:.1f} s wall"}
+
+
+def encode_bench(args, rank, world, local, dist, barrier):
+    """BASELINE configs[4]: encode a 10 GiB seed-3 stream with the first 32768
+    merges the GPU trainer learns on the 1 GiB seed-2 corpus.  Input resident
+    in HBM; timed = the whole encode (pair sort + batched merge replay + ids)."""
+    from llmtokenizer_amd import api
+    tr = api.Engine(local)  # same deterministic merges on every rank
+    tr.synth(args.seed, args.size)
+    tr.train(args.encode_merges)
+    merges = tr.merges()
+    tr.close()
+    total = args.encode_size
+    lo, hi = rank * (total // world), (total if rank == world - 1 else (rank + 1) * (total // world))
+    per = 3 << 30  # bytes per shard context (u32 positions)
+    if world > 1:
+        from llmtokenizer_amd import dist as bdist
+        g = bdist.rccl_group(local)
+        g.synth(0, 3, hi - lo, lo)
+    else:
+        k = max(1, -(-total // per))
+        g = api.ShardGroup(local, local_shards=k)
+        step = total // k
+        for q in range(k):
+            a = q * step
+            b = total if q == k - 1 else a + step
+            g.synth(q, 3, b - a, a)
+    g.encode(merges)  # warm (pools, graphs)
+    barrier()
+    t0 = time.perf_counter()
+    g.encode(merges)
+    t1 = time.perf_counter()
+    barrier()
+    el = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    st = g.stats()
+    n_out = st["n_out"]
+    if dist is not None:
+        import torch
+        t = torch.tensor([n_out], dtype=torch.int64)
+        dist.all_reduce(t)
+        n_out = int(t.item())
+    w = 2 if 256 + len(merges) <= 65536 else 4
+    alg = total + n_out * w  # SURVEY 8(d): input bytes + n_out * w
+    out = {"metric": "encode MB/s, 10 GiB stream through 32k merges", "value": round(total / 1e6 / el, 1),
+           "unit": "MB/s", "ms": round(el * 1e3, 2), "n_gpus": world, "bytes": total, "merges": len(merges),
+           "n_out": n_out, "shards": g.nshards, "batches": st["iterations"], "candidates": st["candidates"],
+           "occurrences": st["occurrences"], "breakdown_ms": {"init": round(st["ms_init"], 2),
+                                                             "replay": round(st["ms_train"], 2)},
+           "roofline": {"bound": "hbm", "achieved": round(alg / el / 1e9, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 5),
+                        "bytes": alg, "note": "whole-job algorithmic bytes (input + n_out*w) / wall"}}
+    g.close()
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_encode_baseline(merges, 3, args.cpu_encode_size)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -86,6 +161,10 @@ def main():
     ap.add_argument("--cpu-merges", type=int, default=16)
     ap.add_argument("--sharded", action="store_true",
                     help="use the sharded (RCCL) path even with one rank")
+    ap.add_argument("--no-encode", action="store_true", help="skip the configs[4] encode measurement")
+    ap.add_argument("--encode-size", type=int, default=10 << 30)
+    ap.add_argument("--encode-merges", type=int, default=32768)
+    ap.add_argument("--cpu-encode-size", type=int, default=256 << 10)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -148,6 +227,10 @@ def main():
         e.set_profile(False)
     if dist is not None:
         dist.barrier()
+    e.close()
+    enc = None
+    if not args.no_encode:
+        enc = encode_bench(args, rank, world, local, dist, barrier)
 
     if rank != 0:
         return
@@ -209,6 +292,8 @@ def main():
             out["roofline_count_pass"]["traffic"] = tr["k_pair_hist"]["traffic_bytes_per_launch"]
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.cpu_size, args.cpu_merges)
+    if enc is not None:
+        out["encode"] = enc
     print(json.dumps(out), flush=True)
 
 

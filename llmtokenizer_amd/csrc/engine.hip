@@ -171,7 +171,6 @@ struct bpe_gpu_ctx {
     int dev = 0;
     hipStream_t st = nullptr;
     bool own_stream = true;
-    bool lean = false;                     // free init scratch at once (large sharded encodes)
     // run configuration (set before setup_run)
     uint32_t fast = 0;                     // schedule-free tie rule everywhere
     uint32_t sharded = 0, shard = 0, nshards = 1;
@@ -212,17 +211,22 @@ int dalloc(bpe_gpu_ctx *c, T **p, size_t count, bool zero = true) {
     size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
     bytes = (bytes + 255) & ~(size_t)255;
     *p = nullptr;
+    // best fit among released buffers of the same size class (<= 1/8 larger)
+    size_t best = c->pool.size();
     for (size_t k = 0; k < c->pool.size(); k++) {
-        if (c->pool[k].second == bytes) {
-            *p = (T *)c->pool[k].first;
-            c->pool.erase(c->pool.begin() + k);
-            break;
-        }
+        const size_t sz = c->pool[k].second;
+        if (sz >= bytes && sz - bytes <= bytes / 8 && (best == c->pool.size() || sz < c->pool[best].second)) best = k;
+    }
+    if (best < c->pool.size()) {
+        *p = (T *)c->pool[best].first;
+        bytes = c->pool[best].second;
+        c->pool.erase(c->pool.begin() + best);
     }
     if (!*p) {
         hipError_t e = hipMalloc((void **)p, bytes);
         if (e != hipSuccess) {
             // return cached memory to the device and retry once
+            (void)hipGetLastError();  // the failed attempt must not stay the sticky error
             for (auto &q : c->pool) hipFree(q.first);
             c->pool.clear();
             e = hipMalloc((void **)p, bytes);
@@ -289,7 +293,14 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.plist, n0, false))) return r;
     // occurrences: at most one per retired token start, plus (sharded) one
     // crossing pair at the right edge per merge
-    if ((r = dalloc(c, &h.occ, n0 + (c->sharded ? (uint64_t)mcap + 64 : 0), false))) return r;
+    // occurrence pool + ids_out in ONE block: before the first merge it is the
+    // counting sort's 8 B/pair scratch (init_sort), so no extra 8n bytes
+    // (sharded: + one crossing occurrence per merge; the slack is sized so the
+    // block is the same for any merge count up to n0/16 and stays pooled)
+    const uint64_t slack = c->sharded ? std::max<uint64_t>((uint64_t)mcap + 64, n0 / 16) : 0;
+    const uint64_t occ_n = (n0 + slack + 2) & ~1ull;  // even: u64-aligned ids_out
+    if ((r = dalloc(c, &h.occ, occ_n + n0, false))) return r;
+    h.ids_out = h.occ + occ_n;
     if (c->sharded) {
         if ((r = dalloc(c, &h.xbuf, 4ull * h.vcap + 2))) return r;
         if ((r = dalloc(c, &h.myrec, EDGE_WORDS))) return r;
@@ -312,7 +323,6 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
     if ((r = dalloc(c, &c->d_tileoff, h.ntiles + 1))) return r;
-    if ((r = dalloc(c, &h.ids_out, n0, false))) return r;
     const uint64_t tn = std::min<uint64_t>(n0, TRACK_LIMIT);
     if ((r = dalloc(c, &h.cpos, encode ? 1 : tn, false))) return r;
     h.scap = encode ? 1024 : pow2_at_least(std::max<uint64_t>(1024, 2 * tn));
@@ -884,19 +894,12 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
         c->prof_launches = 1;
         k_pair_colscan<<<(AA + 255) / 256, 256, 0, c->st>>>(d_hist, d_tot, AA, ntl);
         k_scan_single<<<1, 1024, 0, c->st>>>(d_tot, h.poff, AA);
-        unsigned long long *d_tmp;
-        if (c->lean) {
-            HIPCHK(hipMalloc(&d_tmp, npairs * 8));
-        } else if ((r = dalloc(c, &d_tmp, npairs, false))) {
-            return r;
-        }
+        // scratch = the occurrence pool + ids_out block (>= 2n0 words, untouched
+        // until the first merge)
+        unsigned long long *d_tmp = reinterpret_cast<unsigned long long *>(h.occ);
         k_sort_a<<<ntl, SORT_T, 0, c->st>>>(c->dE, d_hist, tile, d_tmp);
         k_sort_b<<<1024, SORT_T, 0, c->st>>>(c->dE, d_hist, d_tot, ntl, d_tmp);
         HIPCHK(hipGetLastError());
-        if (c->lean) {  // 8 B/byte of scratch back before the next shard sorts
-            HIPCHK(hipStreamSynchronize(c->st));
-            HIPCHK(hipFree(d_tmp));
-        }
     } else {
         HIPCHK(hipMemsetAsync(h.poff, 0, 4ull * (AA + 1), c->st));
     }

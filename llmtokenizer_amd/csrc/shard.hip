@@ -249,7 +249,6 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         if (!c->loaded || c->n0 < 1) return fail(BPE_GPU_ESTATE, "every shard needs at least one byte");
     group_free_graph(g);
     g->encoding = false;
-    for (bpe_gpu_ctx *c : g->cs) c->lean = false;
     g->stats = bpe_gpu_stats{};
     g->merges_done = 0;
     *n_merges = 0;
@@ -382,7 +381,6 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
         c->sharded = 1;
         c->shard = g->shard0 + k;
         c->nshards = g->nshards;
-        c->lean = true;
         if ((r = setup_run(c, (uint32_t)n_merges, true))) return r;
         if (c->d_enc_pairs) hipFree(c->d_enc_pairs);
         HIPCHK(hipMalloc(&c->d_enc_pairs, std::max<size_t>(n_merges, 1) * 8));
@@ -436,8 +434,10 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
     g->stats.n_out = nout;
     g->stats.merges = n_merges;
     g->stats.iterations = C.counters[6];
-    g->stats.candidates = C.counters[4];
-    g->stats.occurrences = C.counters[5];
+    for (bpe_gpu_ctx *c : g->cs) {
+        g->stats.candidates += c->hC->counters[4];
+        g->stats.occurrences += c->hC->counters[5];
+    }
     g->stats.ms_init = t1 - t0;
     g->stats.ms_train = t2 - t1;
     g->stats.ms_total = t2 - t0;
