@@ -2,20 +2,26 @@
 //
 // Semantics: the reference's replace pass (bpe/src/bpe.c:760-779) applied merge
 // by merge in rank order.  Training discovers one merge at a time; encoding
-// knows the whole list, so consecutive merges are applied in BATCHES:
-// merges r..r+k-1 form a batch when no merge's pair (u,v) contains an id of
-// an earlier merge of the batch ({a, b, z}).  Such merges commute exactly:
-// a merge only rewrites tokens of its own two ids and every decision it makes
-// (occurrence validation, a==b run parity) reads only tokens of those ids,
-// which no other merge of the batch touches.  So a batch is scanned against
-// the pre-batch token state and applied at once.
+// knows the whole list, so consecutive merges are applied in BATCHES that
+// commute exactly.  Merges r..r+k-1 form a batch when, for every later merge
+// (c,d) against every earlier one (a,b) of the batch:
+//   * c, d were not created in the batch (c, d != z);
+//   * no id is used on the left in one merge and on the right in another;
+//   * no id of an a==b merge is used by another merge, and (c,d) != (a,b).
+// Then every occurrence of (c,d) in the state after (a,b) is an occurrence
+// in the state before it and vice versa: an x followed by y is untouched by
+// a merge of x with something else, a shared right id likewise, and a==b run
+// pairing only reads tokens no other merge of the batch touches.  So the
+// batch is scanned against the pre-batch token state and applied at once
+// (a 32768-merge list takes ~10^2 batches instead of 3*10^4 merge rounds).
 //
-// Per batch, two kernels (captured 16 batches per hipGraph):
-//   k_scan_batch   candidates of every merge of the batch (byte-pair lists
-//                  or occurrence lists, as in training), validated, written
-//                  to the merge's segment of the scratch buffer;
+// Per batch, three kernels (captured 16 batches per hipGraph):
+//   k_scan_batch   candidates of every merge of the batch (byte-pair lists,
+//                  or the later id's occurrence list filtered by neighbour
+//                  tag), validated, written to the merge's scratch segment;
 //   k_apply_batch  span rewrites + occurrence lists of the new ids; its last
-//                  block forms the next batch into the other descriptor.
+//                  block forms the next batch into the other descriptor;
+//   k_link_batch   neighbour tags of the new occurrence lists (post-batch).
 
 namespace bpeamd {
 
@@ -36,60 +42,75 @@ __device__ inline void enc_desc(const Eng *E, uint32_t u, uint32_t v, uint32_t z
         }
         return;
     }
-    const uint32_t lu = u >= 256 ? E->occ_len[u] : 0xFFFFFFFFu;
-    const uint32_t lv = v >= 256 ? E->occ_len[v] : 0xFFFFFFFFu;
-    if (u == v || lu <= lv) {
+    if (u >= v) {  // the later id's list, filtered by its neighbour tag (nb_tag)
         *off = E->occ_off[u];
-        *len = lu;
+        *len = E->occ_len[u];
     } else {
         *mode = 2;
         *off = E->occ_off[v];
-        *len = lv;
+        *len = E->occ_len[v];
     }
 }
 
-__device__ inline uint32_t bset_slot(uint32_t x) { return (uint32_t)(mix64(x) & (BSET - 1)); }
+// use flags of an id inside a forming batch
+enum : uint8_t { UF_L = 1, UF_R = 2, UF_Z = 4, UF_EQ = 8 };
 
-// Form the batch starting at merge r into *B (one block, >= BMAX threads).
-// occ_len / tlen of every id the candidates depend on are final: an id
-// created inside the batch ends it.
+// Form the batch starting at merge r into *B (one block).  occ_len / tlen of
+// every id the candidates depend on are final: an id created inside the
+// batch ends it.
 __device__ void form_batch(const Eng *__restrict__ E, Ctl *__restrict__ C, EncBatch *__restrict__ B, uint32_t r,
                            uint32_t occ_base) {
     const uint32_t slack = E->sharded ? 1 : 0;  // the edge step may add one occurrence per merge
     __shared__ uint32_t su[BMAX], sv[BMAX], smode[BMAX], soff[BMAX], slen[BMAX];
-    __shared__ uint32_t set[BSET];
+    __shared__ uint32_t mid[BIDS];
+    __shared__ uint8_t mfl[BIDS];
+    __shared__ unsigned long long pk[BPAIRS];
     __shared__ uint32_t snb, stotal;
     const uint32_t tid = threadIdx.x;
     const uint32_t nm = E->n_enc;
-    for (uint32_t x = tid; x < BSET; x += blockDim.x) set[x] = HOLE;
-    if (tid < BMAX && r + tid < nm) {
-        const uint32_t u = E->enc_pairs[2 * (r + tid)], v = E->enc_pairs[2 * (r + tid) + 1];
-        su[tid] = u;
-        sv[tid] = v;
-        enc_desc(E, u, v, 256 + r + tid, &smode[tid], &soff[tid], &slen[tid]);
+    for (uint32_t x = tid; x < BIDS; x += blockDim.x) { mid[x] = HOLE; mfl[x] = 0; }
+    for (uint32_t x = tid; x < BPAIRS; x += blockDim.x) pk[x] = ~0ull;
+    for (uint32_t m = tid; m < BMAX && r + m < nm; m += blockDim.x) {
+        const uint32_t u = E->enc_pairs[2 * (r + m)], v = E->enc_pairs[2 * (r + m) + 1];
+        su[m] = u;
+        sv[m] = v;
+        enc_desc(E, u, v, 256 + r + m, &smode[m], &soff[m], &slen[m]);
     }
     __syncthreads();
     if (tid == 0) {
+        auto slot = [&](uint32_t id) {
+            uint32_t s = (uint32_t)(mix64(id) & (BIDS - 1));
+            while (mid[s] != HOLE && mid[s] != id) s = (s + 1) & (BIDS - 1);
+            return s;
+        };
+        auto pslot = [&](unsigned long long key) {
+            uint32_t s = (uint32_t)(mix64(key) & (BPAIRS - 1));
+            while (pk[s] != ~0ull && pk[s] != key) s = (s + 1) & (BPAIRS - 1);
+            return s;
+        };
         const uint64_t cap = E->n0;  // scratch capacity; one merge never exceeds it
         uint64_t total = 0;
         uint32_t m = 0;
         for (; m < BMAX && r + m < nm; m++) {
-            const uint32_t ids[3] = {su[m], sv[m], 256 + r + m};
+            const uint32_t u = su[m], v = sv[m], z = 256 + r + m;
+            const unsigned long long key = ((unsigned long long)u << 32) | v;
+            const uint32_t iu = slot(u), iv = slot(v);
+            const uint32_t ip = pslot(key);
             if (m > 0) {
-                bool dep = total + slen[m] + slack > cap;
-                for (int q = 0; q < 2 && !dep; q++) {
-                    for (uint32_t s = bset_slot(ids[q]);; s = (s + 1) & (BSET - 1)) {
-                        if (set[s] == HOLE) break;
-                        if (set[s] == ids[q]) { dep = true; break; }
-                    }
-                }
+                const uint8_t fu = mid[iu] == u ? mfl[iu] : 0, fv = mid[iv] == v ? mfl[iv] : 0;
+                const bool dep = ((fu | fv) & (UF_Z | UF_EQ)) || (fu & UF_R) || (fv & UF_L) ||
+                                 (u == v && (fu | fv)) || pk[ip] == key || total + slen[m] + slack > cap;
                 if (dep) break;
             }
-            for (int q = 0; q < 3; q++) {
-                uint32_t s = bset_slot(ids[q]);
-                while (set[s] != HOLE && set[s] != ids[q]) s = (s + 1) & (BSET - 1);
-                set[s] = ids[q];
-            }
+            mid[iu] = u;
+            mfl[iu] |= UF_L | (u == v ? UF_EQ : 0);
+            const uint32_t iv2 = slot(v);  // (u == v: same slot)
+            mid[iv2] = v;
+            mfl[iv2] |= UF_R;
+            const uint32_t iz = slot(z);
+            mid[iz] = z;
+            mfl[iz] |= UF_Z;
+            pk[ip] = key;
             B->seg[m] = (uint32_t)total;
             total += slen[m] + slack;
         }
@@ -99,19 +120,19 @@ __device__ void form_batch(const Eng *__restrict__ E, Ctl *__restrict__ C, EncBa
     }
     __syncthreads();
     const uint32_t nb = snb;
-    if (tid < nb) {
-        const uint32_t u = su[tid], v = sv[tid], z = 256 + r + tid;
+    for (uint32_t m = tid; m < nb; m += blockDim.x) {
+        const uint32_t u = su[m], v = sv[m], z = 256 + r + m;
         const bool valid = u < z && v < z;
         const uint32_t lu = valid ? E->tlen[u] : 1, lv = valid ? E->tlen[v] : 1;
-        B->a[tid] = u;
-        B->b[tid] = v;
-        B->z[tid] = z;
-        B->mode[tid] = smode[tid];
-        B->off[tid] = soff[tid];
-        B->len[tid] = slen[tid];
-        B->la[tid] = lu;
-        B->lb[tid] = lv;
-        B->R[tid] = 0;
+        B->a[m] = u;
+        B->b[m] = v;
+        B->z[m] = z;
+        B->mode[m] = smode[m];
+        B->off[m] = soff[m];
+        B->len[m] = slen[m];
+        B->la[m] = lu;
+        B->lb[m] = lv;
+        B->R[m] = 0;
         E->tlen[z] = valid ? lu + lv : 1;
     }
     if (tid == 0) {
@@ -120,6 +141,30 @@ __device__ void form_batch(const Eng *__restrict__ E, Ctl *__restrict__ C, EncBa
         B->occ_base = occ_base;
         B->r0 = r;
     }
+}
+
+// exclusive prefix of in[0..n) into out[0..n] (out[n] = total), 256 threads
+__device__ inline void block_exscan256(const uint32_t *in, uint32_t *out, uint32_t n) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t per = (n + 255) / 256, lo = threadIdx.x * per, hi = min(n, lo + per);
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; i++) sum += in[i];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (uint32_t k = 0; k < w; k++) run += wsum[k];
+    for (uint32_t i = lo; i < hi; i++) {
+        out[i] = run;
+        run += in[i];
+    }
+    if (threadIdx.x == 255) out[n] = run;  // the last thread's range ends at n (or is empty: run = total)
+    __syncthreads();
 }
 
 // first batch (set-up)
@@ -168,26 +213,27 @@ __global__ __launch_bounds__(ESCAN_T) void k_scan_batch(const Eng *__restrict__ 
     }
     const uint32_t total = B->seg[nb];
     if (blockIdx.x * ESCAN_T >= total && !edge_block) return;
-    __shared__ uint32_t sseg[BMAX + 1], sa[BMAX], sb[BMAX], smode[BMAX], soff[BMAX], sla[BMAX];
+    __shared__ uint32_t sseg[BMAX + 1], sa[BMAX], sb[BMAX], smode[BMAX], soff[BMAX], sla[BMAX], slen[BMAX];
     __shared__ uint32_t shl[BMAX], smy[BMAX];
     __shared__ uint32_t cnt[BMAX], base[BMAX];
     __shared__ uint32_t lpos[ESCAN_T], lm[ESCAN_T], lrk[ESCAN_T];
     __shared__ uint32_t lcount;
     __shared__ Halo6 sh;
-    if (tid <= nb) sseg[tid] = B->seg[tid];
-    if (tid < nb) {
-        sa[tid] = B->a[tid];
-        sb[tid] = B->b[tid];
-        smode[tid] = B->mode[tid];
-        soff[tid] = B->off[tid];
-        sla[tid] = B->la[tid];
-        cnt[tid] = 0;
-        if (SH) {  // halo of merge tid (run counts depend on its a)
+    for (uint32_t m = tid; m <= nb; m += ESCAN_T) sseg[m] = B->seg[m];
+    for (uint32_t m = tid; m < nb; m += ESCAN_T) {
+        sa[m] = B->a[m];
+        sb[m] = B->b[m];
+        smode[m] = B->mode[m];
+        soff[m] = B->off[m];
+        sla[m] = B->la[m];
+        slen[m] = B->len[m];
+        cnt[m] = 0;
+        if (SH) {  // halo of merge m (run counts depend on its a)
             Halo hl;
-            shard_halo(E->erec, E->nshards, E->shard, B->a[tid], &hl);
-            shl[tid] = hl.hlrun;
-            smy[tid] = hl.myidx;
-            if (tid == 0)
+            shard_halo(E->erec, E->nshards, E->shard, B->a[m], &hl);
+            shl[m] = hl.hlrun;
+            smy[m] = hl.myidx;
+            if (m == 0)
                 for (int q = 0; q < 3; q++) { sh.HL[q] = hl.HL[q]; sh.HR[q] = hl.HR[q]; }
         }
     }
@@ -201,19 +247,19 @@ __global__ __launch_bounds__(ESCAN_T) void k_scan_batch(const Eng *__restrict__ 
         const uint32_t t = t0 + tid;
         const uint32_t m = t < total ? seg_of(sseg, nb, t) : 0;
         const uint32_t q = t - sseg[m];
-        if (t < total && q < B->len[m]) {  // (the sharded slack slot is not a candidate)
+        if (t < total && q < slen[m]) {  // (the sharded slack slot is not a candidate)
             const uint32_t a = sa[m], b = sb[m], la = sla[m], md = smode[m];
             bool ok = false;
             int64_t i = 0, j = 0;
             if (md == 2) {
                 j = E->occ[soff[m] + q];
-                if (tok[j] == b) {
+                if (tag_ok(E->occnb[soff[m] + q] >> 8, a) && tok[j] == b) {
                     i = v_left<SH>(tok, dist, j);
                     ok = i >= 0 && tok[i] == a;  // i < 0: the left shard's pair
                 }
             } else {
                 i = md == 0 ? E->plist[soff[m] + q] : E->occ[soff[m] + q];
-                if (tok[i] == a) {
+                if ((md == 0 || tag_ok(E->occnb[soff[m] + q] & 0xFFu, b)) && tok[i] == a) {
                     j = i + la;
                     ok = j < (int64_t)n && tok[j] == b;  // crossing pairs: the edge step
                 }
@@ -251,9 +297,9 @@ __global__ __launch_bounds__(ESCAN_T) void k_scan_batch(const Eng *__restrict__ 
             }
         }
         __syncthreads();
-        if (tid < nb) {
-            base[tid] = cnt[tid] ? atomicAdd(&B->R[tid], cnt[tid]) : 0;
-            cnt[tid] = 0;
+        for (uint32_t mm = tid; mm < nb; mm += ESCAN_T) {
+            base[mm] = cnt[mm] ? atomicAdd(&B->R[mm], cnt[mm]) : 0;
+            cnt[mm] = 0;
         }
         __syncthreads();
         const uint32_t ln = min(lcount, ESCAN_T);
@@ -269,14 +315,14 @@ __global__ __launch_bounds__(ESCAN_T) void k_scan_batch(const Eng *__restrict__ 
         if (tid == 0) C->xleft = HOLE;
         __syncthreads();
         const int64_t F1 = C->F1, L1 = C->L1;
-        if (tid < nb && F1 < (int64_t)n) {
-            const uint32_t a = sa[tid], b = sb[tid];
-            if (sh.HL[0] == a && tok[F1] == b && (a != b || (shl[tid] & 1))) {
+        for (uint32_t m = tid; m < nb && F1 < (int64_t)n; m += ESCAN_T) {
+            const uint32_t a = sa[m], b = sb[m];
+            if (sh.HL[0] == a && tok[F1] == b && (a != b || (shl[m] & 1))) {
                 C->xleft = (uint32_t)F1;
-                C->xleft_lb = B->lb[tid];
+                C->xleft_lb = B->lb[m];
             }
-            if (tok[L1] == a && sh.HR[0] == b && (a != b || !(smy[tid] & 1)))
-                scratch[sseg[tid] + atomicAdd(&B->R[tid], 1u)] = (uint32_t)L1;
+            if (tok[L1] == a && sh.HR[0] == b && (a != b || !(smy[m] & 1)))
+                scratch[sseg[m] + atomicAdd(&B->R[m], 1u)] = (uint32_t)L1;
         }
     }
 }
@@ -289,29 +335,24 @@ __global__ __launch_bounds__(256) void k_apply_batch(const Eng *__restrict__ E, 
     const uint32_t nb = B->nbg;
     __shared__ uint32_t sseg[BMAX + 1], sz[BMAX], sla[BMAX], slb[BMAX], sR[BMAX], spre[BMAX + 1];
     const uint32_t tid = threadIdx.x;
-    if (tid <= nb) sseg[tid] = B->seg[tid];
-    if (tid < nb) {
-        sz[tid] = B->z[tid];
-        sla[tid] = B->la[tid];
-        slb[tid] = B->lb[tid];
-        sR[tid] = B->R[tid];
+    for (uint32_t m = tid; m <= nb; m += blockDim.x) sseg[m] = B->seg[m];
+    for (uint32_t m = tid; m < nb; m += blockDim.x) {
+        sz[m] = B->z[m];
+        sla[m] = B->la[m];
+        slb[m] = B->lb[m];
+        sR[m] = B->R[m];
     }
     __syncthreads();
-    if (tid == 0) {
-        uint32_t run = 0;
-        for (uint32_t m = 0; m < nb; m++) { spre[m] = run; run += sR[m]; }
-        spre[nb] = run;
-    }
-    __syncthreads();
+    block_exscan256(sR, spre, nb);
     const uint32_t occ_base = B->occ_base;
     const uint64_t n = E->n0;
     uint32_t *tok = E->tok, *dist = E->dist;
     if (blockIdx.x == gridDim.x - 1) {
         // bookkeeping of this batch, my retired first token, then the next
         // batch into the other descriptor
-        if (tid < nb) {
-            E->occ_off[sz[tid]] = occ_base + spre[tid];
-            E->occ_len[sz[tid]] = sR[tid];
+        for (uint32_t m = tid; m < nb; m += blockDim.x) {
+            E->occ_off[sz[m]] = occ_base + spre[m];
+            E->occ_len[sz[m]] = sR[m];
         }
         if (tid == 0) {
             C->counters[0] += nb;
@@ -349,6 +390,37 @@ __global__ __launch_bounds__(256) void k_apply_batch(const Eng *__restrict__ E, 
             if (SH && j == L1) C->L1new = (uint32_t)i;
         }
         E->occ[occ_base + spre[m] + q] = (uint32_t)i;
+    }
+}
+
+// Neighbour tags of the batch just applied (post-batch neighbours: other
+// merges of the batch may have replaced them); outside the shard: unknown.
+template <bool SH>
+__global__ __launch_bounds__(256) void k_link_batch(const Eng *__restrict__ E, const Ctl *__restrict__ C) {
+    if (C->stop) return;
+    const EncBatch *B = E->eb + (C->ebp ^ 1u);  // k_apply_batch already flipped to the next batch
+    const uint32_t nb = B->nbg;
+    __shared__ uint32_t sseg[BMAX + 1], sz[BMAX], sR[BMAX], spre[BMAX + 1];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t m = tid; m <= nb; m += blockDim.x) sseg[m] = B->seg[m];
+    for (uint32_t m = tid; m < nb; m += blockDim.x) {
+        sz[m] = B->z[m];
+        sR[m] = B->R[m];
+    }
+    __syncthreads();
+    block_exscan256(sR, spre, nb);
+    const uint32_t total = sseg[nb], occ_base = B->occ_base;
+    const int64_t n = (int64_t)E->n0;
+    const uint32_t *tok = E->tok, *dist = E->dist;
+    for (uint32_t t = blockIdx.x * blockDim.x + tid; t < total; t += gridDim.x * blockDim.x) {
+        const uint32_t m = seg_of(sseg, nb, t);
+        const uint32_t q = t - sseg[m];
+        if (q >= sR[m]) continue;
+        const uint32_t e = occ_base + spre[m] + q;
+        const int64_t i = E->occ[e];
+        const int64_t ps = v_left<SH>(tok, dist, i);
+        const int64_t k = i + E->tlen[sz[m]];
+        E->occnb[e] = nb_tag(ps >= 0 ? tok[ps] : HOLE, k < n ? tok[k] : HOLE);
     }
 }
 

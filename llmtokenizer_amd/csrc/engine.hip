@@ -188,6 +188,7 @@ struct bpe_gpu_ctx {
     uint32_t *d_tileoff = nullptr;
     uint32_t *d_enc_pairs = nullptr;
     hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr;
+    std::vector<hipGraphExec_t> retired;  // replaced graphs, destroyed with the run
     bpe_gpu_stats stats{};
     // profile of the dominant kernel: HIP events captured around every k_scan
     // node of the iteration graphs (bpe_gpu_set_profile)
@@ -253,6 +254,8 @@ void free_train(bpe_gpu_ctx *c, bool release = false) {
         if (*g) (void)hipGraphExecDestroy(*g);
         *g = nullptr;
     }
+    for (hipGraphExec_t g : c->retired) (void)hipGraphExecDestroy(g);
+    c->retired.clear();
     c->ids_ready = false;
 }
 
@@ -301,6 +304,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     const uint64_t occ_n = (n0 + slack + 2) & ~1ull;  // even: u64-aligned ids_out
     if ((r = dalloc(c, &h.occ, occ_n + n0, false))) return r;
     h.ids_out = h.occ + occ_n;
+    if ((r = dalloc(c, &h.occnb, occ_n, false))) return r;
     if (c->sharded) {
         if ((r = dalloc(c, &h.xbuf, 4ull * h.vcap + 2))) return r;
         if ((r = dalloc(c, &h.myrec, EDGE_WORDS))) return r;
@@ -409,10 +413,14 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
     void *news[] = {nkey, ncnt, l1b, l1k, l1t, l1l, l2b, l2k, l2t, l2l};
     for (int k = 0; k < 10; k++) c->train_allocs.push_back({news[k], sizes[k]});
     c->stats.table_grows++;
-    // iteration graphs depend on the table size (level-2 summaries): recapture
-    for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked}) {
-        if (*g) (void)hipGraphExecDestroy(*g);
-        *g = nullptr;
+    // the iteration graphs read every table pointer through the device
+    // descriptor; only the level-2 summary launch depends on the size, so
+    // recapture only when that changes (old graphs are released with the run)
+    if ((ocap / L1W > SELECT_L1_MAX) != (ncap / L1W > SELECT_L1_MAX)) {
+        for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked}) {
+            if (*g) c->retired.push_back(*g);
+            *g = nullptr;
+        }
     }
     return 0;
 }
@@ -501,6 +509,7 @@ int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint
         if (encode) {
             k_scan_batch<false><<<SCAN_BLOCKS, ESCAN_T, 0, c->st>>>(c->dE, c->dC);
             k_apply_batch<false><<<ENC_APPLY_BLOCKS + 1, 256, 0, c->st>>>(c->dE, c->dC);
+            k_link_batch<false><<<ENC_APPLY_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
         } else {
             launch_iteration(c, tracked);
         }

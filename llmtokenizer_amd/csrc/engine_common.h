@@ -42,8 +42,9 @@ enum : uint32_t {
 };
 
 // encode batch descriptor (encode.hip)
-constexpr uint32_t BMAX = 64;        // merges per batch
-constexpr uint32_t BSET = 512;       // LDS hash set of the batch's ids
+constexpr uint32_t BMAX = 512;       // merges per batch
+constexpr uint32_t BIDS = 2048;      // LDS id -> use-flags map of a forming batch (>= 3 BMAX)
+constexpr uint32_t BPAIRS = 1024;    // LDS set of the batch's pairs (> BMAX)
 
 struct EncBatch {
     uint32_t nb, total, occ_base, r0;  // nb: merges formed locally (sharded: a cut proposal)
@@ -70,6 +71,7 @@ struct Eng {
     uint32_t *plist;      // byte-pair positions grouped by rank key (counting sort)
     uint32_t *poff;       // [A*A + 1]
     uint32_t *occ;        // occurrence pool: positions where merged id z was created
+    uint16_t *occnb;      // per occ entry: neighbour tag (kernels.hip nb_tag)
     uint32_t *occ_off;    // [vcap]
     uint32_t *occ_len;    // [vcap]
     uint32_t *merges;     // [2 * mcap]

@@ -105,13 +105,29 @@ __device__ inline int64_t v_right(int64_t p, uint32_t len, int64_t n) {
 
 constexpr uint32_t SCAN_T = 1024;  // threads per k_scan block = candidates per round
 
-// append the block's staged occurrence positions to the new id's list
-__device__ inline void flush_list(uint32_t *list, uint32_t *lcount, uint32_t *gbase, uint32_t *R, uint32_t *occz) {
+// Neighbour tag of an occurrence-list entry: low bytes of the ids left and
+// right of the new token right after it was created (0xFF: none / unknown,
+// matches anything).  A pair (u,v) can only become adjacent when the LATER
+// of u, v is created, so the later id's list filtered by the tag holds every
+// (u,v) occurrence; most non-matching entries cost a coalesced 2-byte read
+// instead of random token gathers.
+__device__ inline uint16_t nb_tag(uint32_t p, uint32_t q) {
+    const uint32_t p8 = p == HOLE ? 0xFFu : (p & 0xFFu), q8 = q == HOLE ? 0xFFu : (q & 0xFFu);
+    return (uint16_t)((p8 << 8) | q8);
+}
+__device__ inline bool tag_ok(uint32_t t8, uint32_t id) { return t8 == 0xFFu || t8 == (id & 0xFFu); }
+
+// append the block's staged occurrence positions (+ tags) to the new id's list
+__device__ inline void flush_list(uint32_t *list, uint16_t *ltag, uint32_t *lcount, uint32_t *gbase, uint32_t *R,
+                                  uint32_t *occz, uint16_t *tagz) {
     __syncthreads();
     const uint32_t n = min(*lcount, SCAN_T);
     if (threadIdx.x == 0) *gbase = n ? atomicAdd(R, n) : 0;
     __syncthreads();
-    if (threadIdx.x < n) occz[*gbase + threadIdx.x] = list[threadIdx.x];
+    if (threadIdx.x < n) {
+        occz[*gbase + threadIdx.x] = list[threadIdx.x];
+        tagz[*gbase + threadIdx.x] = ltag[threadIdx.x];
+    }
     __syncthreads();
     if (threadIdx.x == 0) *lcount = 0;
     __syncthreads();
@@ -124,10 +140,17 @@ __device__ inline void scan_exit_stamp(const Eng *E) {
 }
 
 // stage one occurrence position (single-thread path: walker / shard edge)
-__device__ inline void stage_one(uint32_t *list, uint32_t *lcount, uint32_t *R, uint32_t *occz, uint32_t pos) {
+__device__ inline void stage_one(uint32_t *list, uint16_t *ltag, uint32_t *lcount, uint32_t *R, uint32_t *occz,
+                                 uint16_t *tagz, uint32_t pos, uint16_t tag) {
     const uint32_t slot = atomicAdd(lcount, 1u);
-    if (slot < SCAN_T) list[slot] = pos;
-    else occz[atomicAdd(R, 1u)] = pos;  // overflow: straight out
+    if (slot < SCAN_T) {
+        list[slot] = pos;
+        ltag[slot] = tag;
+    } else {  // overflow: straight out
+        const uint32_t g = atomicAdd(R, 1u);
+        occz[g] = pos;
+        tagz[g] = tag;
+    }
 }
 
 // xbuf[v*vcap + x] = delta v of id x (dense replicas summed), xbuf[4*vcap] = R.
@@ -190,6 +213,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
     const uint32_t la = E->tlen[a], lb = E->tlen[b];
     const bool count = !E->encode;
     uint32_t *occz = E->occ + C->occ_top;
+    uint16_t *tagz = E->occnb + C->occ_top;
+    const uint32_t want = mode == 2 ? a : b;  // tag byte the candidates must carry
     Halo6 h;
 #pragma unroll
     for (int m = 0; m < 3; m++) {
@@ -200,6 +225,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
 
     __shared__ uint32_t s[4][DENSE];
     __shared__ uint32_t list[SCAN_T];
+    __shared__ uint16_t ltag[SCAN_T];
     __shared__ uint32_t lcount, gbase;
     if (count)
         for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) (&s[0][0])[x] = 0;
@@ -213,13 +239,13 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
         if (e < len) {
             if (mode == 2) {
                 j = E->occ[off + e];
-                if (tok[j] == b) {
+                if (tag_ok(E->occnb[off + e] >> 8, want) && tok[j] == b) {
                     i = v_left<SH>(tok, dist, j);
                     ok = i >= 0 && tok[i] == a;  // i < 0: the pair is the left shard's
                 }
             } else {
                 i = (mode == 0) ? E->plist[off + e] : E->occ[off + e];
-                if (tok[i] == a) {
+                if ((mode == 0 || tag_ok(E->occnb[off + e] & 0xFFu, want)) && tok[i] == a) {
                     j = i + la;
                     ok = j < n && tok[j] == b;  // j >= n: crossing pair, handled below
                 }
@@ -229,25 +255,27 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             const uint32_t slot = wave_append(ok, &lcount);  // LDS counter
             if (ok) {
                 list[slot] = (uint32_t)i;
-                if (count) {
-                    const int64_t ps = v_left<SH>(tok, dist, i);
-                    const uint32_t p = id_at<SH>(tok, h, ps, n);
-                    if (p != HOLE) {
-                        bool cov = false;
-                        if (p == b) cov = id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a;
-                        if (!cov) {
-                            vadd(s, E, P, V_DL, p);
-                            vadd(s, E, P, V_IL, p);
-                        }
+                const int64_t ps = v_left<SH>(tok, dist, i);
+                const uint32_t p = id_at<SH>(tok, h, ps, n);
+                bool cov = false;
+                if (p != HOLE) {
+                    if (p == b) cov = id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a;
+                    if (!cov && count) {
+                        vadd(s, E, P, V_DL, p);
+                        vadd(s, E, P, V_IL, p);
                     }
-                    const int64_t k = v_right(j, lb, n);
-                    const uint32_t q = id_at<SH>(tok, h, k, n);
-                    if (q != HOLE) {
+                }
+                const int64_t k = v_right(j, lb, n);
+                const uint32_t q = id_at<SH>(tok, h, k, n);
+                bool nocc = false;
+                if (q != HOLE) {
+                    nocc = q == a && id_at<SH>(tok, h, v_right(k, la, n), n) == b;
+                    if (count) {
                         vadd(s, E, P, V_DR, q);
-                        const bool nocc = q == a && id_at<SH>(tok, h, v_right(k, la, n), n) == b;
                         vadd(s, E, P, V_IR, nocc ? z : q);
                     }
                 }
+                ltag[slot] = nb_tag(cov ? z : p, nocc ? z : q);
             }
         } else if (ok) {
             // a == b: only the thread holding a run's first token walks it,
@@ -266,9 +294,12 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 const int64_t jj = pos + la;
                 if (jj >= n || tok[jj] != a) break;  // crossing pair: the shard-edge step
                 const int64_t k = v_right(jj, la, n);
-                stage_one(list, &lcount, &C->R, occz, (uint32_t)pos);
                 const uint32_t q = id_at<SH>(tok, h, k, n);
                 const bool knext = q == a;
+                const bool nocc = knext && id_at<SH>(tok, h, v_right(k, la, n), n) == a;
+                // left of this pair after the merge: the run's left neighbour, or z
+                const uint32_t pfin = m > 0 ? z : (left ? p : (p == HOLE ? HOLE : z));
+                stage_one(list, ltag, &lcount, &C->R, occz, tagz, (uint32_t)pos, nb_tag(pfin, nocc ? z : q));
                 if (count) {
                     if (m == 0 && left) {
                         vadd(s, E, P, V_DL, p);
@@ -276,7 +307,6 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                     }
                     if (q != HOLE) {
                         vadd(s, E, P, V_DR, q);
-                        const bool nocc = knext && id_at<SH>(tok, h, v_right(k, la, n), n) == a;
                         vadd(s, E, P, V_IR, nocc ? z : q);
                     }
                 }
@@ -284,7 +314,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 pos = k;
             }
         }
-        flush_list(list, &lcount, &gbase, &C->R, occz);
+        flush_list(list, ltag, &lcount, &gbase, &C->R, occz, tagz);
     }
     if (edge_block) {
         // Shard edges.  Right: my last token and the first token after it form
@@ -297,27 +327,29 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 if (h.HL[0] == a && tok[F1] == b && (a != b || (hlrun & 1))) xl = (uint32_t)F1;
                 const int64_t i = C->L1;
                 if (tok[i] == a && h.HR[0] == b && (a != b || !(C->myidx & 1))) {
-                    stage_one(list, &lcount, &C->R, occz, (uint32_t)i);
+                    const int64_t ps = v_left<SH>(tok, dist, i);
+                    const uint32_t p = id_at<SH>(tok, h, ps, n);
+                    bool cov = p == HOLE;
+                    if (!cov) cov = a != b ? (p == b && id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a) : p == a;
+                    const uint32_t q = h.HR[1];
+                    const bool nocc = q == a && h.HR[2] == b;
+                    stage_one(list, ltag, &lcount, &C->R, occz, tagz, (uint32_t)i,
+                              nb_tag(p == HOLE ? HOLE : (cov ? z : p), nocc ? z : q));
                     if (count) {
-                        const int64_t ps = v_left<SH>(tok, dist, i);
-                        const uint32_t p = id_at<SH>(tok, h, ps, n);
-                        bool cov = p == HOLE;
-                        if (!cov) cov = a != b ? (p == b && id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a) : p == a;
                         if (!cov) {
                             vadd(s, E, P, V_DL, p);
                             vadd(s, E, P, V_IL, p);
                         }
-                        const uint32_t q = h.HR[1];
                         if (q != HOLE) {
                             vadd(s, E, P, V_DR, q);
-                            vadd(s, E, P, V_IR, (q == a && h.HR[2] == b) ? z : q);
+                            vadd(s, E, P, V_IR, nocc ? z : q);
                         }
                     }
                 }
             }
             C->xleft = xl;
         }
-        flush_list(list, &lcount, &gbase, &C->R, occz);
+        flush_list(list, ltag, &lcount, &gbase, &C->R, occz, tagz);
     }
     if (count) {
         // flush into replica (block % REPL): ~REPL x fewer same-address atomics
@@ -667,14 +699,10 @@ __device__ inline void commit_merge(const Eng *E, Ctl *C, uint32_t u, uint32_t v
                 off = E->poff[rk];
                 len = E->poff[rk + 1] - off;
             }
-        } else {
-            const uint32_t lu = u >= 256 ? E->occ_len[u] : 0xFFFFFFFFu;
-            const uint32_t lv = v >= 256 ? E->occ_len[v] : 0xFFFFFFFFu;
-            if (u == v || lu <= lv) {
-                mode = 1; off = E->occ_off[u]; len = lu;
-            } else {
-                mode = 2; off = E->occ_off[v]; len = lv;
-            }
+        } else if (u >= v) {  // (u,v) became adjacent when u was created: u's list, tag right == v
+            mode = 1; off = E->occ_off[u]; len = E->occ_len[u];
+        } else {              // ... when v was created: v's list, tag left == u
+            mode = 2; off = E->occ_off[v]; len = E->occ_len[v];
         }
     }
     C->cand_mode = mode;

@@ -74,6 +74,7 @@ struct bpe_gpu_group {
     uint32_t **d_ptrs = nullptr;      // local mode: [xbuf | myrec | erec] pointer tables
     uint32_t **d_ptrs_tmp = nullptr;  // local mode: init-time tables
     hipGraphExec_t graph = nullptr;
+    std::vector<hipGraphExec_t> retired;  // replaced graphs, destroyed with the run
     bool eager = false;               // collectives could not be graph-captured
     bool encoding = false;            // the captured step is an encode batch
     size_t merges_done = 0;
@@ -83,8 +84,11 @@ struct bpe_gpu_group {
 namespace {
 
 int group_free_graph(bpe_gpu_group *g) {
+    if (g->st) (void)hipStreamSynchronize(g->st);
     if (g->graph) (void)hipGraphExecDestroy(g->graph);
     g->graph = nullptr;
+    for (hipGraphExec_t x : g->retired) (void)hipGraphExecDestroy(x);
+    g->retired.clear();
     return 0;
 }
 
@@ -146,6 +150,7 @@ int launch_group_iteration(bpe_gpu_group *g) {
 int launch_group_batch(bpe_gpu_group *g) {
     for (bpe_gpu_ctx *c : g->cs) k_scan_batch<true><<<SCAN_BLOCKS, ESCAN_T, 0, g->st>>>(c->dE, c->dC);
     for (bpe_gpu_ctx *c : g->cs) k_apply_batch<true><<<ENC_APPLY_BLOCKS + 1, 256, 0, g->st>>>(c->dE, c->dC);
+    for (bpe_gpu_ctx *c : g->cs) k_link_batch<true><<<ENC_APPLY_BLOCKS, 256, 0, g->st>>>(c->dE, c->dC);
     for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 0);
     HIPCHK(hipGetLastError());
     return ex_records(g, g->d_ptrs);
@@ -204,7 +209,12 @@ int drive_group(bpe_gpu_group *g) {
             return fail(BPE_GPU_EINTERNAL, C0.err == 1 ? "engine invariant violated (count decrement of an absent pair)"
                                                        : "pair table full");
         case STOP_GROW:
-            group_free_graph(g);
+            // the captured steps read the tables through the device descriptors;
+            // recapture only when the level-2 summary launch appears
+            if (g->cs[0]->h.hcap / L1W <= SELECT_L1_MAX && 4 * g->cs[0]->h.hcap / L1W > SELECT_L1_MAX) {
+                if (g->graph) g->retired.push_back(g->graph);
+                g->graph = nullptr;
+            }
             for (bpe_gpu_ctx *c : g->cs) {
                 c->hC->stop = STOP_NONE;
                 c->hC->full = 1;
