@@ -105,6 +105,30 @@ __device__ inline int64_t v_right(int64_t p, uint32_t len, int64_t n) {
 
 constexpr uint32_t SCAN_T = 1024;  // threads per k_scan block = candidates per round
 
+// tok[i-1 .. i+6] from two ALIGNED 16-byte loads (tok is padded by 8 words):
+// for short tokens a candidate's partner and both neighbours sit in this
+// window, so it costs 2 wide requests instead of 4-5 scattered ones.
+struct TokWin {
+    uint4 w0, w1;
+    int64_t base;
+    __device__ inline bool has(int64_t x) const { return x >= base && x < base + 8; }
+    __device__ inline uint32_t at(int64_t x) const {
+        const uint32_t k = (uint32_t)(x - base);
+        const uint4 w = k < 4 ? w0 : w1;
+        const uint32_t r = k & 3;
+        return r == 0 ? w.x : r == 1 ? w.y : r == 2 ? w.z : w.w;
+    }
+};
+
+__device__ inline TokWin tok_window(const uint32_t *__restrict__ tok, int64_t i) {
+    TokWin W;
+    W.base = (i > 0 ? i - 1 : 0) & ~3ll;
+    const uint4 *p = reinterpret_cast<const uint4 *>(tok + W.base);
+    W.w0 = p[0];
+    W.w1 = p[1];
+    return W;
+}
+
 // Neighbour tag of an occurrence-list entry: low bytes of the ids left and
 // right of the new token right after it was created (0xFF: none / unknown,
 // matches anything).  A pair (u,v) can only become adjacent when the LATER
@@ -236,18 +260,35 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
         const uint32_t e = e0 + threadIdx.x;
         bool ok = false;
         int64_t i = 0, j = 0;
+        // Everything a candidate needs that depends only on its position is
+        // loaded in ONE round trip (the token, its partner, the left slot and
+        // its dist, the right neighbour of the pair): the scan is a chain of
+        // dependent gathers, so round trips, not bytes, set its time.
+        uint32_t tl = HOLE, dl = 0, tr = HOLE;
         if (e < len) {
             if (mode == 2) {
                 j = E->occ[off + e];
                 if (tag_ok(E->occnb[off + e] >> 8, want) && tok[j] == b) {
                     i = v_left<SH>(tok, dist, j);
                     ok = i >= 0 && tok[i] == a;  // i < 0: the pair is the left shard's
+                    if (ok) {
+                        tl = i > 0 ? tok[i - 1] : HOLE;
+                        dl = i > 0 ? dist[i - 1] : 0;
+                        tr = j + lb < n ? tok[j + lb] : HOLE;
+                    }
                 }
             } else {
                 i = (mode == 0) ? E->plist[off + e] : E->occ[off + e];
-                if ((mode == 0 || tag_ok(E->occnb[off + e] & 0xFFu, want)) && tok[i] == a) {
+                if (mode == 0 || tag_ok(E->occnb[off + e] & 0xFFu, want)) {
                     j = i + la;
-                    ok = j < n && tok[j] == b;  // j >= n: crossing pair, handled below
+                    const TokWin W = tok_window(tok, i);
+                    const int64_t kk = j + lb;
+                    const uint32_t t0 = W.at(i);
+                    const uint32_t t1 = j >= n ? HOLE : W.has(j) ? W.at(j) : tok[j];  // j >= n: crossing pair
+                    tl = i > 0 ? W.at(i - 1) : HOLE;
+                    tr = kk >= n ? HOLE : W.has(kk) ? W.at(kk) : tok[kk];
+                    ok = t0 == a && t1 == b && j < n;
+                    if (ok && i > 0 && tl == HOLE) dl = dist[i - 1];  // left token spans slots
                 }
             }
         }
@@ -255,8 +296,13 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             const uint32_t slot = wave_append(ok, &lcount);  // LDS counter
             if (ok) {
                 list[slot] = (uint32_t)i;
-                const int64_t ps = v_left<SH>(tok, dist, i);
-                const uint32_t p = id_at<SH>(tok, h, ps, n);
+                // left neighbour from the preloaded slot i-1 (v_left without reloading)
+                int64_t ps;
+                if (i == 0) ps = -1;
+                else if (tl != HOLE) ps = i - 1;
+                else if (SH && (int64_t)dl > i - 1) ps = -1;
+                else ps = i - 1 - (int64_t)dl;
+                const uint32_t p = (i > 0 && tl != HOLE) ? tl : id_at<SH>(tok, h, ps, n);
                 bool cov = false;
                 if (p != HOLE) {
                     if (p == b) cov = id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a;
@@ -266,7 +312,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                     }
                 }
                 const int64_t k = v_right(j, lb, n);
-                const uint32_t q = id_at<SH>(tok, h, k, n);
+                const uint32_t q = k < n ? tr : id_at<SH>(tok, h, k, n);
                 bool nocc = false;
                 if (q != HOLE) {
                     nocc = q == a && id_at<SH>(tok, h, v_right(k, la, n), n) == b;
