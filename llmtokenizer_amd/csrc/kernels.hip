@@ -721,8 +721,12 @@ __global__ __launch_bounds__(256) void k_rescan2(const Eng *__restrict__ E, Ctl 
     }
 }
 
-// set up iteration for merge (u, v) -> z; returns via Ctl
-__device__ inline void commit_merge(const Eng *E, Ctl *C, uint32_t u, uint32_t v) {
+// set up iteration for merge (u, v) -> z; returns via Ctl.  rank / poff: the
+// byte-rank and byte-pair offset tables (k_select passes LDS copies).
+__device__ inline void commit_merge(const Eng *E, Ctl *C, uint32_t u, uint32_t v, const uint32_t *rank = nullptr,
+                                    const uint32_t *poff = nullptr) {
+    if (!rank) rank = E->rank;
+    if (!poff) poff = E->poff;
     const uint32_t md = C->merges_done;
     const uint32_t z = 256 + md;
     C->a = u;
@@ -738,12 +742,12 @@ __device__ inline void commit_merge(const Eng *E, Ctl *C, uint32_t u, uint32_t v
     uint32_t mode = 1, off = 0, len = 0;
     if (valid) {
         if (u < 256 && v < 256) {
-            const uint32_t ru = E->rank[u], rv = E->rank[v];
+            const uint32_t ru = rank[u], rv = rank[v];
             if (ru != HOLE && rv != HOLE) {
                 const uint32_t rk = ru * E->A + rv;
                 mode = 0;
-                off = E->poff[rk];
-                len = E->poff[rk + 1] - off;
+                off = poff[rk];
+                len = poff[rk + 1] - off;
             }
         } else if (u >= v) {  // (u,v) became adjacent when u was created: u's list, tag right == v
             mode = 1; off = E->occ_off[u]; len = E->occ_len[u];
@@ -772,39 +776,15 @@ __device__ inline void finish_iteration(const Eng *E, Ctl *C) {
 }
 
 // ---------------------------------------------------------------- k_select
-__global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t tracked_graph) {
-    if (C->stop) return;
-    const uint64_t nL1 = E->hcap / L1W;
-    Best mine{0, 0, ~0ull};
-    if (nL1 <= SELECT_L1_MAX) {
-#pragma unroll 4
-        for (uint64_t i = threadIdx.x; i < nL1; i += blockDim.x)
-            if (E->l1best[i]) mine = best_merge(mine, Best{E->l1best[i], E->l1tie[i], E->l1key[i]});
-    } else {
-        const uint64_t nL2 = (nL1 + L2W - 1) / L2W;
-        for (uint64_t i = threadIdx.x; i < nL2; i += blockDim.x)
-            if (E->l2best[i]) mine = best_merge(mine, Best{E->l2best[i], E->l2tie[i], E->l2key[i]});
-    }
-    mine = wave_best(mine);
-    // k_scan's last block exit (blockDim == SCAN_BLOCKS == 1024 stamps)
-    unsigned long long tend = E->scan_tend[threadIdx.x];
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long y = __shfl_xor(tend, o);
-        tend = y > tend ? y : tend;
-    }
-    __shared__ Best sw[16];
-    __shared__ unsigned long long st[16];
-    if ((threadIdx.x & 63) == 0) { sw[threadIdx.x >> 6] = mine; st[threadIdx.x >> 6] = tend; }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    Best r = sw[0];
-    for (uint32_t k = 1; k < blockDim.x / 64; k++) r = best_merge(r, sw[k]);
-    if (C->pending) {  // a merge ran: account its k_scan span
-        for (uint32_t k = 0; k < blockDim.x / 64; k++) tend = st[k] > tend ? st[k] : tend;
-        if (tend > C->scan_t0) {
-            C->scan_ticks += tend - C->scan_t0;
-            C->scan_launches++;
-        }
+constexpr uint32_t EREC_LDS = 1024;   // edge records staged in LDS (64 shards)
+
+// decisions of one selection (thread 0, on the LDS copy of the control block)
+__device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Best r, unsigned long long tend,
+                                   uint32_t tracked_graph, const uint32_t *rank, const uint32_t *poff,
+                                   const uint32_t *erec) {
+    if (C->pending && tend > C->scan_t0) {  // a merge ran: account its k_scan span
+        C->scan_ticks += tend - C->scan_t0;
+        C->scan_launches++;
     }
     finish_iteration(E, C);
     if (!tracked_graph && !E->fast && C->n_live < TRACK_LIMIT) { C->stop = STOP_MODE; return; }
@@ -825,14 +805,73 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
     // untracked tie (n >= 2^20, schedule-dependent in the reference): the
     // project rule is the smallest (a,b) -- r.key already is that key
     if (r.tie > 1) C->counters[2]++;
-    commit_merge(E, C, (uint32_t)(r.key >> 32), (uint32_t)r.key);
+    commit_merge(E, C, (uint32_t)(r.key >> 32), (uint32_t)r.key, rank, poff);
     if (E->sharded) {  // halo of this shard for the merge just chosen
         Halo hl;
-        shard_halo(E->erec, E->nshards, E->shard, C->a, &hl);
+        shard_halo(erec, E->nshards, E->shard, C->a, &hl);
         for (int m = 0; m < 3; m++) { C->HL[m] = hl.HL[m]; C->HR[m] = hl.HR[m]; }
         C->hlrun = hl.hlrun;
         C->myidx = hl.myidx;
     }
+}
+
+// Top-level argmax + the iteration's bookkeeping.  The control block, byte
+// ranks (and edge records) are staged in LDS while the summaries are reduced,
+// so thread 0's decisions start from LDS; the control block is written back
+// at the end.
+__global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl *__restrict__ Cg, uint32_t tracked_graph) {
+    if (Cg->stop) return;
+    __shared__ Ctl sc;
+    __shared__ uint32_t srank[256];
+    uint32_t *spoff = nullptr;
+    __shared__ uint32_t serec[EREC_LDS];
+    constexpr uint32_t CW = sizeof(Ctl) / 4;
+    const uint32_t tid = threadIdx.x;
+    uint32_t *scw = reinterpret_cast<uint32_t *>(&sc);
+    uint32_t *cgw = reinterpret_cast<uint32_t *>(Cg);
+    for (uint32_t x = tid; x < CW; x += blockDim.x) scw[x] = cgw[x];
+    for (uint32_t x = tid; x < 256; x += blockDim.x) srank[x] = E->rank[x];
+    const bool pl = false;  // (staging all byte-pair offsets costs more than the 2 loads it saves)
+    const uint32_t ne = E->sharded ? E->nshards * EDGE_WORDS : 0;
+    const bool el = ne <= EREC_LDS;
+    if (el)
+        for (uint32_t x = tid; x < ne; x += blockDim.x) serec[x] = E->erec[x];
+    const uint64_t nL1 = E->hcap / L1W;
+    Best mine{0, 0, ~0ull};
+    if (nL1 <= SELECT_L1_MAX) {
+#pragma unroll 4
+        for (uint64_t i = tid; i < nL1; i += blockDim.x)
+            if (E->l1best[i]) mine = best_merge(mine, Best{E->l1best[i], E->l1tie[i], E->l1key[i]});
+    } else {
+        const uint64_t nL2 = (nL1 + L2W - 1) / L2W;
+        for (uint64_t i = tid; i < nL2; i += blockDim.x)
+            if (E->l2best[i]) mine = best_merge(mine, Best{E->l2best[i], E->l2tie[i], E->l2key[i]});
+    }
+    mine = wave_best(mine);
+    // k_scan's last block exit (blockDim == SCAN_BLOCKS == 1024 stamps)
+    unsigned long long tend = E->scan_tend[tid];
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(tend, o);
+        tend = y > tend ? y : tend;
+    }
+    __shared__ Best sw[16];
+    __shared__ unsigned long long st[16];
+    if ((tid & 63) == 0) { sw[tid >> 6] = mine; st[tid >> 6] = tend; }
+    __syncthreads();
+    if (tid == 0) {
+        Best r = sw[0];
+        for (uint32_t k = 1; k < blockDim.x / 64; k++) r = best_merge(r, sw[k]);
+        for (uint32_t k = 0; k < blockDim.x / 64; k++) tend = st[k] > tend ? st[k] : tend;
+        select_tail(E, &sc, r, tend, tracked_graph, srank, pl ? spoff : nullptr, el ? serec : E->erec);
+    }
+    __syncthreads();
+    for (uint32_t x = tid; x < CW; x += blockDim.x) cgw[x] = scw[x];
+}
+
+// commit a merge chosen by the host resolver (after STOP_EVENT)
+__global__ void k_commit(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t u, uint32_t v) {
+    commit_merge(E, C, u, v);
+    C->stop = STOP_NONE;
 }
 
 // ------------------------------------------------------------ shard exchange
@@ -956,11 +995,6 @@ __global__ void k_init_cross(const Eng *__restrict__ E, uint32_t *__restrict__ t
     }
 }
 
-// commit a merge chosen by the host resolver (after STOP_EVENT)
-__global__ void k_commit(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t u, uint32_t v) {
-    commit_merge(E, C, u, v);
-    C->stop = STOP_NONE;
-}
 
 // ------------------------------------------------------------ encode driver
 // encode mode: pick merge r = merges_done from the given list
