@@ -75,10 +75,27 @@ struct Halo6 {
     uint32_t HL[3], HR[3];
 };
 
-template <bool SH>
-__device__ inline uint32_t id_at(const uint32_t *__restrict__ tok, const Halo6 &h, int64_t p, int64_t n) {
-    if (p < 0) return SH && p >= -3 ? h.HL[-1 - p] : HOLE;
-    if (p >= n) return SH && p - n < 3 ? h.HR[p - n] : HOLE;
+// The halo of one shard for one merge, derived on first use from the edge
+// records (only lookups that leave the shard need it, so most threads never
+// compute it).
+struct LazyHalo {
+    const Eng *E;
+    uint32_t a;
+    bool ready;
+    Halo h;
+    __device__ inline const Halo &get() {  // sharded contexts only (E->erec)
+        if (!ready) {
+            shard_halo(E->erec, E->nshards, E->shard, a, &h);
+            ready = true;
+        }
+        return h;
+    }
+};
+
+template <bool SH, typename HaloT>
+__device__ inline uint32_t id_at(const uint32_t *__restrict__ tok, HaloT &h, int64_t p, int64_t n) {
+    if (p < 0) return SH && p >= -3 ? h.get().HL[-1 - p] : HOLE;
+    if (p >= n) return SH && p - n < 3 ? h.get().HR[p - n] : HOLE;
     return tok[p];
 }
 
@@ -239,13 +256,9 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
     uint32_t *occz = E->occ + C->occ_top;
     uint16_t *tagz = E->occnb + C->occ_top;
     const uint32_t want = mode == 2 ? a : b;  // tag byte the candidates must carry
-    Halo6 h;
-#pragma unroll
-    for (int m = 0; m < 3; m++) {
-        h.HL[m] = SH ? C->HL[m] : HOLE;
-        h.HR[m] = SH ? C->HR[m] : HOLE;
-    }
-    const uint32_t hlrun = SH ? C->hlrun : 0;
+    // halo of this shard for merge (a, b), from the edge records on first use
+    // (the records' allgather overlaps the previous merge's rescan/select)
+    LazyHalo h{E, a, false, {}};
 
     __shared__ uint32_t s[4][DENSE];
     __shared__ uint32_t list[SCAN_T];
@@ -334,7 +347,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             if (p == a) {
                 start = ps < 0;
                 left = false;
-                if (hlrun & 1) pos = j;  // i pairs with HL[0] (the left shard's pair)
+                if (SH && (h.get().hlrun & 1)) pos = j;  // i pairs with HL[0] (the left shard's pair)
             }
             for (uint32_t m = 0; start; m++) {
                 const int64_t jj = pos + la;
@@ -370,15 +383,16 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             uint32_t xl = HOLE;
             const int64_t F1 = C->F1;
             if (F1 < n) {
-                if (h.HL[0] == a && tok[F1] == b && (a != b || (hlrun & 1))) xl = (uint32_t)F1;
+                const Halo &hh = h.get();
+                if (hh.HL[0] == a && tok[F1] == b && (a != b || (hh.hlrun & 1))) xl = (uint32_t)F1;
                 const int64_t i = C->L1;
-                if (tok[i] == a && h.HR[0] == b && (a != b || !(C->myidx & 1))) {
+                if (tok[i] == a && hh.HR[0] == b && (a != b || !(hh.myidx & 1))) {
                     const int64_t ps = v_left<SH>(tok, dist, i);
                     const uint32_t p = id_at<SH>(tok, h, ps, n);
                     bool cov = p == HOLE;
                     if (!cov) cov = a != b ? (p == b && id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a) : p == a;
-                    const uint32_t q = h.HR[1];
-                    const bool nocc = q == a && h.HR[2] == b;
+                    const uint32_t q = hh.HR[1];
+                    const bool nocc = q == a && hh.HR[2] == b;
                     stage_one(list, ltag, &lcount, &C->R, occz, tagz, (uint32_t)i,
                               nb_tag(p == HOLE ? HOLE : (cov ? z : p), nocc ? z : q));
                     if (count) {
@@ -776,12 +790,10 @@ __device__ inline void finish_iteration(const Eng *E, Ctl *C) {
 }
 
 // ---------------------------------------------------------------- k_select
-constexpr uint32_t EREC_LDS = 1024;   // edge records staged in LDS (64 shards)
 
 // decisions of one selection (thread 0, on the LDS copy of the control block)
 __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Best r, unsigned long long tend,
-                                   uint32_t tracked_graph, const uint32_t *rank, const uint32_t *poff,
-                                   const uint32_t *erec) {
+                                   uint32_t tracked_graph, const uint32_t *rank, const uint32_t *poff) {
     if (C->pending && tend > C->scan_t0) {  // a merge ran: account its k_scan span
         C->scan_ticks += tend - C->scan_t0;
         C->scan_launches++;
@@ -806,17 +818,10 @@ __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Best r, un
     // project rule is the smallest (a,b) -- r.key already is that key
     if (r.tie > 1) C->counters[2]++;
     commit_merge(E, C, (uint32_t)(r.key >> 32), (uint32_t)r.key, rank, poff);
-    if (E->sharded) {  // halo of this shard for the merge just chosen
-        Halo hl;
-        shard_halo(erec, E->nshards, E->shard, C->a, &hl);
-        for (int m = 0; m < 3; m++) { C->HL[m] = hl.HL[m]; C->HR[m] = hl.HR[m]; }
-        C->hlrun = hl.hlrun;
-        C->myidx = hl.myidx;
-    }
 }
 
-// Top-level argmax + the iteration's bookkeeping.  The control block, byte
-// ranks (and edge records) are staged in LDS while the summaries are reduced,
+// Top-level argmax + the iteration's bookkeeping.  The control block and byte
+// ranks are staged in LDS while the summaries are reduced,
 // so thread 0's decisions start from LDS; the control block is written back
 // at the end.
 __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl *__restrict__ Cg, uint32_t tracked_graph) {
@@ -824,7 +829,6 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
     __shared__ Ctl sc;
     __shared__ uint32_t srank[256];
     uint32_t *spoff = nullptr;
-    __shared__ uint32_t serec[EREC_LDS];
     constexpr uint32_t CW = sizeof(Ctl) / 4;
     const uint32_t tid = threadIdx.x;
     uint32_t *scw = reinterpret_cast<uint32_t *>(&sc);
@@ -832,10 +836,6 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
     for (uint32_t x = tid; x < CW; x += blockDim.x) scw[x] = cgw[x];
     for (uint32_t x = tid; x < 256; x += blockDim.x) srank[x] = E->rank[x];
     const bool pl = false;  // (staging all byte-pair offsets costs more than the 2 loads it saves)
-    const uint32_t ne = E->sharded ? E->nshards * EDGE_WORDS : 0;
-    const bool el = ne <= EREC_LDS;
-    if (el)
-        for (uint32_t x = tid; x < ne; x += blockDim.x) serec[x] = E->erec[x];
     const uint64_t nL1 = E->hcap / L1W;
     Best mine{0, 0, ~0ull};
     if (nL1 <= SELECT_L1_MAX) {
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
         Best r = sw[0];
         for (uint32_t k = 1; k < blockDim.x / 64; k++) r = best_merge(r, sw[k]);
         for (uint32_t k = 0; k < blockDim.x / 64; k++) tend = st[k] > tend ? st[k] : tend;
-        select_tail(E, &sc, r, tend, tracked_graph, srank, pl ? spoff : nullptr, el ? serec : E->erec);
+        select_tail(E, &sc, r, tend, tracked_graph, srank, pl ? spoff : nullptr);
     }
     __syncthreads();
     for (uint32_t x = tid; x < CW; x += blockDim.x) cgw[x] = scw[x];
