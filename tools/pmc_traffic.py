@@ -10,6 +10,7 @@ gathers of the per-merge kernels the counter is uncalibrated and reported raw.
 usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <out.json>
 """
 import csv
+import re
 import json
 import sys
 from collections import defaultdict
@@ -24,6 +25,7 @@ def per_kernel(path, counter):
             if r.get("Counter_Name") != counter:
                 continue
             name = r["Kernel_Name"].split("(")[0].replace("bpeamd::", "")
+            name = re.sub(r"<.*>", "", name.replace("void ", "")).strip()  # "void k_scan<false>" -> "k_scan"
             vals[name].append(float(r["Counter_Value"]))
     return vals
 
