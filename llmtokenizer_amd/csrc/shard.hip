@@ -143,6 +143,9 @@ int launch_group_iteration(bpe_gpu_group *g) {
     }
     HIPCHK(hipEventRecord(g->ev_scan, g->st));
     HIPCHK(hipStreamWaitEvent(g->st2, g->ev_scan, 0));
+    // the allreduce is issued before the allgather: RCCL runs one communicator's
+    // collectives in issue order, and only the allreduce is on the critical path
+    if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
     for (bpe_gpu_ctx *c : g->cs) {
         k_apply<<<APPLY_A, 256, 0, g->st2>>>(c->dE, c->dC, APPLY_A);  // role A only
         k_edges<<<1, 256, 0, g->st2>>>(c->dE, c->dC, 0);
@@ -150,7 +153,6 @@ int launch_group_iteration(bpe_gpu_group *g) {
     HIPCHK(hipEventRecord(g->ev_edges, g->st2));
     if ((r = ex_records(g, g->d_ptrs, g->st2))) return r;
     HIPCHK(hipEventRecord(g->ev_recs, g->st2));
-    if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
     for (bpe_gpu_ctx *c : g->cs) k_apply<<<APPLY_B, 256, 0, g->st>>>(c->dE, c->dC, 0);  // role B only
     for (bpe_gpu_ctx *c : g->cs) launch_summaries(c);
     HIPCHK(hipStreamWaitEvent(g->st, g->ev_edges, 0));
