@@ -357,7 +357,6 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     C.n_live = n0;
     for (uint32_t t = 0; t < NTHR; t++) C.Bcur[t] = THREAD_B0;
     C.full = 1;
-    for (int m = 0; m < 3; m++) C.HL[m] = C.HR[m] = HOLE;
     C.F1 = 0;
     C.L1 = n0 ? (uint32_t)(n0 - 1) : 0;
     C.L1new = HOLE;

@@ -135,11 +135,7 @@ struct Ctl {
     unsigned long long scan_t0;       // wall clock at k_scan block 0 entry
     unsigned long long scan_ticks;    // sum over merges of k_scan spans (wall-clock ticks)
     unsigned long long scan_launches;
-    // sharding: tokens around this shard's edges (for the current merge)
-    uint32_t HL[3];                   // ids before the first token start (HL[0] adjacent)
-    uint32_t HR[3];                   // ids after the last token (HR[0] adjacent)
-    uint32_t hlrun;                   // consecutive a's immediately left of the first token
-    uint32_t myidx;                   // run index of the last token (when it is an a)
+    // sharding (the halo itself is derived from the edge records in k_scan)
     uint32_t F1, L1, L1new, xleft;    // first / last token start, pending last, consumed first
     uint32_t xleft_lb;                // length of the consumed first token (encode batches)
     uint32_t done_scan, ebp;          // k_scan blocks finished (sharded); encode batch parity

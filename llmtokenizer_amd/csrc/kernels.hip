@@ -996,17 +996,6 @@ __global__ void k_init_cross(const Eng *__restrict__ E, uint32_t *__restrict__ t
 }
 
 
-// ------------------------------------------------------------ encode driver
-// encode mode: pick merge r = merges_done from the given list
-__global__ void k_enc_next(const Eng *__restrict__ E, Ctl *__restrict__ C, const uint32_t *__restrict__ pairs,
-                           uint32_t n_merges) {
-    if (C->stop) return;
-    finish_iteration(E, C);
-    const uint32_t r = C->merges_done;
-    if (r >= n_merges) { C->stop = STOP_ENC_END; return; }
-    commit_merge(E, C, pairs[2 * r], pairs[2 * r + 1]);
-}
-
 // ------------------------------------------------------------- init kernels
 // tok[i] = byte i (16 bytes per thread, uint4 in / 4 x uint4 out) and the set
 // of byte values present (only presence is needed to rank them)
