@@ -138,7 +138,7 @@ struct Ctl {
     // sharding (the halo itself is derived from the edge records in k_scan)
     uint32_t F1, L1, L1new, xleft;    // first / last token start, pending last, consumed first
     uint32_t xleft_lb;                // length of the consumed first token (encode batches)
-    uint32_t done_scan, ebp;          // k_scan blocks finished (sharded); encode batch parity
+    uint32_t Rg, ebp;                 // sharded: occurrences over all shards; encode batch parity
 };
 
 // Edge record of a shard: its first and last three token ids, the run of the

@@ -53,9 +53,12 @@ __device__ inline uint32_t dval(const Eng *E, uint32_t P, int v, uint32_t x) {
     return sum;
 }
 
+template <bool SH = false>
 __device__ inline void vadd(uint32_t (*s)[DENSE], const Eng *E, uint32_t P, int v, uint32_t x) {
     if (x < DENSE) {
         atomicAdd(&s[v][x], 1u);
+    } else if (SH) {  // sharded: straight into the exchange buffer (no lists)
+        atomicAdd(&E->xbuf[v * E->vcap + x], 1u);
     } else {
         uint32_t old = atomicAdd(&E->vec[P][v][x], 1u);
         if (old == 0) {
@@ -160,10 +163,13 @@ __device__ inline bool tag_ok(uint32_t t8, uint32_t id) { return t8 == 0xFFu || 
 
 // append the block's staged occurrence positions (+ tags) to the new id's list
 __device__ inline void flush_list(uint32_t *list, uint16_t *ltag, uint32_t *lcount, uint32_t *gbase, uint32_t *R,
-                                  uint32_t *occz, uint16_t *tagz) {
+                                  uint32_t *occz, uint16_t *tagz, uint32_t *bcount) {
     __syncthreads();
     const uint32_t n = min(*lcount, SCAN_T);
-    if (threadIdx.x == 0) *gbase = n ? atomicAdd(R, n) : 0;
+    if (threadIdx.x == 0) {
+        *gbase = n ? atomicAdd(R, n) : 0;
+        *bcount += n;  // this block's occurrences (LDS)
+    }
     __syncthreads();
     if (threadIdx.x < n) {
         occz[*gbase + threadIdx.x] = list[threadIdx.x];
@@ -182,7 +188,7 @@ __device__ inline void scan_exit_stamp(const Eng *E) {
 
 // stage one occurrence position (single-thread path: walker / shard edge)
 __device__ inline void stage_one(uint32_t *list, uint16_t *ltag, uint32_t *lcount, uint32_t *R, uint32_t *occz,
-                                 uint16_t *tagz, uint32_t pos, uint16_t tag) {
+                                 uint16_t *tagz, uint32_t pos, uint16_t tag, uint32_t *bcount) {
     const uint32_t slot = atomicAdd(lcount, 1u);
     if (slot < SCAN_T) {
         list[slot] = pos;
@@ -191,43 +197,7 @@ __device__ inline void stage_one(uint32_t *list, uint16_t *ltag, uint32_t *lcoun
         const uint32_t g = atomicAdd(R, 1u);
         occz[g] = pos;
         tagz[g] = tag;
-    }
-}
-
-// xbuf[v*vcap + x] = delta v of id x (dense replicas summed), xbuf[4*vcap] = R.
-// All loads are issued before any sum so one block needs ~2 round trips.
-__device__ inline void pack_exchange(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t P) {
-    const uint32_t vc = E->vcap, nd = min(vc, DENSE);
-    constexpr uint32_t U = 4;
-    for (uint32_t t0 = threadIdx.x; t0 < 4 * nd; t0 += U * SCAN_T) {
-        uint32_t val[U][REPL];
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            const uint32_t t = min(t0 + u * SCAN_T, 4 * nd - 1);
-            const uint32_t v = t / nd, x = t % nd;
-#pragma unroll
-            for (uint32_t r = 0; r < REPL; r++) val[u][r] = aload(&E->vecd[(r * 4 + v) * DENSE + x]);
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < U; u++) {
-            const uint32_t t = t0 + u * SCAN_T;
-            uint32_t sum = 0;
-#pragma unroll
-            for (uint32_t r = 0; r < REPL; r++) sum += val[u][r];
-            if (t < 4 * nd) E->xbuf[(t / nd) * vc + t % nd] = sum;
-        }
-    }
-    if (vc > DENSE) {
-        const uint32_t w = vc - DENSE;
-        for (uint32_t t = threadIdx.x; t < 4 * w; t += SCAN_T) {
-            const uint32_t v = t / w, x = DENSE + t % w;
-            E->xbuf[v * vc + x] = aload(&E->vec[P][v][x]);
-        }
-    }
-    if (threadIdx.x == 0) {
-        E->xbuf[4 * vc] = aload(&C->R);
-        E->xbuf[4 * vc + 1] = 0;
-        C->done_scan = 0;
+        atomicAdd(bcount, 1u);
     }
 }
 
@@ -263,10 +233,10 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
     __shared__ uint32_t s[4][DENSE];
     __shared__ uint32_t list[SCAN_T];
     __shared__ uint16_t ltag[SCAN_T];
-    __shared__ uint32_t lcount, gbase;
+    __shared__ uint32_t lcount, gbase, bR;
     if (count)
         for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) (&s[0][0])[x] = 0;
-    if (threadIdx.x == 0) lcount = 0;
+    if (threadIdx.x == 0) lcount = bR = 0;
     __syncthreads();
 
     for (uint32_t e0 = blockIdx.x * SCAN_T; e0 < len; e0 += gridDim.x * SCAN_T) {
@@ -320,8 +290,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 if (p != HOLE) {
                     if (p == b) cov = id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a;
                     if (!cov && count) {
-                        vadd(s, E, P, V_DL, p);
-                        vadd(s, E, P, V_IL, p);
+                        vadd<SH>(s, E, P, V_DL, p);
+                        vadd<SH>(s, E, P, V_IL, p);
                     }
                 }
                 const int64_t k = v_right(j, lb, n);
@@ -330,8 +300,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 if (q != HOLE) {
                     nocc = q == a && id_at<SH>(tok, h, v_right(k, la, n), n) == b;
                     if (count) {
-                        vadd(s, E, P, V_DR, q);
-                        vadd(s, E, P, V_IR, nocc ? z : q);
+                        vadd<SH>(s, E, P, V_DR, q);
+                        vadd<SH>(s, E, P, V_IR, nocc ? z : q);
                     }
                 }
                 ltag[slot] = nb_tag(cov ? z : p, nocc ? z : q);
@@ -358,22 +328,22 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 const bool nocc = knext && id_at<SH>(tok, h, v_right(k, la, n), n) == a;
                 // left of this pair after the merge: the run's left neighbour, or z
                 const uint32_t pfin = m > 0 ? z : (left ? p : (p == HOLE ? HOLE : z));
-                stage_one(list, ltag, &lcount, &C->R, occz, tagz, (uint32_t)pos, nb_tag(pfin, nocc ? z : q));
+                stage_one(list, ltag, &lcount, &C->R, occz, tagz, (uint32_t)pos, nb_tag(pfin, nocc ? z : q), &bR);
                 if (count) {
                     if (m == 0 && left) {
-                        vadd(s, E, P, V_DL, p);
-                        vadd(s, E, P, V_IL, p);
+                        vadd<SH>(s, E, P, V_DL, p);
+                        vadd<SH>(s, E, P, V_IL, p);
                     }
                     if (q != HOLE) {
-                        vadd(s, E, P, V_DR, q);
-                        vadd(s, E, P, V_IR, nocc ? z : q);
+                        vadd<SH>(s, E, P, V_DR, q);
+                        vadd<SH>(s, E, P, V_IR, nocc ? z : q);
                     }
                 }
                 if (!knext || k >= n) break;
                 pos = k;
             }
         }
-        flush_list(list, ltag, &lcount, &gbase, &C->R, occz, tagz);
+        flush_list(list, ltag, &lcount, &gbase, &C->R, occz, tagz, &bR);
     }
     if (edge_block) {
         // Shard edges.  Right: my last token and the first token after it form
@@ -394,24 +364,24 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                     const uint32_t q = hh.HR[1];
                     const bool nocc = q == a && hh.HR[2] == b;
                     stage_one(list, ltag, &lcount, &C->R, occz, tagz, (uint32_t)i,
-                              nb_tag(p == HOLE ? HOLE : (cov ? z : p), nocc ? z : q));
+                              nb_tag(p == HOLE ? HOLE : (cov ? z : p), nocc ? z : q), &bR);
                     if (count) {
                         if (!cov) {
-                            vadd(s, E, P, V_DL, p);
-                            vadd(s, E, P, V_IL, p);
+                            vadd<SH>(s, E, P, V_DL, p);
+                            vadd<SH>(s, E, P, V_IL, p);
                         }
                         if (q != HOLE) {
-                            vadd(s, E, P, V_DR, q);
-                            vadd(s, E, P, V_IR, nocc ? z : q);
+                            vadd<SH>(s, E, P, V_DR, q);
+                            vadd<SH>(s, E, P, V_IR, nocc ? z : q);
                         }
                     }
                 }
             }
             C->xleft = xl;
         }
-        flush_list(list, ltag, &lcount, &gbase, &C->R, occz, tagz);
+        flush_list(list, ltag, &lcount, &gbase, &C->R, occz, tagz, &bR);
     }
-    if (count) {
+    if (count && !SH) {
         // flush into replica (block % REPL): ~REPL x fewer same-address atomics
         uint32_t *rep = E->vecd + (uint64_t)(blockIdx.x % REPL) * 4 * DENSE;
         for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) {
@@ -419,23 +389,17 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             if (c) atomicAdd(&rep[x], c);  // result unused: no-return atomic
         }
         __syncthreads();
-    }
-    if (SH) {
-        // The last block to finish packs the dense exchange buffer (replicas
-        // summed, ids >= DENSE, R) that the shards allreduce next.  Everything
-        // it reads was produced by agent-scope atomics, drained before the
-        // arrival add; it reads with sc1 loads -- no fence needed (the
-        // returning-counter hand-off of MI355X_MICROARCH.md).
-        __shared__ uint32_t is_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t nact = min(gridDim.x, (len + SCAN_T - 1) / SCAN_T);
-            const uint32_t target = nact < gridDim.x ? nact + 1 : gridDim.x;  // + the edge block
-            is_last = atomicAdd(&C->done_scan, 1u) == target - 1;
+    } else if (count) {
+        // sharded: flush straight into the dense exchange buffer the shards
+        // allreduce next (zeroed by the previous k_rescan1); no pack pass
+        const uint32_t vc = E->vcap;
+        for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) {
+            const uint32_t c = (&s[0][0])[x];
+            const uint32_t v = x / DENSE, id = x % DENSE;
+            if (c && id < vc) atomicAdd(&E->xbuf[v * vc + id], c);
         }
+        if (threadIdx.x == 0 && bR) atomicAdd(&E->xbuf[4 * vc], bR);  // this shard's R, summed
         __syncthreads();
-        if (is_last) pack_exchange(E, C, P);
     }
     scan_exit_stamp(E);
 }
@@ -527,6 +491,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     const uint32_t dense_end = 1 + 4 * W;
     const uint32_t total = dense_end + nl[0] + nl[1] + nl[2] + nl[3];
     const uint32_t Rg = sh ? E->xbuf[4 * E->vcap] : R;  // occurrences over all shards
+    if (sh && blockIdx.x == roleA_blocks && threadIdx.x == 0) C->Rg = Rg;  // for k_select (xbuf is cleared)
     __shared__ uint32_t marks[MARK_CAP];
     __shared__ uint32_t nmark, mbase;
     if (threadIdx.x == 0) nmark = 0;
@@ -665,10 +630,14 @@ __global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl 
     {   // k_apply has consumed this iteration's delta vectors: clear them
         const uint32_t P = C->parity;
         const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
-        for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride) E->vecd[x] = 0;
-        for (int vv = 0; vv < 4; vv++) {
-            const uint32_t nq = E->vnl[P][vv];
-            for (uint32_t t = tid; t < nq; t += stride) E->vec[P][vv][E->vlist[P][vv][t]] = 0;
+        if (E->sharded) {  // (the global R went to Ctl::Rg in k_apply)
+            for (uint32_t x = tid; x < 4 * E->vcap + 2; x += stride) E->xbuf[x] = 0;
+        } else {
+            for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride) E->vecd[x] = 0;
+            for (int vv = 0; vv < 4; vv++) {
+                const uint32_t nq = E->vnl[P][vv];
+                for (uint32_t t = tid; t < nq; t += stride) E->vec[P][vv][E->vlist[P][vv][t]] = 0;
+            }
         }
     }
     const uint64_t B = summary_B(C->D);
@@ -781,7 +750,7 @@ __device__ inline void finish_iteration(const Eng *E, Ctl *C) {
     C->counters[4] += C->cand_len;  // candidates examined by k_scan (profiling)
     C->counters[5] += C->R;         // occurrences replaced
     C->occ_top += C->R;
-    C->n_live -= E->sharded ? E->xbuf[4 * E->vcap] : C->R;
+    C->n_live -= E->sharded ? C->Rg : C->R;
     C->R = 0;
     C->nl1 = 0;
     C->nl2 = 0;

@@ -67,8 +67,7 @@ int rccl_fail(RcclApi *api, const char *what, ncclResult_t e) {
 struct bpe_gpu_group {
     int dev = 0;
     hipStream_t st = nullptr;
-    hipStream_t st2 = nullptr;  // side branch of the training step (role A, edge records)
-    hipEvent_t ev_scan = nullptr, ev_edges = nullptr, ev_recs = nullptr;
+
     std::vector<bpe_gpu_ctx *> cs;  // local shards, in corpus order
     uint32_t nshards = 1, shard0 = 0;
     RcclApi *rccl = nullptr;
@@ -128,36 +127,29 @@ int upload_table(bpe_gpu_group *g, uint32_t **d_tab, const std::vector<uint32_t 
     return 0;
 }
 
-// One merge on every shard, as two dependency chains (graph branches):
-//   main:  k_scan -> allreduce(deltas) -> k_apply role B -> k_rescan1 -> | k_select
-//   side:        -> k_apply role A -> k_edges -> | allgather(edge records) -> |
-// The records feed the NEXT merge's halo (k_scan), so their allgather runs
-// beside the table update instead of after it; k_select waits for role A and
-// k_edges (it finishes the iteration's bookkeeping), the next k_scan for both.
+// One merge on every shard, on one stream (graph branches cost more than
+// they hide: measured ~15 us per merge for a two-branch variant):
+//   k_scan -> allreduce(deltas, R) -> k_apply -> k_edges -> allgather(edge
+//   records) -> k_rescan1 -> k_select
+// k_scan flushes its deltas straight into xbuf; the records feed the next
+// merge's halo, which k_scan derives lazily.
 int launch_group_iteration(bpe_gpu_group *g) {
     int r;
     std::vector<uint32_t *> xb;
     for (bpe_gpu_ctx *c : g->cs) {
-        k_scan<true><<<SCAN_BLOCKS, SCAN_T, 0, g->st>>>(c->dE, c->dC);  // + packs xbuf
+        k_scan<true><<<SCAN_BLOCKS, SCAN_T, 0, g->st>>>(c->dE, c->dC);
         xb.push_back(c->h.xbuf);
     }
-    HIPCHK(hipEventRecord(g->ev_scan, g->st));
-    HIPCHK(hipStreamWaitEvent(g->st2, g->ev_scan, 0));
-    // the allreduce is issued before the allgather: RCCL runs one communicator's
-    // collectives in issue order, and only the allreduce is on the critical path
     if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
     for (bpe_gpu_ctx *c : g->cs) {
-        k_apply<<<APPLY_A, 256, 0, g->st2>>>(c->dE, c->dC, APPLY_A);  // role A only
-        k_edges<<<1, 256, 0, g->st2>>>(c->dE, c->dC, 0);
+        k_apply<<<APPLY_A + APPLY_B, 256, 0, g->st>>>(c->dE, c->dC, APPLY_A);
+        k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 0);
     }
-    HIPCHK(hipEventRecord(g->ev_edges, g->st2));
-    if ((r = ex_records(g, g->d_ptrs, g->st2))) return r;
-    HIPCHK(hipEventRecord(g->ev_recs, g->st2));
-    for (bpe_gpu_ctx *c : g->cs) k_apply<<<APPLY_B, 256, 0, g->st>>>(c->dE, c->dC, 0);  // role B only
-    for (bpe_gpu_ctx *c : g->cs) launch_summaries(c);
-    HIPCHK(hipStreamWaitEvent(g->st, g->ev_edges, 0));
-    for (bpe_gpu_ctx *c : g->cs) k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
-    HIPCHK(hipStreamWaitEvent(g->st, g->ev_recs, 0));
+    if ((r = ex_records(g, g->d_ptrs))) return r;
+    for (bpe_gpu_ctx *c : g->cs) {
+        launch_summaries(c);
+        k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
+    }
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -504,10 +496,7 @@ int bpe_gpu_group_create(int device, int local_shards, int nranks, int rank, con
     int r;
     hipError_t e = hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking);
     if (e != hipSuccess) { delete g; return fail(BPE_GPU_EHIP, "hipStreamCreate", e); }
-    e = hipStreamCreateWithFlags(&g->st2, hipStreamNonBlocking);
-    for (hipEvent_t *ev : {&g->ev_scan, &g->ev_edges, &g->ev_recs})
-        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
-    if (e != hipSuccess) { bpe_gpu_group_destroy(g); return fail(BPE_GPU_EHIP, "stream/event create", e); }
+
     if (comm_id) {
         if ((r = rccl_api(&g->rccl))) { bpe_gpu_group_destroy(g); return r; }
         ncclUniqueId u;
@@ -543,9 +532,6 @@ void bpe_gpu_group_destroy(bpe_gpu_group *g) {
     if (g->d_ptrs) hipFree(g->d_ptrs);
     if (g->d_ptrs_tmp) hipFree(g->d_ptrs_tmp);
     if (g->comm) (void)g->rccl->commDestroy(g->comm);
-    for (hipEvent_t ev : {g->ev_scan, g->ev_edges, g->ev_recs})
-        if (ev) (void)hipEventDestroy(ev);
-    if (g->st2) (void)hipStreamDestroy(g->st2);
     if (g->st) (void)hipStreamDestroy(g->st);
     delete g;
 }
