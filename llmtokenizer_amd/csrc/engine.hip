@@ -433,8 +433,9 @@ void launch_stats(bpe_gpu_ctx *c) {
     k_stat_final<<<1, 64, 0, c->st>>>(c->dE, c->dC);
 }
 
-void launch_summaries(bpe_gpu_ctx *c) {
-    k_rescan1<<<RESCAN1_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+// edges: + the block that writes the shard's edge record (sharded training)
+void launch_summaries(bpe_gpu_ctx *c, bool edges = false) {
+    k_rescan1<<<RESCAN1_BLOCKS + (edges ? 1 : 0), 256, 0, c->st>>>(c->dE, c->dC, edges ? 1 : 0);
     if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
 }
 

@@ -625,11 +625,20 @@ __device__ inline Best wave_best(Best m) {
 constexpr uint64_t SELECT_L1_MAX = 16384;  // k_select reduces level 1 directly up to this
 
 // one wave per dirty level-1 block (256 slots, 4 per lane)
-__global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+__device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C);
+
+// edges = 1 (sharded training): one extra block writes this shard's edge
+// record (it only needs k_apply's span writes) beside the rescans
+__global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl *__restrict__ C, int edges) {
     if (C->stop) return;
+    const uint32_t nblk = gridDim.x - (edges ? 1 : 0);
+    if (blockIdx.x >= nblk) {
+        edge_record_block(E, C);
+        return;
+    }
     {   // k_apply has consumed this iteration's delta vectors: clear them
         const uint32_t P = C->parity;
-        const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+        const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = nblk * blockDim.x;
         if (E->sharded) {  // (the global R went to Ctl::Rg in k_apply)
             for (uint32_t x = tid; x < 4 * E->vcap + 2; x += stride) E->xbuf[x] = 0;
         } else {
@@ -646,7 +655,7 @@ __global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl 
     const uint64_t nwork = full ? nL1 : C->nl1;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const uint64_t nwaves = (uint64_t)nblk * (blockDim.x / 64);
     for (uint64_t w = wid; w < nwork; w += nwaves) {
         const uint32_t blk = full ? (uint32_t)w : E->l1list[w];
         Best mine{0, 0, ~0ull};

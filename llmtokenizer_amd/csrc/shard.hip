@@ -129,8 +129,8 @@ int upload_table(bpe_gpu_group *g, uint32_t **d_tab, const std::vector<uint32_t 
 
 // One merge on every shard, on one stream (graph branches cost more than
 // they hide: measured ~15 us per merge for a two-branch variant):
-//   k_scan -> allreduce(deltas, R) -> k_apply -> k_edges -> allgather(edge
-//   records) -> k_rescan1 -> k_select
+//   k_scan -> allreduce(deltas, R) -> k_apply -> k_rescan1 (+ the edge record
+//   in one extra block) -> allgather(edge records) -> k_select
 // k_scan flushes its deltas straight into xbuf; the records feed the next
 // merge's halo, which k_scan derives lazily.
 int launch_group_iteration(bpe_gpu_group *g) {
@@ -141,15 +141,10 @@ int launch_group_iteration(bpe_gpu_group *g) {
         xb.push_back(c->h.xbuf);
     }
     if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
-    for (bpe_gpu_ctx *c : g->cs) {
-        k_apply<<<APPLY_A + APPLY_B, 256, 0, g->st>>>(c->dE, c->dC, APPLY_A);
-        k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 0);
-    }
+    for (bpe_gpu_ctx *c : g->cs) k_apply<<<APPLY_A + APPLY_B, 256, 0, g->st>>>(c->dE, c->dC, APPLY_A);
+    for (bpe_gpu_ctx *c : g->cs) launch_summaries(c, true);  // + the edge record
     if ((r = ex_records(g, g->d_ptrs))) return r;
-    for (bpe_gpu_ctx *c : g->cs) {
-        launch_summaries(c);
-        k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
-    }
+    for (bpe_gpu_ctx *c : g->cs) k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
     HIPCHK(hipGetLastError());
     return 0;
 }
