@@ -1117,13 +1117,15 @@ __device__ inline uint32_t tile_count(const uint32_t *hist, const uint32_t *tot,
 constexpr uint32_t SORT_T = 1024, SORT_PER = 8, SORT_CH = SORT_T * SORT_PER;
 
 struct SortLds {
-    unsigned long long ent[SORT_CH];  // staged entries in local bin order
-    uint8_t bin[SORT_CH];             // their bins
+    uint32_t ent[SORT_CH];  // staged positions in local bin order
+    uint8_t hi[SORT_CH];    // their high byte (pass A: second-byte rank, emitted as k2 << 32)
+    uint8_t bin[SORT_CH];   // their bins
     uint32_t cnt[256], lstart[256], gcur[256], gstart[256];
-};
+};  // 50 KB: three 1024-thread blocks per CU
 
 // local counting sort of this thread's SORT_PER (bin, entry) pairs, then a
-// coalesced copy of every bin's run to out[gcur[bin] ...]; gcur advances
+// coalesced copy of every bin's run to out[gcur[bin] ...]; gcur advances.
+// vals: position | hi << 32 (hi < 256); out64: emit (hi << 32 | position).
 __device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const unsigned long long *vals, uint32_t nb,
                                      void *out, bool out64) {
     for (uint32_t x = threadIdx.x; x < nb; x += SORT_T) L.cnt[x] = 0;
@@ -1132,22 +1134,42 @@ __device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const uns
 #pragma unroll
     for (uint32_t k = 0; k < SORT_PER; k++) rank[k] = bins[k] < nb ? atomicAdd(&L.cnt[bins[k]], 1u) : 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t r = 0;
-        for (uint32_t x = 0; x < nb; x++) {
-            L.lstart[x] = r;
-            L.gstart[x] = L.gcur[x];
-            L.gcur[x] += L.cnt[x];
-            r += L.cnt[x];
+    if (threadIdx.x < 64) {
+        // wave-parallel exclusive scan over the (<= 256) bins, 4 per lane
+        const uint32_t lane = threadIdx.x;
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t x = lane * 4 + q;
+            c[q] = x < nb ? L.cnt[x] : 0;
+            sum += c[q];
         }
-        L.cnt[0] = r;  // total staged (cnt[] no longer needed)
+        uint32_t incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if ((int)lane >= o) incl += y;
+        }
+        uint32_t r = incl - sum;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t x = lane * 4 + q;
+            if (x < nb) {
+                L.lstart[x] = r;
+                L.gstart[x] = L.gcur[x];
+                L.gcur[x] += c[q];
+            }
+            r += c[q];
+        }
+        const uint32_t total = __shfl(incl, 63);
+        if (lane == 0) L.cnt[0] = total;  // total staged (cnt[] no longer needed)
     }
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < SORT_PER; k++)
         if (bins[k] < nb) {
             const uint32_t s = L.lstart[bins[k]] + rank[k];
-            L.ent[s] = vals[k];
+            L.ent[s] = (uint32_t)vals[k];
+            L.hi[s] = (uint8_t)(vals[k] >> 32);
             L.bin[s] = (uint8_t)bins[k];
         }
     __syncthreads();
@@ -1155,8 +1177,8 @@ __device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const uns
     for (uint32_t s = threadIdx.x; s < total; s += SORT_T) {
         const uint32_t bn = L.bin[s];
         const uint32_t d = L.gstart[bn] + (s - L.lstart[bn]);
-        if (out64) reinterpret_cast<unsigned long long *>(out)[d] = L.ent[s];
-        else reinterpret_cast<uint32_t *>(out)[d] = (uint32_t)L.ent[s];
+        if (out64) reinterpret_cast<unsigned long long *>(out)[d] = ((unsigned long long)L.hi[s] << 32) | L.ent[s];
+        else reinterpret_cast<uint32_t *>(out)[d] = L.ent[s];
     }
     __syncthreads();
 }
