@@ -50,9 +50,21 @@ double now_ms() {
 }
 
 constexpr uint32_t ITERS_PER_GRAPH = 16;
-constexpr uint32_t SCAN_BLOCKS = 1024;  // == k_select's block size (it reduces the exit stamps)
-constexpr uint32_t APPLY_A = 256, APPLY_B = 64;
-constexpr uint32_t RESCAN1_BLOCKS = 1024, RESCAN2_BLOCKS = 128;
+// launch grids (BPE_GRID="scan,rescan1,applyA,applyB" overrides them for tuning runs)
+uint32_t SCAN_BLOCKS = 1024;  // <= k_select's block size (it reduces the exit stamps)
+uint32_t APPLY_A = 256, APPLY_B = 64;
+uint32_t RESCAN1_BLOCKS = 1024;
+constexpr uint32_t RESCAN2_BLOCKS = 128;
+struct GridInit {
+    GridInit() {
+        if (const char *g = getenv("BPE_GRID")) {
+            unsigned s = 0, r = 0, a = 0, b = 0;
+            if (sscanf(g, "%u,%u,%u,%u", &s, &r, &a, &b) == 4 && s >= 1 && s <= 1024 && r >= 1 && a >= 1 && b >= 1) {
+                SCAN_BLOCKS = s; RESCAN1_BLOCKS = r; APPLY_A = a; APPLY_B = b;
+            }
+        }
+    }
+} grid_init;
 constexpr uint32_t ENC_APPLY_BLOCKS = 1024;
 
 struct Query {
@@ -323,7 +335,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         if ((r = dalloc(c, &h.vnl[p], 4))) return r;
     }
     if ((r = dalloc(c, &h.vecd, encode ? 1 : (size_t)REPL * 4 * DENSE))) return r;
-    if ((r = dalloc(c, &h.scan_tend, SCAN_BLOCKS))) return r;
+    if ((r = dalloc(c, &h.scan_tend, 1024))) return r;
+    h.scan_blocks = SCAN_BLOCKS;
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
     if ((r = dalloc(c, &c->d_tileoff, h.ntiles + 1))) return r;

@@ -101,6 +101,7 @@ struct Eng {
     uint32_t *aux;        // per-slot scratch for the resolver (first thread)
     unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
     uint32_t fast;        // 1: schedule-free tie rule everywhere (no tracking)
+    uint32_t scan_blocks; // k_scan grid (entries of scan_tend)
     // corpus sharding (one shard per context; nshards == 1 -> no halo traffic)
     uint32_t sharded, shard, nshards;
     uint32_t *xbuf;       // [4*vcap + 2] per-merge exchange: dense deltas | R | flags (allreduced)

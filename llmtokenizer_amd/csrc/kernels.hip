@@ -826,8 +826,8 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
             if (E->l2best[i]) mine = best_merge(mine, Best{E->l2best[i], E->l2tie[i], E->l2key[i]});
     }
     mine = wave_best(mine);
-    // k_scan's last block exit (blockDim == SCAN_BLOCKS == 1024 stamps)
-    unsigned long long tend = E->scan_tend[tid];
+    // k_scan's last block exit (one stamp per k_scan block, <= blockDim)
+    unsigned long long tend = tid < E->scan_blocks ? E->scan_tend[tid] : 0ull;
     for (int o = 32; o > 0; o >>= 1) {
         const unsigned long long y = __shfl_xor(tend, o);
         tend = y > tend ? y : tend;
