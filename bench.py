@@ -276,7 +276,8 @@ def main():
                          "total_engine": round(st["ms_total"], 3)},
         "engine": {k2: st[k2] for k2 in ("n_out", "iterations", "distinct_pairs", "merged_buckets",
                                           "tracked_iters", "tie_events", "edge_events", "rule_ties",
-                                          "table_grows", "keys")},
+                                          "table_grows", "keys", "l1_rescanned", "spec_hits",
+                                          "spec_misses")},
     }
     # HBM traffic per launch from the committed rocprofv3 PMC passes
     # (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE in separate runs)

@@ -61,6 +61,9 @@ typedef struct {
     double ms_count_pass;     /* the one corpus-wide pair-count pass (k_pair_hist) */
     uint64_t candidates;      /* candidate positions examined by the scans      */
     uint64_t occurrences;     /* pair occurrences replaced                       */
+    uint64_t l1_rescanned;    /* level-1 summary blocks rescanned                 */
+    uint64_t spec_hits;       /* next merges found by the speculative scan        */
+    uint64_t spec_misses;     /* mispredicted next merges (host re-scan)          */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */

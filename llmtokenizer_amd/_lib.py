@@ -5,7 +5,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libbpe_amd.so")
+LIB_PATH = os.environ.get("BPE_LIB") or os.path.join(HERE, "libbpe_amd.so")  # BPE_LIB: A/B runs
 
 # every symbol include/*.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -38,7 +38,7 @@ class GpuStats(ctypes.Structure):
         "n_in", "n_out", "merges", "iterations", "distinct_pairs", "merged_buckets",
         "tracked_iters", "tie_events", "edge_events", "rule_ties", "table_grows", "keys")] + \
         [(n, ctypes.c_double) for n in ("ms_init", "ms_train", "ms_total", "ms_count_pass")] + \
-        [(n, ctypes.c_uint64) for n in ("candidates", "occurrences")]
+        [(n, ctypes.c_uint64) for n in ("candidates", "occurrences", "l1_rescanned", "spec_hits", "spec_misses")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -66,6 +66,23 @@ struct GridInit {
     }
 } grid_init;
 constexpr uint32_t ENC_APPLY_BLOCKS = 1024;
+// speculative one-shard graph (k_rescan_spec): rescan blocks of 1024 threads,
+// then the predicted merge's scan blocks.  BPE_SPEC=0 disables it;
+// BPE_SPEC_GRID="rescan,scan" overrides the split for tuning runs.
+uint32_t SPEC_RB = 64, SPEC_SB = 192;
+bool SPEC_ON = true;
+struct SpecInit {
+    SpecInit() {
+        if (const char *e = getenv("BPE_SPEC")) SPEC_ON = atoi(e) != 0;
+        if (const char *g = getenv("BPE_SPEC_GRID")) {
+            unsigned r = 0, s = 0;
+            if (sscanf(g, "%u,%u", &r, &s) == 2 && r >= 1 && r <= 1024 && s >= 1 && s <= 1024) {
+                SPEC_RB = r; SPEC_SB = s;
+            }
+        }
+    }
+} spec_init;
+constexpr uint32_t STAMPS = 2048;  // exit-stamp slots (>= any stamping grid)
 
 struct Query {
     uint32_t t, bucket, firstc, flags;  // flags: 1 rho, 2 nb_less(new), 4 list mates
@@ -334,9 +351,10 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         }
         if ((r = dalloc(c, &h.vnl[p], 4))) return r;
     }
-    if ((r = dalloc(c, &h.vecd, encode ? 1 : (size_t)REPL * 4 * DENSE))) return r;
-    if ((r = dalloc(c, &h.scan_tend, 1024))) return r;
-    h.scan_blocks = SCAN_BLOCKS;
+    if ((r = dalloc(c, &h.vecd, encode ? 1 : (size_t)2 * REPL * 4 * DENSE))) return r;
+    if ((r = dalloc(c, &h.scan_tend, STAMPS))) return r;
+    h.spec_on = SPEC_ON && !encode && !c->sharded;
+    h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? SPEC_RB + SPEC_SB : 0);
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
     if ((r = dalloc(c, &c->d_tileoff, h.ntiles + 1))) return r;
@@ -360,9 +378,13 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.l1key, nL1))) return r;
     if ((r = dalloc(c, &h.l1tie, nL1))) return r;
     if ((r = dalloc(c, &h.l1list, nL1 + 4ull * DENSE + 4ull * h.vcap + 64, false))) return r;
+    if ((r = dalloc(c, &h.l1v2, nL1))) return r;
+    if ((r = dalloc(c, &h.l1k2, nL1))) return r;
     if ((r = dalloc(c, &h.l2best, nL2))) return r;
     if ((r = dalloc(c, &h.l2key, nL2))) return r;
     if ((r = dalloc(c, &h.l2tie, nL2))) return r;
+    if ((r = dalloc(c, &h.l2v2, nL2))) return r;
+    if ((r = dalloc(c, &h.l2k2, nL2))) return r;
     if ((r = dalloc(c, &h.l2list, nL1 + 4ull * DENSE + 4ull * h.vcap + 64, false))) return r;
     // control block
     Ctl &C = *c->hC;
@@ -392,20 +414,25 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
     HIPCHK(hipMemsetAsync(ncnt, 0, ncap * sizeof(uint32_t), c->st));
     const uint64_t nL1 = ncap / L1W, nL2 = (nL1 + L2W - 1) / L2W;
     const uint64_t nlist = nL1 + 4ull * DENSE + 4ull * h.vcap + 64;
-    unsigned long long *l1b, *l1k, *l2b, *l2k;
+    unsigned long long *l1b, *l1k, *l2b, *l2k, *l1v, *l1q, *l2v, *l2q;
     uint32_t *l1t, *l1l, *l2t, *l2l;
     HIPCHK(hipMalloc(&l1b, nL1 * 8));
     HIPCHK(hipMalloc(&l1k, nL1 * 8));
     HIPCHK(hipMalloc(&l1t, nL1 * 4));
     HIPCHK(hipMalloc(&l1l, nlist * 4));
+    HIPCHK(hipMalloc(&l1v, nL1 * 8));
+    HIPCHK(hipMalloc(&l1q, nL1 * 8));
     HIPCHK(hipMalloc(&l2b, nL2 * 8));
     HIPCHK(hipMalloc(&l2k, nL2 * 8));
     HIPCHK(hipMalloc(&l2t, nL2 * 4));
     HIPCHK(hipMalloc(&l2l, nlist * 4));
-    void *olds[] = {h.hkey, h.hcnt, h.l1best, h.l1key, h.l1tie, h.l1list, h.l2best, h.l2key, h.l2tie, h.l2list};
+    HIPCHK(hipMalloc(&l2v, nL2 * 8));
+    HIPCHK(hipMalloc(&l2q, nL2 * 8));
+    void *olds[] = {h.hkey, h.hcnt, h.l1best, h.l1key, h.l1tie, h.l1list, h.l2best, h.l2key, h.l2tie, h.l2list,
+                    h.l1v2, h.l1k2, h.l2v2, h.l2k2};
     h.hkey = nkey; h.hcnt = ncnt; h.hcap = ncap;
-    h.l1best = l1b; h.l1key = l1k; h.l1tie = l1t; h.l1list = l1l;
-    h.l2best = l2b; h.l2key = l2k; h.l2tie = l2t; h.l2list = l2l;
+    h.l1best = l1b; h.l1key = l1k; h.l1tie = l1t; h.l1list = l1l; h.l1v2 = l1v; h.l1k2 = l1q;
+    h.l2best = l2b; h.l2key = l2k; h.l2tie = l2t; h.l2list = l2l; h.l2v2 = l2v; h.l2k2 = l2q;
     int r;
     if ((r = push_desc(c))) return r;
     c->hC->nkeys = 0;
@@ -421,9 +448,10 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
             }
         (void)hipFree(p);
     }
-    const size_t sizes[] = {ncap * 8, ncap * 4, nL1 * 8, nL1 * 8, nL1 * 4, nlist * 4, nL2 * 8, nL2 * 8, nL2 * 4, nlist * 4};
-    void *news[] = {nkey, ncnt, l1b, l1k, l1t, l1l, l2b, l2k, l2t, l2l};
-    for (int k = 0; k < 10; k++) c->train_allocs.push_back({news[k], sizes[k]});
+    const size_t sizes[] = {ncap * 8, ncap * 4, nL1 * 8, nL1 * 8, nL1 * 4, nlist * 4, nL2 * 8, nL2 * 8, nL2 * 4, nlist * 4,
+                            nL1 * 8, nL1 * 8, nL2 * 8, nL2 * 8};
+    void *news[] = {nkey, ncnt, l1b, l1k, l1t, l1l, l2b, l2k, l2t, l2l, l1v, l1q, l2v, l2q};
+    for (int k = 0; k < 14; k++) c->train_allocs.push_back({news[k], sizes[k]});
     c->stats.table_grows++;
     // the iteration graphs read every table pointer through the device
     // descriptor; only the level-2 summary launch depends on the size, so
@@ -453,11 +481,28 @@ void launch_summaries(bpe_gpu_ctx *c, bool edges = false) {
 }
 
 void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
+    if (c->h.spec_on && !tracked) {
+        // speculative: the merge's scan already ran (k_rescan_spec of the
+        // previous iteration, or the host after a miss)
+        k_apply<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
+        k_rescan_spec<<<SPEC_RB + SPEC_SB, SCAN_T, 0, c->st>>>(c->dE, c->dC, SPEC_RB);
+        if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+        k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, SEL_SPEC);
+        return;
+    }
     k_scan<false><<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
     k_apply<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
     if (tracked) launch_stats(c);
     launch_summaries(c);
-    k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? 1u : 0u);
+    k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
+}
+
+// speculative graph entry after a host-side stop: drop what a speculative
+// scan left in the other parity, then scan the committed merge for real
+void launch_redo(bpe_gpu_ctx *c) {
+    k_spec_clear<<<64, 256, 0, c->st>>>(c->dE, c->dC);
+    k_spec_reset<<<1, 64, 0, c->st>>>(c->dE, c->dC);
+    k_scan<false><<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
 }
 
 // Splice event-record nodes around every k_scan node of a captured (linear)
@@ -486,7 +531,7 @@ int add_scan_events(bpe_gpu_ctx *c, hipGraph_t g, bool tracked) {
         if (ty == hipGraphNodeTypeKernel) {
             hipKernelNodeParams kp{};
             HIPCHK(hipGraphKernelNodeGetParams(cur, &kp));
-            if (kp.func == (void *)k_scan<false>) {
+            if (kp.func == (void *)k_scan<false> || kp.func == (void *)k_rescan_spec) {
                 size_t np = 0;
                 hipGraphNode_t pred = nullptr;
                 HIPCHK(hipGraphNodeGetDependencies(cur, nullptr, &np));
@@ -779,6 +824,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
     Resolver res{c};
     int last_graph = -1;             // graph replayed last (0 plain, 1 tracked)
     uint64_t iters_before = 0;
+    bool need_scan = true;           // speculative graph: the committed merge is not scanned yet
     for (;;) {
         if ((r = pull_ctl(c))) return r;
         Ctl &C = *c->hC;
@@ -807,6 +853,8 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
                 g = tracked ? &c->g_tracked : &c->g_plain;
                 if (!*g && (r = capture(c, g, tracked, false))) return r;
                 last_graph = tracked ? 1 : 0;
+                if (!tracked && c->h.spec_on && need_scan) launch_redo(c);
+                need_scan = false;
             }
             HIPCHK(hipGraphLaunch(*g, c->st));
             break;
@@ -817,12 +865,17 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             return 0;
         case STOP_ERROR:
             return fail(BPE_GPU_EINTERNAL, C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : "thread-stat table full");
+        case STOP_REDO:  // missed prediction: k_select committed the real merge
+            C.stop = STOP_NONE;
+            if ((r = push_ctl(c))) return r;
+            need_scan = true;
+            break;
         case STOP_MODE:
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;
             launch_stats(c);
             launch_summaries(c);
-            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, 1u);
+            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, SEL_TRACKED);
             HIPCHK(hipGetLastError());
             break;
         case STOP_GROW: {
@@ -832,8 +885,9 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             if ((r = grow_table(c, c->h.hcap * 4))) return r;
             const bool tracked = !c->h.fast && C.n_live < TRACK_LIMIT;
             launch_summaries(c);
-            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? 1u : 0u);
+            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
             HIPCHK(hipGetLastError());
+            need_scan = true;
             break;
         }
         case STOP_EVENT: {
@@ -949,9 +1003,15 @@ void fill_profile(bpe_gpu_ctx *c) {
     if (C.scan_launches) {
         int khz = 0;
         (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
-        c->prof_name = "k_scan";
+        // algorithmic bytes per merge: the scan reads 8 B per candidate (list
+        // entry + token) and moves 20 B per occurrence; with the speculative
+        // graph the span is k_rescan_spec's, which also reads 12 B per slot
+        // of every dirty level-1 block
+        const bool spec = c->h.spec_on && C.counters[7];
+        c->prof_name = spec ? "k_rescan_spec" : "k_scan";
         c->prof_ms = khz > 0 ? (double)C.scan_ticks / C.scan_launches / khz : 0;
-        c->prof_bytes = (8.0 * C.counters[4] + 20.0 * C.counters[5]) / std::max<double>(1.0, C.counters[0]);
+        c->prof_bytes = (8.0 * C.counters[4] + 20.0 * C.counters[5] + (spec ? 12.0 * L1W * C.counters[6] : 0.0)) /
+                        std::max<double>(1.0, C.counters[0]);
         c->prof_launches = C.scan_launches;
     }
     c->event_ms = c->scan_n ? c->scan_ms / c->scan_n : 0;
@@ -1105,7 +1165,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     const bool tracked = !c->fast && c->n0 < TRACK_LIMIT;
     if (tracked) launch_stats(c);
     launch_summaries(c);
-    k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? 1u : 0u);
+    k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));
     const double t1 = now_ms();
@@ -1127,6 +1187,13 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.keys = C.nkeys;
     c->stats.candidates = C.counters[4];
     c->stats.occurrences = C.counters[5];
+    c->stats.l1_rescanned = C.counters[6];
+    c->stats.spec_hits = C.counters[7];
+    c->stats.spec_misses = C.counters[8];
+    if (getenv("BPE_DEBUG"))
+        fprintf(stderr, "select phases (ticks/iter): reduce %.1f merge %.1f tail %.1f\n",
+                (double)C.counters[9] / C.counters[0], (double)C.counters[10] / C.counters[0],
+                (double)C.counters[11] / C.counters[0]);
     c->stats.ms_init = t1 - t0;
     c->stats.ms_train = t2 - t1;
     c->stats.ms_total = t2 - t0;

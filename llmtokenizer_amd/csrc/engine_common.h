@@ -39,7 +39,11 @@ enum : uint32_t {
     STOP_ERROR = 5,    // invariant violated (decrement of a missing key ...)
     STOP_ENC_END = 6,  // encode: merge list exhausted
     STOP_MODE = 7,     // n fell below 2^21: switch to the tracked iteration graph
+    STOP_REDO = 8,     // speculative graph: the predicted next merge was wrong, host scans
 };
+
+// k_select's graph argument
+enum : uint32_t { SEL_PLAIN = 0, SEL_TRACKED = 1, SEL_SPEC = 2 };
 
 // encode batch descriptor (encode.hip)
 constexpr uint32_t BMAX = 512;       // merges per batch
@@ -78,7 +82,7 @@ struct Eng {
     uint32_t *vec[2][4];  // delta vectors (dec-left, dec-right, inc-left, inc-right), 2 parities
     uint32_t *vlist[2][4];
     uint32_t *vnl[2];     // [4] list lengths
-    uint32_t *vecd;       // [REPL][4][DENSE] replicated dense accumulators (ids < DENSE)
+    uint32_t *vecd;       // [2][REPL][4][DENSE] replicated dense accumulators (ids < DENSE), 2 parities
     // pair-count table: open addressing on (a,b), never deletes (count may hit 0)
     uint64_t hcap;        // power of two
     unsigned long long *hkey;  // key + 1, 0 = empty
@@ -87,8 +91,10 @@ struct Eng {
     // best packed value, number of keys holding it, smallest such key
     unsigned long long *l1best, *l1key;
     uint32_t *l1tie, *l1list;
+    unsigned long long *l1v2, *l1k2;  // runner-up value / key per level-1 block
     unsigned long long *l2best, *l2key;
     uint32_t *l2tie, *l2list;
+    unsigned long long *l2v2, *l2k2;
     // per-thread history tracking (n < TRACK_LIMIT)
     uint64_t scap;        // stats table capacity (power of two)
     unsigned long long *skey;  // ((t << 60) | (a << 30) | b) + 1
@@ -101,6 +107,7 @@ struct Eng {
     uint32_t *aux;        // per-slot scratch for the resolver (first thread)
     unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
     uint32_t fast;        // 1: schedule-free tie rule everywhere (no tracking)
+    uint32_t spec_on;     // 1: one-shard training with the speculative next-merge scan
     uint32_t scan_blocks; // k_scan grid (entries of scan_tend)
     // corpus sharding (one shard per context; nshards == 1 -> no halo traffic)
     uint32_t sharded, shard, nshards;
@@ -131,8 +138,9 @@ struct Ctl {
     uint32_t follows[NTHR];
     uint32_t last_c[NTHR];            // last pair position (compacted) per thread
     unsigned long long stat_n;        // n of the tracked iteration
-    unsigned long long counters[8];   // 0 iterations, 1 tracked, 2 rule ties, 3 events,
-                                      // 4 candidates scanned, 5 occurrences replaced
+    unsigned long long counters[12];  // 0 iterations, 1 tracked, 2 rule ties, 3 events,
+                                      // 4 candidates scanned, 5 occurrences replaced,
+                                      // 6 level-1 blocks rescanned, 7 / 8 predictions held / missed
     unsigned long long scan_t0;       // wall clock at k_scan block 0 entry
     unsigned long long scan_ticks;    // sum over merges of k_scan spans (wall-clock ticks)
     unsigned long long scan_launches;
@@ -140,6 +148,10 @@ struct Ctl {
     uint32_t F1, L1, L1new, xleft;    // first / last token start, pending last, consumed first
     uint32_t xleft_lb;                // length of the consumed first token (encode batches)
     uint32_t Rg, ebp;                 // sharded: occurrences over all shards; encode batch parity
+    // speculative next merge (one-shard training): predicted pair, its
+    // candidate list, occurrences found by k_rescan_spec, armed flag
+    uint32_t sa, sb, s_mode, s_off;
+    uint32_t s_len, sR, spec, spad;
 };
 
 // Edge record of a shard: its first and last three token ids, the run of the

@@ -49,7 +49,7 @@ __device__ inline uint32_t dval(const Eng *E, uint32_t P, int v, uint32_t x) {
     if (x >= DENSE) return E->vec[P][v][x];
     uint32_t sum = 0;
 #pragma unroll
-    for (uint32_t r = 0; r < REPL; r++) sum += E->vecd[(r * 4 + v) * DENSE + x];
+    for (uint32_t r = 0; r < REPL; r++) sum += E->vecd[((P * REPL + r) * 4 + v) * DENSE + x];
     return sum;
 }
 
@@ -182,8 +182,8 @@ __device__ inline void flush_list(uint32_t *list, uint16_t *ltag, uint32_t *lcou
 
 // in-kernel timing (bench.py's roofline): block 0 stamps the entry, every
 // block stamps its exit; k_select folds max(exit) - entry into Ctl
-__device__ inline void scan_exit_stamp(const Eng *E) {
-    if (threadIdx.x == 0) E->scan_tend[blockIdx.x] = wall_clock64();
+__device__ inline void scan_exit_stamp(const Eng *E, uint32_t bid) {
+    if (threadIdx.x == 0) E->scan_tend[bid] = wall_clock64();
 }
 
 // stage one occurrence position (single-thread path: walker / shard edge)
@@ -202,29 +202,34 @@ __device__ inline void stage_one(uint32_t *list, uint16_t *ltag, uint32_t *lcoun
 }
 
 // SH: sharded corpus (halo lookups, shard-edge step); the one-shard instance
-// compiles to the plain position-space scan
-template <bool SH>
-__global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl *__restrict__ C) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) C->scan_t0 = wall_clock64();
-    if (C->stop) return;
-    const uint32_t len = C->cand_len;
+// compiles to the plain position-space scan.  SPEC: the speculative scan of
+// the predicted next merge (C->sa, C->sb) -> z + 1 that k_rescan_spec runs
+// beside the current merge's rescan: deltas into the other parity, its
+// occurrence list right after the current merge's, counted in C->sR.
+// bid / nblk: this block's index among the scan blocks of the launch.
+template <bool SH, bool SPEC>
+__device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t bid, uint32_t nblk,
+                                 uint32_t stamp0 = 0) {
+    const uint32_t len = SPEC ? C->s_len : C->cand_len;
     // the shard-edge step runs in the last block, which usually has no
     // candidates, so its dependent loads overlap the other blocks' work
-    const bool edge_block = SH && blockIdx.x == gridDim.x - 1;
-    if (blockIdx.x * SCAN_T >= len && !edge_block) {  // block-uniform
-        scan_exit_stamp(E);
+    const bool edge_block = SH && bid == nblk - 1;
+    if (bid * SCAN_T >= len && !edge_block) {  // block-uniform
+        scan_exit_stamp(E, stamp0 + bid);
         return;
     }
-    const uint32_t a = C->a, b = C->b, z = C->z;
-    const uint32_t mode = C->cand_mode, off = C->cand_off;
-    const uint32_t P = C->parity;
+    const uint32_t a = SPEC ? C->sa : C->a, b = SPEC ? C->sb : C->b, z = SPEC ? C->z + 1 : C->z;
+    const uint32_t mode = SPEC ? C->s_mode : C->cand_mode, off = SPEC ? C->s_off : C->cand_off;
+    const uint32_t P = SPEC ? C->parity ^ 1u : C->parity;
+    uint32_t *const Rc = SPEC ? &C->sR : &C->R;
     const int64_t n = (int64_t)E->n0;
     const uint32_t *__restrict__ tok = E->tok;
     const uint32_t *__restrict__ dist = E->dist;
     const uint32_t la = E->tlen[a], lb = E->tlen[b];
     const bool count = !E->encode;
-    uint32_t *occz = E->occ + C->occ_top;
-    uint16_t *tagz = E->occnb + C->occ_top;
+    const uint32_t obase = SPEC ? C->occ_top + C->R : C->occ_top;
+    uint32_t *occz = E->occ + obase;
+    uint16_t *tagz = E->occnb + obase;
     const uint32_t want = mode == 2 ? a : b;  // tag byte the candidates must carry
     // halo of this shard for merge (a, b), from the edge records on first use
     // (the records' allgather overlaps the previous merge's rescan/select)
@@ -239,7 +244,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
     if (threadIdx.x == 0) lcount = bR = 0;
     __syncthreads();
 
-    for (uint32_t e0 = blockIdx.x * SCAN_T; e0 < len; e0 += gridDim.x * SCAN_T) {
+    for (uint32_t e0 = bid * SCAN_T; e0 < len; e0 += nblk * SCAN_T) {
         const uint32_t e = e0 + threadIdx.x;
         bool ok = false;
         int64_t i = 0, j = 0;
@@ -328,7 +333,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 const bool nocc = knext && id_at<SH>(tok, h, v_right(k, la, n), n) == a;
                 // left of this pair after the merge: the run's left neighbour, or z
                 const uint32_t pfin = m > 0 ? z : (left ? p : (p == HOLE ? HOLE : z));
-                stage_one(list, ltag, &lcount, &C->R, occz, tagz, (uint32_t)pos, nb_tag(pfin, nocc ? z : q), &bR);
+                stage_one(list, ltag, &lcount, Rc, occz, tagz, (uint32_t)pos, nb_tag(pfin, nocc ? z : q), &bR);
                 if (count) {
                     if (m == 0 && left) {
                         vadd<SH>(s, E, P, V_DL, p);
@@ -343,7 +348,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                 pos = k;
             }
         }
-        flush_list(list, ltag, &lcount, &gbase, &C->R, occz, tagz, &bR);
+        flush_list(list, ltag, &lcount, &gbase, Rc, occz, tagz, &bR);
     }
     if (edge_block) {
         // Shard edges.  Right: my last token and the first token after it form
@@ -363,7 +368,7 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
                     if (!cov) cov = a != b ? (p == b && id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a) : p == a;
                     const uint32_t q = hh.HR[1];
                     const bool nocc = q == a && hh.HR[2] == b;
-                    stage_one(list, ltag, &lcount, &C->R, occz, tagz, (uint32_t)i,
+                    stage_one(list, ltag, &lcount, Rc, occz, tagz, (uint32_t)i,
                               nb_tag(p == HOLE ? HOLE : (cov ? z : p), nocc ? z : q), &bR);
                     if (count) {
                         if (!cov) {
@@ -379,11 +384,11 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
             }
             C->xleft = xl;
         }
-        flush_list(list, ltag, &lcount, &gbase, &C->R, occz, tagz, &bR);
+        flush_list(list, ltag, &lcount, &gbase, Rc, occz, tagz, &bR);
     }
     if (count && !SH) {
         // flush into replica (block % REPL): ~REPL x fewer same-address atomics
-        uint32_t *rep = E->vecd + (uint64_t)(blockIdx.x % REPL) * 4 * DENSE;
+        uint32_t *rep = E->vecd + (uint64_t)(P * REPL + bid % REPL) * 4 * DENSE;
         for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) {
             const uint32_t c = (&s[0][0])[x];
             if (c) atomicAdd(&rep[x], c);  // result unused: no-return atomic
@@ -401,7 +406,14 @@ __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl 
         if (threadIdx.x == 0 && bR) atomicAdd(&E->xbuf[4 * vc], bR);  // this shard's R, summed
         __syncthreads();
     }
-    scan_exit_stamp(E);
+    scan_exit_stamp(E, stamp0 + bid);
+}
+
+template <bool SH>
+__global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) C->scan_t0 = wall_clock64();
+    if (C->stop) return;
+    scan_body<SH, false>(E, C, blockIdx.x, gridDim.x);
 }
 
 // --------------------------------------------------------------- pair table
@@ -438,6 +450,31 @@ __device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v)
     return ~0ull;  // table full: callers flag STOP_ERROR
 }
 
+// candidate list of pair (u, v): mode 0 the byte pair's position list, 1 / 2
+// the occurrence list of the later-created id (filtered by its tags)
+__device__ inline void cand_of(const Eng *E, uint32_t u, uint32_t v, bool valid, const uint32_t *rank,
+                               const uint32_t *poff, uint32_t *mode_o, uint32_t *off_o, uint32_t *len_o) {
+    uint32_t mode = 1, off = 0, len = 0;
+    if (valid) {
+        if (u < 256 && v < 256) {
+            const uint32_t ru = rank[u], rv = rank[v];
+            if (ru != HOLE && rv != HOLE) {
+                const uint32_t rk = ru * E->A + rv;
+                mode = 0;
+                off = poff[rk];
+                len = poff[rk + 1] - off;
+            }
+        } else if (u >= v) {  // (u,v) became adjacent when u was created: u's list, tag right == v
+            mode = 1; off = E->occ_off[u]; len = E->occ_len[u];
+        } else {              // ... when v was created: v's list, tag left == u
+            mode = 2; off = E->occ_off[v]; len = E->occ_len[v];
+        }
+    }
+    *mode_o = mode;
+    *off_o = off;
+    *len_o = len;
+}
+
 // ---------------------------------------------------------------- k_apply
 constexpr uint32_t MARK_CAP = 1024;
 
@@ -465,6 +502,10 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
             E->occ_off[z] = C->occ_top;
             E->occ_len[z] = R;
             C->pending = 1;
+            if (E->spec_on) {  // speculative graph: k_select left these to us
+                E->tlen[z] = (a < z && b < z) ? la + lb : 1;
+                if (C->spec) cand_of(E, C->sa, C->sb, true, E->rank, E->poff, &C->s_mode, &C->s_off, &C->s_len);
+            }
             const uint32_t xl = sh ? C->xleft : HOLE;
             if (xl != HOLE) {  // my first token is the b of the left shard's pair
                 tok[xl] = HOLE;
@@ -550,12 +591,17 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
                     C->err = d > 0 ? 2 : 1;
                     C->stop = STOP_ERROR;
                 } else {
+                    blk = (uint32_t)(slot / L1W);
                     const uint32_t old = E->hcnt[slot];
+                    const unsigned long long bv2 = E->l1v2[blk];  // loaded beside the count
                     const uint32_t nw = (uint32_t)((long long)old + d);
                     E->hcnt[slot] = nw;
                     dD += (long long)(nw != 0) - (long long)(old != 0);
-                    blk = (uint32_t)(slot / L1W);
-                    mark = true;
+                    // the level-1 summary (best + runner-up) only changes if the
+                    // key reaches the block's runner-up before or after the
+                    // update; a B change rescans everything anyway
+                    const unsigned long long hi = pack_val(old > nw ? old : nw, u, v, C->B);
+                    mark = hi >= bv2;
                 }
             }
         }
@@ -611,15 +657,46 @@ __device__ inline Best best_merge(Best x, Best y) {
     return Best{x.v, x.tie + y.tie, x.key < y.key ? x.key : y.key};
 }
 
-__device__ inline Best wave_best(Best m) {
+// The best (as above) plus the runner-up key in the total order (value
+// descending, key ascending): the next merge k_select predicts.
+struct Top2 {
+    Best b;
+    unsigned long long v2, k2;
+};
+
+__device__ inline bool ahead(unsigned long long va, unsigned long long ka, unsigned long long vb,
+                             unsigned long long kb) {
+    return va > vb || (va == vb && ka < kb);
+}
+
+__device__ inline Top2 top2_merge(Top2 x, Top2 y) {
+    Top2 r;
+    r.b = best_merge(x.b, y.b);
+    // runner-up: the loser's first or the winner's second
+    const bool xw = ahead(x.b.v, x.b.key, y.b.v, y.b.key);
+    const unsigned long long lv = xw ? y.b.v : x.b.v, lk = xw ? y.b.key : x.b.key;
+    const unsigned long long sv = xw ? x.v2 : y.v2, sk = xw ? x.k2 : y.k2;
+    const bool l = ahead(lv, lk, sv, sk);
+    r.v2 = l ? lv : sv;
+    r.k2 = l ? lk : sk;
+    return r;
+}
+
+__device__ inline Top2 wave_top2(Top2 m) {
     for (int o = 32; o > 0; o >>= 1) {
-        Best y;
-        y.v = __shfl_xor(m.v, o);
-        y.tie = __shfl_xor(m.tie, o);
-        y.key = __shfl_xor(m.key, o);
-        m = best_merge(m, y);
+        Top2 y;
+        y.b.v = __shfl_xor(m.b.v, o);
+        y.b.tie = __shfl_xor(m.b.tie, o);
+        y.b.key = __shfl_xor(m.b.key, o);
+        y.v2 = __shfl_xor(m.v2, o);
+        y.k2 = __shfl_xor(m.k2, o);
+        m = top2_merge(m, y);
     }
     return m;  // identical in every lane
+}
+
+__device__ inline Top2 top2_one(unsigned long long v, uint32_t tie, unsigned long long key) {
+    return Top2{Best{v, tie, key}, 0, ~0ull};
 }
 
 constexpr uint64_t SELECT_L1_MAX = 16384;  // k_select reduces level 1 directly up to this
@@ -629,20 +706,17 @@ __device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C
 
 // edges = 1 (sharded training): one extra block writes this shard's edge
 // record (it only needs k_apply's span writes) beside the rescans
-__global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl *__restrict__ C, int edges) {
-    if (C->stop) return;
-    const uint32_t nblk = gridDim.x - (edges ? 1 : 0);
-    if (blockIdx.x >= nblk) {
-        edge_record_block(E, C);
-        return;
-    }
+// bid / nblk: this block's index among the launch's rescan blocks (any
+// block size: the work is one wave per dirty level-1 block)
+__device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t bid, uint32_t nblk) {
     {   // k_apply has consumed this iteration's delta vectors: clear them
         const uint32_t P = C->parity;
-        const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = nblk * blockDim.x;
+        const uint32_t tid = bid * blockDim.x + threadIdx.x, stride = nblk * blockDim.x;
         if (E->sharded) {  // (the global R went to Ctl::Rg in k_apply)
             for (uint32_t x = tid; x < 4 * E->vcap + 2; x += stride) E->xbuf[x] = 0;
         } else {
-            for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride) E->vecd[x] = 0;
+            uint32_t *vd = E->vecd + (uint64_t)P * REPL * 4 * DENSE;
+            for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride) vd[x] = 0;
             for (int vv = 0; vv < 4; vv++) {
                 const uint32_t nq = E->vnl[P][vv];
                 for (uint32_t t = tid; t < nq; t += stride) E->vec[P][vv][E->vlist[P][vv][t]] = 0;
@@ -654,33 +728,72 @@ __global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl 
     const uint64_t nL1 = E->hcap / L1W;
     const uint64_t nwork = full ? nL1 : C->nl1;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    const uint64_t wid = (uint64_t)bid * (blockDim.x / 64) + threadIdx.x / 64;
     const uint64_t nwaves = (uint64_t)nblk * (blockDim.x / 64);
     for (uint64_t w = wid; w < nwork; w += nwaves) {
         const uint32_t blk = full ? (uint32_t)w : E->l1list[w];
-        Best mine{0, 0, ~0ull};
-        uint32_t cnt[L1W / 64];
-        unsigned long long key[L1W / 64];
+        Top2 mine = top2_one(0, 0, ~0ull);
+        // two halves of 8 slots per lane, each half's counts and keys loaded
+        // together (one round trip per half; half the registers of one pass)
+        constexpr uint32_t HQ = L1W / 128;
 #pragma unroll
-        for (uint32_t q = 0; q < L1W / 64; q++) {  // all loads first: one round trip
-            const uint64_t slot = (uint64_t)blk * L1W + q * 64 + lane;
-            cnt[q] = E->hcnt[slot];
-            key[q] = E->hkey[slot];
-        }
+        for (uint32_t h = 0; h < 2; h++) {
+            uint32_t cnt[HQ];
+            unsigned long long key[HQ];
 #pragma unroll
-        for (uint32_t q = 0; q < L1W / 64; q++) {
-            if (cnt[q]) {
-                const unsigned long long k = key[q] - 1;
-                mine = best_merge(mine, Best{pack_val(cnt[q], (uint32_t)(k >> 32), (uint32_t)k, B), 1, k});
+            for (uint32_t q = 0; q < HQ; q++) {
+                const uint64_t slot = (uint64_t)blk * L1W + (h * HQ + q) * 64 + lane;
+                cnt[q] = E->hcnt[slot];
+                key[q] = E->hkey[slot];
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < HQ; q++) {
+                if (cnt[q]) {
+                    const unsigned long long k = key[q] - 1;
+                    mine = top2_merge(mine, top2_one(pack_val(cnt[q], (uint32_t)(k >> 32), (uint32_t)k, B), 1, k));
+                }
             }
         }
-        const Best r = wave_best(mine);
+        const Top2 r = wave_top2(mine);
         if (lane == 0) {
-            E->l1best[blk] = r.v;
-            E->l1tie[blk] = r.v ? r.tie : 0;
-            E->l1key[blk] = r.key;
+            E->l1best[blk] = r.b.v;
+            E->l1tie[blk] = r.b.v ? r.b.tie : 0;
+            E->l1key[blk] = r.b.key;
+            E->l1v2[blk] = r.v2;
+            E->l1k2[blk] = r.k2;
             if (!full) E->l2list[w] = blk / L2W;  // duplicates are harmless
         }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl *__restrict__ C, int edges) {
+    if (C->stop) return;
+    const uint32_t nblk = gridDim.x - (edges ? 1 : 0);
+    if (blockIdx.x >= nblk) {
+        edge_record_block(E, C);
+        return;
+    }
+    rescan1_body(E, C, blockIdx.x, nblk);
+}
+
+// Speculative pipeline (one-shard training graph): the current merge's
+// rescan (blocks [0, rblocks)) and, beside it, the scan of the merge k_select
+// predicted to come next (the runner-up of the last selection; the rest of
+// the grid).  The scan only reads tokens, which k_apply has finished
+// rewriting, so the two are independent; k_select checks the prediction and
+// either adopts the scan (flips the delta parity) or asks the host for the
+// real scan (STOP_REDO).  Every block stamps its exit for the in-kernel span.
+__global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ E, Ctl *__restrict__ C,
+                                                         uint32_t rblocks) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) C->scan_t0 = wall_clock64();
+    if (C->stop) return;
+    if (blockIdx.x < rblocks) {
+        rescan1_body(E, C, blockIdx.x, rblocks);
+        scan_exit_stamp(E, blockIdx.x);
+    } else if (C->spec) {
+        scan_body<false, true>(E, C, blockIdx.x - rblocks, gridDim.x - rblocks, rblocks);
+    } else {
+        scan_exit_stamp(E, blockIdx.x);
     }
 }
 
@@ -699,16 +812,19 @@ __global__ __launch_bounds__(256) void k_rescan2(const Eng *__restrict__ E, Ctl 
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
     for (uint64_t w = wid; w < nwork; w += nwaves) {
         const uint32_t b2 = full ? (uint32_t)w : E->l2list[w];
-        Best mine{0, 0, ~0ull};
+        Top2 mine = top2_one(0, 0, ~0ull);
         for (uint32_t q = 0; q < L2W / 64; q++) {
             const uint64_t i1 = (uint64_t)b2 * L2W + q * 64 + lane;
-            if (i1 < nL1 && E->l1best[i1]) mine = best_merge(mine, Best{E->l1best[i1], E->l1tie[i1], E->l1key[i1]});
+            if (i1 < nL1 && E->l1best[i1])
+                mine = top2_merge(mine, Top2{Best{E->l1best[i1], E->l1tie[i1], E->l1key[i1]}, E->l1v2[i1], E->l1k2[i1]});
         }
-        const Best r = wave_best(mine);
+        const Top2 r = wave_top2(mine);
         if (lane == 0) {
-            E->l2best[b2] = r.v;
-            E->l2tie[b2] = r.v ? r.tie : 0;
-            E->l2key[b2] = r.key;
+            E->l2best[b2] = r.b.v;
+            E->l2tie[b2] = r.b.v ? r.b.tie : 0;
+            E->l2key[b2] = r.b.key;
+            E->l2v2[b2] = r.v2;
+            E->l2k2[b2] = r.k2;
         }
     }
 }
@@ -731,25 +847,7 @@ __device__ inline void commit_merge(const Eng *E, Ctl *C, uint32_t u, uint32_t v
     C->merges_done = md + 1;
     const bool valid = u < z && v < z;  // ids must already exist
     E->tlen[z] = valid ? E->tlen[u] + E->tlen[v] : 1;
-    uint32_t mode = 1, off = 0, len = 0;
-    if (valid) {
-        if (u < 256 && v < 256) {
-            const uint32_t ru = rank[u], rv = rank[v];
-            if (ru != HOLE && rv != HOLE) {
-                const uint32_t rk = ru * E->A + rv;
-                mode = 0;
-                off = poff[rk];
-                len = poff[rk + 1] - off;
-            }
-        } else if (u >= v) {  // (u,v) became adjacent when u was created: u's list, tag right == v
-            mode = 1; off = E->occ_off[u]; len = E->occ_len[u];
-        } else {              // ... when v was created: v's list, tag left == u
-            mode = 2; off = E->occ_off[v]; len = E->occ_len[v];
-        }
-    }
-    C->cand_mode = mode;
-    C->cand_off = off;
-    C->cand_len = len;
+    cand_of(E, u, v, valid, rank, poff, &C->cand_mode, &C->cand_off, &C->cand_len);
 }
 
 // bookkeeping of the iteration that just ran (k_scan / k_apply)
@@ -769,13 +867,20 @@ __device__ inline void finish_iteration(const Eng *E, Ctl *C) {
 
 // ---------------------------------------------------------------- k_select
 
-// decisions of one selection (thread 0, on the LDS copy of the control block)
-__device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Best r, unsigned long long tend,
-                                   uint32_t tracked_graph, const uint32_t *rank, const uint32_t *poff) {
-    if (C->pending && tend > C->scan_t0) {  // a merge ran: account its k_scan span
+// decisions of one selection (thread 0, on the LDS copy of the control block).
+// graph: SEL_PLAIN / SEL_TRACKED / SEL_SPEC (the speculative one-shard graph,
+// whose k_rescan_spec ran the scan of the prediction armed last time).
+__device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Top2 r2, unsigned long long tend,
+                                   uint32_t graph, const uint32_t *rank, const uint32_t *poff) {
+    const Best r = r2.b;
+    const uint32_t tracked_graph = graph == SEL_TRACKED;
+    if (C->pending && tend > C->scan_t0) {  // a merge ran: account its scan span
         C->scan_ticks += tend - C->scan_t0;
         C->scan_launches++;
     }
+    if (C->pending) C->counters[6] += (C->full || summary_B(C->D) != C->B) ? E->hcap / L1W : C->nl1;
+    const uint32_t was_spec = graph == SEL_SPEC ? C->spec : 0;  // a scan of (sa, sb) ran since
+    C->spec = 0;
     finish_iteration(E, C);
     if (!tracked_graph && !E->fast && C->n_live < TRACK_LIMIT) { C->stop = STOP_MODE; return; }
     const uint64_t D = C->D;
@@ -795,15 +900,89 @@ __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Best r, un
     // untracked tie (n >= 2^20, schedule-dependent in the reference): the
     // project rule is the smallest (a,b) -- r.key already is that key
     if (r.tie > 1) C->counters[2]++;
-    commit_merge(E, C, (uint32_t)(r.key >> 32), (uint32_t)r.key, rank, poff);
+    const uint32_t u = (uint32_t)(r.key >> 32), v = (uint32_t)r.key;
+    if (!E->spec_on || tracked || tracked_graph) {
+        commit_merge(E, C, u, v, rank, poff);
+        return;
+    }
+    // speculative graph: a held prediction needs no global load here (the
+    // next k_apply writes tlen[z] and looks up the new prediction's list)
+    const bool hit = was_spec && u == C->sa && v == C->sb;
+    const uint32_t md = C->merges_done, z = 256 + md;
+    uint32_t cm = C->s_mode, co = C->s_off, cl = C->s_len;  // a held prediction's list
+    if (!hit) cand_of(E, u, v, u < z && v < z, rank ? rank : E->rank, poff ? poff : E->poff, &cm, &co, &cl);
+    const bool arm = r2.v2 && (uint32_t)(r2.v2 >> 32) > 1 && md + 1 < E->mcap;
+    E->merges[2 * md] = u;
+    E->merges[2 * md + 1] = v;
+    C->a = u;
+    C->b = v;
+    C->z = z;
+    C->merges_done = md + 1;
+    C->cand_mode = cm;
+    C->cand_off = co;
+    C->cand_len = cl;
+    if (hit) {  // prediction held: adopt its scan
+        C->R = C->sR;
+        C->parity ^= 1u;
+        C->counters[7]++;
+    } else if (graph == SEL_SPEC) {  // the host runs the real scan
+        C->stop = STOP_REDO;
+        C->counters[8]++;
+    }
+    // predict the merge after this one: the runner-up of this selection
+    C->sR = 0;
+    C->sa = (uint32_t)(r2.k2 >> 32);
+    C->sb = (uint32_t)r2.k2;
+    C->spec = arm ? 1u : 0u;
+}
+
+// One wave's top-2 (+ tie count of the best) over its share of n summary
+// entries (entries tid, tid + blockDim, ...), result in every lane.  The best
+// values alone (8 B per entry) give the wave's second-largest best M2 (with
+// multiplicity); only entries whose best reaches M2 can hold the wave's best
+// or runner-up, so only those few load their key / tie / runner-up.
+__device__ inline Top2 summary_top2(const unsigned long long *best, const uint32_t *tie,
+                                    const unsigned long long *key, const unsigned long long *v2,
+                                    const unsigned long long *k2, uint64_t n) {
+    constexpr uint32_t PER = SELECT_L1_MAX / 1024;
+    const uint32_t tid = threadIdx.x;
+    unsigned long long v[PER];
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        const uint64_t i = tid + (uint64_t)k * blockDim.x;
+        v[k] = i < n ? best[i] : 0ull;
+    }
+    unsigned long long m1 = 0, m2 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        m2 = max(m2, min(m1, v[k]));
+        m1 = max(m1, v[k]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y1 = __shfl_xor(m1, o), y2 = __shfl_xor(m2, o);
+        m2 = max(max(m2, y2), min(m1, y1));
+        m1 = max(m1, y1);
+    }
+    const unsigned long long t = m2 ? m2 : 1ull;  // one live entry: M2 = 0
+    Top2 mine = top2_one(0, 0, ~0ull);
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        const uint64_t i = tid + (uint64_t)k * blockDim.x;
+        if (v[k] >= t) mine = top2_merge(mine, Top2{Best{v[k], tie[i], key[i]}, v2[i], k2[i]});
+    }
+    for (uint64_t i = tid + (uint64_t)PER * blockDim.x; i < n; i += blockDim.x)  // (tables beyond 2^32 slots)
+        if (best[i]) mine = top2_merge(mine, Top2{Best{best[i], tie[i], key[i]}, v2[i], k2[i]});
+    return wave_top2(mine);
 }
 
 // Top-level argmax + the iteration's bookkeeping.  The control block and byte
 // ranks are staged in LDS while the summaries are reduced,
 // so thread 0's decisions start from LDS; the control block is written back
 // at the end.
-__global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl *__restrict__ Cg, uint32_t tracked_graph) {
+__global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl *__restrict__ Cg, uint32_t graph) {
     if (Cg->stop) return;
+    const unsigned long long sc_t0 = wall_clock64();
+    unsigned long long sc_t1 = 0;
     __shared__ Ctl sc;
     __shared__ uint32_t srank[256];
     uint32_t *spoff = nullptr;
@@ -814,36 +993,66 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
     for (uint32_t x = tid; x < CW; x += blockDim.x) scw[x] = cgw[x];
     for (uint32_t x = tid; x < 256; x += blockDim.x) srank[x] = E->rank[x];
     const bool pl = false;  // (staging all byte-pair offsets costs more than the 2 loads it saves)
+    // scan-block exit stamps: loaded first so they overlap the reduction
+    unsigned long long tend = 0;
+    for (uint32_t x = tid; x < E->scan_blocks; x += blockDim.x) tend = max(tend, E->scan_tend[x]);
     const uint64_t nL1 = E->hcap / L1W;
-    Best mine{0, 0, ~0ull};
-    if (nL1 <= SELECT_L1_MAX) {
-#pragma unroll 4
-        for (uint64_t i = tid; i < nL1; i += blockDim.x)
-            if (E->l1best[i]) mine = best_merge(mine, Best{E->l1best[i], E->l1tie[i], E->l1key[i]});
-    } else {
-        const uint64_t nL2 = (nL1 + L2W - 1) / L2W;
-        for (uint64_t i = tid; i < nL2; i += blockDim.x)
-            if (E->l2best[i]) mine = best_merge(mine, Best{E->l2best[i], E->l2tie[i], E->l2key[i]});
-    }
-    mine = wave_best(mine);
+    const bool lvl1 = nL1 <= SELECT_L1_MAX;
+    Top2 mine = summary_top2(lvl1 ? E->l1best : E->l2best, lvl1 ? E->l1tie : E->l2tie, lvl1 ? E->l1key : E->l2key,
+                             lvl1 ? E->l1v2 : E->l2v2, lvl1 ? E->l1k2 : E->l2k2,
+                             lvl1 ? nL1 : (nL1 + L2W - 1) / L2W);
+    if (tid == 0) sc_t1 = wall_clock64();
     // k_scan's last block exit (one stamp per k_scan block, <= blockDim)
-    unsigned long long tend = tid < E->scan_blocks ? E->scan_tend[tid] : 0ull;
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long y = __shfl_xor(tend, o);
-        tend = y > tend ? y : tend;
-    }
-    __shared__ Best sw[16];
+    for (int o = 32; o > 0; o >>= 1) tend = max(tend, (unsigned long long)__shfl_xor(tend, o));
+    __shared__ Top2 sw[16];
     __shared__ unsigned long long st[16];
     if ((tid & 63) == 0) { sw[tid >> 6] = mine; st[tid >> 6] = tend; }
     __syncthreads();
+    if (tid < 64) {  // wave 0 merges the 16 wave results (4 shuffle steps)
+        Top2 w = tid < blockDim.x / 64 ? sw[tid] : top2_one(0, 0, ~0ull);
+        for (int o = 8; o > 0; o >>= 1) {
+            Top2 y;
+            y.b.v = __shfl_xor(w.b.v, o);
+            y.b.tie = __shfl_xor(w.b.tie, o);
+            y.b.key = __shfl_xor(w.b.key, o);
+            y.v2 = __shfl_xor(w.v2, o);
+            y.k2 = __shfl_xor(w.k2, o);
+            w = top2_merge(w, y);
+        }
+        if (tid == 0) sw[0] = w;
+    }
     if (tid == 0) {
-        Best r = sw[0];
-        for (uint32_t k = 1; k < blockDim.x / 64; k++) r = best_merge(r, sw[k]);
-        for (uint32_t k = 0; k < blockDim.x / 64; k++) tend = st[k] > tend ? st[k] : tend;
-        select_tail(E, &sc, r, tend, tracked_graph, srank, pl ? spoff : nullptr);
+        const Top2 r2 = sw[0];
+        for (uint32_t k = 0; k < blockDim.x / 64; k++) tend = max(tend, st[k]);
+        const unsigned long long t2 = wall_clock64();
+        select_tail(E, &sc, r2, tend, graph, srank, pl ? spoff : nullptr);
+        const unsigned long long t3 = wall_clock64();
+        sc.counters[9] += sc_t1 - sc_t0;   // (select phase timing, temporary)
+        sc.counters[10] += t2 - sc_t1;
+        sc.counters[11] += t3 - t2;
     }
     __syncthreads();
     for (uint32_t x = tid; x < CW; x += blockDim.x) cgw[x] = scw[x];
+}
+
+// after a missed prediction (or any host-side stop): clear the other
+// parity's delta vectors the speculative scan may have filled
+__global__ __launch_bounds__(256) void k_spec_clear(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    const uint32_t Q = C->parity ^ 1u;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    uint32_t *vd = E->vecd + (uint64_t)Q * REPL * 4 * DENSE;
+    for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride) vd[x] = 0;
+    for (int vv = 0; vv < 4; vv++) {
+        const uint32_t nq = E->vnl[Q][vv];
+        for (uint32_t t = tid; t < nq; t += stride) E->vec[Q][vv][E->vlist[Q][vv][t]] = 0;
+    }
+}
+
+// second half: list lengths and the speculative count (after k_spec_clear)
+__global__ void k_spec_reset(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    const uint32_t Q = C->parity ^ 1u;
+    if (threadIdx.x < 4) E->vnl[Q][threadIdx.x] = 0;
+    if (threadIdx.x == 0) C->sR = 0;
 }
 
 // commit a merge chosen by the host resolver (after STOP_EVENT)
