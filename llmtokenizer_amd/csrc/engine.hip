@@ -70,14 +70,19 @@ constexpr uint32_t ENC_APPLY_BLOCKS = 1024;
 // then the predicted merge's scan blocks.  BPE_SPEC=0 disables it;
 // BPE_SPEC_GRID="rescan,scan" overrides the split for tuning runs.
 uint32_t SPEC_RB = 64, SPEC_SB = 192;
+uint32_t FUSED_A = 64, FUSED_B = 16;  // k_fused apply blocks (1024 threads): span rewrite, table update
 bool SPEC_ON = true;
 struct SpecInit {
     SpecInit() {
         if (const char *e = getenv("BPE_SPEC")) SPEC_ON = atoi(e) != 0;
         if (const char *g = getenv("BPE_SPEC_GRID")) {
-            unsigned r = 0, s = 0;
-            if (sscanf(g, "%u,%u", &r, &s) == 2 && r >= 1 && r <= 1024 && s >= 1 && s <= 1024) {
+            unsigned r = 0, s = 0, a = 0, b = 0;
+            const int k = sscanf(g, "%u,%u,%u,%u", &r, &s, &a, &b);
+            if (k >= 2 && r >= 1 && r <= 1024 && s >= 1 && s <= 1024) {
                 SPEC_RB = r; SPEC_SB = s;
+            }
+            if (k == 4 && a >= 1 && b >= 1) {
+                FUSED_A = a; FUSED_B = b;
             }
         }
     }
@@ -377,7 +382,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.l1best, nL1))) return r;
     if ((r = dalloc(c, &h.l1key, nL1))) return r;
     if ((r = dalloc(c, &h.l1tie, nL1))) return r;
-    if ((r = dalloc(c, &h.l1list, nL1 + 4ull * DENSE + 4ull * h.vcap + 64, false))) return r;
+    h.l1cap = nL1 + 4ull * DENSE + 4ull * h.vcap + 64;
+    if ((r = dalloc(c, &h.l1list, 2 * h.l1cap, false))) return r;
     if ((r = dalloc(c, &h.l1v2, nL1))) return r;
     if ((r = dalloc(c, &h.l1k2, nL1))) return r;
     if ((r = dalloc(c, &h.l2best, nL2))) return r;
@@ -419,7 +425,7 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
     HIPCHK(hipMalloc(&l1b, nL1 * 8));
     HIPCHK(hipMalloc(&l1k, nL1 * 8));
     HIPCHK(hipMalloc(&l1t, nL1 * 4));
-    HIPCHK(hipMalloc(&l1l, nlist * 4));
+    HIPCHK(hipMalloc(&l1l, 2 * nlist * 4));
     HIPCHK(hipMalloc(&l1v, nL1 * 8));
     HIPCHK(hipMalloc(&l1q, nL1 * 8));
     HIPCHK(hipMalloc(&l2b, nL2 * 8));
@@ -432,6 +438,7 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
                     h.l1v2, h.l1k2, h.l2v2, h.l2k2};
     h.hkey = nkey; h.hcnt = ncnt; h.hcap = ncap;
     h.l1best = l1b; h.l1key = l1k; h.l1tie = l1t; h.l1list = l1l; h.l1v2 = l1v; h.l1k2 = l1q;
+    h.l1cap = nlist;
     h.l2best = l2b; h.l2key = l2k; h.l2tie = l2t; h.l2list = l2l; h.l2v2 = l2v; h.l2k2 = l2q;
     int r;
     if ((r = push_desc(c))) return r;
@@ -448,7 +455,7 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
             }
         (void)hipFree(p);
     }
-    const size_t sizes[] = {ncap * 8, ncap * 4, nL1 * 8, nL1 * 8, nL1 * 4, nlist * 4, nL2 * 8, nL2 * 8, nL2 * 4, nlist * 4,
+    const size_t sizes[] = {ncap * 8, ncap * 4, nL1 * 8, nL1 * 8, nL1 * 4, 2 * nlist * 4, nL2 * 8, nL2 * 8, nL2 * 4, nlist * 4,
                             nL1 * 8, nL1 * 8, nL2 * 8, nL2 * 8};
     void *news[] = {nkey, ncnt, l1b, l1k, l1t, l1l, l2b, l2k, l2t, l2l, l1v, l1q, l2v, l2q};
     for (int k = 0; k < 14; k++) c->train_allocs.push_back({news[k], sizes[k]});
@@ -482,12 +489,11 @@ void launch_summaries(bpe_gpu_ctx *c, bool edges = false) {
 
 void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
     if (c->h.spec_on && !tracked) {
-        // speculative: the merge's scan already ran (k_rescan_spec of the
-        // previous iteration, or the host after a miss)
-        k_apply<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
+        // fused speculative graph: entered with the current merge applied
+        // (by the previous k_fused, or the host after a stop)
         k_rescan_spec<<<SPEC_RB + SPEC_SB, SCAN_T, 0, c->st>>>(c->dE, c->dC, SPEC_RB);
         if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
-        k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, SEL_SPEC);
+        k_fused<<<1 + FUSED_A + FUSED_B, 1024, 0, c->st>>>(c->dE, c->dC, FUSED_A);
         return;
     }
     k_scan<false><<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
@@ -497,12 +503,18 @@ void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
     k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
 }
 
-// speculative graph entry after a host-side stop: drop what a speculative
-// scan left in the other parity, then scan the committed merge for real
-void launch_redo(bpe_gpu_ctx *c) {
+// fused graph, after any stop: revert the speculative apply if the stopping
+// selection ran beside one, and drop the other parity's speculative state
+void launch_spec_revert(bpe_gpu_ctx *c, bool undo) {
+    if (undo) k_undo<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
     k_spec_clear<<<64, 256, 0, c->st>>>(c->dE, c->dC);
     k_spec_reset<<<1, 64, 0, c->st>>>(c->dE, c->dC);
+}
+
+// fused graph entry: scan and apply the committed merge for real
+void launch_redo(bpe_gpu_ctx *c) {
     k_scan<false><<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
+    k_apply<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
 }
 
 // Splice event-record nodes around every k_scan node of a captured (linear)
@@ -840,6 +852,13 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
                     (void)hipGetLastError();  // do not leave a sticky error behind
                 }
             }
+        }
+        if (!encode && last_graph == 0 && c->h.spec_on && C.stop != STOP_NONE && C.stop != STOP_ERROR) {
+            // the fused graph stopped: revert the speculative apply that ran
+            // beside the stopping selection (if any), clear the other parity
+            launch_spec_revert(c, C.spec_z != 0 && C.spec_z == C.stop_z + 1);
+            HIPCHK(hipGetLastError());
+            if ((r = pull_ctl(c))) return r;
         }
         last_graph = -1;
         iters_before = C.counters[0];

@@ -10,6 +10,7 @@
 // rewrites the whole u32 array per merge, bpe/src/bpe.c:760-777).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace bpeamd {
@@ -43,7 +44,7 @@ enum : uint32_t {
 };
 
 // k_select's graph argument
-enum : uint32_t { SEL_PLAIN = 0, SEL_TRACKED = 1, SEL_SPEC = 2 };
+enum : uint32_t { SEL_PLAIN = 0, SEL_TRACKED = 1, SEL_FUSED = 2 };
 
 // encode batch descriptor (encode.hip)
 constexpr uint32_t BMAX = 512;       // merges per batch
@@ -90,7 +91,8 @@ struct Eng {
     // max summaries: level 1 = 256 slots, level 2 = 256 level-1 entries;
     // best packed value, number of keys holding it, smallest such key
     unsigned long long *l1best, *l1key;
-    uint32_t *l1tie, *l1list;
+    uint32_t *l1tie, *l1list;        // l1list: [2][l1cap] dirty level-1 blocks, per parity
+    uint64_t l1cap;
     unsigned long long *l1v2, *l1k2;  // runner-up value / key per level-1 block
     unsigned long long *l2best, *l2key;
     uint32_t *l2tie, *l2list;
@@ -120,17 +122,21 @@ struct Eng {
     EncBatch *eb;         // [2] double-buffered batch descriptors
 };
 
+// Control block.  Everything up to Dp is owned by k_select, which stages it in
+// LDS and writes it back whole; the tail section is written by k_apply and
+// k_rescan_spec, which in the fused speculative graph run while k_select does
+// (k_select touches the tail only with single-word stores to the slot of the
+// merge it finishes).  Per-merge slots are indexed by the delta parity.
 struct Ctl {
     uint32_t a, b, z, stop;
     uint32_t merges_done, parity, R, occ_top;
-    uint32_t cand_mode, cand_off, cand_len, nl1;
+    uint32_t cand_mode, cand_off, cand_len, stop_z;  // stop_z: z when a selection stopped
     uint32_t nl2, full, event, ties;
     unsigned long long n_live;
-    unsigned long long D;
+    unsigned long long D;      // distinct pairs, folded through the last finished merge
     unsigned long long B;      // B used by the level summaries
-    unsigned long long nkeys;
     unsigned long long W;      // packed best of the last selection
-    uint32_t edge, pending, wslot, err;
+    uint32_t edge, wslot, pad0, pad1;
     unsigned long long Bcur[NTHR];    // per-thread table sizes (history)
     unsigned long long Bstart[NTHR];  // sizes at the start of the tracked iteration
     unsigned long long Bfin[NTHR];    // sizes after its count phase
@@ -149,10 +155,21 @@ struct Ctl {
     uint32_t xleft_lb;                // length of the consumed first token (encode batches)
     uint32_t Rg, ebp;                 // sharded: occurrences over all shards; encode batch parity
     // speculative next merge (one-shard training): predicted pair, its
-    // candidate list, occurrences found by k_rescan_spec, armed flag
+    // candidate list, armed flag; occurrences k_rescan_spec found, per parity
     uint32_t sa, sb, s_mode, s_off;
-    uint32_t s_len, sR, spec, spad;
+    uint32_t s_len, spec, sRp[2];
+    // ---- tail: written by k_apply / k_rescan_spec (see above)
+    unsigned long long Dp[2];   // D delta of the merge applied with parity p (finish_iteration folds it)
+    unsigned long long nkeys;   // pair-table slots in use
+    uint32_t nl1p[2];           // dirty level-1 blocks listed by the merge applied with parity p
+    uint32_t pend[2];           // a merge with parity p was applied and is not finished yet
+    uint32_t err, spec_z;       // error code; z of the last speculatively applied merge
+    // k_rescan_spec's descriptor of the merge the fused graph applies speculatively
+    uint32_t nx_valid, nx_a, nx_b, nx_z;
+    uint32_t nx_P, nx_occ, nx_pad0, nx_pad1;
+    unsigned long long nx_B;
 };
+constexpr uint32_t CTL_SELECT_WORDS = offsetof(Ctl, Dp) / 4;  // k_select's write-back
 
 // Edge record of a shard: its first and last three token ids, the run of the
 // last id at its end, and whether the whole shard is that run.  The halo a

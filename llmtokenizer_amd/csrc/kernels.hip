@@ -201,6 +201,35 @@ __device__ inline void stage_one(uint32_t *list, uint16_t *ltag, uint32_t *lcoun
     }
 }
 
+// The control-block words the per-merge kernels need, loaded together before
+// the stop check: one round trip instead of a stop load followed by dependent
+// ones (Ctl lives in HBM between launches).
+struct Snap {
+    uint32_t stop, a, b, z, parity, R, occ_top, mode, off, len, nl1, full, spec, sa, sb, s_mode, s_off, s_len;
+    unsigned long long D, B;  // D: distinct pairs after the merge applied last (base + its delta)
+};
+
+__device__ inline Snap snap(const Ctl *C) {
+    Snap s;
+    s.stop = C->stop; s.a = C->a; s.b = C->b; s.z = C->z;
+    s.parity = C->parity; s.R = C->R; s.occ_top = C->occ_top;
+    s.mode = C->cand_mode; s.off = C->cand_off; s.len = C->cand_len;
+    s.nl1 = C->nl1p[s.parity]; s.full = C->full;
+    s.spec = C->spec; s.sa = C->sa; s.sb = C->sb; s.s_mode = C->s_mode; s.s_off = C->s_off; s.s_len = C->s_len;
+    s.D = C->D + C->Dp[s.parity]; s.B = C->B;
+    return s;
+}
+
+// the fused graph's speculative k_apply: the merge k_rescan_spec described
+__device__ inline Snap snap_next(const Ctl *C) {
+    Snap s = {};
+    s.stop = C->nx_valid ? 0u : 1u;
+    s.a = C->nx_a; s.b = C->nx_b; s.z = C->nx_z; s.parity = C->nx_P; s.occ_top = C->nx_occ;
+    s.R = C->sRp[s.parity];
+    s.B = C->nx_B;
+    return s;
+}
+
 // SH: sharded corpus (halo lookups, shard-edge step); the one-shard instance
 // compiles to the plain position-space scan.  SPEC: the speculative scan of
 // the predicted next merge (C->sa, C->sb) -> z + 1 that k_rescan_spec runs
@@ -208,9 +237,9 @@ __device__ inline void stage_one(uint32_t *list, uint16_t *ltag, uint32_t *lcoun
 // occurrence list right after the current merge's, counted in C->sR.
 // bid / nblk: this block's index among the scan blocks of the launch.
 template <bool SH, bool SPEC>
-__device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t bid, uint32_t nblk,
-                                 uint32_t stamp0 = 0) {
-    const uint32_t len = SPEC ? C->s_len : C->cand_len;
+__device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__restrict__ C, const Snap &S, uint32_t bid,
+                                          uint32_t nblk, uint32_t stamp0 = 0) {
+    const uint32_t len = SPEC ? S.s_len : S.len;
     // the shard-edge step runs in the last block, which usually has no
     // candidates, so its dependent loads overlap the other blocks' work
     const bool edge_block = SH && bid == nblk - 1;
@@ -218,16 +247,16 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
         scan_exit_stamp(E, stamp0 + bid);
         return;
     }
-    const uint32_t a = SPEC ? C->sa : C->a, b = SPEC ? C->sb : C->b, z = SPEC ? C->z + 1 : C->z;
-    const uint32_t mode = SPEC ? C->s_mode : C->cand_mode, off = SPEC ? C->s_off : C->cand_off;
-    const uint32_t P = SPEC ? C->parity ^ 1u : C->parity;
-    uint32_t *const Rc = SPEC ? &C->sR : &C->R;
+    const uint32_t a = SPEC ? S.sa : S.a, b = SPEC ? S.sb : S.b, z = SPEC ? S.z + 1 : S.z;
+    const uint32_t mode = SPEC ? S.s_mode : S.mode, off = SPEC ? S.s_off : S.off;
+    const uint32_t P = SPEC ? S.parity ^ 1u : S.parity;
+    uint32_t *const Rc = SPEC ? &C->sRp[S.parity ^ 1u] : &C->R;
     const int64_t n = (int64_t)E->n0;
     const uint32_t *__restrict__ tok = E->tok;
     const uint32_t *__restrict__ dist = E->dist;
     const uint32_t la = E->tlen[a], lb = E->tlen[b];
     const bool count = !E->encode;
-    const uint32_t obase = SPEC ? C->occ_top + C->R : C->occ_top;
+    const uint32_t obase = SPEC ? S.occ_top + S.R : S.occ_top;
     uint32_t *occz = E->occ + obase;
     uint16_t *tagz = E->occnb + obase;
     const uint32_t want = mode == 2 ? a : b;  // tag byte the candidates must carry
@@ -412,8 +441,9 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
 template <bool SH>
 __global__ __launch_bounds__(SCAN_T) void k_scan(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (blockIdx.x == 0 && threadIdx.x == 0) C->scan_t0 = wall_clock64();
-    if (C->stop) return;
-    scan_body<SH, false>(E, C, blockIdx.x, gridDim.x);
+    const Snap S = snap(C);
+    if (S.stop) return;
+    scan_body<SH, false>(E, C, S, blockIdx.x, gridDim.x);
 }
 
 // --------------------------------------------------------------- pair table
@@ -478,19 +508,31 @@ __device__ inline void cand_of(const Eng *E, uint32_t u, uint32_t v, bool valid,
 // ---------------------------------------------------------------- k_apply
 constexpr uint32_t MARK_CAP = 1024;
 
-__device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks) {
-    const uint32_t a = C->a, b = C->b, z = C->z, R = C->R, P = C->parity;
-    if (blockIdx.x < roleA_blocks) {
+// bid / nblk: this block among the launch's apply blocks (the fused kernel
+// runs k_select in its block 0).  UNDO: revert a speculatively applied merge
+// (tokens back to a b, negated table deltas; the level summaries were never
+// rebuilt from the speculative counts, so they stay valid).
+template <bool UNDO>
+__device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C, const Snap &S, uint32_t bid,
+                                  uint32_t nblk, uint32_t roleA_blocks) {
+    const uint32_t a = S.a, b = S.b, z = S.z, R = S.R, P = S.parity;
+    if (bid < roleA_blocks) {
         const uint32_t la = E->tlen[a], lb = E->tlen[b];
-        const uint32_t *occz = E->occ + C->occ_top;
+        const uint32_t *occz = E->occ + S.occ_top;
         uint32_t *tok = E->tok;
         uint32_t *dist = E->dist;
         const uint64_t n = E->n0;
         const bool sh = E->sharded;
         const uint64_t L1 = C->L1;
-        for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < R; e += roleA_blocks * blockDim.x) {
+        for (uint32_t e = bid * blockDim.x + threadIdx.x; e < R; e += roleA_blocks * blockDim.x) {
             const uint64_t i = occz[e];
             const uint64_t j = i + la, k = j + lb;
+            if (UNDO) {  // (one shard: j < n; b's end slot had its own start distance)
+                tok[i] = a;
+                tok[j] = b;
+                if (lb > 1) dist[k - 1] = lb - 1;
+                continue;
+            }
             tok[i] = z;
             if (j < n) {  // else: b starts in a later shard, which retires it
                 tok[j] = HOLE;
@@ -498,14 +540,11 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
                 if (sh && j == L1) C->L1new = (uint32_t)i;
             }
         }
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            E->occ_off[z] = C->occ_top;
+        if (!UNDO && bid == 0 && threadIdx.x == 0) {
+            E->occ_off[z] = S.occ_top;
             E->occ_len[z] = R;
-            C->pending = 1;
-            if (E->spec_on) {  // speculative graph: k_select left these to us
-                E->tlen[z] = (a < z && b < z) ? la + lb : 1;
-                if (C->spec) cand_of(E, C->sa, C->sb, true, E->rank, E->poff, &C->s_mode, &C->s_off, &C->s_len);
-            }
+            C->pend[P] = 1;
+            if (E->spec_on) E->tlen[z] = (a < z && b < z) ? la + lb : 1;  // (the fused k_select does not)
             const uint32_t xl = sh ? C->xleft : HOLE;
             if (xl != HOLE) {  // my first token is the b of the left shard's pair
                 tok[xl] = HOLE;
@@ -522,7 +561,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     //   [1, 1+4*DENSE)      dense ids of DR (b,x), DL (x,a), IR (z,x), IL (x,z)
     //   then the listed ids >= DENSE of DR, DL, IR, IL
     //   sharded: [1, 1+4*vcap) the allreduced dense vectors in xbuf, no lists
-    const uint32_t nB = gridDim.x - roleA_blocks;
+    const uint32_t nB = nblk - roleA_blocks;
     const uint32_t stride = nB * blockDim.x;
     uint32_t *const *lst = E->vlist[P];
     const bool sh = E->sharded;
@@ -532,13 +571,13 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     const uint32_t dense_end = 1 + 4 * W;
     const uint32_t total = dense_end + nl[0] + nl[1] + nl[2] + nl[3];
     const uint32_t Rg = sh ? E->xbuf[4 * E->vcap] : R;  // occurrences over all shards
-    if (sh && blockIdx.x == roleA_blocks && threadIdx.x == 0) C->Rg = Rg;  // for k_select (xbuf is cleared)
+    if (sh && bid == roleA_blocks && threadIdx.x == 0) C->Rg = Rg;  // for k_select (xbuf is cleared)
     __shared__ uint32_t marks[MARK_CAP];
     __shared__ uint32_t nmark, mbase;
     if (threadIdx.x == 0) nmark = 0;
     __syncthreads();
     long long dD = 0;
-    const uint32_t base0 = (blockIdx.x - roleA_blocks) * blockDim.x;
+    const uint32_t base0 = (bid - roleA_blocks) * blockDim.x;
     for (uint32_t t0 = base0; t0 < total; t0 += stride) {  // uniform trip count per block
         const uint32_t t = t0 + threadIdx.x;
         bool mark = false;
@@ -585,11 +624,11 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
         if (owner) {
             long long d = -(long long)vdr - (long long)vdl + (long long)vir + (long long)vil;
             if (u == a && v == b) d -= Rg;
+            if (UNDO) d = -d;
             if (d != 0) {
                 const uint64_t slot = d > 0 ? hinsert(E, C, u, v) : hfind(E, u, v);
                 if (slot == ~0ull) {
-                    C->err = d > 0 ? 2 : 1;
-                    C->stop = STOP_ERROR;
+                    C->err = d > 0 ? 2 : 1;  // k_select stops on it
                 } else {
                     blk = (uint32_t)(slot / L1W);
                     const uint32_t old = E->hcnt[slot];
@@ -600,8 +639,8 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
                     // the level-1 summary (best + runner-up) only changes if the
                     // key reaches the block's runner-up before or after the
                     // update; a B change rescans everything anyway
-                    const unsigned long long hi = pack_val(old > nw ? old : nw, u, v, C->B);
-                    mark = hi >= bv2;
+                    const unsigned long long hi = pack_val(old > nw ? old : nw, u, v, S.B);
+                    mark = !UNDO && hi >= bv2;
                 }
             }
         }
@@ -609,29 +648,38 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
         if (mark) marks[p] = blk;
         __syncthreads();
         if (nmark > MARK_CAP - blockDim.x || t0 + stride >= total) {
-            if (threadIdx.x == 0) mbase = nmark ? atomicAdd(&C->nl1, nmark) : 0;
+            if (threadIdx.x == 0) mbase = nmark ? atomicAdd(&C->nl1p[P], nmark) : 0;
             __syncthreads();
-            for (uint32_t k = threadIdx.x; k < nmark; k += blockDim.x) E->l1list[mbase + k] = marks[k];
+            uint32_t *l1l = E->l1list + (uint64_t)P * E->l1cap;
+            for (uint32_t k = threadIdx.x; k < nmark; k += blockDim.x) l1l[mbase + k] = marks[k];
             __syncthreads();
             if (threadIdx.x == 0) nmark = 0;
             __syncthreads();
         }
     }
-    // block-reduce dD
-    __shared__ long long sd[256];
-    sd[threadIdx.x] = dD;
+    // block-reduce dD (any block size up to 1024) into this parity's delta
+    for (int o = 32; o > 0; o >>= 1) dD += __shfl_xor(dD, o);
+    __shared__ long long sd[16];
+    if ((threadIdx.x & 63) == 0) sd[threadIdx.x >> 6] = dD;
     __syncthreads();
-    for (uint32_t w = blockDim.x / 2; w > 0; w >>= 1) {
-        if (threadIdx.x < w) sd[threadIdx.x] += sd[threadIdx.x + w];
-        __syncthreads();
+    if (threadIdx.x == 0) {
+        long long t = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) t += sd[w];
+        if (t != 0) atomicAdd(&C->Dp[P], (unsigned long long)t);
     }
-    if (threadIdx.x == 0 && sd[0] != 0) atomicAdd(&C->D, (unsigned long long)sd[0]);
 }
 
 __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *__restrict__ C,
                                                 uint32_t roleA_blocks) {
-    if (C->stop) return;
-    apply_body(E, C, roleA_blocks);
+    const Snap S = snap(C);
+    if (S.stop) return;
+    apply_body<false>(E, C, S, blockIdx.x, gridDim.x, roleA_blocks);
+}
+
+// revert the fused graph's speculative apply (host, after a stop)
+__global__ __launch_bounds__(256) void k_undo(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks) {
+    const Snap S = snap_next(C);
+    apply_body<true>(E, C, S, blockIdx.x, gridDim.x, roleA_blocks);
 }
 
 // -------------------------------------------------------- summary rescans
@@ -708,9 +756,10 @@ __device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C
 // record (it only needs k_apply's span writes) beside the rescans
 // bid / nblk: this block's index among the launch's rescan blocks (any
 // block size: the work is one wave per dirty level-1 block)
-__device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t bid, uint32_t nblk) {
+__device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__restrict__ C, const Snap &S, uint32_t bid,
+                                             uint32_t nblk) {
     {   // k_apply has consumed this iteration's delta vectors: clear them
-        const uint32_t P = C->parity;
+        const uint32_t P = S.parity;
         const uint32_t tid = bid * blockDim.x + threadIdx.x, stride = nblk * blockDim.x;
         if (E->sharded) {  // (the global R went to Ctl::Rg in k_apply)
             for (uint32_t x = tid; x < 4 * E->vcap + 2; x += stride) E->xbuf[x] = 0;
@@ -723,15 +772,15 @@ __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__r
             }
         }
     }
-    const uint64_t B = summary_B(C->D);
-    const bool full = C->full || B != C->B;
+    const uint64_t B = summary_B(S.D);
+    const bool full = S.full || B != S.B;
     const uint64_t nL1 = E->hcap / L1W;
-    const uint64_t nwork = full ? nL1 : C->nl1;
+    const uint64_t nwork = full ? nL1 : S.nl1;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wid = (uint64_t)bid * (blockDim.x / 64) + threadIdx.x / 64;
     const uint64_t nwaves = (uint64_t)nblk * (blockDim.x / 64);
     for (uint64_t w = wid; w < nwork; w += nwaves) {
-        const uint32_t blk = full ? (uint32_t)w : E->l1list[w];
+        const uint32_t blk = full ? (uint32_t)w : E->l1list[(uint64_t)S.parity * E->l1cap + w];
         Top2 mine = top2_one(0, 0, ~0ull);
         // two halves of 8 slots per lane, each half's counts and keys loaded
         // together (one round trip per half; half the registers of one pass)
@@ -767,13 +816,14 @@ __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__r
 }
 
 __global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl *__restrict__ C, int edges) {
-    if (C->stop) return;
+    const Snap S = snap(C);
+    if (S.stop) return;
     const uint32_t nblk = gridDim.x - (edges ? 1 : 0);
     if (blockIdx.x >= nblk) {
         edge_record_block(E, C);
         return;
     }
-    rescan1_body(E, C, blockIdx.x, nblk);
+    rescan1_body(E, C, S, blockIdx.x, nblk);
 }
 
 // Speculative pipeline (one-shard training graph): the current merge's
@@ -785,13 +835,28 @@ __global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl 
 // real scan (STOP_REDO).  Every block stamps its exit for the in-kernel span.
 __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ E, Ctl *__restrict__ C,
                                                          uint32_t rblocks) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) C->scan_t0 = wall_clock64();
-    if (C->stop) return;
+    const Snap S = snap(C);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        C->scan_t0 = wall_clock64();
+        // descriptor of the merge the fused kernel applies next (if predicted):
+        // k_select rewrites the head of Ctl while that apply runs
+        // (after a stop only the flag is cleared: k_undo reads the fields)
+        C->nx_valid = !S.stop && S.spec;
+        if (!S.stop) {
+            C->nx_a = S.sa;
+            C->nx_b = S.sb;
+            C->nx_z = S.z + 1;
+            C->nx_P = S.parity ^ 1u;
+            C->nx_occ = S.occ_top + S.R;
+            C->nx_B = summary_B(S.D);  // the B this launch's summaries are built with
+        }
+    }
+    if (S.stop) return;
     if (blockIdx.x < rblocks) {
-        rescan1_body(E, C, blockIdx.x, rblocks);
+        rescan1_body(E, C, S, blockIdx.x, rblocks);
         scan_exit_stamp(E, blockIdx.x);
-    } else if (C->spec) {
-        scan_body<false, true>(E, C, blockIdx.x - rblocks, gridDim.x - rblocks, rblocks);
+    } else if (S.spec) {
+        scan_body<false, true>(E, C, S, blockIdx.x - rblocks, gridDim.x - rblocks, rblocks);
     } else {
         scan_exit_stamp(E, blockIdx.x);
     }
@@ -803,10 +868,11 @@ __global__ __launch_bounds__(256) void k_rescan2(const Eng *__restrict__ E, Ctl 
     if (C->stop) return;
     const uint64_t nL1 = E->hcap / L1W;
     if (nL1 <= SELECT_L1_MAX) return;
-    const uint64_t B = summary_B(C->D);
-    const bool full = C->full || B != C->B;
+    const Snap S = snap(C);
+    const uint64_t B = summary_B(S.D);
+    const bool full = S.full || B != S.B;
     const uint64_t nL2 = (nL1 + L2W - 1) / L2W;
-    const uint64_t nwork = full ? nL2 : C->nl1;
+    const uint64_t nwork = full ? nL2 : S.nl1;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
@@ -851,37 +917,47 @@ __device__ inline void commit_merge(const Eng *E, Ctl *C, uint32_t u, uint32_t v
 }
 
 // bookkeeping of the iteration that just ran (k_scan / k_apply)
-__device__ inline void finish_iteration(const Eng *E, Ctl *C) {
-    if (!C->pending) return;
-    C->pending = 0;
+// C: k_select's staged copy; Cg: the control block in HBM (the tail section
+// is cleared there, slot P only: the fused graph's speculative k_apply owns
+// the other slot meanwhile)
+__device__ inline void finish_iteration(const Eng *E, Ctl *C, Ctl *Cg) {
+    const uint32_t P = C->parity;
+    if (!C->pend[P]) return;
+    Cg->pend[P] = 0;
     C->counters[4] += C->cand_len;  // candidates examined by k_scan (profiling)
     C->counters[5] += C->R;         // occurrences replaced
     C->occ_top += C->R;
     C->n_live -= E->sharded ? C->Rg : C->R;
     C->R = 0;
-    C->nl1 = 0;
+    C->D += C->Dp[P];               // fold the merge's distinct-pair delta
+    Cg->Dp[P] = 0;
+    Cg->nl1p[P] = 0;
     C->nl2 = 0;
-    for (int v = 0; v < 4; v++) E->vnl[C->parity][v] = 0;  // entries zeroed by k_rescan1
+    for (int v = 0; v < 4; v++) E->vnl[P][v] = 0;  // entries zeroed by k_rescan1
     C->counters[0]++;
 }
 
 // ---------------------------------------------------------------- k_select
 
-// decisions of one selection (thread 0, on the LDS copy of the control block).
-// graph: SEL_PLAIN / SEL_TRACKED / SEL_SPEC (the speculative one-shard graph,
-// whose k_rescan_spec ran the scan of the prediction armed last time).
-__device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Top2 r2, unsigned long long tend,
+// decisions of one selection (thread 0, on the LDS copy C of the control
+// block; Cg is the block in HBM).  graph: SEL_PLAIN / SEL_TRACKED / SEL_FUSED
+// (the speculative one-shard graph: k_rescan_spec scanned the prediction armed
+// last time, and the fused kernel is applying it while this runs).
+__device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Ctl *Cg, Top2 r2, unsigned long long tend,
                                    uint32_t graph, const uint32_t *rank, const uint32_t *poff) {
     const Best r = r2.b;
     const uint32_t tracked_graph = graph == SEL_TRACKED;
-    if (C->pending && tend > C->scan_t0) {  // a merge ran: account its scan span
+    const uint32_t P0 = C->parity;
+    if (C->pend[P0] && tend > C->scan_t0) {  // a merge ran: account its scan span
         C->scan_ticks += tend - C->scan_t0;
         C->scan_launches++;
     }
-    if (C->pending) C->counters[6] += (C->full || summary_B(C->D) != C->B) ? E->hcap / L1W : C->nl1;
-    const uint32_t was_spec = graph == SEL_SPEC ? C->spec : 0;  // a scan of (sa, sb) ran since
+    if (C->pend[P0]) C->counters[6] += (C->full || summary_B(C->D + C->Dp[P0]) != C->B) ? E->hcap / L1W : C->nl1p[P0];
+    const uint32_t was_spec = graph == SEL_FUSED ? C->spec : 0;  // the prediction's scan ran since
     C->spec = 0;
-    finish_iteration(E, C);
+    C->stop_z = C->z;
+    finish_iteration(E, C, Cg);
+    if (C->err) { C->stop = STOP_ERROR; return; }
     if (!tracked_graph && !E->fast && C->n_live < TRACK_LIMIT) { C->stop = STOP_MODE; return; }
     const uint64_t D = C->D;
     uint32_t edge;
@@ -905,13 +981,19 @@ __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Top2 r2, u
         commit_merge(E, C, u, v, rank, poff);
         return;
     }
-    // speculative graph: a held prediction needs no global load here (the
-    // next k_apply writes tlen[z] and looks up the new prediction's list)
+    if (!rank) rank = E->rank;
+    if (!poff) poff = E->poff;
+    // speculative: a held prediction's scan (and, in the fused graph, its
+    // apply) is adopted; tlen[z] is written by k_apply
     const bool hit = was_spec && u == C->sa && v == C->sb;
     const uint32_t md = C->merges_done, z = 256 + md;
     uint32_t cm = C->s_mode, co = C->s_off, cl = C->s_len;  // a held prediction's list
-    if (!hit) cand_of(E, u, v, u < z && v < z, rank ? rank : E->rank, poff ? poff : E->poff, &cm, &co, &cl);
+    if (!hit) cand_of(E, u, v, u < z && v < z, rank, poff, &cm, &co, &cl);
+    // predict the merge after this one: the runner-up of this selection
     const bool arm = r2.v2 && (uint32_t)(r2.v2 >> 32) > 1 && md + 1 < E->mcap;
+    const uint32_t pa = (uint32_t)(r2.k2 >> 32), pb = (uint32_t)r2.k2;
+    uint32_t pm = 0, po = 0, pl = 0;
+    if (arm) cand_of(E, pa, pb, true, rank, poff, &pm, &po, &pl);
     E->merges[2 * md] = u;
     E->merges[2 * md + 1] = v;
     C->a = u;
@@ -921,18 +1003,20 @@ __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Top2 r2, u
     C->cand_mode = cm;
     C->cand_off = co;
     C->cand_len = cl;
-    if (hit) {  // prediction held: adopt its scan
-        C->R = C->sR;
-        C->parity ^= 1u;
+    if (hit) {  // adopt the speculative scan (+ apply): its parity becomes current
+        C->R = C->sRp[P0 ^ 1u];
+        C->sRp[P0] = 0;  // the slot the next speculative scan counts into
+        C->parity = P0 ^ 1u;
         C->counters[7]++;
-    } else if (graph == SEL_SPEC) {  // the host runs the real scan
+    } else if (graph == SEL_FUSED) {  // the host reverts the speculative apply and scans
         C->stop = STOP_REDO;
         C->counters[8]++;
     }
-    // predict the merge after this one: the runner-up of this selection
-    C->sR = 0;
-    C->sa = (uint32_t)(r2.k2 >> 32);
-    C->sb = (uint32_t)r2.k2;
+    C->sa = pa;
+    C->sb = pb;
+    C->s_mode = pm;
+    C->s_off = po;
+    C->s_len = pl;
     C->spec = arm ? 1u : 0u;
 }
 
@@ -979,8 +1063,7 @@ __device__ inline Top2 summary_top2(const unsigned long long *best, const uint32
 // ranks are staged in LDS while the summaries are reduced,
 // so thread 0's decisions start from LDS; the control block is written back
 // at the end.
-__global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl *__restrict__ Cg, uint32_t graph) {
-    if (Cg->stop) return;
+__device__ __forceinline__ void select_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, uint32_t graph) {
     const unsigned long long sc_t0 = wall_clock64();
     unsigned long long sc_t1 = 0;
     __shared__ Ctl sc;
@@ -1008,6 +1091,7 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
     __shared__ unsigned long long st[16];
     if ((tid & 63) == 0) { sw[tid >> 6] = mine; st[tid >> 6] = tend; }
     __syncthreads();
+    if (sc.stop) return;  // (checked on the staged copy: no separate round trip)
     if (tid < 64) {  // wave 0 merges the 16 wave results (4 shuffle steps)
         Top2 w = tid < blockDim.x / 64 ? sw[tid] : top2_one(0, 0, ~0ull);
         for (int o = 8; o > 0; o >>= 1) {
@@ -1025,14 +1109,35 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
         const Top2 r2 = sw[0];
         for (uint32_t k = 0; k < blockDim.x / 64; k++) tend = max(tend, st[k]);
         const unsigned long long t2 = wall_clock64();
-        select_tail(E, &sc, r2, tend, graph, srank, pl ? spoff : nullptr);
+        select_tail(E, &sc, Cg, r2, tend, graph, srank, pl ? spoff : nullptr);
         const unsigned long long t3 = wall_clock64();
         sc.counters[9] += sc_t1 - sc_t0;   // (select phase timing, temporary)
         sc.counters[10] += t2 - sc_t1;
         sc.counters[11] += t3 - t2;
     }
     __syncthreads();
-    for (uint32_t x = tid; x < CW; x += blockDim.x) cgw[x] = scw[x];
+    for (uint32_t x = tid; x < CTL_SELECT_WORDS; x += blockDim.x) cgw[x] = scw[x];
+}
+
+__global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl *__restrict__ Cg, uint32_t graph) {
+    select_block(E, Cg, graph);
+}
+
+// The fused speculative graph's second kernel: k_select (block 0) decides the
+// next merge while the other blocks apply the predicted one, which
+// k_rescan_spec already scanned.  The two touch disjoint state: k_select
+// reads the level summaries and its own control words; the apply rewrites
+// tokens and pair counts and writes only the control block's tail.  A wrong
+// prediction (or any stop) is reverted by the host (k_undo).
+__global__ __launch_bounds__(1024) void k_fused(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks) {
+    if (blockIdx.x == 0) {
+        select_block(E, C, SEL_FUSED);
+        return;
+    }
+    const Snap S = snap_next(C);
+    if (S.stop) return;
+    apply_body<false>(E, C, S, blockIdx.x - 1, gridDim.x - 1, roleA_blocks);
+    if (blockIdx.x == 1 && threadIdx.x == 0) C->spec_z = S.z;
 }
 
 // after a missed prediction (or any host-side stop): clear the other
@@ -1048,11 +1153,19 @@ __global__ __launch_bounds__(256) void k_spec_clear(const Eng *__restrict__ E, C
     }
 }
 
-// second half: list lengths and the speculative count (after k_spec_clear)
+// second half: list lengths, the speculative count and the other parity's
+// tail slots (after k_spec_clear / k_undo)
 __global__ void k_spec_reset(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     const uint32_t Q = C->parity ^ 1u;
     if (threadIdx.x < 4) E->vnl[Q][threadIdx.x] = 0;
-    if (threadIdx.x == 0) C->sR = 0;
+    if (threadIdx.x == 0) {
+        C->sRp[Q] = 0;
+        C->Dp[Q] = 0;
+        C->nl1p[Q] = 0;
+        C->pend[Q] = 0;
+        C->spec_z = 0;
+        C->nx_valid = 0;
+    }
 }
 
 // commit a merge chosen by the host resolver (after STOP_EVENT)
