@@ -5,7 +5,7 @@ set -o pipefail
 OUT=${OUT:-gpurun_out}
 TAG=${TAG:-run}
 mkdir -p $OUT/prof_$TAG
-timeout -k 10 600 python -m pytest tests -q -m gpu -x > $OUT/tests_$TAG.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/tests_$TAG.log 2>&1
 echo "tests rc=$?" >> $OUT/tests_$TAG.log
 timeout -k 10 300 python bench.py > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || exit 1
 export TMPDIR=/tmp
