@@ -12,10 +12,12 @@ with the final ids compacted in HBM.
 value = n_gpus * corpus_MB * K / wall   (MB = 1e6 bytes)
 
 Multi-GPU (torchrun, one rank per GPU): ONE training job over an N GiB
-corpus cut into N contiguous 1 GiB shards (weak scaling).  Every merge
-allreduces the shards' count deltas and allgathers their 16-word edge records
-over RCCL (libbpe_amd.so's own communicator; torch.distributed/gloo only
-carries the RCCL id, the barrier and the max over ranks).  The merges are
+corpus cut into N contiguous 1 GiB shards (weak scaling).  Every merge sums
+the shards' count deltas and gathers their 16-word edge records: by default
+one push kernel per exchange over xGMI into the peers' IPC-mapped mailboxes
+(BPE_XPORT=rccl: RCCL collectives on libbpe_amd.so's own communicator);
+torch.distributed/gloo only carries the set-up handles, the barrier and the
+max over ranks.  The merges are
 checked identical on every rank.  value = N * 1073.7 MB * K / wall.
 
 The JSON line also carries
@@ -104,7 +106,7 @@ def encode_bench(args, rank, world, local, dist, barrier):
     per = 3 << 30  # bytes per shard context (u32 positions)
     if world > 1:
         from llmtokenizer_amd import dist as bdist
-        g = bdist.rccl_group(local)
+        g = bdist.group(local, len(merges))
         g.synth(0, 3, hi - lo, lo)
     else:
         k = max(1, -(-total // per))
@@ -160,7 +162,7 @@ def main():
     ap.add_argument("--cpu-size", type=int, default=64 << 20)
     ap.add_argument("--cpu-merges", type=int, default=16)
     ap.add_argument("--sharded", action="store_true",
-                    help="use the sharded (RCCL) path even with one rank")
+                    help="use the sharded path even with one rank")
     ap.add_argument("--no-encode", action="store_true", help="skip the configs[4] encode measurement")
     ap.add_argument("--encode-size", type=int, default=10 << 30)
     ap.add_argument("--encode-merges", type=int, default=32768)
@@ -183,7 +185,7 @@ def main():
     from llmtokenizer_amd import api
     if sharded:
         from llmtokenizer_amd import dist as bdist
-        e = bdist.rccl_group(local)
+        e = bdist.group(local, max(args.steps, args.warmup))
         e.synth(0, args.seed, args.size, offset=rank * args.size)  # resident in HBM before timing
     else:
         e = api.Engine(local)
@@ -216,6 +218,7 @@ def main():
         dist.all_gather_object(digests, hashlib.md5(e.merges().tobytes()).hexdigest())
         same = len(set(digests)) == 1
     st = e.stats()
+    transport = e.transport() if sharded else "none"
     name, kms, kbytes, launches = e.kernel_profile()  # live, in-kernel wall clock
     ev_ms, ev_n = 0.0, 0
     if not sharded:
@@ -254,9 +257,10 @@ def main():
         "data": "synthetic (random_text.txt-shaped, splitmix64 seed %d, generated in HBM)" % args.seed,
         "config": {"workload": "configs[3]: 1 GiB corpus/GPU, %d merges" % args.steps,
                    "corpus_bytes_per_gpu": args.size, "corpus_bytes_total": args.size * world, "merges": k,
-                   "parallelism": ("dp%d: one training job, %d contiguous corpus shards, per merge RCCL allreduce "
-                                   "of count deltas + allgather of edge records" % (world, world)) if sharded
-                   else "single GPU",
+                   "parallelism": ("dp%d: one training job, %d contiguous corpus shards, per merge a sum of count "
+                                   "deltas + a gather of edge records over %s" %
+                                   (world, world, {"p2p": "xGMI P2P mailboxes", "rccl": "RCCL"}.get(transport, transport)))
+                   if sharded else "single GPU",
                    "merges_identical_across_ranks": same},
         # dominant kernel of the timed run: k_scan (latency-bound random gathers);
         # algorithmic bytes per launch = 8 B/candidate + 20 B/occurrence

@@ -143,12 +143,25 @@ int bpe_gpu_event_profile(bpe_gpu_ctx *ctx, double *avg_ms, uint64_t *launches);
  *   comm_id != NULL: one shard per rank, ranks exchange over RCCL (xGMI);
  *                    comm_id = the 128-byte id rank 0 got from
  *                    bpe_gpu_comm_id(), passed to every rank.
+ * and bpe_gpu_group_create_p2p: one shard per rank, each exchange is one
+ * push kernel over xGMI into the peers' IPC-mapped mailboxes (no RCCL on the
+ * per-merge path).  Every rank creates its group, the host side gathers the
+ * BPE_GPU_P2P_HANDLE_BYTES handles in rank order (any host collective) and
+ * passes them to bpe_gpu_group_p2p_connect.  max_merges bounds the merges a
+ * train call may make (it sizes the mailbox).  A rank that waits longer than
+ * BPE_P2P_TIMEOUT_S seconds (default 30) for a peer fails with
+ * BPE_GPU_EINTERNAL instead of hanging.
  * ---------------------------------------------------------------------- */
+#define BPE_GPU_P2P_HANDLE_BYTES 64
+#define BPE_GPU_P2P_MAX_RANKS 16
 typedef struct bpe_gpu_group bpe_gpu_group;
 
 int bpe_gpu_comm_id(uint8_t *id, size_t cap);
 int bpe_gpu_group_create(int device, int local_shards, int nranks, int rank, const uint8_t *comm_id,
                          bpe_gpu_group **out);
+int bpe_gpu_group_create_p2p(int device, int nranks, int rank, long max_merges, uint8_t *handle, size_t cap,
+                             bpe_gpu_group **out);
+int bpe_gpu_group_p2p_connect(bpe_gpu_group *g, const uint8_t *handles, size_t each);
 void bpe_gpu_group_destroy(bpe_gpu_group *g);
 int bpe_gpu_group_shards(bpe_gpu_group *g, int *local_shards, int *nshards, int *first_shard);
 /* shard k (local index) of the group */
@@ -168,6 +181,8 @@ int bpe_gpu_group_kernel_profile(bpe_gpu_group *g, int k, const char **name, dou
                                  double *bytes_per_launch, uint64_t *launches);
 /* 1 when the per-merge exchange runs inside captured HIP graphs */
 int bpe_gpu_group_exchange_mode(bpe_gpu_group *g, int *graph_captured);
+/* transport of the exchange: 0 one device, 1 RCCL, 2 P2P mailboxes */
+int bpe_gpu_group_transport(bpe_gpu_group *g, int *kind);
 
 /* The halo shard `me` derives from all edge records for a merge (a, b):
  * out8 = {HL[0..2], HR[0..2], hlrun, myidx} (pure function, no GPU; exported

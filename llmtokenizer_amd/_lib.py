@@ -30,6 +30,7 @@ EXPORTS = [
     "bpe_gpu_comm_id", "bpe_gpu_group_create", "bpe_gpu_group_destroy", "bpe_gpu_group_shards",
     "bpe_gpu_group_load", "bpe_gpu_group_synth", "bpe_gpu_group_train", "bpe_gpu_group_encode", "bpe_gpu_group_fetch_merges",
     "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo", "bpe_gpu_group_kernel_profile",
+    "bpe_gpu_group_create_p2p", "bpe_gpu_group_p2p_connect", "bpe_gpu_group_transport",
 ]
 
 
@@ -77,6 +78,10 @@ def load():
     ip = ctypes.POINTER(ctypes.c_int)
     L.bpe_gpu_comm_id.argtypes = [vp, sz]
     L.bpe_gpu_group_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(vp)]
+    L.bpe_gpu_group_create_p2p.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long, vp, sz,
+                                           ctypes.POINTER(vp)]
+    L.bpe_gpu_group_p2p_connect.argtypes = [vp, vp, sz]
+    L.bpe_gpu_group_transport.argtypes = [vp, ip]
     L.bpe_gpu_group_destroy.argtypes = [vp]
     L.bpe_gpu_group_destroy.restype = None
     L.bpe_gpu_group_shards.argtypes = [vp, ip, ip, ip]

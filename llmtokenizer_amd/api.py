@@ -247,17 +247,41 @@ class ShardGroup:
     Shards hold contiguous slices of the corpus in order; merges are the same
     on every shard and the corpus ids are the shards' ids concatenated."""
 
-    def __init__(self, device=0, local_shards=1, nranks=1, rank=0, comm_id=None):
+    P2P_HANDLE_BYTES = 64  # bpe_gpu.h BPE_GPU_P2P_HANDLE_BYTES
+
+    def __init__(self, device=0, local_shards=1, nranks=1, rank=0, comm_id=None, p2p_max_merges=None):
+        """p2p_max_merges: one shard per rank over P2P mailboxes (bpe_gpu_group_create_p2p);
+        then gather every rank's .p2p_handle in rank order and call p2p_connect()."""
         self.L = _lib.load()
         self.g = ctypes.c_void_p()
-        cid = None
-        if comm_id is not None:
-            cid = ctypes.create_string_buffer(bytes(comm_id), len(comm_id))
-        _lib.check(self.L.bpe_gpu_group_create(int(device), int(local_shards), int(nranks), int(rank),
-                                               cid, ctypes.byref(self.g)), "group_create")
+        self.p2p_handle = None
+        if p2p_max_merges is not None:
+            h = ctypes.create_string_buffer(self.P2P_HANDLE_BYTES)
+            _lib.check(self.L.bpe_gpu_group_create_p2p(int(device), int(nranks), int(rank), int(p2p_max_merges),
+                                                       h, self.P2P_HANDLE_BYTES, ctypes.byref(self.g)),
+                       "group_create_p2p")
+            self.p2p_handle = h.raw
+        else:
+            cid = None
+            if comm_id is not None:
+                cid = ctypes.create_string_buffer(bytes(comm_id), len(comm_id))
+            _lib.check(self.L.bpe_gpu_group_create(int(device), int(local_shards), int(nranks), int(rank),
+                                                   cid, ctypes.byref(self.g)), "group_create")
         k, n, f = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.check(self.L.bpe_gpu_group_shards(self.g, ctypes.byref(k), ctypes.byref(n), ctypes.byref(f)), "shards")
         self.local_shards, self.nshards, self.first_shard = k.value, n.value, f.value
+
+    def p2p_connect(self, handles):
+        """handles: every rank's p2p_handle, in rank order"""
+        hs = b"".join(bytes(h) for h in handles)
+        buf = ctypes.create_string_buffer(hs, len(hs))
+        _lib.check(self.L.bpe_gpu_group_p2p_connect(self.g, buf, self.P2P_HANDLE_BYTES), "p2p_connect")
+
+    def transport(self):
+        """'local' (one device), 'rccl' or 'p2p'"""
+        v = ctypes.c_int()
+        _lib.check(self.L.bpe_gpu_group_transport(self.g, ctypes.byref(v)), "transport")
+        return ("local", "rccl", "p2p")[v.value]
 
     def close(self):
         if self.g:

@@ -1,0 +1,135 @@
+// p2p.hip -- the per-merge exchange of a multi-GPU shard group as one-shot
+// pushes over xGMI into IPC-mapped mailboxes (included by shard.hip).
+//
+// Every rank owns one mailbox in its own HBM, allocated uncached so that
+// stores arriving from peer GPUs are visible to polling loads without any
+// cache maintenance on the receiving side.  Each rank maps every peer's
+// mailbox (hipIpcOpenMemHandle).  An exchange is ONE small kernel per rank:
+//
+//   push   my buffer into slot [parity][me] of every rank's mailbox
+//          (posted remote stores), system-scope release, then my flag word
+//          in every mailbox := seq
+//   wait   until every rank's flag in MY mailbox reached seq
+//   reduce the W slots of this parity (sum) / copy them (gather)
+//
+// seq is a per-channel counter kept on the device, so the kernels replay
+// inside hipGraphs.  Slots alternate by parity: a rank can be at most one
+// exchange ahead of any other (it cannot finish exchange s+1 before every
+// rank pushed s+1, which each does only after consuming s), so exchange
+// s+1 never overwrites a slot exchange s still reads.  Every wait is bounded
+// by a wall-clock timeout: a dead peer turns into an error, never a hang.
+// Two channels: 0 = count-delta sum (dense over ids), 1 = edge-record gather.
+#pragma once
+#include "engine_common.h"
+
+namespace bpeamd {
+
+constexpr uint32_t P2P_MAXR = 16;            // ranks per group
+constexpr uint32_t MB_FLAG0 = 0;             // [rank * 16]: sum channel flags (one 64-B line each)
+constexpr uint32_t MB_FLAG1 = 16 * P2P_MAXR; // [rank * 16]: gather channel flags
+constexpr uint32_t MB_DATA1 = 32 * P2P_MAXR; // [2][P2P_MAXR][EDGE_WORDS]
+constexpr uint32_t MB_DATA0 = MB_DATA1 + 2 * P2P_MAXR * EDGE_WORDS;  // [2][W][c0]
+enum { XS_SEQ0 = 0, XS_PUSH0 = 1, XS_SEQ1 = 2, XS_ERR = 3 };
+constexpr uint32_t P2P_ERR_BIT = 16;  // Ctl::err bit of a timed-out exchange
+
+struct P2P {
+    uint32_t *mb[P2P_MAXR];      // every rank's mailbox, mapped here (mb[rank]: my own)
+    uint32_t W, rank, c0, pad;   // ranks, my rank, words per sum slot (multiple of 4)
+    uint32_t *xs;                // my counters: seq0, pushes0, seq1, err (plain device memory)
+    uint32_t *err;               // extra error word (the training run's Ctl::err) or null
+    unsigned long long timeout;  // wall-clock ticks a wait may take
+};
+
+__device__ inline uint32_t sys_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// spin until *p reached want (wrapping compare); false (+ error words) on timeout
+__device__ inline bool p2p_wait(const P2P *X, const uint32_t *p, uint32_t want, unsigned long long t0) {
+    while ((int32_t)(sys_load(p) - want) < 0) {
+        if (wall_clock64() - t0 > X->timeout) {
+            atomicOr(X->xs + XS_ERR, 1u);
+            if (X->err) atomicOr(X->err, P2P_ERR_BIT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+
+// every storing wave drains its stores, the block meets, one lane releases at
+// system scope (L2 write-back) and then stores the flag words
+__device__ inline void p2p_release_point() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// Sum channel: buf[0..count) := sum over ranks of their buf.  Grid = W
+// blocks: block k pushes to rank (me + k) % W and reduces a 1/W share.
+__global__ __launch_bounds__(256) void k_p2p_sum(const P2P *__restrict__ X, uint32_t *__restrict__ buf,
+                                                 uint32_t count) {
+    const uint32_t W = X->W, me = X->rank, c0 = X->c0, tid = threadIdx.x;
+    const uint32_t seq = X->xs[XS_SEQ0] + 1u, par = seq & 1u;
+    const uint32_t p = (me + blockIdx.x) % W;
+    uint32_t *dst = X->mb[p] + MB_DATA0 + ((uint64_t)par * W + me) * c0;
+    const uint32_t nv = count / 4;
+    for (uint32_t i = tid; i < nv; i += blockDim.x)
+        reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(buf)[i];
+    for (uint32_t i = nv * 4 + tid; i < count; i += blockDim.x) dst[i] = buf[i];
+    p2p_release_point();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+        __hip_atomic_store(X->mb[p] + MB_FLAG0 + 16 * me, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // my buffer may be overwritten once all my blocks have pushed it
+        __hip_atomic_fetch_add(X->xs + XS_PUSH0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned long long t0 = wall_clock64();
+    if (tid < W) p2p_wait(X, X->mb[me] + MB_FLAG0 + 16 * tid, seq, t0);
+    else if (tid == 64) p2p_wait(X, X->xs + XS_PUSH0, W * seq, t0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __syncthreads();
+    const uint32_t *src = X->mb[me] + MB_DATA0 + (uint64_t)par * W * c0;
+    const uint32_t share = (((count + W - 1) / W + 3) / 4) * 4;  // words per block, multiple of 4
+    const uint32_t lo = blockIdx.x * share, hi = min(count, lo + share);
+    const uint32_t hv = lo + ((hi > lo ? hi - lo : 0) & ~3u);
+    for (uint32_t i = lo + 4 * tid; i < hv; i += 4 * blockDim.x) {
+        uint4 s = make_uint4(0, 0, 0, 0);
+        for (uint32_t r = 0; r < W; r++) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(src + (uint64_t)r * c0 + i);
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        *reinterpret_cast<uint4 *>(buf + i) = s;
+    }
+    for (uint32_t i = hv + tid; i < hi; i += blockDim.x) {
+        uint32_t s = 0;
+        for (uint32_t r = 0; r < W; r++) s += src[(uint64_t)r * c0 + i];
+        buf[i] = s;
+    }
+    // every block read seq before it pushed; block 0 passed the push count
+    if (blockIdx.x == 0 && tid == 0) X->xs[XS_SEQ0] = seq;
+}
+
+// Gather channel: dst[r * EDGE_WORDS + w] := rank r's src[w].  One wave.
+__global__ __launch_bounds__(64) void k_p2p_gather(const P2P *__restrict__ X, const uint32_t *__restrict__ src,
+                                                   uint32_t *__restrict__ dst) {
+    const uint32_t W = X->W, me = X->rank, tid = threadIdx.x;
+    const uint32_t seq = X->xs[XS_SEQ1] + 1u, par = seq & 1u;
+    const uint32_t v = tid < EDGE_WORDS ? src[tid] : 0;
+    for (uint32_t p = 0; p < W; p++)
+        if (tid < EDGE_WORDS) X->mb[p][MB_DATA1 + ((uint64_t)par * P2P_MAXR + me) * EDGE_WORDS + tid] = v;
+    p2p_release_point();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        for (uint32_t p = 0; p < W; p++)
+            __hip_atomic_store(X->mb[p] + MB_FLAG1 + 16 * me, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const unsigned long long t0 = wall_clock64();
+    if (tid < W) p2p_wait(X, X->mb[me] + MB_FLAG1 + 16 * tid, seq, t0);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __syncthreads();
+    const uint32_t *s = X->mb[me] + MB_DATA1 + (uint64_t)par * P2P_MAXR * EDGE_WORDS;
+    for (uint32_t t = tid; t < W * EDGE_WORDS; t += blockDim.x) dst[t] = s[t];
+    if (tid == 0) X->xs[XS_SEQ1] = seq;
+}
+
+}  // namespace bpeamd

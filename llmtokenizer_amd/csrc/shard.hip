@@ -11,13 +11,17 @@
 //      derives the tokens just outside its edges for the next merge
 //      (shard_halo): pairs across an edge belong to the left shard, runs of
 //      a==b continue their pairing parity across edges.
-// Across GPUs the exchange is RCCL over xGMI (librccl, loaded at run time);
-// within one device it is a sum / gather kernel over the shards' buffers.
+// Across GPUs the exchange is a one-shot push kernel over xGMI into
+// IPC-mapped mailboxes (p2p.hip; groups made by bpe_gpu_group_create_p2p),
+// or RCCL (librccl, loaded at run time; groups made with an RCCL id); within
+// one device it is a sum / gather kernel over the shards' buffers.
 // Ties are decided by the schedule-free rule (smallest (a,b) among the
 // maximal (count, bucket) keys) in every iteration: for corpora of >= 2^20
 // tokens this is the single-GPU engine's rule as well, so 1 GPU == N GPUs.
 #include <dlfcn.h>
 #include <rccl/rccl.h>
+
+#include "p2p.hip"
 
 namespace {
 
@@ -76,6 +80,14 @@ struct bpe_gpu_group {
     uint32_t **d_ptrs_tmp = nullptr;  // local mode: init-time tables
     hipGraphExec_t graph = nullptr;
     std::vector<hipGraphExec_t> retired;  // replaced graphs, destroyed with the run
+    // P2P transport (p2p.hip): my mailbox (uncached, IPC-exported), the peers'
+    // mailboxes mapped here, the counters and the descriptor the kernels read
+    bool p2p = false, p2p_ready = false;
+    uint32_t *mailbox = nullptr;
+    uint32_t *xs = nullptr;
+    P2P hp{};
+    P2P *d_p2p = nullptr;
+    std::vector<void *> opened;
     bool eager = false;               // collectives could not be graph-captured
     bool encoding = false;            // the captured step is an encode batch
     size_t merges_done = 0;
@@ -83,6 +95,9 @@ struct bpe_gpu_group {
 };
 
 namespace {
+
+// one device: the exchange is a sum / gather kernel over pointer tables
+bool local_mode(const bpe_gpu_group *g) { return !g->rccl && !g->p2p; }
 
 int group_free_graph(bpe_gpu_group *g) {
     if (g->st) (void)hipStreamSynchronize(g->st);
@@ -95,6 +110,12 @@ int group_free_graph(bpe_gpu_group *g) {
 
 // sum-allreduce of `count` u32 at bufs[k] (one per local shard), in place
 int ex_allreduce(bpe_gpu_group *g, uint32_t **d_tab, const std::vector<uint32_t *> &bufs, size_t count) {
+    if (g->p2p) {
+        if (count > g->hp.c0) return fail(BPE_GPU_ERANGE, "p2p mailbox smaller than the exchange (max_merges)");
+        k_p2p_sum<<<g->hp.W, 256, 0, g->st>>>(g->d_p2p, bufs[0], (uint32_t)count);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
     if (g->rccl) {
         ncclResult_t e = g->rccl->allReduce(bufs[0], bufs[0], count, ncclUint32, ncclSum, g->comm, g->st);
         if (e != ncclSuccess) return rccl_fail(g->rccl, "ncclAllReduce", e);
@@ -111,6 +132,11 @@ int ex_allreduce(bpe_gpu_group *g, uint32_t **d_tab, const std::vector<uint32_t 
 int ex_records(bpe_gpu_group *g, uint32_t **d_tab, hipStream_t st = nullptr) {
     bpe_gpu_ctx *c0 = g->cs[0];
     if (!st) st = g->st;
+    if (g->p2p) {
+        k_p2p_gather<<<1, 64, 0, st>>>(g->d_p2p, c0->h.myrec, c0->h.erec);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
     if (g->rccl) {
         ncclResult_t e = g->rccl->allGather(c0->h.myrec, c0->h.erec, EDGE_WORDS, ncclUint32, g->comm, st);
         if (e != ncclSuccess) return rccl_fail(g->rccl, "ncclAllGather", e);
@@ -120,6 +146,15 @@ int ex_records(bpe_gpu_group *g, uint32_t **d_tab, hipStream_t st = nullptr) {
     k_xgather<<<1, 256, 0, st>>>(d_tab + K, d_tab + 2 * K, K, EDGE_WORDS);
     HIPCHK(hipGetLastError());
     return 0;
+}
+
+// a timed-out P2P wait (dead or diverged peer) surfaces here as an error
+int p2p_check(bpe_gpu_group *g) {
+    if (!g->p2p) return 0;
+    uint32_t e = 0;
+    HIPCHK(hipMemcpyAsync(&e, g->xs + XS_ERR, 4, hipMemcpyDeviceToHost, g->st));
+    HIPCHK(hipStreamSynchronize(g->st));
+    return e ? fail(BPE_GPU_EINTERNAL, "p2p exchange timed out (a peer rank stopped or diverged)") : 0;
 }
 
 int upload_table(bpe_gpu_group *g, uint32_t **d_tab, const std::vector<uint32_t *> &ptrs) {
@@ -209,8 +244,9 @@ int drive_group(bpe_gpu_group *g) {
         case STOP_ENC_END:
             return 0;
         case STOP_ERROR:
-            return fail(BPE_GPU_EINTERNAL, C0.err == 1 ? "engine invariant violated (count decrement of an absent pair)"
-                                                       : "pair table full");
+            return fail(BPE_GPU_EINTERNAL, (C0.err & P2P_ERR_BIT) ? "p2p exchange timed out (a peer rank stopped or diverged)"
+                                           : C0.err == 1 ? "engine invariant violated (count decrement of an absent pair)"
+                                                         : "pair table full");
         case STOP_GROW:
             // the captured steps read the tables through the device descriptors;
             // recapture only when the level-2 summary launch appears
@@ -240,9 +276,21 @@ int drive_group(bpe_gpu_group *g) {
 int group_total(bpe_gpu_group *g, uint64_t *tot) {
     uint64_t local = 0;
     for (bpe_gpu_ctx *c : g->cs) local += c->n0;
-    if (!g->rccl) {
+    if (local_mode(g)) {
         *tot = local;
         return 0;
+    }
+    if (g->p2p) {  // n0 < 2^32 per rank, <= 16 ranks: 24-bit halves sum without carry
+        uint32_t *d = g->xs + 4;
+        const uint32_t w[4] = {(uint32_t)(local & 0xFFFFFF), (uint32_t)(local >> 24), 0, 0};
+        HIPCHK(hipMemcpyAsync(d, w, 16, hipMemcpyHostToDevice, g->st));
+        int r;
+        if ((r = ex_allreduce(g, nullptr, {d}, 4))) return r;
+        uint32_t o[4];
+        HIPCHK(hipMemcpyAsync(o, d, 16, hipMemcpyDeviceToHost, g->st));
+        HIPCHK(hipStreamSynchronize(g->st));
+        *tot = (uint64_t)o[0] + ((uint64_t)o[1] << 24);
+        return p2p_check(g);
     }
     uint64_t *d;
     HIPCHK(hipMalloc(&d, 8));
@@ -287,7 +335,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         if ((r = push_ctl(c))) return r;
     }
     // pointer tables for the one-device exchange
-    if (!g->rccl) {
+    if (local_mode(g)) {
         if (!g->d_ptrs) {
             HIPCHK(hipMalloc(&g->d_ptrs, 3ull * K * sizeof(uint32_t *)));
             HIPCHK(hipMalloc(&g->d_ptrs_tmp, (size_t)K * sizeof(uint32_t *)));
@@ -302,7 +350,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     std::vector<uint32_t *> bh(K);
     for (uint32_t k = 0; k < K; k++)
         if ((r = init_presence(g->cs[k], &bh[k]))) return r;
-    if (!g->rccl && (r = upload_table(g, g->d_ptrs_tmp, bh))) return r;
+    if (local_mode(g) && (r = upload_table(g, g->d_ptrs_tmp, bh))) return r;
     if ((r = ex_allreduce(g, g->d_ptrs_tmp, bh, 256))) return r;
     std::vector<uint32_t> pres(256);
     HIPCHK(hipMemcpyAsync(pres.data(), bh[0], 1024, hipMemcpyDeviceToHost, g->st));
@@ -317,7 +365,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     if ((r = ex_records(g, g->d_ptrs))) return r;
     for (uint32_t k = 0; k < K; k++) k_init_cross<<<1, 64, 0, g->st>>>(g->cs[k]->dE, tot[k]);
     const uint32_t A = g->cs[0]->h.A, AA = A * A;
-    if (!g->rccl && (r = upload_table(g, g->d_ptrs_tmp, tot))) return r;
+    if (local_mode(g) && (r = upload_table(g, g->d_ptrs_tmp, tot))) return r;
     if (AA && (r = ex_allreduce(g, g->d_ptrs_tmp, tot, AA))) return r;
     for (uint32_t k = 0; k < K; k++) {
         bpe_gpu_ctx *c = g->cs[k];
@@ -339,10 +387,12 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(g->st));
+    if ((r = p2p_check(g))) return r;
     const double t1 = now_ms();
     if ((r = drive_group(g))) return r;
     HIPCHK(hipStreamSynchronize(g->st));
     const double t2 = now_ms();
+    if ((r = p2p_check(g))) return r;
     uint64_t nout = 0;
     for (bpe_gpu_ctx *c : g->cs) {
         if ((r = pull_ctl(c))) return r;
@@ -399,7 +449,7 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
         HIPCHK(hipMalloc(&c->d_enc_pairs, std::max<size_t>(n_merges, 1) * 8));
         if (n_merges) HIPCHK(hipMemcpyAsync(c->d_enc_pairs, pairs, n_merges * 8, hipMemcpyHostToDevice, g->st));
     }
-    if (!g->rccl) {
+    if (local_mode(g)) {
         if (!g->d_ptrs) {
             HIPCHK(hipMalloc(&g->d_ptrs, 3ull * K * sizeof(uint32_t *)));
             HIPCHK(hipMalloc(&g->d_ptrs_tmp, (size_t)K * sizeof(uint32_t *)));
@@ -431,9 +481,11 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
     if ((r = ex_records(g, g->d_ptrs))) return r;
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(g->st));
+    if ((r = p2p_check(g))) return r;
     const double t1 = now_ms();
     if ((r = drive_group(g))) return r;
     HIPCHK(hipStreamSynchronize(g->st));
+    if ((r = p2p_check(g))) return r;
     uint64_t nout = 0;
     for (bpe_gpu_ctx *c : g->cs) {
         if ((r = pull_ctl(c))) return r;
@@ -518,6 +570,81 @@ int bpe_gpu_group_create(int device, int local_shards, int nranks, int rank, con
     return 0;
 }
 
+int bpe_gpu_group_create_p2p(int device, int nranks, int rank, long max_merges, uint8_t *handle, size_t cap,
+                             bpe_gpu_group **out) {
+    if (!out || !handle || cap < BPE_GPU_P2P_HANDLE_BYTES || nranks < 1 || nranks > (int)P2P_MAXR || rank < 0 ||
+        rank >= nranks || max_merges < 0 || max_merges > (1l << 24))
+        return BPE_GPU_EINVAL;
+    static_assert(sizeof(hipIpcMemHandle_t) <= BPE_GPU_P2P_HANDLE_BYTES, "IPC handle size");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return fail(BPE_GPU_ENODEV, "no such device");
+    HIPCHK(hipSetDevice(device));
+    bpe_gpu_group *g = new bpe_gpu_group();
+    g->dev = device;
+    g->p2p = true;
+    g->nshards = (uint32_t)nranks;
+    g->shard0 = (uint32_t)rank;
+    int r;
+    hipError_t e = hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete g; return fail(BPE_GPU_EHIP, "hipStreamCreate", e); }
+    // sum slots hold the per-merge delta vectors (4 * (256 + merges) + 2
+    // words) and the set-up exchanges (byte-pair counts: up to 256^2 words)
+    const uint64_t c0 = ((std::max<uint64_t>(65536, 4ull * (256 + (uint64_t)max_merges) + 2) + 3) / 4) * 4;
+    const size_t bytes = ((size_t)MB_DATA0 + 2ull * nranks * c0) * 4;
+    e = hipExtMallocWithFlags((void **)&g->mailbox, bytes, hipDeviceMallocUncached);
+    if (e != hipSuccess) { g->mailbox = nullptr; bpe_gpu_group_destroy(g); return fail(BPE_GPU_ENOMEM, "uncached mailbox", e); }
+    if ((e = hipMemset(g->mailbox, 0, bytes)) != hipSuccess ||
+        (e = hipMalloc(&g->xs, 64)) != hipSuccess || (e = hipMemset(g->xs, 0, 64)) != hipSuccess ||
+        (e = hipMalloc(&g->d_p2p, sizeof(P2P))) != hipSuccess) {
+        bpe_gpu_group_destroy(g);
+        return fail(BPE_GPU_EHIP, "p2p set-up", e);
+    }
+    hipIpcMemHandle_t h;
+    if ((e = hipIpcGetMemHandle(&h, g->mailbox)) != hipSuccess) {
+        bpe_gpu_group_destroy(g);
+        return fail(BPE_GPU_EHIP, "hipIpcGetMemHandle", e);
+    }
+    memset(handle, 0, BPE_GPU_P2P_HANDLE_BYTES);
+    memcpy(handle, &h, sizeof h);
+    g->hp.W = (uint32_t)nranks;
+    g->hp.rank = (uint32_t)rank;
+    g->hp.c0 = (uint32_t)c0;
+    g->hp.xs = g->xs;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
+    double tmo = 30.0;
+    if (const char *t = getenv("BPE_P2P_TIMEOUT_S")) tmo = std::max(0.01, atof(t));
+    g->hp.timeout = (unsigned long long)(tmo * 1000.0 * khz);
+    bpe_gpu_ctx *c;
+    if ((r = ctx_new(device, g->st, &c))) { bpe_gpu_group_destroy(g); return r; }
+    g->cs.push_back(c);
+    g->hp.err = &c->dC->err;
+    *out = g;
+    return 0;
+}
+
+int bpe_gpu_group_p2p_connect(bpe_gpu_group *g, const uint8_t *handles, size_t each) {
+    if (!g || !g->p2p || !handles || each < sizeof(hipIpcMemHandle_t)) return BPE_GPU_EINVAL;
+    if (g->p2p_ready) return fail(BPE_GPU_ESTATE, "p2p group already connected");
+    HIPCHK(hipSetDevice(g->dev));
+    for (uint32_t p = 0; p < g->hp.W; p++) {
+        if (p == g->hp.rank) {
+            g->hp.mb[p] = g->mailbox;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        memcpy(&h, handles + (size_t)p * each, sizeof h);
+        void *ptr = nullptr;
+        hipError_t e = hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) return fail(BPE_GPU_EHIP, "hipIpcOpenMemHandle", e);
+        g->opened.push_back(ptr);
+        g->hp.mb[p] = (uint32_t *)ptr;
+    }
+    HIPCHK(hipMemcpy(g->d_p2p, &g->hp, sizeof(P2P), hipMemcpyHostToDevice));
+    g->p2p_ready = true;
+    return 0;
+}
+
 void bpe_gpu_group_destroy(bpe_gpu_group *g) {
     if (!g) return;
     (void)hipSetDevice(g->dev);
@@ -527,6 +654,10 @@ void bpe_gpu_group_destroy(bpe_gpu_group *g) {
     if (g->d_ptrs) hipFree(g->d_ptrs);
     if (g->d_ptrs_tmp) hipFree(g->d_ptrs_tmp);
     if (g->comm) (void)g->rccl->commDestroy(g->comm);
+    for (void *p : g->opened) (void)hipIpcCloseMemHandle(p);
+    if (g->mailbox) hipFree(g->mailbox);
+    if (g->xs) hipFree(g->xs);
+    if (g->d_p2p) hipFree(g->d_p2p);
     if (g->st) (void)hipStreamDestroy(g->st);
     delete g;
 }
@@ -555,12 +686,14 @@ int bpe_gpu_group_synth(bpe_gpu_group *g, int k, uint64_t seed, size_t n, uint64
 
 int bpe_gpu_group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     if (!g || !n_merges) return BPE_GPU_EINVAL;
+    if (g->p2p && !g->p2p_ready) return fail(BPE_GPU_ESTATE, "p2p group not connected");
     HIPCHK(hipSetDevice(g->dev));
     return group_train(g, max_merges, n_merges);
 }
 
 int bpe_gpu_group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
     if (!g || (!pairs && n_merges)) return BPE_GPU_EINVAL;
+    if (g->p2p && !g->p2p_ready) return fail(BPE_GPU_ESTATE, "p2p group not connected");
     HIPCHK(hipSetDevice(g->dev));
     return group_encode(g, pairs, n_merges);
 }
@@ -592,6 +725,12 @@ int bpe_gpu_group_kernel_profile(bpe_gpu_group *g, int k, const char **name, dou
 int bpe_gpu_group_exchange_mode(bpe_gpu_group *g, int *graph_captured) {
     if (!g || !graph_captured) return BPE_GPU_EINVAL;
     *graph_captured = g->eager ? 0 : 1;
+    return 0;
+}
+
+int bpe_gpu_group_transport(bpe_gpu_group *g, int *kind) {
+    if (!g || !kind) return BPE_GPU_EINVAL;
+    *kind = g->p2p ? 2 : g->rccl ? 1 : 0;
     return 0;
 }
 
