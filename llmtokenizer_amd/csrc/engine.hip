@@ -208,6 +208,9 @@ struct bpe_gpu_ctx {
     // run configuration (set before setup_run)
     uint32_t fast = 0;                     // schedule-free tie rule everywhere
     uint32_t sharded = 0, shard = 0, nshards = 1;
+    uint32_t xfused = 0;                   // fused sharded step (P2P group, shard.hip)
+    const P2P *xp2p = nullptr;             // its exchange descriptor (device)
+    unsigned long long xtimeout = 0;       // its wait bound (wall-clock ticks)
     Eng h{};
     Eng *dE = nullptr;
     Ctl *dC = nullptr;
@@ -339,8 +342,11 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.occ, occ_n + n0, false))) return r;
     h.ids_out = h.occ + occ_n;
     if ((r = dalloc(c, &h.occnb, occ_n, false))) return r;
+    h.xfused = c->sharded && c->xfused && !encode;
+    h.xtimeout = c->xtimeout;
+    h.xstride = (uint32_t)(((4ull * h.vcap + 2) + 63) & ~63ull);
     if (c->sharded) {
-        if ((r = dalloc(c, &h.xbuf, 4ull * h.vcap + 2))) return r;
+        if ((r = dalloc(c, &h.xbuf, 2ull * h.xstride))) return r;
         if ((r = dalloc(c, &h.myrec, EDGE_WORDS))) return r;
         if ((r = dalloc(c, &h.erec, (size_t)EDGE_WORDS * c->nshards))) return r;
     } else {
@@ -358,8 +364,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     }
     if ((r = dalloc(c, &h.vecd, encode ? 1 : (size_t)2 * REPL * 4 * DENSE))) return r;
     if ((r = dalloc(c, &h.scan_tend, STAMPS))) return r;
-    h.spec_on = SPEC_ON && !encode && !c->sharded;
-    h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? SPEC_RB + SPEC_SB : 0);
+    h.spec_on = SPEC_ON && !encode && (!c->sharded || h.xfused);
+    h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? 1 + SPEC_RB + SPEC_SB : 0);
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
     if ((r = dalloc(c, &c->d_tileoff, h.ntiles + 1))) return r;
@@ -402,6 +408,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     C.L1 = n0 ? (uint32_t)(n0 - 1) : 0;
     C.L1new = HOLE;
     C.xleft = HOLE;
+    C.erec_ready = 1;  // (the set-up gathers the records before the first scan)
     if ((r = push_ctl(c))) return r;
     return push_desc(c);
 }
@@ -493,7 +500,7 @@ void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
         // (by the previous k_fused, or the host after a stop)
         k_rescan_spec<<<SPEC_RB + SPEC_SB, SCAN_T, 0, c->st>>>(c->dE, c->dC, SPEC_RB);
         if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
-        k_fused<<<1 + FUSED_A + FUSED_B, 1024, 0, c->st>>>(c->dE, c->dC, FUSED_A);
+        k_fused<<<1 + FUSED_A + FUSED_B, 1024, 0, c->st>>>(c->dE, c->dC, FUSED_A, nullptr);
         return;
     }
     k_scan<false><<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
@@ -506,7 +513,7 @@ void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
 // fused graph, after any stop: revert the speculative apply if the stopping
 // selection ran beside one, and drop the other parity's speculative state
 void launch_spec_revert(bpe_gpu_ctx *c, bool undo) {
-    if (undo) k_undo<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
+    if (undo) k_undo<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A, c->xp2p);
     k_spec_clear<<<64, 256, 0, c->st>>>(c->dE, c->dC);
     k_spec_reset<<<1, 64, 0, c->st>>>(c->dE, c->dC);
 }
@@ -1027,7 +1034,7 @@ void fill_profile(bpe_gpu_ctx *c) {
         // graph the span is k_rescan_spec's, which also reads 12 B per slot
         // of every dirty level-1 block
         const bool spec = c->h.spec_on && C.counters[7];
-        c->prof_name = spec ? "k_rescan_spec" : "k_scan";
+        c->prof_name = spec ? (c->h.xfused ? "k_rescan_spec_sh" : "k_rescan_spec") : "k_scan";
         c->prof_ms = khz > 0 ? (double)C.scan_ticks / C.scan_launches / khz : 0;
         c->prof_bytes = (8.0 * C.counters[4] + 20.0 * C.counters[5] + (spec ? 12.0 * L1W * C.counters[6] : 0.0)) /
                         std::max<double>(1.0, C.counters[0]);

@@ -113,7 +113,10 @@ struct Eng {
     uint32_t scan_blocks; // k_scan grid (entries of scan_tend)
     // corpus sharding (one shard per context; nshards == 1 -> no halo traffic)
     uint32_t sharded, shard, nshards;
-    uint32_t *xbuf;       // [4*vcap + 2] per-merge exchange: dense deltas | R | flags (allreduced)
+    uint32_t *xbuf;       // [2][xstride] per-merge exchange, per delta parity: dense deltas | R (summed)
+    uint32_t xstride;     // words per parity of xbuf (>= 4*vcap + 2, multiple of 64)
+    uint32_t xfused;      // sharded speculative step with in-kernel P2P exchanges (shard.hip)
+    unsigned long long xtimeout;  // wall-clock ticks a wait for a peer may take
     uint32_t *myrec;      // [EDGE_WORDS] this shard's edge record
     uint32_t *erec;       // [nshards * EDGE_WORDS] all edge records (allgathered)
     // encode (batched replay of a merge list)
@@ -150,10 +153,6 @@ struct Ctl {
     unsigned long long scan_t0;       // wall clock at k_scan block 0 entry
     unsigned long long scan_ticks;    // sum over merges of k_scan spans (wall-clock ticks)
     unsigned long long scan_launches;
-    // sharding (the halo itself is derived from the edge records in k_scan)
-    uint32_t F1, L1, L1new, xleft;    // first / last token start, pending last, consumed first
-    uint32_t xleft_lb;                // length of the consumed first token (encode batches)
-    uint32_t Rg, ebp;                 // sharded: occurrences over all shards; encode batch parity
     // speculative next merge (one-shard training): predicted pair, its
     // candidate list, armed flag; occurrences k_rescan_spec found, per parity
     uint32_t sa, sb, s_mode, s_off;
@@ -168,6 +167,17 @@ struct Ctl {
     uint32_t nx_valid, nx_a, nx_b, nx_z;
     uint32_t nx_P, nx_occ, nx_pad0, nx_pad1;
     unsigned long long nx_B;
+    // sharding (the halo itself is derived from the edge records in k_scan);
+    // in the tail because the fused sharded step's apply writes them while
+    // k_select runs
+    uint32_t F1, L1, L1new, xleft;    // first / last token start, pending last, consumed first
+    uint32_t xleft_lb;                // length of the consumed first token (encode batches)
+    uint32_t ebp;                     // encode batch parity
+    uint32_t Rgp[2];                  // sharded: occurrences over all shards of the merge with parity p
+    uint32_t erec_ready;              // fused sharded step: erec holds the records of the current tokens
+    uint32_t adone;                   // fused sharded step: k_fused_sh apply blocks done with the spans
+    uint32_t nx_seq0, nx_live;        // fused sharded step: the delta exchange's sequence number; K1 ran
+    unsigned long long xdbg[4];       // fused sharded step timing sums (BPE_DEBUG; wall-clock ticks)
 };
 constexpr uint32_t CTL_SELECT_WORDS = offsetof(Ctl, Dp) / 4;  // k_select's write-back
 

@@ -18,6 +18,7 @@
 //              the next iteration.
 //   k_stat_*   per-thread table tracking for n < 2^21 (tie emulation).
 #include "engine_common.h"
+#include "p2p.hip"
 
 namespace bpeamd {
 
@@ -26,6 +27,9 @@ __device__ inline uint32_t lane_id() { return __lane_id(); }
 // load that bypasses the (non-coherent) vector L1: values other blocks of the
 // same kernel produced before a fence
 __device__ inline uint32_t aload(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline unsigned long long aload64(const unsigned long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -40,6 +44,9 @@ __device__ inline uint32_t wave_append(bool pred, uint32_t *counter) {
     base = __shfl(base, leader);
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
+
+// the sharded exchange buffer of delta parity P
+__device__ inline uint32_t *xbufp(const Eng *E, uint32_t P) { return E->xbuf + (uint64_t)P * E->xstride; }
 
 // Delta vectors: ids < DENSE are aggregated in LDS and flushed with
 // fire-and-forget atomics (k_apply enumerates them densely); rarer ids >= DENSE
@@ -58,7 +65,7 @@ __device__ inline void vadd(uint32_t (*s)[DENSE], const Eng *E, uint32_t P, int 
     if (x < DENSE) {
         atomicAdd(&s[v][x], 1u);
     } else if (SH) {  // sharded: straight into the exchange buffer (no lists)
-        atomicAdd(&E->xbuf[v * E->vcap + x], 1u);
+        atomicAdd(&xbufp(E, P)[v * E->vcap + x], 1u);
     } else {
         uint32_t old = atomicAdd(&E->vec[P][v][x], 1u);
         if (old == 0) {
@@ -81,13 +88,31 @@ struct Halo6 {
 // The halo of one shard for one merge, derived on first use from the edge
 // records (only lookups that leave the shard need it, so most threads never
 // compute it).
+// In the fused sharded step the records of the current tokens arrive while
+// the scan runs (the edge block gathers them): a lookup that needs the halo
+// waits for Ctl::erec_ready (bounded by the exchange timeout).
+__device__ inline void wait_records(const Eng *E, Ctl *C) {
+    const unsigned long long t0 = wall_clock64();
+    while (!aload(&C->erec_ready)) {
+        if (wall_clock64() - t0 > E->xtimeout) {
+            atomicOr(&C->err, P2P_ERR_BIT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 struct LazyHalo {
     const Eng *E;
+    Ctl *C;
     uint32_t a;
+    bool wait;
     bool ready;
     Halo h;
     __device__ inline const Halo &get() {  // sharded contexts only (E->erec)
         if (!ready) {
+            if (wait) wait_records(E, C);
             shard_halo(E->erec, E->nshards, E->shard, a, &h);
             ready = true;
         }
@@ -236,15 +261,25 @@ __device__ inline Snap snap_next(const Ctl *C) {
 // beside the current merge's rescan: deltas into the other parity, its
 // occurrence list right after the current merge's, counted in C->sR.
 // bid / nblk: this block's index among the scan blocks of the launch.
-template <bool SH, bool SPEC>
+// XW: the fused sharded step (k_rescan_spec_sh): the edge block (no
+// candidates of its own) first pulls every rank's record of the current
+// tokens from the P2P mailbox into erec; lookups that need the halo wait for
+// it.  The deltas leave through k_fused_sh.
+__device__ void records_pull_block(const Eng *__restrict__ E, Ctl *__restrict__ C, const P2P *__restrict__ X);
+__device__ void push_exchange_block(const P2P *__restrict__ X, const uint32_t *__restrict__ buf, uint32_t count,
+                                    uint32_t seq);
+__device__ void records_push_block(const Eng *__restrict__ E, Ctl *__restrict__ C, const P2P *__restrict__ X,
+                                   uint32_t apply_blocks);
+
+template <bool SH, bool SPEC, bool XW = false>
 __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__restrict__ C, const Snap &S, uint32_t bid,
-                                          uint32_t nblk, uint32_t stamp0 = 0) {
+                                          uint32_t nblk, const P2P *__restrict__ X = nullptr) {
     const uint32_t len = SPEC ? S.s_len : S.len;
     // the shard-edge step runs in the last block, which usually has no
     // candidates, so its dependent loads overlap the other blocks' work
     const bool edge_block = SH && bid == nblk - 1;
-    if (bid * SCAN_T >= len && !edge_block) {  // block-uniform
-        scan_exit_stamp(E, stamp0 + bid);
+    if (!XW && bid * SCAN_T >= len && !edge_block) {  // block-uniform
+        scan_exit_stamp(E, blockIdx.x);
         return;
     }
     const uint32_t a = SPEC ? S.sa : S.a, b = SPEC ? S.sb : S.b, z = SPEC ? S.z + 1 : S.z;
@@ -262,7 +297,7 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
     const uint32_t want = mode == 2 ? a : b;  // tag byte the candidates must carry
     // halo of this shard for merge (a, b), from the edge records on first use
     // (the records' allgather overlaps the previous merge's rescan/select)
-    LazyHalo h{E, a, false, {}};
+    LazyHalo h{E, C, a, XW, false, {}};
 
     __shared__ uint32_t s[4][DENSE];
     __shared__ uint32_t list[SCAN_T];
@@ -272,8 +307,15 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
         for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) (&s[0][0])[x] = 0;
     if (threadIdx.x == 0) lcount = bR = 0;
     __syncthreads();
+    if (XW && edge_block) {
+        const unsigned long long t0 = wall_clock64();
+        records_pull_block(E, C, X);
+        if (threadIdx.x == 0) C->xdbg[0] += wall_clock64() - t0;
+    }
 
-    for (uint32_t e0 = bid * SCAN_T; e0 < len; e0 += nblk * SCAN_T) {
+    // XW: the edge block takes no candidates (it exchanges the records first)
+    const uint32_t ncand = XW ? nblk - 1 : nblk;
+    for (uint32_t e0 = bid * SCAN_T; e0 < len && bid < ncand; e0 += ncand * SCAN_T) {
         const uint32_t e = e0 + threadIdx.x;
         bool ok = false;
         int64_t i = 0, j = 0;
@@ -427,15 +469,16 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
         // sharded: flush straight into the dense exchange buffer the shards
         // allreduce next (zeroed by the previous k_rescan1); no pack pass
         const uint32_t vc = E->vcap;
+        uint32_t *xb = xbufp(E, P);
         for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) {
             const uint32_t c = (&s[0][0])[x];
             const uint32_t v = x / DENSE, id = x % DENSE;
-            if (c && id < vc) atomicAdd(&E->xbuf[v * vc + id], c);
+            if (c && id < vc) atomicAdd(&xb[v * vc + id], c);
         }
-        if (threadIdx.x == 0 && bR) atomicAdd(&E->xbuf[4 * vc], bR);  // this shard's R, summed
+        if (threadIdx.x == 0 && bR) atomicAdd(&xb[4 * vc], bR);  // this shard's R, summed
         __syncthreads();
     }
-    scan_exit_stamp(E, stamp0 + bid);
+    scan_exit_stamp(E, blockIdx.x);
 }
 
 template <bool SH>
@@ -512,9 +555,12 @@ constexpr uint32_t MARK_CAP = 1024;
 // runs k_select in its block 0).  UNDO: revert a speculatively applied merge
 // (tokens back to a b, negated table deltas; the level summaries were never
 // rebuilt from the speculative counts, so they stay valid).
+// X != null (fused sharded step): the deltas are not reduced into xbuf; role
+// B waits for every rank's push of them (P2P channel 0) and sums the W
+// mailbox slots as it reads them, beside k_select.
 template <bool UNDO>
 __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C, const Snap &S, uint32_t bid,
-                                  uint32_t nblk, uint32_t roleA_blocks) {
+                                  uint32_t nblk, uint32_t roleA_blocks, const P2P *__restrict__ X = nullptr) {
     const uint32_t a = S.a, b = S.b, z = S.z, R = S.R, P = S.parity;
     if (bid < roleA_blocks) {
         const uint32_t la = E->tlen[a], lb = E->tlen[b];
@@ -527,10 +573,12 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
         for (uint32_t e = bid * blockDim.x + threadIdx.x; e < R; e += roleA_blocks * blockDim.x) {
             const uint64_t i = occz[e];
             const uint64_t j = i + la, k = j + lb;
-            if (UNDO) {  // (one shard: j < n; b's end slot had its own start distance)
+            if (UNDO) {  // b's end slot had its own start distance (j >= n: b is a later shard's)
                 tok[i] = a;
-                tok[j] = b;
-                if (lb > 1) dist[k - 1] = lb - 1;
+                if (j < n) {
+                    tok[j] = b;
+                    if (lb > 1 && k - 1 < n) dist[k - 1] = lb - 1;
+                }
                 continue;
             }
             tok[i] = z;
@@ -552,6 +600,20 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
                 if (end - 1 < n) dist[end - 1] = MARK;
                 C->F1 = (uint32_t)(end < n ? end : n);
             }
+            if (sh) C->erec_ready = 0;  // the tokens at my edges may have changed
+        }
+        if (UNDO && sh && bid == 0 && threadIdx.x == 0) {
+            // the speculative apply retired my first token / moved my last one:
+            // put both back; the records gathered before it are current again
+            const uint32_t xl = C->xleft;
+            if (xl != HOLE) {
+                tok[xl] = b;
+                const uint64_t end = (uint64_t)xl + lb;
+                if (lb > 1 && end - 1 < n) dist[end - 1] = lb - 1;
+                C->F1 = xl;
+            }
+            C->L1new = HOLE;
+            C->erec_ready = 1;
         }
         return;
     }
@@ -570,8 +632,24 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     for (int v = 0; v < 4; v++) nl[v] = sh ? 0 : E->vnl[P][v];
     const uint32_t dense_end = 1 + 4 * W;
     const uint32_t total = dense_end + nl[0] + nl[1] + nl[2] + nl[3];
-    const uint32_t Rg = sh ? E->xbuf[4 * E->vcap] : R;  // occurrences over all shards
-    if (sh && bid == roleA_blocks && threadIdx.x == 0) C->Rg = Rg;  // for k_select (xbuf is cleared)
+    const uint32_t *xbP = sh ? xbufp(E, P) : nullptr;
+    uint32_t XW = 1, xc0 = 0;  // ranks summed on read, their slot stride
+    if (sh && X) {
+        const uint32_t seq = C->nx_seq0;  // the push k_fused_sh's block 1 makes
+        const unsigned long long t0 = wall_clock64();
+        if (threadIdx.x < X->W) p2p_wait(X, X->mb[X->rank] + MB_FLAG0 + 16 * threadIdx.x, seq, t0);
+        if (X->fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        __syncthreads();
+        XW = X->W;
+        xc0 = X->c0;
+        xbP = X->mb[X->rank] + MB_DATA0 + (uint64_t)(seq & 1u) * XW * xc0;
+    }
+    uint32_t Rg = R;  // occurrences over all shards
+    if (sh) {
+        Rg = 0;
+        for (uint32_t r = 0; r < XW; r++) Rg += xbP[(uint64_t)r * xc0 + 4 * E->vcap];
+    }
+    if (!UNDO && sh && bid == roleA_blocks && threadIdx.x == 0) C->Rgp[P] = Rg;  // for k_select (xbuf is cleared)
     __shared__ uint32_t marks[MARK_CAP];
     __shared__ uint32_t nmark, mbase;
     if (threadIdx.x == 0) nmark = 0;
@@ -604,11 +682,13 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
         // the four delta values that can touch key (u, v), loaded together
         uint32_t vdr = 0, vdl = 0, vir = 0, vil = 0;
         if (cat >= 0 && sh) {
-            const uint32_t *xb = E->xbuf, vc = E->vcap;
-            vdr = u == b && v < vc ? xb[V_DR * vc + v] : 0;
-            vdl = v == a && u < vc ? xb[V_DL * vc + u] : 0;
-            vir = u == z && v < vc ? xb[V_IR * vc + v] : 0;
-            vil = v == z && u < vc ? xb[V_IL * vc + u] : 0;
+            const uint32_t *xb = xbP, vc = E->vcap;
+            for (uint32_t r = 0; r < XW; r++, xb += xc0) {  // (one pass: XW == 1)
+                vdr += u == b && v < vc ? xb[V_DR * vc + v] : 0;
+                vdl += v == a && u < vc ? xb[V_DL * vc + u] : 0;
+                vir += u == z && v < vc ? xb[V_IR * vc + v] : 0;
+                vil += v == z && u < vc ? xb[V_IL * vc + u] : 0;
+            }
         } else if (cat >= 0) {
             vdr = u == b ? dval(E, P, V_DR, v) : 0;
             vdl = v == a ? dval(E, P, V_DL, u) : 0;
@@ -677,9 +757,10 @@ __global__ __launch_bounds__(256) void k_apply(const Eng *__restrict__ E, Ctl *_
 }
 
 // revert the fused graph's speculative apply (host, after a stop)
-__global__ __launch_bounds__(256) void k_undo(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks) {
+__global__ __launch_bounds__(256) void k_undo(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks,
+                                               const P2P *__restrict__ X) {
     const Snap S = snap_next(C);
-    apply_body<true>(E, C, S, blockIdx.x, gridDim.x, roleA_blocks);
+    apply_body<true>(E, C, S, blockIdx.x, gridDim.x, roleA_blocks, X);
 }
 
 // -------------------------------------------------------- summary rescans
@@ -761,8 +842,9 @@ __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__r
     {   // k_apply has consumed this iteration's delta vectors: clear them
         const uint32_t P = S.parity;
         const uint32_t tid = bid * blockDim.x + threadIdx.x, stride = nblk * blockDim.x;
-        if (E->sharded) {  // (the global R went to Ctl::Rg in k_apply)
-            for (uint32_t x = tid; x < 4 * E->vcap + 2; x += stride) E->xbuf[x] = 0;
+        if (E->sharded) {  // (the global R went to Ctl::Rgp in k_apply)
+            uint32_t *xb = xbufp(E, P);
+            for (uint32_t x = tid; x < 4 * E->vcap + 2; x += stride) xb[x] = 0;
         } else {
             uint32_t *vd = E->vecd + (uint64_t)P * REPL * 4 * DENSE;
             for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride) vd[x] = 0;
@@ -833,30 +915,71 @@ __global__ __launch_bounds__(256) void k_rescan1(const Eng *__restrict__ E, Ctl 
 // rewriting, so the two are independent; k_select checks the prediction and
 // either adopts the scan (flips the delta parity) or asks the host for the
 // real scan (STOP_REDO).  Every block stamps its exit for the in-kernel span.
+// descriptor of the merge the fused kernel applies next (if predicted):
+// k_select rewrites the head of Ctl while that apply runs (after a stop only
+// the flag is cleared: k_undo reads the fields); thread 0 of block 0
+__device__ inline void spec_descriptor(Ctl *C, const Snap &S) {
+    C->scan_t0 = wall_clock64();
+    C->nx_valid = !S.stop && S.spec;
+    if (!S.stop) {
+        C->nx_a = S.sa;
+        C->nx_b = S.sb;
+        C->nx_z = S.z + 1;
+        C->nx_P = S.parity ^ 1u;
+        C->nx_occ = S.occ_top + S.R;
+        C->nx_B = summary_B(S.D);  // the B this launch's summaries are built with
+    }
+}
+
 __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ E, Ctl *__restrict__ C,
                                                          uint32_t rblocks) {
     const Snap S = snap(C);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        C->scan_t0 = wall_clock64();
-        // descriptor of the merge the fused kernel applies next (if predicted):
-        // k_select rewrites the head of Ctl while that apply runs
-        // (after a stop only the flag is cleared: k_undo reads the fields)
-        C->nx_valid = !S.stop && S.spec;
-        if (!S.stop) {
-            C->nx_a = S.sa;
-            C->nx_b = S.sb;
-            C->nx_z = S.z + 1;
-            C->nx_P = S.parity ^ 1u;
-            C->nx_occ = S.occ_top + S.R;
-            C->nx_B = summary_B(S.D);  // the B this launch's summaries are built with
-        }
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) spec_descriptor(C, S);
     if (S.stop) return;
     if (blockIdx.x < rblocks) {
         rescan1_body(E, C, S, blockIdx.x, rblocks);
         scan_exit_stamp(E, blockIdx.x);
     } else if (S.spec) {
-        scan_body<false, true>(E, C, S, blockIdx.x - rblocks, gridDim.x - rblocks, rblocks);
+        scan_body<false, true>(E, C, S, blockIdx.x - rblocks, gridDim.x - rblocks);
+    } else {
+        scan_exit_stamp(E, blockIdx.x);
+    }
+}
+
+// The fused sharded step's first kernel (P2P groups, one shard per rank):
+//   block 0            the edge block: every rank's record of the current
+//                      tokens (pushed by their last k_fused_sh) pulled from
+//                      the mailbox into erec and published to the other
+//                      blocks; then the shard-edge step of the predicted merge
+//   [1, 1 + rblocks)   the current merge's summary rescan
+//   the rest           the predicted merge's scan (halo lookups wait for the
+//                      records), deltas into xbuf[P] for k_fused_sh to push
+// Grid <= 2 blocks per CU so that all blocks are resident (the edge block is
+// dispatched first).
+__global__ __launch_bounds__(SCAN_T) void k_rescan_spec_sh(const Eng *__restrict__ E, Ctl *__restrict__ C,
+                                                            uint32_t rblocks, const P2P *__restrict__ X) {
+    const Snap S = snap(C);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        spec_descriptor(C, S);
+        // k_fused_sh pushes the deltas with it.  After a stop the field stays:
+        // k_undo waits for the push the stopping step made with it.
+        if (!S.stop) C->nx_seq0 = X->xs[XS_SEQ0] + 1u;
+        C->nx_live = !S.stop;
+    }
+    if (S.stop) return;
+    const uint32_t nscan = gridDim.x - rblocks;  // scan blocks, the edge block included
+    if (blockIdx.x == 0) {
+        if (S.spec) {
+            scan_body<true, true, true>(E, C, S, nscan - 1, nscan, X);
+        } else {
+            records_pull_block(E, C, X);
+            scan_exit_stamp(E, 0);
+        }
+    } else if (blockIdx.x <= rblocks) {
+        rescan1_body(E, C, S, blockIdx.x - 1, rblocks);
+        scan_exit_stamp(E, blockIdx.x);
+    } else if (S.spec) {
+        scan_body<true, true, true>(E, C, S, blockIdx.x - 1 - rblocks, nscan, X);
     } else {
         scan_exit_stamp(E, blockIdx.x);
     }
@@ -927,7 +1050,7 @@ __device__ inline void finish_iteration(const Eng *E, Ctl *C, Ctl *Cg) {
     C->counters[4] += C->cand_len;  // candidates examined by k_scan (profiling)
     C->counters[5] += C->R;         // occurrences replaced
     C->occ_top += C->R;
-    C->n_live -= E->sharded ? C->Rg : C->R;
+    C->n_live -= E->sharded ? C->Rgp[P] : C->R;
     C->R = 0;
     C->D += C->Dp[P];               // fold the merge's distinct-pair delta
     Cg->Dp[P] = 0;
@@ -1129,15 +1252,58 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
 // reads the level summaries and its own control words; the apply rewrites
 // tokens and pair counts and writes only the control block's tail.  A wrong
 // prediction (or any stop) is reverted by the host (k_undo).
-__global__ __launch_bounds__(1024) void k_fused(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks) {
+__global__ __launch_bounds__(1024) void k_fused(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks,
+                                                const P2P *__restrict__ X) {
     if (blockIdx.x == 0) {
         select_block(E, C, SEL_FUSED);
         return;
     }
     const Snap S = snap_next(C);
     if (S.stop) return;
-    apply_body<false>(E, C, S, blockIdx.x - 1, gridDim.x - 1, roleA_blocks);
+    apply_body<false>(E, C, S, blockIdx.x - 1, gridDim.x - 1, roleA_blocks, X);
     if (blockIdx.x == 1 && threadIdx.x == 0) C->spec_z = S.z;
+}
+
+// The fused sharded step's second kernel (P2P groups, one shard per rank):
+//   block 0          k_select
+//   block 1          pushes the predicted merge's deltas (K1 accumulated them
+//                    in xbuf) to every rank (P2P channel 0)
+//   [2, 2 + nA)      apply role A: my spans; then each signals Ctl::adone
+//   next nB blocks   apply role B: waits for every rank's deltas, sums them
+//                    from the mailbox slots into my replica of the table
+//   last block       my record of the new tokens, pushed to every rank
+//                    (channel 1) for the next K1, once role A is done
+// A wrong prediction (or any stop) is reverted by the host as in k_fused.
+__global__ __launch_bounds__(1024) void k_fused_sh(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks,
+                                                   const P2P *__restrict__ X) {
+    const uint32_t nap = gridDim.x - 3;  // apply blocks
+    if (blockIdx.x == 0) {
+        select_block(E, C, SEL_FUSED);
+        return;
+    }
+    if (!C->nx_live) return;  // K1 saw a stop: nothing was scanned or pulled
+    const bool valid = C->nx_valid;
+    if (blockIdx.x == 1) {
+        if (valid) push_exchange_block(X, xbufp(E, C->nx_P), 4 * E->vcap + 2, C->nx_seq0);
+        return;
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        records_push_block(E, C, X, valid ? roleA_blocks : 0);
+        return;
+    }
+    if (!valid) return;
+    const Snap S = snap_next(C);
+    const uint32_t bid = blockIdx.x - 2;
+    apply_body<false>(E, C, S, bid, nap, roleA_blocks, X);
+    if (bid < roleA_blocks) {  // spans written: the record block may read them
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __hip_atomic_fetch_add(&C->adone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (bid == 0 && threadIdx.x == 0) C->spec_z = S.z;
 }
 
 // after a missed prediction (or any host-side stop): clear the other
@@ -1145,6 +1311,11 @@ __global__ __launch_bounds__(1024) void k_fused(const Eng *__restrict__ E, Ctl *
 __global__ __launch_bounds__(256) void k_spec_clear(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     const uint32_t Q = C->parity ^ 1u;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+    if (E->sharded) {
+        uint32_t *xb = xbufp(E, Q);
+        for (uint32_t x = tid; x < 4 * E->vcap + 2; x += stride) xb[x] = 0;
+        return;
+    }
     uint32_t *vd = E->vecd + (uint64_t)Q * REPL * 4 * DENSE;
     for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride) vd[x] = 0;
     for (int vv = 0; vv < 4; vv++) {
@@ -1160,6 +1331,7 @@ __global__ void k_spec_reset(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (threadIdx.x < 4) E->vnl[Q][threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         C->sRp[Q] = 0;
+        C->Rgp[Q] = 0;
         C->Dp[Q] = 0;
         C->nl1p[Q] = 0;
         C->pend[Q] = 0;
@@ -1175,13 +1347,14 @@ __global__ void k_commit(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_
 }
 
 // ------------------------------------------------------------ shard exchange
-// exclusive prefix of a predicate over a 256-thread block, and its total
+// exclusive prefix of a predicate over the first 256 threads of a block (the
+// others pass false), and its total; every thread of the block calls it
 __device__ inline uint32_t block_prefix256(bool pred, uint32_t *total) {
     __shared__ uint32_t wsum[4];
     const unsigned long long m = __ballot(pred);
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t in_wave = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+    if (lane == 0 && w < 4) wsum[w] = (uint32_t)__popcll(m);
     __syncthreads();
     uint32_t before = 0, tot = 0;
     for (uint32_t k = 0; k < 4; k++) {
@@ -1193,14 +1366,15 @@ __device__ inline uint32_t block_prefix256(bool pred, uint32_t *total) {
     return before + in_wave;
 }
 
-// This shard's edge record (256 threads).  Token starts are exactly the
-// non-HOLE slots of [F1, L1], so the first / last tokens are found with
-// block-wide ballots over 256-slot windows (one round trip when tokens are
-// short) instead of a dependent walk.
-__device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C) {
-    __shared__ uint32_t rec[EDGE_WORDS];
+// This shard's edge record into rec (LDS), by the first 256 threads of the
+// block (every thread calls it).  Token starts are exactly the non-HOLE slots
+// of [F1, L1], so the first / last tokens are found with block-wide ballots
+// over 256-slot windows (one round trip when tokens are short) instead of a
+// dependent walk.
+__device__ void edge_record_compute(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t *rec) {
     __shared__ uint32_t sF1, sL1, slast, firstdiff;
     const uint32_t tid = threadIdx.x, T = 256;
+    const bool act = tid < T;
     const uint32_t *tok = E->tok;
     if (tid == 0) {
         const uint32_t l1n = aload(&C->L1new);
@@ -1220,7 +1394,7 @@ __device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C
         uint32_t found = 0;
         for (int64_t base = F1; found < 7 && base <= L1; base += T) {
             const int64_t p = base + tid;
-            const uint32_t v = p <= L1 ? aload(&tok[p]) : HOLE;
+            const uint32_t v = act && p <= L1 ? aload(&tok[p]) : HOLE;
             uint32_t tot;
             const uint32_t r = found + block_prefix256(v != HOLE, &tot);
             if (v != HOLE && r < 3) rec[ER_F + r] = v;
@@ -1232,8 +1406,8 @@ __device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C
         uint32_t foundL = 0;
         bool done = false;
         for (int64_t top = L1; top >= F1 && (!done || foundL < 3); top -= T) {
-            const int64_t p = top - tid;  // rank from the end grows with tid
-            const uint32_t v = p >= F1 ? aload(&tok[p]) : HOLE;
+            const int64_t p = top - (int64_t)tid;  // rank from the end grows with tid
+            const uint32_t v = act && p >= F1 ? aload(&tok[p]) : HOLE;
             uint32_t tot;
             const uint32_t r = foundL + block_prefix256(v != HOLE, &tot);
             if (v != HOLE && r < 3) rec[ER_L + r] = v;
@@ -1255,7 +1429,95 @@ __device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C
         rec[ER_CUT] = E->encode ? E->eb[C->ebp].nb : 0;
     }
     __syncthreads();
+}
+
+__device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    __shared__ uint32_t rec[EDGE_WORDS];
+    edge_record_compute(E, C, rec);
+    if (threadIdx.x < EDGE_WORDS) E->myrec[threadIdx.x] = rec[threadIdx.x];
+}
+
+// Fused sharded step, K1's edge block: every rank's record of the current
+// tokens, pushed by the ranks' last k_fused_sh (or the host's set-up /
+// redo gather: channel 1's latest sequence number either way), from my
+// mailbox into erec; then published to the other blocks (Ctl::erec_ready)
+__device__ void records_pull_block(const Eng *__restrict__ E, Ctl *__restrict__ C, const P2P *__restrict__ X) {
+    const uint32_t W = X->W, me = X->rank, tid = threadIdx.x;
+    const uint32_t seq = X->xs[XS_SEQ1], par = seq & 1u;
+    const unsigned long long t0 = wall_clock64();
+    if (tid < W) p2p_wait(X, X->mb[me] + MB_FLAG1 + 16 * tid, seq, t0);
+    if (X->fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __syncthreads();
+    const uint32_t *src = X->mb[me] + MB_DATA1 + (uint64_t)par * P2P_MAXR * EDGE_WORDS;
+    if (tid < W * EDGE_WORDS) E->erec[tid] = src[tid];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&C->erec_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Fused sharded step, k_fused_sh block 1: the deltas K1 accumulated in buf
+// pushed into slot [parity][me] of every rank's mailbox (P2P channel 0),
+// then my flag in every mailbox := seq.  Nobody waits here: the apply's
+// role B waits for all W flags and sums the slots as it reads them.
+__device__ void push_exchange_block(const P2P *__restrict__ X, const uint32_t *__restrict__ buf, uint32_t count,
+                                    uint32_t seq) {
+    const uint32_t W = X->W, me = X->rank, c0 = X->c0, tid = threadIdx.x, T = blockDim.x;
+    const uint32_t par = seq & 1u;
+    const uint32_t nv = count / 4;
+    for (uint32_t p = 0; p < W; p++) {
+        uint32_t *dst = X->mb[p] + MB_DATA0 + ((uint64_t)par * W + me) * c0;
+        for (uint32_t i = tid; i < nv; i += T)
+            reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(buf)[i];
+        for (uint32_t i = nv * 4 + tid; i < count; i += T) dst[i] = buf[i];
+    }
+    p2p_release_point();
+    if (tid == 0) {
+        if (X->fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        for (uint32_t p = 0; p < W; p++)
+            __hip_atomic_store(X->mb[p] + MB_FLAG0 + 16 * me, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // keep k_p2p_sum's push count in step (it waits for W per exchange)
+        __hip_atomic_fetch_add(X->xs + XS_PUSH0, W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        X->xs[XS_SEQ0] = seq;
+    }
+}
+
+// Fused sharded step, k_fused_sh's last block: once the apply blocks have
+// rewritten my spans, my record of the new tokens pushed into every rank's
+// mailbox (channel 1) for the next K1; nobody waits here either.
+__device__ void records_push_block(const Eng *__restrict__ E, Ctl *__restrict__ C, const P2P *__restrict__ X,
+                                   uint32_t apply_blocks) {
+    __shared__ uint32_t rec[EDGE_WORDS];
+    const uint32_t W = X->W, me = X->rank, tid = threadIdx.x;
+    if (tid == 0 && apply_blocks) {
+        const unsigned long long t0 = wall_clock64();
+        while (aload(&C->adone) < apply_blocks) {
+            if (wall_clock64() - t0 > X->timeout) {
+                atomicOr(&C->err, P2P_ERR_BIT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        C->adone = 0;
+    }
+    __syncthreads();
+    edge_record_compute(E, C, rec);
+    const uint32_t seq = X->xs[XS_SEQ1] + 1u, par = seq & 1u;
+    if (tid < W * EDGE_WORDS) {
+        const uint32_t p = tid / EDGE_WORDS, w = tid % EDGE_WORDS;
+        X->mb[p][MB_DATA1 + ((uint64_t)par * P2P_MAXR + me) * EDGE_WORDS + w] = rec[w];
+    }
     if (tid < EDGE_WORDS) E->myrec[tid] = rec[tid];
+    p2p_release_point();
+    if (tid == 0) {
+        if (X->fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        for (uint32_t p = 0; p < W; p++)
+            __hip_atomic_store(X->mb[p] + MB_FLAG1 + 16 * me, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        X->xs[XS_SEQ1] = seq;
+    }
 }
 
 // edge record after k_apply (its span writes are visible at the kernel

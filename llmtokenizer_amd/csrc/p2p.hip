@@ -34,7 +34,9 @@ constexpr uint32_t P2P_ERR_BIT = 16;  // Ctl::err bit of a timed-out exchange
 
 struct P2P {
     uint32_t *mb[P2P_MAXR];      // every rank's mailbox, mapped here (mb[rank]: my own)
-    uint32_t W, rank, c0, pad;   // ranks, my rank, words per sum slot (multiple of 4)
+    uint32_t W, rank, c0;        // ranks, my rank, words per sum slot (multiple of 4)
+    uint32_t fence;              // 1: system-scope release / acquire around the mailbox
+                                 // traffic (0: rely on the uncached mapping alone)
     uint32_t *xs;                // my counters: seq0, pushes0, seq1, err (plain device memory)
     uint32_t *err;               // extra error word (the training run's Ctl::err) or null
     unsigned long long timeout;  // wall-clock ticks a wait may take
@@ -78,7 +80,7 @@ __global__ __launch_bounds__(256) void k_p2p_sum(const P2P *__restrict__ X, uint
     for (uint32_t i = nv * 4 + tid; i < count; i += blockDim.x) dst[i] = buf[i];
     p2p_release_point();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+        if (X->fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
         __hip_atomic_store(X->mb[p] + MB_FLAG0 + 16 * me, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         // my buffer may be overwritten once all my blocks have pushed it
         __hip_atomic_fetch_add(X->xs + XS_PUSH0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -86,7 +88,7 @@ __global__ __launch_bounds__(256) void k_p2p_sum(const P2P *__restrict__ X, uint
     const unsigned long long t0 = wall_clock64();
     if (tid < W) p2p_wait(X, X->mb[me] + MB_FLAG0 + 16 * tid, seq, t0);
     else if (tid == 64) p2p_wait(X, X->xs + XS_PUSH0, W * seq, t0);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (X->fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     __syncthreads();
     const uint32_t *src = X->mb[me] + MB_DATA0 + (uint64_t)par * W * c0;
     const uint32_t share = (((count + W - 1) / W + 3) / 4) * 4;  // words per block, multiple of 4
@@ -119,13 +121,13 @@ __global__ __launch_bounds__(64) void k_p2p_gather(const P2P *__restrict__ X, co
         if (tid < EDGE_WORDS) X->mb[p][MB_DATA1 + ((uint64_t)par * P2P_MAXR + me) * EDGE_WORDS + tid] = v;
     p2p_release_point();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        if (X->fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         for (uint32_t p = 0; p < W; p++)
             __hip_atomic_store(X->mb[p] + MB_FLAG1 + 16 * me, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     const unsigned long long t0 = wall_clock64();
     if (tid < W) p2p_wait(X, X->mb[me] + MB_FLAG1 + 16 * tid, seq, t0);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (X->fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     __syncthreads();
     const uint32_t *s = X->mb[me] + MB_DATA1 + (uint64_t)par * P2P_MAXR * EDGE_WORDS;
     for (uint32_t t = tid; t < W * EDGE_WORDS; t += blockDim.x) dst[t] = s[t];

@@ -21,7 +21,6 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
-#include "p2p.hip"
 
 namespace {
 
@@ -98,6 +97,9 @@ namespace {
 
 // one device: the exchange is a sum / gather kernel over pointer tables
 bool local_mode(const bpe_gpu_group *g) { return !g->rccl && !g->p2p; }
+
+// BPE_FUSED_SH=0: P2P groups run the unfused sharded step (A/B runs)
+bool FUSED_SH = !getenv("BPE_FUSED_SH") || atoi(getenv("BPE_FUSED_SH")) != 0;
 
 int group_free_graph(bpe_gpu_group *g) {
     if (g->st) (void)hipStreamSynchronize(g->st);
@@ -194,7 +196,49 @@ int launch_group_batch(bpe_gpu_group *g) {
     return ex_records(g, g->d_ptrs);
 }
 
-int group_step(bpe_gpu_group *g) { return g->encoding ? launch_group_batch(g) : launch_group_iteration(g); }
+// Fused sharded step (P2P groups, one shard per rank), the multi-GPU form of
+// the one-shard speculative graph:
+//   k_rescan_spec_sh  every rank's records of the current tokens pulled from
+//                     the mailbox, the current merge's rescan, the predicted
+//                     next merge's scan (deltas into xbuf)
+//   k_fused_sh        k_select beside: the delta push to every rank, the
+//                     apply of the predicted merge (role B sums the ranks'
+//                     deltas from the mailbox), the push of my new record
+// Two launches per merge; both exchanges are pushes that overlap k_select,
+// and no kernel waits on a peer unless that peer is behind.
+bool group_fused(const bpe_gpu_group *g) { return g->p2p && g->cs.size() == 1 && g->cs[0]->h.xfused; }
+
+void launch_group_fused(bpe_gpu_group *g) {
+    bpe_gpu_ctx *c = g->cs[0];
+    k_rescan_spec_sh<<<1 + SPEC_RB + SPEC_SB, SCAN_T, 0, g->st>>>(c->dE, c->dC, SPEC_RB, g->d_p2p);
+    if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, g->st>>>(c->dE, c->dC);
+    k_fused_sh<<<3 + FUSED_A + FUSED_B, 1024, 0, g->st>>>(c->dE, c->dC, FUSED_A, g->d_p2p);
+}
+
+// fused step entry (after set-up or a stop): the committed merge scanned,
+// summed and applied for real; its delta parity is the control block's
+int launch_group_redo(bpe_gpu_group *g) {
+    bpe_gpu_ctx *c = g->cs[0];
+    k_scan<true><<<SCAN_BLOCKS, SCAN_T, 0, g->st>>>(c->dE, c->dC);
+    int r;
+    if ((r = ex_allreduce(g, nullptr, {c->h.xbuf + (uint64_t)c->hC->parity * c->h.xstride}, 4ull * c->h.vcap + 2)))
+        return r;
+    k_apply<<<APPLY_A + APPLY_B, 256, 0, g->st>>>(c->dE, c->dC, APPLY_A);
+    // the records of the new tokens, for the next k_rescan_spec_sh
+    k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 0);
+    HIPCHK(hipGetLastError());
+    return ex_records(g, nullptr);
+}
+
+int group_step(bpe_gpu_group *g) {
+    if (g->encoding) return launch_group_batch(g);
+    if (group_fused(g)) {
+        launch_group_fused(g);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
+    return launch_group_iteration(g);
+}
 
 int capture_group(bpe_gpu_group *g) {
     hipGraph_t gr;
@@ -218,6 +262,9 @@ int capture_group(bpe_gpu_group *g) {
 
 int drive_group(bpe_gpu_group *g) {
     int r;
+    const bool fused = !g->encoding && group_fused(g);
+    bool need_scan = true;     // fused: the committed merge is not scanned yet
+    bool ran_fused = false;    // fused: the last launch was the fused graph
     for (;;) {
         for (bpe_gpu_ctx *c : g->cs)
             if ((r = pull_ctl(c))) return r;
@@ -225,8 +272,30 @@ int drive_group(bpe_gpu_group *g) {
         for (bpe_gpu_ctx *c : g->cs)
             if (c->hC->stop != C0.stop || c->hC->merges_done != C0.merges_done || c->hC->D != C0.D)
                 return fail(BPE_GPU_EINTERNAL, "shards diverged");
+        if (fused && ran_fused && C0.stop != STOP_NONE && C0.stop != STOP_ERROR) {
+            // the fused graph stopped: revert the speculative apply that ran
+            // beside the stopping selection (if any), clear the other parity
+            bpe_gpu_ctx *c = g->cs[0];
+            launch_spec_revert(c, C0.spec_z != 0 && C0.spec_z == C0.stop_z + 1);
+            HIPCHK(hipGetLastError());
+            if ((r = pull_ctl(c))) return r;
+        }
+        ran_fused = false;
         switch (C0.stop) {
+        case STOP_REDO: {  // missed prediction: k_select committed the real merge
+            if (!fused) return fail(BPE_GPU_EINTERNAL, "unexpected stop state in sharded training");
+            bpe_gpu_ctx *c = g->cs[0];
+            c->hC->stop = STOP_NONE;
+            if ((r = push_ctl(c))) return r;
+            need_scan = true;
+            break;
+        }
         case STOP_NONE:
+            if (fused) {
+                if (need_scan && (r = launch_group_redo(g))) return r;
+                need_scan = false;
+                ran_fused = true;
+            }
             if (!g->graph && !g->eager && capture_group(g)) {
                 // collectives that refuse stream capture: launch eagerly
                 g->eager = true;
@@ -265,6 +334,7 @@ int drive_group(bpe_gpu_group *g) {
                 k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
             }
             HIPCHK(hipGetLastError());
+            need_scan = true;
             break;
         default:
             return fail(BPE_GPU_EINTERNAL, "unexpected stop state in sharded training");
@@ -330,6 +400,9 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         c->sharded = 1;
         c->shard = g->shard0 + k;
         c->nshards = g->nshards;
+        c->xfused = g->p2p && K == 1 && FUSED_SH;
+        c->xtimeout = g->hp.timeout;
+        c->xp2p = c->xfused ? g->d_p2p : nullptr;
         if ((r = setup_run(c, (uint32_t)cap, false))) return r;
         c->hC->n_live = ntot;  // global token count (the tracking thresholds are global)
         if ((r = push_ctl(c))) return r;
@@ -379,7 +452,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         std::vector<uint32_t *> xb;
         for (auto *c : g->cs) xb.push_back(c->h.xbuf);
         if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
-        for (auto *c : g->cs) HIPCHK(hipMemsetAsync(c->h.xbuf, 0, (4ull * c->h.vcap + 2) * 4, g->st));
+        for (auto *c : g->cs) HIPCHK(hipMemsetAsync(c->h.xbuf, 0, 2ull * c->h.xstride * 4, g->st));
     }
     for (bpe_gpu_ctx *c : g->cs) {
         launch_summaries(c);
@@ -412,6 +485,14 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     g->stats.rule_ties = C.counters[2];
     g->stats.keys = C.nkeys;
     g->stats.table_grows = g->cs[0]->stats.table_grows;
+    g->stats.l1_rescanned = C.counters[6];
+    if (getenv("BPE_DEBUG") && C.counters[7])
+        fprintf(stderr, "fused sharded K1 (us/merge): records pulled after %.2f; select phases (us): "
+                "reduce %.2f merge %.2f tail %.2f\n", C.xdbg[0] / 100.0 / C.counters[7],
+                C.counters[9] / 100.0 / C.counters[0], C.counters[10] / 100.0 / C.counters[0],
+                C.counters[11] / 100.0 / C.counters[0]);
+    g->stats.spec_hits = C.counters[7];
+    g->stats.spec_misses = C.counters[8];
     g->stats.ms_init = t1 - t0;
     g->stats.ms_train = t2 - t1;
     g->stats.ms_total = t2 - t0;
@@ -442,6 +523,8 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
         c->merges_done = 0;
         c->fast = 1;
         c->sharded = 1;
+        c->xfused = 0;
+        c->xp2p = nullptr;
         c->shard = g->shard0 + k;
         c->nshards = g->nshards;
         if ((r = setup_run(c, (uint32_t)n_merges, true))) return r;
@@ -615,6 +698,8 @@ int bpe_gpu_group_create_p2p(int device, int nranks, int rank, long max_merges, 
     double tmo = 30.0;
     if (const char *t = getenv("BPE_P2P_TIMEOUT_S")) tmo = std::max(0.01, atof(t));
     g->hp.timeout = (unsigned long long)(tmo * 1000.0 * khz);
+    g->hp.fence = 1;
+    if (const char *f = getenv("BPE_P2P_FENCE")) g->hp.fence = atoi(f) != 0;
     bpe_gpu_ctx *c;
     if ((r = ctx_new(device, g->st, &c))) { bpe_gpu_group_destroy(g); return r; }
     g->cs.push_back(c);

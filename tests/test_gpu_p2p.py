@@ -1,9 +1,11 @@
-"""GPU parity of the P2P transport (p2p.hip): shard groups whose ranks are
+"""GPU parity of the P2P transport (p2p.hip) and the fused sharded step
+(kernels.hip k_rescan_spec_sh / k_fused): shard groups whose ranks are
 separate processes exchanging through IPC-mapped uncached mailboxes.  On the
 one-GPU test box every rank maps the same device, which exercises the whole
-protocol (handles, pushes, flags, parity slots, graph replay) except the xGMI
-hop itself.  Bit-exact bar: merges and concatenated ids equal the one-device
-shard group with the same cuts, the single-GPU engine and the oracle (RULE)."""
+protocol (handles, pushes, flags, parity slots, graph replay, speculative
+hits and reverted misses) except the xGMI hop itself.  Bit-exact bar: merges
+and concatenated ids equal the one-device shard group with the same cuts,
+the single-GPU engine and the oracle (RULE)."""
 import os
 import random
 import socket
@@ -21,6 +23,16 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def corpus(spec):
+    """synth:SEED:N (random_text-shaped) | alpha:SEED:N:LETTERS (small alphabet)"""
+    f = spec.split(":")
+    if f[0] == "synth":
+        return synth_bytes(int(f[1]), int(f[2]))
+    rng = random.Random(int(f[1]))
+    letters = f[3].encode()
+    return bytes(rng.choice(letters) for _ in range(int(f[2])))
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -29,15 +41,15 @@ def _port():
     return p
 
 
-def _run_ranks(tmp_path, world, mode, seed, n, mm, cuts, extra=()):
+def _run_ranks(tmp_path, world, mode, spec, mm, cuts, extra=()):
     port = _port()
     env = dict(os.environ, BPE_P2P_TIMEOUT_S="20")
     procs, outs = [], []
     for r in range(world):
-        o = str(tmp_path / f"{mode}_r{r}.npz")
+        o = str(tmp_path / f"{mode}_{world}_r{r}.npz")
         outs.append(o)
         cmd = [sys.executable, os.path.join(HERE, "p2p_worker.py"), str(r), str(world), str(port), o, mode,
-               str(seed), str(n), str(mm), ",".join(map(str, cuts)), *extra]
+               spec, str(mm), ",".join(map(str, cuts)), *extra]
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
     for p in procs:
@@ -60,22 +72,48 @@ def _local(data, cuts, mm):
     return g.merges(), g.all_ids()
 
 
-def test_p2p_single_rank_equals_engine():
-    """W = 1: the push / flag / reduce kernels against the plain engine"""
-    n = 3 << 20
-    data = synth_bytes(981, n)
-    g = api.ShardGroup(0, nranks=1, rank=0, p2p_max_merges=300)
+def _single_rank(data, mm):
+    g = api.ShardGroup(0, nranks=1, rank=0, p2p_max_merges=max(mm, 0) if mm >= 0 else len(data))
     g.p2p_connect([g.p2p_handle])
     assert g.transport() == "p2p"
     g.load(0, data)
-    g.train(300)
+    g.train(mm)
+    return g
+
+
+def test_p2p_single_rank_equals_engine():
+    """W = 1: the fused step (records / delta pushes to itself) against the plain engine"""
+    n = 3 << 20
+    data = synth_bytes(981, n)
+    g = _single_rank(data, 300)
     e = api.Engine(0)
     e.load(data)
     e.train(300)
     assert (g.merges() == e.merges()).all()
     assert (g.all_ids() == e.ids()).all()
+    assert g.stats()["spec_hits"] > 0
     g.train(300)  # second run on the same group: the sequence counters carry over
     assert (g.merges() == e.merges()).all()
+
+
+def test_p2p_single_rank_spec_hits_and_misses():
+    """fused sharded step on small alphabets (many missed predictions, each
+    reverted by the host) and text (hits): bit-exact vs the oracle (RULE)"""
+    rng = random.Random(777)
+    hits = misses = 0
+    for k in range(10):
+        alpha = rng.choice(["ab", "abc", "aab", "abcd", "a b", "abcdefgh"])
+        n = rng.randint(200, 30000)
+        mm = rng.choice([-1, 50, 300])
+        data = corpus(f"alpha:{k}:{n}:{alpha}")
+        g = _single_rank(data, mm)
+        om, oi, _ = O.train(data, mm, O.RULE)
+        assert (g.merges() == om).all() and (g.all_ids() == oi).all(), (alpha, n, mm)
+        st = g.stats()
+        hits += st["spec_hits"]
+        misses += st["spec_misses"]
+        g.close()
+    assert hits > 0 and misses > 0, (hits, misses)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -83,11 +121,27 @@ def test_p2p_ranks_equal_local_group(tmp_path, world):
     n = 4 << 20
     rng = random.Random(world)
     cuts = [0] + sorted(rng.sample(range(1, n), world - 1)) + [n]
-    res = _run_ranks(tmp_path, world, "train", 982, n, 400, cuts)
+    res = _run_ranks(tmp_path, world, "train", f"synth:982:{n}", 400, cuts)
     m0, ids0 = _local(synth_bytes(982, n), cuts, 400)
     for r in res:
         assert (r["merges"] == m0).all()
     assert (np.concatenate([r["ids"] for r in res]) == ids0).all()
+    print("ms_train per rank:", [float(r["stats"][0]) for r in res], "hits/misses:", res[0]["stats"][1:])
+
+
+def test_p2p_ranks_misses_across_edges(tmp_path):
+    """3 ranks on a small alphabet (long a==b runs across shard edges, many
+    reverted predictions): vs the oracle (RULE)"""
+    n = 20000
+    spec = f"alpha:5:{n}:aab"
+    data = corpus(spec)
+    cuts = [0, 7, 9000, n]
+    res = _run_ranks(tmp_path, 3, "train", spec, 300, cuts)
+    om, oids, _ = O.train(data, 300, O.RULE)
+    for r in res:
+        assert (r["merges"] == om).all()
+    assert (np.concatenate([r["ids"] for r in res]) == oids).all()
+    assert res[0]["stats"][2] > 0, "no missed prediction exercised"
 
 
 def test_p2p_ranks_small_vs_oracle_and_encode(tmp_path):
@@ -96,12 +150,12 @@ def test_p2p_ranks_small_vs_oracle_and_encode(tmp_path):
     n = 3000
     data = synth_bytes(983, n)
     cuts = [0, 1, 1700, n]
-    res = _run_ranks(tmp_path, 3, "train", 983, n, 200, cuts)
+    res = _run_ranks(tmp_path, 3, "train", f"synth:983:{n}", 200, cuts)
     om, oids, _ = O.train(data, 200, O.RULE)
     assert (res[0]["merges"] == om).all()
     assert (np.concatenate([r["ids"] for r in res]) == oids).all()
     mfile = str(tmp_path / "m.npz")
     np.savez(mfile, merges=om)
     text = synth_bytes(984, 5000)
-    enc = _run_ranks(tmp_path, 3, "encode", 984, 5000, 200, [0, 2000, 2001, 5000], extra=(mfile,))
+    enc = _run_ranks(tmp_path, 3, "encode", "synth:984:5000", 200, [0, 2000, 2001, 5000], extra=(mfile,))
     assert (np.concatenate([r["ids"] for r in enc]) == O.encode(text, om)).all()
