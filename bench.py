@@ -241,6 +241,7 @@ def main():
     value = world * corpus_mb * k / elapsed
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     cp_ms = st["ms_count_pass"]
+    cp_name = "k_pair_hist_span" if st["count_pass_span"] else "k_pair_hist"
     cp_achieved = args.size / (cp_ms * 1e-3) / 1e9 if cp_ms > 0 else 0.0
     out = {
         "metric": "corpus MB/s per merge iter (train), 1 GiB synthetic corpus per GPU",
@@ -272,7 +273,7 @@ def main():
                      "note": "per-merge kernel is bound by dependent-load latency, not bandwidth; "
                              "event nodes add their own latency to the measured span"},
         # the one corpus-wide streaming pass (pair count over 1 B/token, V = 256)
-        "roofline_count_pass": {"kernel": "k_pair_hist", "bound": "hbm", "achieved": round(cp_achieved, 1),
+        "roofline_count_pass": {"kernel": cp_name, "bound": "hbm", "achieved": round(cp_achieved, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": round(cp_achieved / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": args.size, "avg_ms": round(cp_ms, 4)},
@@ -293,8 +294,8 @@ def main():
             out["roofline"]["traffic"] = tr[name]["traffic_bytes_per_launch"]
             out["roofline"]["traffic_source"] = ("profiles/r1_pmc_traffic.json (FETCH_SIZE raw, uncalibrated for "
                                                  "4-byte gathers, + WRITE_SIZE; 256-merge run)")
-        if "k_pair_hist" in tr:
-            out["roofline_count_pass"]["traffic"] = tr["k_pair_hist"]["traffic_bytes_per_launch"]
+        if cp_name in tr:
+            out["roofline_count_pass"]["traffic"] = tr[cp_name]["traffic_bytes_per_launch"]
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.cpu_size, args.cpu_merges)
     if enc is not None:

@@ -64,6 +64,7 @@ typedef struct {
     uint64_t l1_rescanned;    /* level-1 summary blocks rescanned                 */
     uint64_t spec_hits;       /* next merges found by the speculative scan        */
     uint64_t spec_misses;     /* mispredicted next merges (host re-scan)          */
+    uint64_t count_pass_span; /* 1: the count pass ran in span form (k_pair_hist_span) */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */

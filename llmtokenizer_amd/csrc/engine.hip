@@ -981,18 +981,24 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
         hipEvent_t e0, e1;
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
+        // byte values present span [lo, lo + S): the span form when S is small
+        const uint32_t lo = unrank.empty() ? 0 : unrank.front();
+        const uint32_t S = unrank.empty() ? 0 : unrank.back() - lo + 1;
+        const bool span = S >= 1 && S <= SPAN_MAX && !(getenv("BPE_HIST_SPAN") && !atoi(getenv("BPE_HIST_SPAN")));
         HIPCHK(hipEventRecord(e0, c->st));
-        k_pair_hist<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
+        if (span) k_pair_hist_span<<<ntl, 1024, 0, c->st>>>(c->dE, d_hist, tile, lo, S);
+        else k_pair_hist<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
         HIPCHK(hipEventRecord(e1, c->st));
         HIPCHK(hipEventSynchronize(e1));
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, e0, e1));
         hipEventDestroy(e0);
         hipEventDestroy(e1);
-        c->prof_name = "k_pair_hist";
+        c->prof_name = span ? "k_pair_hist_span" : "k_pair_hist";
         c->stats.ms_count_pass = ms;
+        c->stats.count_pass_span = span;
         c->prof_ms = ms;
-        c->prof_bytes = (double)c->n0 * parts;  // 1 B/token (V = 256), re-read once per bin part
+        c->prof_bytes = (double)c->n0 * (span ? 1 : parts);  // 1 B/token (V = 256), re-read once per bin part
         c->prof_launches = 1;
         k_pair_colscan<<<(AA + 255) / 256, 256, 0, c->st>>>(d_hist, d_tot, AA, ntl);
         k_scan_single<<<1, 1024, 0, c->st>>>(d_tot, h.poff, AA);

@@ -1629,6 +1629,76 @@ __global__ __launch_bounds__(1024) void k_pair_hist(const Eng *__restrict__ E, u
     for (uint32_t k = lo + threadIdx.x; k < hi; k += blockDim.x) hist[(uint64_t)tl * AA + k] = h[k - lo];
 }
 
+// Span form of k_pair_hist, for corpora whose byte values lie in [lo, lo + S)
+// with S <= SPAN_MAX (text): the bin of pair (x, y) is (x - lo) * S + (y - lo),
+// computed from the bytes alone, so each pair costs ONE LDS operation (the
+// bin add) instead of two (rank lookup + add): the count pass is bound by
+// LDS bank cycles, not by HBM.  Bins are written out in rank-key order, so
+// hist[] is identical to k_pair_hist's.  Per thread and round: two 16-byte
+// loads in flight (chunks c and c + blockDim); the byte after a chunk comes
+// from the next lane's load (one 1-byte load per wave for lane 63).
+constexpr uint32_t SPAN_MAX = 128;
+
+__device__ __forceinline__ void span_count(uint32_t *h, const uint4 v, uint32_t nxt, uint32_t S, uint32_t off,
+                                           uint32_t lim) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t prev = w[0] & 0xFF;
+    if (lim >= 16) {
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+            const uint32_t cur = k < 15 ? (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFF : nxt;
+            atomicAdd(&h[prev * S + cur - off], 1u);
+            prev = cur;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+            const uint32_t cur = k < 15 ? (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFF : nxt;
+            if (k < lim) atomicAdd(&h[prev * S + cur - off], 1u);
+            prev = cur;
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_pair_hist_span(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
+                                                         uint64_t tile, uint32_t lo, uint32_t S) {
+    __shared__ uint32_t h[SPAN_MAX * SPAN_MAX];
+    __shared__ uint32_t ur[256];
+    const uint32_t A = E->A, AA = A * A, SS = S * S;
+    const uint32_t tl = blockIdx.x, T = blockDim.x, lane = threadIdx.x & 63;
+    for (uint32_t i = threadIdx.x; i < SS; i += T) h[i] = 0;
+    for (uint32_t x = threadIdx.x; x < 256; x += T) {
+        const uint32_t r = E->rank[x];
+        if (r != HOLE) ur[r] = x;
+    }
+    __syncthreads();
+    const uint64_t n0 = E->n0;
+    const uint64_t s = (uint64_t)tl * tile, e = min(n0 - 1, s + tile);  // pair positions [s, e), tile % 16 == 0
+    const uint4 *src = reinterpret_cast<const uint4 *>(E->bytes);
+    const uint8_t *bytes = E->bytes;
+    const uint32_t off = lo * S + lo;
+    // every lane runs every round (the next-byte shuffle needs its neighbour)
+    for (uint64_t base = s / 16; base * 16 < e; base += 2ull * T) {
+        const uint64_t c0 = base + threadIdx.x, c1 = c0 + T;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        const uint4 v0 = c0 * 16 < n0 ? src[c0] : z;  // (bytes is padded to whole 16-byte groups)
+        const uint4 v1 = c1 * 16 < n0 ? src[c1] : z;
+        uint32_t n0x = __shfl_down(v0.x, 1) & 0xFF, n1x = __shfl_down(v1.x, 1) & 0xFF;
+        if (lane == 63) {
+            n0x = (c0 + 1) * 16 < n0 ? bytes[(c0 + 1) * 16] : 0;
+            n1x = (c1 + 1) * 16 < n0 ? bytes[(c1 + 1) * 16] : 0;
+        }
+        const uint64_t p0 = c0 * 16, p1 = c1 * 16;
+        if (p0 < e) span_count(h, v0, n0x, S, off, (uint32_t)min<uint64_t>(16, e - p0));
+        if (p1 < e) span_count(h, v1, n1x, S, off, (uint32_t)min<uint64_t>(16, e - p1));
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < AA; k += T) {
+        const uint32_t x = ur[k / A] - lo, y = ur[k % A] - lo;
+        hist[(uint64_t)tl * AA + k] = h[x * S + y];
+    }
+}
+
 // column scan over tiles: hist[t][k] := sum_{t' < t} hist[t'][k]; tot[k] = total
 __global__ void k_pair_colscan(uint32_t *__restrict__ hist, uint32_t *__restrict__ tot, uint32_t AA, uint32_t ntiles) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;

@@ -497,6 +497,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     g->stats.ms_train = t2 - t1;
     g->stats.ms_total = t2 - t0;
     g->stats.ms_count_pass = g->cs[0]->stats.ms_count_pass;
+    g->stats.count_pass_span = g->cs[0]->stats.count_pass_span;
     return 0;
 }
 
