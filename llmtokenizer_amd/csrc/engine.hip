@@ -364,6 +364,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     }
     if ((r = dalloc(c, &h.vecd, encode ? 1 : (size_t)2 * REPL * 4 * DENSE))) return r;
     if ((r = dalloc(c, &h.scan_tend, STAMPS))) return r;
+    h.dbgts = nullptr;
+    if (getenv("BPE_DEBUG_TS") && !encode && (r = dalloc(c, &h.dbgts, (size_t)TS_SLOTS * 8))) return r;
     h.spec_on = SPEC_ON && !encode && (!c->sharded || h.xfused);
     h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? 1 + SPEC_RB + SPEC_SB : 0);
     h.ntiles = (n0 + CTILE - 1) / CTILE;
@@ -377,8 +379,18 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.sfirst, h.scap))) return r;
     // pair table
     if (!encode) {
-        uint64_t want = 4ull * (65536 + 16ull * (256 + std::min<uint64_t>(mcap, 4096)));
+        // keys (distinct pairs ever seen) grow by up to ~1.2 k per merge on
+        // uniform text (1 GiB: 1.25 M after 1024 merges) and never exceed the
+        // positions: size for that under the half-full rule so that typical
+        // runs never regrow (a regrowth is a host round trip + rehash), capped
+        // where k_select stops reducing level 1 directly
+        const uint64_t keys = std::min<uint64_t>(n0, 65536 + 1536ull * mcap);
+        uint64_t want = std::max<uint64_t>(2 * keys, 4ull * (65536 + 16ull * (256 + std::min<uint64_t>(mcap, 4096))));
+        want = std::min<uint64_t>(want, (uint64_t)SELECT_L1_MAX * L1W);
+        // BPE_TABLE_SLOTS: initial size override (tests drive the regrowth path with it)
         h.hcap = pow2_at_least(std::max<uint64_t>(want, 1ull << 17));
+        if (const char *t = getenv("BPE_TABLE_SLOTS"))
+            h.hcap = pow2_at_least(std::max<uint64_t>((uint64_t)std::max(0ll, atoll(t)), 1ull << 15));
     } else {
         h.hcap = 1ull << 16;
     }
@@ -929,30 +941,71 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
     }
 }
 
+// BPE_DEBUG_TS: average per-merge block timeline of the speculative graph,
+// relative to K1's first block entry (us); merges with every stamp present
+void print_timeline(bpe_gpu_ctx *c, uint32_t zlast) {
+    std::vector<unsigned long long> t((size_t)TS_SLOTS * 8);
+    if (hipMemcpy(t.data(), c->h.dbgts, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    int ikhz = 0;
+    (void)hipDeviceGetAttribute(&ikhz, hipDeviceAttributeWallClockRate, c->dev);
+    const double khz = ikhz > 0 ? ikhz : 100000.0;
+    double sum[8] = {}, gap = 0;
+    uint32_t n = 0, ng = 0;
+    static const char *nm[8] = {"K1 first in", "K1 rescan out", "K1 scan out", "K2 first in",
+                                "K2 select out", "K2 applyA out", "K2 applyB out", "K1 last in"};
+    for (uint32_t z = 257; z < zlast && z < TS_SLOTS; z++) {
+        const unsigned long long *r = &t[(size_t)z * 8];
+        bool ok = true;
+        for (int k = 0; k < 8; k++) ok = ok && r[k] != 0;
+        if (!ok) continue;
+        const double k1 = (double)~r[TS_K1_IN];
+        for (int k = 0; k < 8; k++) {
+            const double v = (k == TS_K1_IN || k == TS_K2_IN) ? (double)~r[k] : (double)r[k];
+            sum[k] += (v - k1) * 1000.0 / khz;
+        }
+        n++;
+        const unsigned long long *q = &t[(size_t)(z + 1) * 8];
+        if (z + 1 < zlast && q[TS_K1_IN]) {
+            const double end2 = (double)std::max(r[TS_K2_SELECT], std::max(r[TS_K2_APPLY_A], r[TS_K2_APPLY_B]));
+            gap += ((double)~q[TS_K1_IN] - end2) * 1000.0 / khz;
+            ng++;
+        }
+    }
+    if (!n) return;
+    fprintf(stderr, "block timeline over %u merges (us from K1's first block entry):", n);
+    for (int k = 1; k < 8; k++) fprintf(stderr, " %s %.2f;", nm[k], sum[k] / n);
+    fprintf(stderr, " K2 end -> next K1 in %.2f\n", ng ? gap / ng : 0.0);
+}
+
 int compact_ids(bpe_gpu_ctx *c) {
-    k_live_count<<<1024, 256, 0, c->st>>>(c->dE, c->dC, 0);
-    k_live_scan<<<1, 1024, 0, c->st>>>(c->dE, c->dC, 0, c->d_tileoff);
-    k_live_write<<<1024, 256, 0, c->st>>>(c->dE, c->dC, 0, c->d_tileoff, 0);
+    // single pass (k_live_compact): tile status words + ticket + total, zeroed
+    int r;
+    const uint64_t ntl = c->h.ntiles;
+    unsigned long long *d_status;
+    if ((r = dalloc(c, &d_status, ntl + 1, false))) return r;
+    uint32_t *d_ticket = reinterpret_cast<uint32_t *>(d_status + ntl);
+    HIPCHK(hipMemsetAsync(d_status, 0, (ntl + 1) * 8, c->st));
+    if (ntl) k_live_compact<<<(uint32_t)ntl, LC_T, 0, c->st>>>(c->dE, d_status, d_ticket, d_ticket + 1);
     HIPCHK(hipGetLastError());
     uint32_t tot = 0;
-    HIPCHK(hipMemcpyAsync(&tot, c->d_tileoff + c->h.ntiles, 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(&tot, d_ticket + 1, 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     c->ids_len = tot;
     c->ids_ready = true;
     return 0;
 }
 
-// init phase 1: tok[] = bytes and the set of byte values present
+// init phase 1: the set of byte values present (tok[] is written in phase 2)
 int init_presence(bpe_gpu_ctx *c, uint32_t **d_bh) {
     int r;
     if ((r = dalloc(c, d_bh, 256))) return r;
-    k_init_tok<<<1024, 256, 0, c->st>>>(c->dE, *d_bh);
+    k_init_tok<false, true><<<1024, 256, 0, c->st>>>(c->dE, *d_bh);
     HIPCHK(hipGetLastError());
     return 0;
 }
 
 // init phase 2: byte ranks (from the presence vector `bh`, nonzero = present),
-// token lengths, counting sort of byte-pair positions by rank key
+// token lengths, tok[] = bytes, counting sort of byte-pair positions by rank key
 int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint32_t> *unrank_out,
               uint32_t **d_tot_out) {
     Eng &h = c->h;
@@ -970,21 +1023,24 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
     // counting sort of pair positions by rank key
     const uint64_t npairs = c->n0 - 1;
     uint64_t tile = std::max<uint64_t>(1 << 16, (npairs + 1023) / 1024);
-    tile = (tile + 15) & ~15ull;  // kernels read 16-byte groups
+    tile = (tile + 1023) & ~1023ull;  // kernels read 16-byte groups / 1-KB blocks (k_pair_hist_span)
     const uint32_t ntl = (uint32_t)((npairs + tile - 1) / tile);
     const uint32_t parts = (AA + HBINS - 1) / HBINS;
     uint32_t *d_hist, *d_tot;
     if ((r = dalloc(c, &d_hist, (size_t)ntl * AA, false))) return r;
     if ((r = dalloc(c, &d_tot, AA + 1))) return r;
+    // byte values present span [lo, lo + S): the span form of the count pass
+    // (which also writes tok[]) when S is small
+    const uint32_t lo = unrank.empty() ? 0 : unrank.front();
+    const uint32_t S = unrank.empty() ? 0 : unrank.back() - lo + 1;
+    const bool span = npairs > 0 && S >= 1 && S <= SPAN_MAX &&
+                      !(getenv("BPE_HIST_SPAN") && !atoi(getenv("BPE_HIST_SPAN")));
+    if (!span) k_tok_words<<<1024, 256, 0, c->st>>>(c->dE);
     if (npairs > 0) {
         // the one full pass over the corpus: time it with events on our stream
         hipEvent_t e0, e1;
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
-        // byte values present span [lo, lo + S): the span form when S is small
-        const uint32_t lo = unrank.empty() ? 0 : unrank.front();
-        const uint32_t S = unrank.empty() ? 0 : unrank.back() - lo + 1;
-        const bool span = S >= 1 && S <= SPAN_MAX && !(getenv("BPE_HIST_SPAN") && !atoi(getenv("BPE_HIST_SPAN")));
         HIPCHK(hipEventRecord(e0, c->st));
         if (span) k_pair_hist_span<<<ntl, 1024, 0, c->st>>>(c->dE, d_hist, tile, lo, S);
         else k_pair_hist<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
@@ -998,15 +1054,23 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
         c->stats.ms_count_pass = ms;
         c->stats.count_pass_span = span;
         c->prof_ms = ms;
-        c->prof_bytes = (double)c->n0 * (span ? 1 : parts);  // 1 B/token (V = 256), re-read once per bin part
+        // 1 B/token read (V = 256; re-read once per bin part), + 4 B/token tok[] write when fused
+        c->prof_bytes = (double)c->n0 * (span ? 5 : parts);
         c->prof_launches = 1;
-        k_pair_colscan<<<(AA + 255) / 256, 256, 0, c->st>>>(d_hist, d_tot, AA, ntl);
+        const uint32_t per = (ntl + COLSCAN_GROUPS - 1) / COLSCAN_GROUPS;
+        const uint32_t ngr = (ntl + per - 1) / per;
+        uint32_t *d_gsum;
+        if ((r = dalloc(c, &d_gsum, (size_t)ngr * AA, false))) return r;
+        const dim3 cgrid((AA + 255) / 256, ngr);
+        k_pair_colsum<<<cgrid, 256, 0, c->st>>>(d_hist, d_gsum, AA, ntl, per);
+        k_pair_colscan<<<cgrid, 256, 0, c->st>>>(d_hist, d_gsum, d_tot, AA, ntl, per);
         k_scan_single<<<1, 1024, 0, c->st>>>(d_tot, h.poff, AA);
         // scratch = the occurrence pool + ids_out block (>= 2n0 words, untouched
         // until the first merge)
-        unsigned long long *d_tmp = reinterpret_cast<unsigned long long *>(h.occ);
+        if (tile > (1ull << SORT_LOCAL_BITS)) return fail(BPE_GPU_EINTERNAL, "sort tile exceeds 2^24 positions");
+        uint32_t *d_tmp = h.occ;
         k_sort_a<<<ntl, SORT_T, 0, c->st>>>(c->dE, d_hist, tile, d_tmp);
-        k_sort_b<<<1024, SORT_T, 0, c->st>>>(c->dE, d_hist, d_tot, ntl, d_tmp);
+        k_sort_b<<<1024, SORT_T, 0, c->st>>>(c->dE, d_hist, d_tot, ntl, tile, d_tmp);
         HIPCHK(hipGetLastError());
     } else {
         HIPCHK(hipMemsetAsync(h.poff, 0, 4ull * (AA + 1), c->st));
@@ -1222,6 +1286,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.l1_rescanned = C.counters[6];
     c->stats.spec_hits = C.counters[7];
     c->stats.spec_misses = C.counters[8];
+    if (c->h.dbgts) print_timeline(c, C.z);
     if (getenv("BPE_DEBUG"))
         fprintf(stderr, "select phases (ticks/iter): reduce %.1f merge %.1f tail %.1f\n",
                 (double)C.counters[9] / C.counters[0], (double)C.counters[10] / C.counters[0],
@@ -1287,7 +1352,7 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
     } else {
         uint32_t *d_bh;
         if ((r = dalloc(c, &d_bh, 256))) return r;
-        k_init_tok<<<1, 256, 0, c->st>>>(c->dE, d_bh);
+        k_init_tok<true, true><<<1, 256, 0, c->st>>>(c->dE, d_bh);
     }
     // merges in commuting batches: first batch, then graphs of (scan, apply + next batch)
     EncBatch *d_eb;

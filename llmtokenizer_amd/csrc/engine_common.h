@@ -28,6 +28,10 @@ constexpr uint32_t L1W = 1024;           // slots per level-1 summary block
 constexpr uint32_t L2W = 256;            // level-1 entries per level-2 summary
 constexpr uint32_t MARK = 0xFFFFFFFFu;   // dist[] of an end slot whose token starts in an earlier shard
 constexpr uint32_t EDGE_WORDS = 16;      // words per shard edge record
+constexpr uint32_t TS_SLOTS = 4096;      // merges kept by the debug block timeline
+// debug timeline slots (wall clock; entries stored complemented so that
+// atomicMax keeps the earliest): K1 = k_rescan_spec, K2 = k_fused
+enum { TS_K1_IN = 0, TS_K1_RESCAN, TS_K1_SCAN, TS_K2_IN, TS_K2_SELECT, TS_K2_APPLY_A, TS_K2_APPLY_B, TS_K1_LASTIN };
 
 enum { V_DL = 0, V_DR = 1, V_IL = 2, V_IR = 3 };
 
@@ -108,6 +112,7 @@ struct Eng {
     uint32_t *ids_out;    // compaction output
     uint32_t *aux;        // per-slot scratch for the resolver (first thread)
     unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
+    unsigned long long *dbgts;      // [TS_SLOTS][8] per-merge block timeline (BPE_DEBUG_TS) or null
     uint32_t fast;        // 1: schedule-free tie rule everywhere (no tracking)
     uint32_t spec_on;     // 1: one-shard training with the speculative next-merge scan
     uint32_t scan_blocks; // k_scan grid (entries of scan_tend)

@@ -211,6 +211,13 @@ __device__ inline void scan_exit_stamp(const Eng *E, uint32_t bid) {
     if (threadIdx.x == 0) E->scan_tend[bid] = wall_clock64();
 }
 
+// debug block timeline (E->dbgts, BPE_DEBUG_TS): one stamp per block
+__device__ inline void ts_mark(const Eng *E, uint32_t z, uint32_t slot, bool entry) {
+    if (!E->dbgts || threadIdx.x != 0) return;
+    const unsigned long long t = wall_clock64();
+    atomicMax(&E->dbgts[(uint64_t)(z % TS_SLOTS) * 8 + slot], entry ? ~t : t);
+}
+
 // stage one occurrence position (single-thread path: walker / shard edge)
 __device__ inline void stage_one(uint32_t *list, uint16_t *ltag, uint32_t *lcount, uint32_t *R, uint32_t *occz,
                                  uint16_t *tagz, uint32_t pos, uint16_t tag, uint32_t *bcount) {
@@ -936,11 +943,15 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ 
     const Snap S = snap(C);
     if (blockIdx.x == 0 && threadIdx.x == 0) spec_descriptor(C, S);
     if (S.stop) return;
+    ts_mark(E, S.z, TS_K1_IN, true);
+    ts_mark(E, S.z, TS_K1_LASTIN, false);
     if (blockIdx.x < rblocks) {
         rescan1_body(E, C, S, blockIdx.x, rblocks);
         scan_exit_stamp(E, blockIdx.x);
+        ts_mark(E, S.z, TS_K1_RESCAN, false);
     } else if (S.spec) {
         scan_body<false, true>(E, C, S, blockIdx.x - rblocks, gridDim.x - rblocks);
+        ts_mark(E, S.z, TS_K1_SCAN, false);
     } else {
         scan_exit_stamp(E, blockIdx.x);
     }
@@ -1255,12 +1266,17 @@ __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl 
 __global__ __launch_bounds__(1024) void k_fused(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleA_blocks,
                                                 const P2P *__restrict__ X) {
     if (blockIdx.x == 0) {
+        const uint32_t z0 = C->z;  // the current merge (select moves on)
+        ts_mark(E, z0, TS_K2_IN, true);
         select_block(E, C, SEL_FUSED);
+        ts_mark(E, z0, TS_K2_SELECT, false);
         return;
     }
     const Snap S = snap_next(C);
     if (S.stop) return;
+    ts_mark(E, S.z - 1, TS_K2_IN, true);
     apply_body<false>(E, C, S, blockIdx.x - 1, gridDim.x - 1, roleA_blocks, X);
+    ts_mark(E, S.z - 1, blockIdx.x - 1 < roleA_blocks ? TS_K2_APPLY_A : TS_K2_APPLY_B, false);
     if (blockIdx.x == 1 && threadIdx.x == 0) C->spec_z = S.z;
 }
 
@@ -1559,12 +1575,17 @@ __global__ void k_init_cross(const Eng *__restrict__ E, uint32_t *__restrict__ t
 
 
 // ------------------------------------------------------------- init kernels
-// tok[i] = byte i (16 bytes per thread, uint4 in / 4 x uint4 out) and the set
-// of byte values present (only presence is needed to rank them)
+// tok[i] = byte i (16 bytes per thread, uint4 in / 4 x uint4 out) and / or
+// the set of byte values present (only presence is needed to rank them).
+// Training runs presence alone first; tok is then written by the count pass
+// (k_pair_hist_span) or by the TOK-only instance.
+template <bool TOK, bool PRES>
 __global__ __launch_bounds__(256) void k_init_tok(const Eng *__restrict__ E, uint32_t *__restrict__ present) {
     __shared__ uint32_t seen[256];
-    for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x) seen[x] = 0;
-    __syncthreads();
+    if (PRES) {
+        for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x) seen[x] = 0;
+        __syncthreads();
+    }
     const uint64_t n0 = E->n0, nv = n0 / 16;
     const uint4 *src = reinterpret_cast<const uint4 *>(E->bytes);
     uint4 *dst = reinterpret_cast<uint4 *>(E->tok);
@@ -1575,19 +1596,23 @@ __global__ __launch_bounds__(256) void k_init_tok(const Eng *__restrict__ E, uin
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t b0 = w[q] & 0xFF, b1 = (w[q] >> 8) & 0xFF, b2 = (w[q] >> 16) & 0xFF, b3 = w[q] >> 24;
-            dst[4 * c + q] = make_uint4(b0, b1, b2, b3);
-            seen[b0] = 1; seen[b1] = 1; seen[b2] = 1; seen[b3] = 1;  // benign same-value races
+            if (TOK) dst[4 * c + q] = make_uint4(b0, b1, b2, b3);
+            if (PRES) { seen[b0] = 1; seen[b1] = 1; seen[b2] = 1; seen[b3] = 1; }  // benign same-value races
         }
     }
     if (blockIdx.x == 0)
         for (uint64_t k = nv * 16 + threadIdx.x; k < n0; k += blockDim.x) {
-            E->tok[k] = E->bytes[k];
-            seen[E->bytes[k]] = 1;
+            if (TOK) E->tok[k] = E->bytes[k];
+            if (PRES) seen[E->bytes[k]] = 1;
         }
-    __syncthreads();
-    for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x)
-        if (seen[x] && !present[x]) atomicOr(&present[x], 1u);
+    if (PRES) {
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x)
+            if (seen[x] && !present[x]) atomicOr(&present[x], 1u);
+    }
 }
+template __global__ void k_init_tok<true, true>(const Eng *, uint32_t *);
+template __global__ void k_init_tok<false, true>(const Eng *, uint32_t *);
 
 // per-(tile, part) histogram of byte-pair rank keys; LDS u32 bins.
 // 16 pair positions per thread from one uint4 load (+1 byte of the next).
@@ -1629,7 +1654,8 @@ __global__ __launch_bounds__(1024) void k_pair_hist(const Eng *__restrict__ E, u
     for (uint32_t k = lo + threadIdx.x; k < hi; k += blockDim.x) hist[(uint64_t)tl * AA + k] = h[k - lo];
 }
 
-// Span form of k_pair_hist, for corpora whose byte values lie in [lo, lo + S)
+// Span form of k_pair_hist (it also writes the initial tok[]), for corpora
+// whose byte values lie in [lo, lo + S)
 // with S <= SPAN_MAX (text): the bin of pair (x, y) is (x - lo) * S + (y - lo),
 // computed from the bytes alone, so each pair costs ONE LDS operation (the
 // bin add) instead of two (rank lookup + add): the count pass is bound by
@@ -1639,27 +1665,61 @@ __global__ __launch_bounds__(1024) void k_pair_hist(const Eng *__restrict__ E, u
 // from the next lane's load (one 1-byte load per wave for lane 63).
 constexpr uint32_t SPAN_MAX = 128;
 
-__device__ __forceinline__ void span_count(uint32_t *h, const uint4 v, uint32_t nxt, uint32_t S, uint32_t off,
-                                           uint32_t lim) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    uint32_t prev = w[0] & 0xFF;
-    if (lim >= 16) {
-#pragma unroll
-        for (uint32_t k = 0; k < 16; k++) {
-            const uint32_t cur = k < 15 ? (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFF : nxt;
-            atomicAdd(&h[prev * S + cur - off], 1u);
-            prev = cur;
-        }
+// Word-granular layout shared by the passes that write the initial tok[]:
+// a wave owns 1 KB blocks of the corpus; lane L of round q (0..3) holds byte
+// word 64q + L, so each dword load is one coalesced 256-B access and each
+// uint4 store of the 4 widened tokens one contiguous 1-KB run (16-B lanes at
+// a 64-B stride left half-written lines behind: 2.2 TB/s).
+__device__ __forceinline__ uint4 widen4(uint32_t w) {
+    return make_uint4(w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFF, w >> 24);
+}
+
+// the 4 pairs starting in word w (next = the following byte); lim < 4 near the tile end
+__device__ __forceinline__ void span_count4(uint32_t *h, uint32_t w, uint32_t next, uint32_t S, uint32_t off,
+                                            uint32_t lim) {
+    const uint32_t b0 = w & 0xFF, b1 = (w >> 8) & 0xFF, b2 = (w >> 16) & 0xFF, b3 = w >> 24, b4 = next & 0xFF;
+    if (lim >= 4) {
+        atomicAdd(&h[b0 * S + b1 - off], 1u);
+        atomicAdd(&h[b1 * S + b2 - off], 1u);
+        atomicAdd(&h[b2 * S + b3 - off], 1u);
+        atomicAdd(&h[b3 * S + b4 - off], 1u);
     } else {
-#pragma unroll
-        for (uint32_t k = 0; k < 16; k++) {
-            const uint32_t cur = k < 15 ? (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFF : nxt;
-            if (k < lim) atomicAdd(&h[prev * S + cur - off], 1u);
-            prev = cur;
-        }
+        if (lim > 0) atomicAdd(&h[b0 * S + b1 - off], 1u);
+        if (lim > 1) atomicAdd(&h[b1 * S + b2 - off], 1u);
+        if (lim > 2) atomicAdd(&h[b2 * S + b3 - off], 1u);
     }
 }
 
+// one 1-KB block kb of a wave: count its pairs below e (HIST), write its full
+// token words (TOK); w[q] = word 64q + lane of the block
+template <bool HIST, bool TOK>
+__device__ __forceinline__ void kb_body(uint32_t *h, uint4 *tok, const uint8_t *bytes, uint64_t kb, const uint32_t w[4],
+                                        uint64_t e, uint64_t n0, uint32_t S, uint32_t off) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint64_t wi = kb * 256 + 64 * q + lane, p = wi * 4;
+        if (HIST) {
+            uint32_t nxt = __shfl_down(w[q], 1);
+            if (q < 3) {
+                const uint32_t f = __shfl(w[q + 1], 0);
+                if (lane == 63) nxt = f;
+            } else if (lane == 63) {
+                nxt = (kb + 1) * 1024 < n0 ? bytes[(kb + 1) * 1024] : 0;
+            }
+            if (p < e) span_count4(h, w[q], nxt, S, off, (uint32_t)min<uint64_t>(4, e - p));
+        }
+        if (TOK && p + 4 <= n0) tok[wi] = widen4(w[q]);
+    }
+}
+
+// Span form of k_pair_hist (it also writes the initial tok[]), for corpora
+// whose byte values lie in [lo, lo + S) with S <= SPAN_MAX (text): the bin of
+// pair (x, y) is (x - lo) * S + (y - lo), computed from the bytes alone, so
+// each pair costs ONE LDS operation (the bin add) instead of two (rank lookup
+// + add).  Bins are written out in rank-key order, so hist[] is identical to
+// k_pair_hist's.  Tiles are 1-KB aligned; each wave walks its own 1-KB blocks,
+// two in flight (8 dword loads per lane).
 __global__ __launch_bounds__(1024) void k_pair_hist_span(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
                                                          uint64_t tile, uint32_t lo, uint32_t S) {
     __shared__ uint32_t h[SPAN_MAX * SPAN_MAX];
@@ -1673,25 +1733,28 @@ __global__ __launch_bounds__(1024) void k_pair_hist_span(const Eng *__restrict__
     }
     __syncthreads();
     const uint64_t n0 = E->n0;
-    const uint64_t s = (uint64_t)tl * tile, e = min(n0 - 1, s + tile);  // pair positions [s, e), tile % 16 == 0
-    const uint4 *src = reinterpret_cast<const uint4 *>(E->bytes);
+    const uint64_t s = (uint64_t)tl * tile, e = min(n0 - 1, s + tile);  // pair positions [s, e), tile % 1024 == 0
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(E->bytes);
     const uint8_t *bytes = E->bytes;
+    uint4 *tok = reinterpret_cast<uint4 *>(E->tok);
     const uint32_t off = lo * S + lo;
-    // every lane runs every round (the next-byte shuffle needs its neighbour)
-    for (uint64_t base = s / 16; base * 16 < e; base += 2ull * T) {
-        const uint64_t c0 = base + threadIdx.x, c1 = c0 + T;
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        const uint4 v0 = c0 * 16 < n0 ? src[c0] : z;  // (bytes is padded to whole 16-byte groups)
-        const uint4 v1 = c1 * 16 < n0 ? src[c1] : z;
-        uint32_t n0x = __shfl_down(v0.x, 1) & 0xFF, n1x = __shfl_down(v1.x, 1) & 0xFF;
-        if (lane == 63) {
-            n0x = (c0 + 1) * 16 < n0 ? bytes[(c0 + 1) * 16] : 0;
-            n1x = (c1 + 1) * 16 < n0 ? bytes[(c1 + 1) * 16] : 0;
+    const uint64_t nw = T / 64, kb0 = s / 1024, kb1 = (e + 1023) / 1024;
+    const uint64_t nwords = (n0 + 3) / 4;  // (bytes is zero-padded past n0)
+    for (uint64_t kb = kb0 + (threadIdx.x >> 6); kb < kb1; kb += 2 * nw) {  // wave-uniform
+        const uint64_t kc = kb + nw;
+        uint32_t wa[4], wb[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint64_t ia = kb * 256 + 64 * q + lane, ib = kc * 256 + 64 * q + lane;
+            wa[q] = ia < nwords ? src[ia] : 0u;
+            wb[q] = kc < kb1 && ib < nwords ? src[ib] : 0u;
         }
-        const uint64_t p0 = c0 * 16, p1 = c1 * 16;
-        if (p0 < e) span_count(h, v0, n0x, S, off, (uint32_t)min<uint64_t>(16, e - p0));
-        if (p1 < e) span_count(h, v1, n1x, S, off, (uint32_t)min<uint64_t>(16, e - p1));
+        kb_body<true, true>(h, tok, bytes, kb, wa, e, n0, S, off);
+        if (kc < kb1) kb_body<true, true>(h, tok, bytes, kc, wb, e, n0, S, off);
     }
+    // the tail of the last partial word (every full word lies in some tile's blocks)
+    if (tl == gridDim.x - 1)
+        for (uint64_t k = n0 / 4 * 4 + threadIdx.x; k < n0; k += T) E->tok[k] = bytes[k];
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < AA; k += T) {
         const uint32_t x = ur[k / A] - lo, y = ur[k % A] - lo;
@@ -1699,17 +1762,64 @@ __global__ __launch_bounds__(1024) void k_pair_hist_span(const Eng *__restrict__
     }
 }
 
-// column scan over tiles: hist[t][k] := sum_{t' < t} hist[t'][k]; tot[k] = total
-__global__ void k_pair_colscan(uint32_t *__restrict__ hist, uint32_t *__restrict__ tot, uint32_t AA, uint32_t ntiles) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+// tok[] = bytes alone, in the same coalesced layout (count passes other than
+// the span form): grid-stride over 1-KB blocks, one per wave
+__global__ __launch_bounds__(256) void k_tok_words(const Eng *__restrict__ E) {
+    const uint64_t n0 = E->n0, nwords = (n0 + 3) / 4, nkb = (n0 + 1023) / 1024;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(E->bytes);
+    uint4 *tok = reinterpret_cast<uint4 *>(E->tok);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nwv = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t kb = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); kb < nkb; kb += nwv) {
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint64_t i = kb * 256 + 64 * q + lane;
+            w[q] = i < nwords ? src[i] : 0u;
+        }
+        kb_body<false, true>(nullptr, tok, E->bytes, kb, w, 0, n0, 0, 0);
+    }
+    if (blockIdx.x == 0)
+        for (uint64_t k = n0 / 4 * 4 + threadIdx.x; k < n0; k += blockDim.x) E->tok[k] = E->bytes[k];
+}
+
+// column scan over tiles: hist[t][k] := sum_{t' < t} hist[t'][k]; tot[k] =
+// total.  Two launches over a (key, tile group) grid so that every CU has
+// independent loads in flight (one thread per key walking all tiles keeps
+// only AA / 256 blocks busy): sums per group, then each group's walk starts
+// from the sum of the groups before it.
+constexpr uint32_t COLSCAN_GROUPS = 64;
+
+__global__ __launch_bounds__(256) void k_pair_colsum(const uint32_t *__restrict__ hist, uint32_t *__restrict__ gsum,
+                                                     uint32_t AA, uint32_t ntiles, uint32_t per) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x, g = blockIdx.y;
+    if (k >= AA) return;
+    const uint32_t t0 = g * per, t1 = min(ntiles, t0 + per);
+    uint32_t sum = 0;
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; t++) sum += hist[(uint64_t)t * AA + k];
+    gsum[(uint64_t)g * AA + k] = sum;
+}
+
+__global__ __launch_bounds__(256) void k_pair_colscan(uint32_t *__restrict__ hist, const uint32_t *__restrict__ gsum,
+                                                      uint32_t *__restrict__ tot, uint32_t AA, uint32_t ntiles,
+                                                      uint32_t per) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x, g = blockIdx.y;
     if (k >= AA) return;
     uint32_t run = 0;
-    for (uint32_t t = 0; t < ntiles; t++) {
-        const uint32_t c = hist[(uint64_t)t * AA + k];
-        hist[(uint64_t)t * AA + k] = run;
-        run += c;
+    for (uint32_t q = 0; q < g; q++) run += gsum[(uint64_t)q * AA + k];
+    const uint32_t t0 = g * per, t1 = min(ntiles, t0 + per);
+    uint32_t c[8];
+    for (uint32_t t = t0; t < t1; t += 8) {
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) c[q] = t + q < t1 ? hist[(uint64_t)(t + q) * AA + k] : 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 8; q++) {
+            if (t + q < t1) hist[(uint64_t)(t + q) * AA + k] = run;
+            run += c[q];
+        }
     }
-    tot[k] = run;
+    if (g == gridDim.y - 1) tot[k] = run;
 }
 
 // exclusive scan of in[0..n) into out[0..n], out[n] = total; one block of
@@ -1767,21 +1877,23 @@ __device__ inline uint32_t tile_count(const uint32_t *hist, const uint32_t *tot,
 
 // Both passes sort CH-element chunks inside LDS first (local counting sort),
 // then copy each bin's run out contiguously: consecutive lanes store to
-// consecutive addresses.
+// consecutive addresses.  Pass A's entries are packed into 4 bytes: the
+// second byte's rank in the top 8 bits, the position relative to the tile
+// start in the low 24 (tile <= 2^24), so each pass moves 4 B per pair.
 constexpr uint32_t SORT_T = 1024, SORT_PER = 8, SORT_CH = SORT_T * SORT_PER;
+constexpr uint32_t SORT_LOCAL_BITS = 24;
 
 struct SortLds {
-    uint32_t ent[SORT_CH];  // staged positions in local bin order
-    uint8_t hi[SORT_CH];    // their high byte (pass A: second-byte rank, emitted as k2 << 32)
+    uint32_t ent[SORT_CH];  // staged entries in local bin order
     uint8_t bin[SORT_CH];   // their bins
     uint32_t cnt[256], lstart[256], gcur[256], gstart[256];
-};  // 50 KB: three 1024-thread blocks per CU
+};  // 44 KB: three 1024-thread blocks per CU
 
 // local counting sort of this thread's SORT_PER (bin, entry) pairs, then a
 // coalesced copy of every bin's run to out[gcur[bin] ...]; gcur advances.
-// vals: position | hi << 32 (hi < 256); out64: emit (hi << 32 | position).
-__device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const unsigned long long *vals, uint32_t nb,
-                                     void *out, bool out64) {
+// bins[k] >= nb: no entry.
+__device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const uint32_t *vals, uint32_t nb,
+                                     uint32_t *__restrict__ out) {
     for (uint32_t x = threadIdx.x; x < nb; x += SORT_T) L.cnt[x] = 0;
     __syncthreads();
     uint32_t rank[SORT_PER];
@@ -1822,25 +1934,22 @@ __device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const uns
     for (uint32_t k = 0; k < SORT_PER; k++)
         if (bins[k] < nb) {
             const uint32_t s = L.lstart[bins[k]] + rank[k];
-            L.ent[s] = (uint32_t)vals[k];
-            L.hi[s] = (uint8_t)(vals[k] >> 32);
+            L.ent[s] = vals[k];
             L.bin[s] = (uint8_t)bins[k];
         }
     __syncthreads();
     const uint32_t total = L.cnt[0];
     for (uint32_t s = threadIdx.x; s < total; s += SORT_T) {
         const uint32_t bn = L.bin[s];
-        const uint32_t d = L.gstart[bn] + (s - L.lstart[bn]);
-        if (out64) reinterpret_cast<unsigned long long *>(out)[d] = ((unsigned long long)L.hi[s] << 32) | L.ent[s];
-        else reinterpret_cast<uint32_t *>(out)[d] = L.ent[s];
+        out[L.gstart[bn] + (s - L.lstart[bn])] = L.ent[s];
     }
     __syncthreads();
 }
 
-// pass A: tile t -> entries (k2 << 32 | position) grouped by k1, in the same
-// slot range plist will use for that tile's k1 group
+// pass A: tile t -> packed entries (k2 << 24 | position - tile start) grouped
+// by k1, in the same slot range plist will use for that tile's k1 group
 __global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
-                                                   uint64_t tile, unsigned long long *__restrict__ tmp) {
+                                                   uint64_t tile, uint32_t *__restrict__ tmp) {
     __shared__ SortLds L;
     __shared__ uint32_t rk[256];
     const uint32_t A = E->A, AA = A * A;
@@ -1856,8 +1965,7 @@ __global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, co
     const uint64_t s = (uint64_t)t * tile, e = min(n0 - 1, s + tile);
     // each thread takes SORT_PER = 8 consecutive positions per round (uint2 load + 1 byte)
     for (uint64_t p0 = s + threadIdx.x * SORT_PER; p0 - threadIdx.x * SORT_PER < e; p0 += SORT_CH) {
-        uint32_t bins[SORT_PER];
-        unsigned long long vals[SORT_PER];
+        uint32_t bins[SORT_PER], vals[SORT_PER];
         uint32_t by[SORT_PER + 1] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         if (p0 < e) {
             const uint2 w = *reinterpret_cast<const uint2 *>(E->bytes + p0);
@@ -1869,21 +1977,23 @@ __global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, co
         for (uint32_t k = 0; k < SORT_PER; k++) {
             const bool in = p0 + k < e;
             bins[k] = in ? rk[by[k]] : 256u;
-            vals[k] = in ? (((unsigned long long)rk[by[k + 1]] << 32) | (uint32_t)(p0 + k)) : 0ull;
+            vals[k] = in ? (rk[by[k + 1]] << SORT_LOCAL_BITS) | (uint32_t)(p0 + k - s) : 0u;
         }
-        lds_sort_emit(L, bins, vals, A, tmp, true);
+        lds_sort_emit(L, bins, vals, A, tmp);
     }
 }
 
 // pass B: unit (tile t, first rank k1) -> plist by second rank
 __global__ __launch_bounds__(SORT_T) void k_sort_b(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
-                                                   const uint32_t *__restrict__ tot, uint32_t ntl,
-                                                   const unsigned long long *__restrict__ tmp) {
+                                                   const uint32_t *__restrict__ tot, uint32_t ntl, uint64_t tile,
+                                                   const uint32_t *__restrict__ tmp) {
     __shared__ SortLds L;
     __shared__ uint32_t range[2];
     const uint32_t A = E->A, AA = A * A;
+    constexpr uint32_t LOCAL = (1u << SORT_LOCAL_BITS) - 1;
     for (uint32_t u = blockIdx.x; u < ntl * A; u += gridDim.x) {
         const uint32_t t = u / A, k1 = u % A;
+        const uint32_t tbase = (uint32_t)((uint64_t)t * tile);  // positions are u32 (n0 <= 2^32 - 2)
         __syncthreads();
         if (threadIdx.x == 0) { range[0] = E->poff[k1 * A]; range[1] = 0; }
         __syncthreads();
@@ -1896,16 +2006,15 @@ __global__ __launch_bounds__(SORT_T) void k_sort_b(const Eng *__restrict__ E, co
         __syncthreads();
         const uint32_t lo = range[0], n = range[1];
         for (uint32_t q0 = 0; q0 < n; q0 += SORT_CH) {
-            uint32_t bins[SORT_PER];
-            unsigned long long vals[SORT_PER];
+            uint32_t bins[SORT_PER], vals[SORT_PER];
 #pragma unroll
             for (uint32_t k = 0; k < SORT_PER; k++) {
                 const uint32_t q = q0 + k * SORT_T + threadIdx.x;  // coalesced reads
-                const unsigned long long w = q < n ? tmp[lo + q] : 0ull;
-                bins[k] = q < n ? (uint32_t)(w >> 32) : 256u;
-                vals[k] = (uint32_t)w;
+                const uint32_t w = q < n ? tmp[lo + q] : 0u;
+                bins[k] = q < n ? w >> SORT_LOCAL_BITS : 256u;
+                vals[k] = tbase + (w & LOCAL);
             }
-            lds_sort_emit(L, bins, vals, A, E->plist, false);
+            lds_sort_emit(L, bins, vals, A, E->plist);
         }
     }
 }
@@ -2025,6 +2134,103 @@ __global__ __launch_bounds__(256) void k_live_write(const Eng *__restrict__ E, c
             base += ws[0] + ws[1] + ws[2] + ws[3];
             __syncthreads();
         }
+    }
+}
+
+// Single-pass compaction of the live tokens into ids_out: CTILE-token tiles
+// taken in ticket order (so every tile a block waits on is held by a block
+// that started earlier), decoupled look-back over per-tile status words
+// (flag << 32 | count: 1 = this tile's aggregate, 2 = inclusive prefix),
+// one 64-bit agent-scope word per tile so flag and value travel together.
+// The tile stays in registers (16 x uint4 per thread) across the look-back;
+// each wave stages a round's live tokens in LDS and stores them as one
+// coalesced run.  Replaces k_live_count + k_live_scan + k_live_write for the
+// final ids (one read of tok instead of two).
+constexpr uint32_t LC_T = 256, LC_R = CTILE / (4 * LC_T);  // 16 rounds of 4 tokens per thread
+constexpr unsigned long long LC_AGG = 1ull << 32, LC_INC = 2ull << 32;
+
+__device__ inline void lc_publish(unsigned long long *st, unsigned long long v) {
+    __hip_atomic_store(st, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(LC_T) void k_live_compact(const Eng *__restrict__ E, unsigned long long *__restrict__ status,
+                                                       uint32_t *__restrict__ ticket, uint32_t *__restrict__ total) {
+    __shared__ uint32_t tile_s, excl_s;
+    __shared__ uint32_t woff[LC_R * 4];   // (round, wave) -> exclusive offset within the tile
+    __shared__ uint32_t stage[4][4 * 64];  // per-wave staging of one round's live tokens
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) tile_s = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint64_t t = tile_s, n0 = E->n0, ntl = E->ntiles;
+    uint4 v[LC_R];
+    uint32_t pre[LC_R];  // this lane's exclusive prefix within its wave, per round
+#pragma unroll
+    for (uint32_t r = 0; r < LC_R; r++) (void)live4(E->tok, t * CTILE + r * 4 * LC_T + tid * 4, n0, &v[r]);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (uint32_t r = 0; r < LC_R; r++) {
+        const uint32_t c = (v[r].x != HOLE) + (v[r].y != HOLE) + (v[r].z != HOLE) + (v[r].w != HOLE);
+        // c in 0..4: prefix and total from three ballots
+        const unsigned long long b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+        pre[r] = (uint32_t)__popcll(b0 & lt) + 2u * (uint32_t)__popcll(b1 & lt) + 4u * (uint32_t)__popcll(b2 & lt);
+        if (lane == 0) woff[r * 4 + w] = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
+    }
+    __syncthreads();
+    if (w == 0) {
+        // (round, wave) totals -> exclusive offsets: one entry per lane
+        const uint32_t x = woff[lane];
+        uint32_t incl = x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if ((int)lane >= o) incl += y;
+        }
+        woff[lane] = incl - x;
+        const uint32_t agg = __shfl(incl, 63);
+        if (lane == 0) lc_publish(&status[t], (t == 0 ? LC_INC : LC_AGG) | agg);
+        // look-back: 64 predecessors per round, nearest first
+        uint32_t excl = 0;
+        for (int64_t top = (int64_t)t - 1; top >= 0;) {
+            const int64_t idx = top - (int64_t)lane;
+            const unsigned long long sv =
+                idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : LC_INC;
+            const uint32_t flag = (uint32_t)(sv >> 32);
+            const unsigned long long inc = __ballot(flag == 2), none = __ballot(flag == 0);
+            const uint32_t k = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive prefix
+            const unsigned long long upto = k >= 63 ? ~0ull : ((1ull << (k + 1)) - 1ull);
+            if (none & upto) {  // a predecessor in the way has not published yet
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            uint32_t part = lane <= k ? (uint32_t)sv : 0u;
+            for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+            excl += part;
+            if (k < 64) break;
+            top -= 64;
+        }
+        if (lane == 0) {
+            if (t > 0) lc_publish(&status[t], LC_INC | (excl + agg));
+            if (t == ntl - 1) *total = excl + agg;
+            excl_s = excl;
+        }
+    }
+    __syncthreads();
+    const uint32_t base = excl_s;
+    uint32_t *out = E->ids_out;
+    uint32_t *sg = stage[w];
+#pragma unroll
+    for (uint32_t r = 0; r < LC_R; r++) {
+        const uint32_t x4[4] = {v[r].x, v[r].y, v[r].z, v[r].w};
+        uint32_t o = pre[r];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (x4[q] != HOLE) sg[o++] = x4[q];
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's staging stores landed
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t cnt = __shfl(o, 63);  // lane 63's end = the wave's total this round
+        const uint32_t dst = base + woff[r * 4 + w];
+        for (uint32_t k = lane; k < cnt; k += 64) out[dst + k] = sg[k];
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
     }
 }
 

@@ -136,3 +136,24 @@ def test_1g_properties_after_many_merges():
     sub = ids[:1 << 20]
     dec = e.decode(sub, merges)
     assert dec == synth_bytes(2, len(dec))
+
+
+def test_table_regrowth_matches_presized(monkeypatch):
+    """The pair table is sized so that typical runs never regrow; a forced
+    small table (BPE_TABLE_SLOTS) drives the regrowth path (host round trip,
+    rehash, full summary rebuild, graph recapture) and must give the same
+    merges and ids as the presized run and the oracle."""
+    data = synth_bytes(905, 1 << 20)
+    e = api.Engine(0)
+    e.load(data)
+    e.train(400)
+    m0, i0 = e.merges(), e.ids()
+    assert e.stats()["table_grows"] == 0
+    monkeypatch.setenv("BPE_TABLE_SLOTS", str(1 << 15))
+    e2 = api.Engine(0)
+    e2.load(data)
+    e2.train(400)
+    assert e2.stats()["table_grows"] >= 1
+    assert (e2.merges() == m0).all() and (e2.ids() == i0).all()
+    om, oids, _ = O.train(data, 400, O.EMU)
+    assert (m0 == om).all() and (i0 == oids).all()
