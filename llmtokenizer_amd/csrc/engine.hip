@@ -326,7 +326,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.nshards = c->nshards;
     const uint64_t n0 = c->n0;
     int r;
-    if ((r = dalloc(c, &h.tok, n0 + 8, false))) return r;  // + 8: k_scan's 2x16-byte windows
+    if ((r = dalloc(c, &h.tok, n0 + 32, false))) return r;  // + 32: k_scan's token windows (TokWinW)
     if ((r = dalloc(c, &h.dist, n0, false))) return r;  // read only where written (left_start)
     if ((r = dalloc(c, &h.tlen, h.vcap))) return r;
     if ((r = dalloc(c, &h.rank, 256))) return r;
@@ -365,7 +365,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.vecd, encode ? 1 : (size_t)2 * REPL * 4 * DENSE))) return r;
     if ((r = dalloc(c, &h.scan_tend, STAMPS))) return r;
     h.dbgts = nullptr;
-    if (getenv("BPE_DEBUG_TS") && !encode && (r = dalloc(c, &h.dbgts, (size_t)TS_SLOTS * 8))) return r;
+    if (getenv("BPE_DEBUG_TS") && !encode && (r = dalloc(c, &h.dbgts, (size_t)TS_SLOTS * TS_N))) return r;
     h.spec_on = SPEC_ON && !encode && (!c->sharded || h.xfused);
     h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? 1 + SPEC_RB + SPEC_SB : 0);
     h.ntiles = (n0 + CTILE - 1) / CTILE;
@@ -944,27 +944,29 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
 // BPE_DEBUG_TS: average per-merge block timeline of the speculative graph,
 // relative to K1's first block entry (us); merges with every stamp present
 void print_timeline(bpe_gpu_ctx *c, uint32_t zlast) {
-    std::vector<unsigned long long> t((size_t)TS_SLOTS * 8);
+    std::vector<unsigned long long> t((size_t)TS_SLOTS * TS_N);
     if (hipMemcpy(t.data(), c->h.dbgts, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     int ikhz = 0;
     (void)hipDeviceGetAttribute(&ikhz, hipDeviceAttributeWallClockRate, c->dev);
     const double khz = ikhz > 0 ? ikhz : 100000.0;
-    double sum[8] = {}, gap = 0;
+    double sum[TS_N] = {}, gap = 0;
     uint32_t n = 0, ng = 0;
-    static const char *nm[8] = {"K1 first in", "K1 rescan out", "K1 scan out", "K2 first in",
-                                "K2 select out", "K2 applyA out", "K2 applyB out", "K1 last in"};
+    static const char *nm[TS_N] = {"K1 first in", "K1 rescan out", "K1 scan out", "K2 first in",
+                                   "K2 select out", "K2 applyA out", "K2 applyB out", "K1 last in",
+                                   "scan cands done", "scan list flushed", "scan deltas flushed",
+                                   "B deltas loaded", "B table updated", "B marks listed"};
     for (uint32_t z = 257; z < zlast && z < TS_SLOTS; z++) {
-        const unsigned long long *r = &t[(size_t)z * 8];
+        const unsigned long long *r = &t[(size_t)z * TS_N];
         bool ok = true;
-        for (int k = 0; k < 8; k++) ok = ok && r[k] != 0;
+        for (int k = 0; k < TS_N; k++) ok = ok && r[k] != 0;
         if (!ok) continue;
         const double k1 = (double)~r[TS_K1_IN];
-        for (int k = 0; k < 8; k++) {
+        for (int k = 0; k < TS_N; k++) {
             const double v = (k == TS_K1_IN || k == TS_K2_IN) ? (double)~r[k] : (double)r[k];
             sum[k] += (v - k1) * 1000.0 / khz;
         }
         n++;
-        const unsigned long long *q = &t[(size_t)(z + 1) * 8];
+        const unsigned long long *q = &t[(size_t)(z + 1) * TS_N];
         if (z + 1 < zlast && q[TS_K1_IN]) {
             const double end2 = (double)std::max(r[TS_K2_SELECT], std::max(r[TS_K2_APPLY_A], r[TS_K2_APPLY_B]));
             gap += ((double)~q[TS_K1_IN] - end2) * 1000.0 / khz;
@@ -973,7 +975,7 @@ void print_timeline(bpe_gpu_ctx *c, uint32_t zlast) {
     }
     if (!n) return;
     fprintf(stderr, "block timeline over %u merges (us from K1's first block entry):", n);
-    for (int k = 1; k < 8; k++) fprintf(stderr, " %s %.2f;", nm[k], sum[k] / n);
+    for (int k = 1; k < TS_N; k++) fprintf(stderr, " %s %.2f;", nm[k], sum[k] / n);
     fprintf(stderr, " K2 end -> next K1 in %.2f\n", ng ? gap / ng : 0.0);
 }
 

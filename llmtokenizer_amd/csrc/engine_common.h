@@ -31,7 +31,8 @@ constexpr uint32_t EDGE_WORDS = 16;      // words per shard edge record
 constexpr uint32_t TS_SLOTS = 4096;      // merges kept by the debug block timeline
 // debug timeline slots (wall clock; entries stored complemented so that
 // atomicMax keeps the earliest): K1 = k_rescan_spec, K2 = k_fused
-enum { TS_K1_IN = 0, TS_K1_RESCAN, TS_K1_SCAN, TS_K2_IN, TS_K2_SELECT, TS_K2_APPLY_A, TS_K2_APPLY_B, TS_K1_LASTIN };
+enum { TS_K1_IN = 0, TS_K1_RESCAN, TS_K1_SCAN, TS_K2_IN, TS_K2_SELECT, TS_K2_APPLY_A, TS_K2_APPLY_B, TS_K1_LASTIN,
+       TS_S_CAND, TS_S_LIST, TS_S_DELTA, TS_B_DVAL, TS_B_TABLE, TS_B_MARKS, TS_N };
 
 enum { V_DL = 0, V_DR = 1, V_IL = 2, V_IR = 3 };
 

@@ -211,11 +211,18 @@ __device__ inline void scan_exit_stamp(const Eng *E, uint32_t bid) {
     if (threadIdx.x == 0) E->scan_tend[bid] = wall_clock64();
 }
 
-// debug block timeline (E->dbgts, BPE_DEBUG_TS): one stamp per block
-__device__ inline void ts_mark(const Eng *E, uint32_t z, uint32_t slot, bool entry) {
-    if (!E->dbgts || threadIdx.x != 0) return;
+// debug block timeline (E->dbgts, BPE_DEBUG_TS): one stamp per block.
+// sync: after every wave of the block drained its memory operations (a
+// stamp alone can issue before the loads of the phase it closes returned)
+__device__ inline void ts_mark(const Eng *E, uint32_t z, uint32_t slot, bool entry, bool sync = false) {
+    if (!E->dbgts) return;
+    if (sync) {
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
     const unsigned long long t = wall_clock64();
-    atomicMax(&E->dbgts[(uint64_t)(z % TS_SLOTS) * 8 + slot], entry ? ~t : t);
+    atomicMax(&E->dbgts[(uint64_t)(z % TS_SLOTS) * TS_N + slot], entry ? ~t : t);
 }
 
 // stage one occurrence position (single-thread path: walker / shard edge)
@@ -426,7 +433,9 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
                 pos = k;
             }
         }
+        if (SPEC && e0 + ncand * SCAN_T >= len) ts_mark(E, S.z, TS_S_CAND, false);
         flush_list(list, ltag, &lcount, &gbase, Rc, occz, tagz, &bR);
+        if (SPEC && e0 + ncand * SCAN_T >= len) ts_mark(E, S.z, TS_S_LIST, false);
     }
     if (edge_block) {
         // Shard edges.  Right: my last token and the first token after it form
@@ -485,6 +494,7 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
         if (threadIdx.x == 0 && bR) atomicAdd(&xb[4 * vc], bR);  // this shard's R, summed
         __syncthreads();
     }
+    if (SPEC) ts_mark(E, S.z, TS_S_DELTA, false);
     scan_exit_stamp(E, blockIdx.x);
 }
 
@@ -510,7 +520,9 @@ __device__ inline uint64_t hfind(const Eng *E, uint32_t u, uint32_t v) {
     return ~0ull;
 }
 
-__device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v) {
+// nins != null: count a new key there instead of in C->nkeys (the caller
+// adds its block's total once: ~200 same-address atomics per merge otherwise)
+__device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v, uint32_t *nins = nullptr) {
     const unsigned long long key = (((unsigned long long)u << 32) | v) + 1ull;
     const uint64_t m = E->hcap - 1;
     uint64_t s = mix64(key) & m;
@@ -520,7 +532,8 @@ __device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v)
         if (k == 0) {
             unsigned long long prev = atomicCAS(&E->hkey[s], 0ull, key);
             if (prev == 0) {
-                atomicAdd(&C->nkeys, 1ull);
+                if (nins) *nins += 1;
+                else atomicAdd(&C->nkeys, 1ull);
                 return s;
             }
             if (prev == key) return s;
@@ -662,6 +675,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     if (threadIdx.x == 0) nmark = 0;
     __syncthreads();
     long long dD = 0;
+    uint32_t nins = 0;  // keys this thread inserted
     const uint32_t base0 = (bid - roleA_blocks) * blockDim.x;
     for (uint32_t t0 = base0; t0 < total; t0 += stride) {  // uniform trip count per block
         const uint32_t t = t0 + threadIdx.x;
@@ -702,6 +716,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
             vir = u == z ? dval(E, P, V_IR, v) : 0;
             vil = v == z ? dval(E, P, V_IL, u) : 0;
         }
+        if (!UNDO) ts_mark(E, z - 1, TS_B_DVAL, false, true);
         bool owner = cat >= 0;
         if (owner && cat == 4) owner = Rg != 0;
         if (owner && cat == V_DR) owner = vdr != 0 && !(u == a && v == b);
@@ -713,7 +728,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
             if (u == a && v == b) d -= Rg;
             if (UNDO) d = -d;
             if (d != 0) {
-                const uint64_t slot = d > 0 ? hinsert(E, C, u, v) : hfind(E, u, v);
+                const uint64_t slot = d > 0 ? hinsert(E, C, u, v, &nins) : hfind(E, u, v);
                 if (slot == ~0ull) {
                     C->err = d > 0 ? 2 : 1;  // k_select stops on it
                 } else {
@@ -734,25 +749,39 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
         const uint32_t p = wave_append(mark, &nmark);
         if (mark) marks[p] = blk;
         __syncthreads();
+        if (!UNDO) ts_mark(E, z - 1, TS_B_TABLE, false, true);
         if (nmark > MARK_CAP - blockDim.x || t0 + stride >= total) {
             if (threadIdx.x == 0) mbase = nmark ? atomicAdd(&C->nl1p[P], nmark) : 0;
             __syncthreads();
             uint32_t *l1l = E->l1list + (uint64_t)P * E->l1cap;
             for (uint32_t k = threadIdx.x; k < nmark; k += blockDim.x) l1l[mbase + k] = marks[k];
+            if (!UNDO) ts_mark(E, z - 1, TS_B_MARKS, false);
             __syncthreads();
             if (threadIdx.x == 0) nmark = 0;
             __syncthreads();
         }
     }
-    // block-reduce dD (any block size up to 1024) into this parity's delta
-    for (int o = 32; o > 0; o >>= 1) dD += __shfl_xor(dD, o);
+    // block-reduce dD and the inserted keys (any block size up to 1024)
+    for (int o = 32; o > 0; o >>= 1) {
+        dD += __shfl_xor(dD, o);
+        nins += __shfl_xor(nins, o);
+    }
     __shared__ long long sd[16];
-    if ((threadIdx.x & 63) == 0) sd[threadIdx.x >> 6] = dD;
+    __shared__ uint32_t si[16];
+    if ((threadIdx.x & 63) == 0) {
+        sd[threadIdx.x >> 6] = dD;
+        si[threadIdx.x >> 6] = nins;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         long long t = 0;
-        for (uint32_t w = 0; w < blockDim.x / 64; w++) t += sd[w];
+        unsigned long long ni = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) {
+            t += sd[w];
+            ni += si[w];
+        }
         if (t != 0) atomicAdd(&C->Dp[P], (unsigned long long)t);
+        if (ni != 0) atomicAdd(&C->nkeys, ni);
     }
 }
 
@@ -836,6 +865,7 @@ __device__ inline Top2 top2_one(unsigned long long v, uint32_t tie, unsigned lon
 }
 
 constexpr uint64_t SELECT_L1_MAX = 16384;  // k_select reduces level 1 directly up to this
+constexpr uint32_t SUM_ONE_RT = 4;         // summaries <= 4 x 1024 entries: reduced in one round trip
 
 // one wave per dirty level-1 block (256 slots, 4 per lane)
 __device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C);
@@ -1164,6 +1194,26 @@ __device__ inline Top2 summary_top2(const unsigned long long *best, const uint32
                                     const unsigned long long *k2, uint64_t n) {
     constexpr uint32_t PER = SELECT_L1_MAX / 1024;
     const uint32_t tid = threadIdx.x;
+    if (n <= SUM_ONE_RT * (uint64_t)blockDim.x) {
+        // small summaries: every field of every entry in one round trip
+        unsigned long long bv[SUM_ONE_RT], kv[SUM_ONE_RT], v2v[SUM_ONE_RT], k2v[SUM_ONE_RT];
+        uint32_t tv[SUM_ONE_RT];
+#pragma unroll
+        for (uint32_t k = 0; k < SUM_ONE_RT; k++) {
+            const uint64_t i = tid + (uint64_t)k * blockDim.x;
+            const bool in = i < n;
+            bv[k] = in ? best[i] : 0ull;
+            tv[k] = in ? tie[i] : 0u;
+            kv[k] = in ? key[i] : 0ull;
+            v2v[k] = in ? v2[i] : 0ull;
+            k2v[k] = in ? k2[i] : ~0ull;
+        }
+        Top2 mine = top2_one(0, 0, ~0ull);
+#pragma unroll
+        for (uint32_t k = 0; k < SUM_ONE_RT; k++)
+            if (bv[k]) mine = top2_merge(mine, Top2{Best{bv[k], tv[k], kv[k]}, v2v[k], k2v[k]});
+        return wave_top2(mine);
+    }
     unsigned long long v[PER];
 #pragma unroll
     for (uint32_t k = 0; k < PER; k++) {
@@ -1207,10 +1257,13 @@ __device__ __forceinline__ void select_block(const Eng *__restrict__ E, Ctl *__r
     const uint32_t tid = threadIdx.x;
     uint32_t *scw = reinterpret_cast<uint32_t *>(&sc);
     uint32_t *cgw = reinterpret_cast<uint32_t *>(Cg);
-    for (uint32_t x = tid; x < CW; x += blockDim.x) scw[x] = cgw[x];
-    for (uint32_t x = tid; x < 256; x += blockDim.x) srank[x] = E->rank[x];
+    // the control block and byte ranks go to LDS only after the summary loads
+    // are in flight (an LDS store of a loaded word would hold them back a
+    // round trip); scan-block exit stamps likewise overlap the reduction
+    static_assert(sizeof(Ctl) / 4 <= 1024, "Ctl staged one word per thread");
+    const uint32_t cw_v = tid < CW ? cgw[tid] : 0u;
+    const uint32_t rk_v = tid < 256 ? E->rank[tid] : 0u;
     const bool pl = false;  // (staging all byte-pair offsets costs more than the 2 loads it saves)
-    // scan-block exit stamps: loaded first so they overlap the reduction
     unsigned long long tend = 0;
     for (uint32_t x = tid; x < E->scan_blocks; x += blockDim.x) tend = max(tend, E->scan_tend[x]);
     const uint64_t nL1 = E->hcap / L1W;
@@ -1218,6 +1271,8 @@ __device__ __forceinline__ void select_block(const Eng *__restrict__ E, Ctl *__r
     Top2 mine = summary_top2(lvl1 ? E->l1best : E->l2best, lvl1 ? E->l1tie : E->l2tie, lvl1 ? E->l1key : E->l2key,
                              lvl1 ? E->l1v2 : E->l2v2, lvl1 ? E->l1k2 : E->l2k2,
                              lvl1 ? nL1 : (nL1 + L2W - 1) / L2W);
+    if (tid < CW) scw[tid] = cw_v;
+    if (tid < 256) srank[tid] = rk_v;
     if (tid == 0) sc_t1 = wall_clock64();
     // k_scan's last block exit (one stamp per k_scan block, <= blockDim)
     for (int o = 32; o > 0; o >>= 1) tend = max(tend, (unsigned long long)__shfl_xor(tend, o));
