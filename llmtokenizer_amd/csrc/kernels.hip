@@ -2010,9 +2010,11 @@ __global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, co
     const uint32_t A = E->A, AA = A * A;
     const uint32_t t = blockIdx.x;
     for (uint32_t x = threadIdx.x; x < 256; x += SORT_T) rk[x] = E->rank[x];
-    if (threadIdx.x < A) {
+    if (threadIdx.x < A) {  // (independent loads: unrolled so they are in flight together)
         uint32_t s0 = E->poff[threadIdx.x * A];
-        for (uint32_t k2 = 0; k2 < A; k2++) s0 += hist[(uint64_t)t * AA + threadIdx.x * A + k2];
+        const uint32_t *hr = hist + (uint64_t)t * AA + threadIdx.x * A;
+#pragma unroll 16
+        for (uint32_t k2 = 0; k2 < A; k2++) s0 += hr[k2];
         L.gcur[threadIdx.x] = s0;
     }
     __syncthreads();
@@ -2046,20 +2048,37 @@ __global__ __launch_bounds__(SORT_T) void k_sort_b(const Eng *__restrict__ E, co
     __shared__ uint32_t range[2];
     const uint32_t A = E->A, AA = A * A;
     constexpr uint32_t LOCAL = (1u << SORT_LOCAL_BITS) - 1;
-    for (uint32_t u = blockIdx.x; u < ntl * A; u += gridDim.x) {
-        const uint32_t t = u / A, k1 = u % A;
+    // a unit's set-up words (thread k2 < A: its bin's count before tile t, the
+    // bin's plist offset, its count in tile t; every thread: the k1 group's
+    // offset), loaded one unit ahead so their round trip overlaps the chunks
+    const uint32_t nu = ntl * A;
+    uint32_t nb = 0, np = 0, nc = 0, ng = 0;
+    auto prefetch = [&](uint32_t u) {
+        if (u >= nu) return;
+        const uint32_t t = u / A, k1 = u % A, k2 = threadIdx.x;
+        ng = E->poff[k1 * A];
+        if (k2 < A) {
+            nb = hist[(uint64_t)t * AA + k1 * A + k2];
+            np = E->poff[k1 * A + k2];
+            nc = tile_count(hist, tot, t, ntl, AA, k1 * A + k2);
+        }
+    };
+    prefetch(blockIdx.x);
+    for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
+        const uint32_t t = u / A;
         const uint32_t tbase = (uint32_t)((uint64_t)t * tile);  // positions are u32 (n0 <= 2^32 - 2)
+        const uint32_t before = nb, pk = np, cnt = nc, g0 = ng;
         __syncthreads();
-        if (threadIdx.x == 0) { range[0] = E->poff[k1 * A]; range[1] = 0; }
+        if (threadIdx.x == 0) { range[0] = g0; range[1] = 0; }
         __syncthreads();
-        for (uint32_t k2 = threadIdx.x; k2 < A; k2 += SORT_T) {
-            const uint32_t before = hist[(uint64_t)t * AA + k1 * A + k2];
-            L.gcur[k2] = E->poff[k1 * A + k2] + before;
+        if (threadIdx.x < A) {
+            L.gcur[threadIdx.x] = pk + before;
             atomicAdd(&range[0], before);
-            atomicAdd(&range[1], tile_count(hist, tot, t, ntl, AA, k1 * A + k2));
+            atomicAdd(&range[1], cnt);
         }
         __syncthreads();
         const uint32_t lo = range[0], n = range[1];
+        prefetch(u + gridDim.x);
         for (uint32_t q0 = 0; q0 < n; q0 += SORT_CH) {
             uint32_t bins[SORT_PER], vals[SORT_PER];
 #pragma unroll
