@@ -31,7 +31,10 @@ The JSON line also carries
                   timed on this host on a bounded sample (rank 0, N=1 only).
 """
 import argparse
+import csv
+import glob
 import json
+import re
 import os
 import subprocess
 import sys
@@ -289,6 +292,21 @@ def main():
                                           "table_grows", "keys", "l1_rescanned", "spec_hits",
                                           "spec_misses")},
     }
+    # the committed rocprofv3 --kernel-trace --stats summary of this command
+    # (profiles/): its per-launch average includes dispatch and completion
+    # signalling, which the in-kernel span (first block entry -> last block
+    # exit) does not; both are reported
+    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r1_v*_train_kernel_stats.csv")),
+                  key=lambda p: int(re.search(r"_v(\d+)_", p).group(1)))
+    if prof:
+        with open(prof[-1]) as f:
+            for r in csv.DictReader(f):
+                if r["Name"].split("(")[0].replace("bpeamd::", "").replace("void ", "").strip() == name:
+                    rp_ms = float(r["AverageNs"]) / 1e6
+                    out["roofline"]["avg_ms_rocprof"] = round(rp_ms, 5)
+                    out["roofline"]["frac_at_rocprof_avg"] = round(kbytes / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                    out["roofline"]["rocprof_summary"] = os.path.relpath(prof[-1], ROOT)
+                    break
     # HBM traffic per launch from the committed rocprofv3 PMC passes
     # (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE in separate runs)
     pmc = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")

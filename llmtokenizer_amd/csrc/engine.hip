@@ -326,7 +326,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.nshards = c->nshards;
     const uint64_t n0 = c->n0;
     int r;
-    if ((r = dalloc(c, &h.tok, n0 + 32, false))) return r;  // + 32: k_scan's token windows (TokWinW)
+    if ((r = dalloc(c, &h.tok, n0 + 8, false))) return r;  // + 8: k_scan's 2x16-byte windows
     if ((r = dalloc(c, &h.dist, n0, false))) return r;  // read only where written (left_start)
     if ((r = dalloc(c, &h.tlen, h.vcap))) return r;
     if ((r = dalloc(c, &h.rank, 256))) return r;
