@@ -954,7 +954,8 @@ void print_timeline(bpe_gpu_ctx *c, uint32_t zlast) {
     static const char *nm[TS_N] = {"K1 first in", "K1 rescan out", "K1 scan out", "K2 first in",
                                    "K2 select out", "K2 applyA out", "K2 applyB out", "K1 last in",
                                    "scan cands done", "scan list flushed", "scan deltas flushed",
-                                   "B deltas loaded", "B table updated", "B marks listed"};
+                                   "B deltas loaded", "B table updated", "B marks listed",
+                                   "B last insert done", "B last find done"};
     for (uint32_t z = 257; z < zlast && z < TS_SLOTS; z++) {
         const unsigned long long *r = &t[(size_t)z * TS_N];
         bool ok = true;

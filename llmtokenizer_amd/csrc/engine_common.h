@@ -32,7 +32,7 @@ constexpr uint32_t TS_SLOTS = 4096;      // merges kept by the debug block timel
 // debug timeline slots (wall clock; entries stored complemented so that
 // atomicMax keeps the earliest): K1 = k_rescan_spec, K2 = k_fused
 enum { TS_K1_IN = 0, TS_K1_RESCAN, TS_K1_SCAN, TS_K2_IN, TS_K2_SELECT, TS_K2_APPLY_A, TS_K2_APPLY_B, TS_K1_LASTIN,
-       TS_S_CAND, TS_S_LIST, TS_S_DELTA, TS_B_DVAL, TS_B_TABLE, TS_B_MARKS, TS_N };
+       TS_S_CAND, TS_S_LIST, TS_S_DELTA, TS_B_DVAL, TS_B_TABLE, TS_B_MARKS, TS_B_PROBE, TS_B_COUNT, TS_N };
 
 enum { V_DL = 0, V_DR = 1, V_IL = 2, V_IR = 3 };
 
@@ -113,7 +113,7 @@ struct Eng {
     uint32_t *ids_out;    // compaction output
     uint32_t *aux;        // per-slot scratch for the resolver (first thread)
     unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
-    unsigned long long *dbgts;      // [TS_SLOTS][8] per-merge block timeline (BPE_DEBUG_TS) or null
+    unsigned long long *dbgts;      // [TS_SLOTS][TS_N] per-merge block timeline (BPE_DEBUG_TS) or null
     uint32_t fast;        // 1: schedule-free tie rule everywhere (no tracking)
     uint32_t spec_on;     // 1: one-shard training with the speculative next-merge scan
     uint32_t scan_blocks; // k_scan grid (entries of scan_tend)

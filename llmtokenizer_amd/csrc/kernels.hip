@@ -543,6 +543,33 @@ __device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v,
     return ~0ull;  // table full: callers flag STOP_ERROR
 }
 
+// hinsert for apply role B: *fresh = the key took an empty slot (its count
+// is 0), with that slot's level-1 runner-up loaded beside the CAS in *bv2;
+// inserted keys counted in *nins
+__device__ inline uint64_t hinsert_b(const Eng *E, uint32_t u, uint32_t v, uint32_t *nins, bool *fresh,
+                                     unsigned long long *bv2) {
+    const unsigned long long key = (((unsigned long long)u << 32) | v) + 1ull;
+    const uint64_t m = E->hcap - 1;
+    uint64_t s = mix64(key) & m;
+    for (uint64_t p = 0; p <= m; p++) {
+        const unsigned long long k = __hip_atomic_load(&E->hkey[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == key) return s;
+        if (k == 0) {
+            const unsigned long long b2 = E->l1v2[s / L1W];
+            const unsigned long long prev = atomicCAS(&E->hkey[s], 0ull, key);
+            if (prev == 0) {
+                *nins += 1;
+                *fresh = true;
+                *bv2 = b2;
+                return s;
+            }
+            if (prev == key) return s;
+        }
+        s = (s + 1) & m;
+    }
+    return ~0ull;  // table full: callers flag STOP_ERROR
+}
+
 // candidate list of pair (u, v): mode 0 the byte pair's position list, 1 / 2
 // the occurrence list of the later-created id (filtered by its tags)
 __device__ inline void cand_of(const Eng *E, uint32_t u, uint32_t v, bool valid, const uint32_t *rank,
@@ -676,6 +703,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     __syncthreads();
     long long dD = 0;
     uint32_t nins = 0;  // keys this thread inserted
+    unsigned long long tprobe = 0, tcount = 0;  // debug timeline (BPE_DEBUG_TS)
     const uint32_t base0 = (bid - roleA_blocks) * blockDim.x;
     for (uint32_t t0 = base0; t0 < total; t0 += stride) {  // uniform trip count per block
         const uint32_t t = t0 + threadIdx.x;
@@ -728,13 +756,19 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
             if (u == a && v == b) d -= Rg;
             if (UNDO) d = -d;
             if (d != 0) {
-                const uint64_t slot = d > 0 ? hinsert(E, C, u, v, &nins) : hfind(E, u, v);
+                // a key inserted into a fresh slot has count 0 and brings its
+                // block's summary runner-up along with the CAS: no load after it
+                bool fresh = false;
+                unsigned long long fbv2 = 0;
+                const uint64_t slot = d > 0 ? hinsert_b(E, u, v, &nins, &fresh, &fbv2) : hfind(E, u, v);
+                if (!UNDO && E->dbgts) (d > 0 ? tprobe : tcount) = wall_clock64();  // (debug: insert / find)
                 if (slot == ~0ull) {
                     C->err = d > 0 ? 2 : 1;  // k_select stops on it
                 } else {
                     blk = (uint32_t)(slot / L1W);
-                    const uint32_t old = E->hcnt[slot];
-                    const unsigned long long bv2 = E->l1v2[blk];  // loaded beside the count
+                    const uint32_t old = fresh ? 0u : E->hcnt[slot];
+                    const unsigned long long bv2 = fresh ? fbv2 : E->l1v2[blk];  // loaded beside the count
+
                     const uint32_t nw = (uint32_t)((long long)old + d);
                     E->hcnt[slot] = nw;
                     dD += (long long)(nw != 0) - (long long)(old != 0);
@@ -750,6 +784,18 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
         if (mark) marks[p] = blk;
         __syncthreads();
         if (!UNDO) ts_mark(E, z - 1, TS_B_TABLE, false, true);
+        if (!UNDO && E->dbgts) {  // the block's latest probe / count load
+            __shared__ unsigned long long tp, tc;
+            if (threadIdx.x == 0) tp = tc = 0;
+            __syncthreads();
+            if (tprobe) atomicMax(&tp, tprobe);
+            if (tcount) atomicMax(&tc, tcount);
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                if (tp) atomicMax(&E->dbgts[(uint64_t)((z - 1) % TS_SLOTS) * TS_N + TS_B_PROBE], tp);
+                if (tc) atomicMax(&E->dbgts[(uint64_t)((z - 1) % TS_SLOTS) * TS_N + TS_B_COUNT], tc);
+            }
+        }
         if (nmark > MARK_CAP - blockDim.x || t0 + stride >= total) {
             if (threadIdx.x == 0) mbase = nmark ? atomicAdd(&C->nl1p[P], nmark) : 0;
             __syncthreads();
