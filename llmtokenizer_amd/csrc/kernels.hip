@@ -551,20 +551,18 @@ __device__ inline uint64_t hinsert_b(const Eng *E, uint32_t u, uint32_t v, uint3
     const unsigned long long key = (((unsigned long long)u << 32) | v) + 1ull;
     const uint64_t m = E->hcap - 1;
     uint64_t s = mix64(key) & m;
+    // CAS walk: each probe is one round trip (the CAS returns the slot's key),
+    // not a load followed by a CAS -- role B's keys with d > 0 are new ones
     for (uint64_t p = 0; p <= m; p++) {
-        const unsigned long long k = __hip_atomic_load(&E->hkey[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == key) return s;
-        if (k == 0) {
-            const unsigned long long b2 = E->l1v2[s / L1W];
-            const unsigned long long prev = atomicCAS(&E->hkey[s], 0ull, key);
-            if (prev == 0) {
-                *nins += 1;
-                *fresh = true;
-                *bv2 = b2;
-                return s;
-            }
-            if (prev == key) return s;
+        const unsigned long long b2 = E->l1v2[s / L1W];
+        const unsigned long long prev = atomicCAS(&E->hkey[s], 0ull, key);
+        if (prev == 0) {
+            *nins += 1;
+            *fresh = true;
+            *bv2 = b2;
+            return s;
         }
+        if (prev == key) return s;
         s = (s + 1) & m;
     }
     return ~0ull;  // table full: callers flag STOP_ERROR
