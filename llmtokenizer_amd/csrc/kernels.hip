@@ -543,6 +543,33 @@ __device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v,
     return ~0ull;  // table full: callers flag STOP_ERROR
 }
 
+// hfind for apply role B: the home slot's key, count and level-1 runner-up
+// in one round trip (*hit: found there, *cnt / *bv2 valid)
+__device__ inline uint64_t hfind_b(const Eng *E, uint32_t u, uint32_t v, bool *hit, uint32_t *cnt,
+                                   unsigned long long *bv2) {
+    const unsigned long long key = (((unsigned long long)u << 32) | v) + 1ull;
+    const uint64_t m = E->hcap - 1;
+    const uint64_t s0 = mix64(key) & m;
+    const unsigned long long k0 = E->hkey[s0];
+    const uint32_t c0 = E->hcnt[s0];
+    const unsigned long long b0 = E->l1v2[s0 / L1W];
+    if (k0 == key) {
+        *hit = true;
+        *cnt = c0;
+        *bv2 = b0;
+        return s0;
+    }
+    if (k0 == 0) return ~0ull;
+    uint64_t s = (s0 + 1) & m;
+    for (uint64_t p = 1; p <= m; p++) {
+        const unsigned long long k = E->hkey[s];
+        if (k == key) return s;
+        if (k == 0) return ~0ull;
+        s = (s + 1) & m;
+    }
+    return ~0ull;
+}
+
 // hinsert for apply role B: *fresh = the key took an empty slot (its count
 // is 0), with that slot's level-1 runner-up loaded beside the CAS in *bv2;
 // inserted keys counted in *nins
@@ -756,15 +783,16 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
             if (d != 0) {
                 // a key inserted into a fresh slot has count 0 and brings its
                 // block's summary runner-up along with the CAS: no load after it
-                bool fresh = false;
+                bool fresh = false;  // count and runner-up already in fold / fbv2
+                uint32_t fold = 0;
                 unsigned long long fbv2 = 0;
-                const uint64_t slot = d > 0 ? hinsert_b(E, u, v, &nins, &fresh, &fbv2) : hfind(E, u, v);
+                const uint64_t slot = d > 0 ? hinsert_b(E, u, v, &nins, &fresh, &fbv2) : hfind_b(E, u, v, &fresh, &fold, &fbv2);
                 if (!UNDO && E->dbgts) (d > 0 ? tprobe : tcount) = wall_clock64();  // (debug: insert / find)
                 if (slot == ~0ull) {
                     C->err = d > 0 ? 2 : 1;  // k_select stops on it
                 } else {
                     blk = (uint32_t)(slot / L1W);
-                    const uint32_t old = fresh ? 0u : E->hcnt[slot];
+                    const uint32_t old = fresh ? fold : E->hcnt[slot];
                     const unsigned long long bv2 = fresh ? fbv2 : E->l1v2[blk];  // loaded beside the count
 
                     const uint32_t nw = (uint32_t)((long long)old + d);
