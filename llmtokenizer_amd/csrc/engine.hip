@@ -72,6 +72,7 @@ constexpr uint32_t ENC_APPLY_BLOCKS = 1024;
 uint32_t SPEC_RB = 64, SPEC_SB = 192;
 uint32_t FUSED_A = 64, FUSED_B = 16;  // k_fused apply blocks (1024 threads): span rewrite, table update
 bool SPEC_ON = true;
+bool PIPE_ON = !getenv("BPE_PIPE") || atoi(getenv("BPE_PIPE")) != 0;  // pipelined graph replays (drive)
 struct SpecInit {
     SpecInit() {
         if (const char *e = getenv("BPE_SPEC")) SPEC_ON = atoi(e) != 0;
@@ -215,6 +216,8 @@ struct bpe_gpu_ctx {
     Eng *dE = nullptr;
     Ctl *dC = nullptr;
     Ctl *hC = nullptr;  // pinned
+    volatile uint32_t *hprobe = nullptr;  // pinned, device-mapped (Eng::hprobe)
+    hipEvent_t ev_probe[2] = {};          // after each queued graph (pipelined drive)
     uint64_t n0 = 0;
     bool loaded = false;
     bool ids_ready = false;
@@ -850,6 +853,28 @@ struct Resolver {
     }
 };
 
+// Replays of the speculative graph with the next replay already queued
+// behind the running one, so the device never waits for the host between
+// graphs.  The host learns of a stop from the probe k_select writes when it
+// stops (Eng::hprobe); a replay queued behind a stop finds the stop set and
+// every kernel in it exits at once.  Returns with the stream still busy (the
+// caller's pull_ctl synchronises).  Nothing is queued past the merge cap.
+int replay_pipelined(bpe_gpu_ctx *c, hipGraphExec_t g, uint64_t merges_done) {
+    *c->hprobe = STOP_NONE;  // the stream is idle here (the caller pulled the control block)
+    HIPCHK(hipGraphLaunch(g, c->st));
+    uint64_t queued = merges_done + ITERS_PER_GRAPH;  // merges done once the queued replays end (at most)
+    for (int q = 0;; q ^= 1) {
+        HIPCHK(hipEventRecord(c->ev_probe[q], c->st));
+        const bool ahead = queued < c->h.mcap;
+        if (ahead) {
+            HIPCHK(hipGraphLaunch(g, c->st));
+            queued += ITERS_PER_GRAPH;
+        }
+        HIPCHK(hipEventSynchronize(c->ev_probe[q]));
+        if (*c->hprobe != STOP_NONE || !ahead) return 0;
+    }
+}
+
 int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
     int r;
     Resolver res{c};
@@ -893,6 +918,10 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
                 last_graph = tracked ? 1 : 0;
                 if (!tracked && c->h.spec_on && need_scan) launch_redo(c);
                 need_scan = false;
+                if (!tracked && c->h.spec_on && !c->profile && PIPE_ON) {
+                    if ((r = replay_pipelined(c, *g, C.merges_done))) return r;
+                    break;
+                }
             }
             HIPCHK(hipGraphLaunch(*g, c->st));
             break;
@@ -1132,6 +1161,12 @@ int ctx_new(int device, hipStream_t shared, bpe_gpu_ctx **out) {
     HIPCHK(hipMalloc(&c->dC, sizeof(Ctl)));
     HIPCHK(hipHostMalloc(&c->hC, sizeof(Ctl), hipHostMallocDefault));
     memset(&c->h, 0, sizeof(Eng));
+    uint32_t *probe = nullptr;
+    HIPCHK(hipHostMalloc(&probe, 64, hipHostMallocMapped));
+    *probe = 0;
+    c->hprobe = probe;
+    HIPCHK(hipHostGetDevicePointer((void **)&c->h.hprobe, probe, 0));
+    for (auto &e : c->ev_probe) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     *out = c;
     return 0;
 }
@@ -1184,6 +1219,9 @@ void bpe_gpu_destroy(bpe_gpu_ctx *c) {
     if (c->dE) hipFree(c->dE);
     if (c->dC) hipFree(c->dC);
     if (c->hC) hipHostFree(c->hC);
+    if (c->hprobe) hipHostFree((void *)c->hprobe);
+    for (auto &e : c->ev_probe)
+        if (e) (void)hipEventDestroy(e);
     if (c->d_enc_pairs) hipFree(c->d_enc_pairs);
     for (auto &a : c->ev)
         for (auto &b : a)

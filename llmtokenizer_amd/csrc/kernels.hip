@@ -1378,6 +1378,10 @@ __device__ __forceinline__ void select_block(const Eng *__restrict__ E, Ctl *__r
     }
     __syncthreads();
     for (uint32_t x = tid; x < CTL_SELECT_WORDS; x += blockDim.x) cgw[x] = scw[x];
+    if (tid == 0 && sc.stop != STOP_NONE && E->hprobe) {  // once per stop: tell the host
+        __hip_atomic_store(E->hprobe, sc.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
 }
 
 __global__ __launch_bounds__(1024) void k_select(const Eng *__restrict__ E, Ctl *__restrict__ Cg, uint32_t graph) {

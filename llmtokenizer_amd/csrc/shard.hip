@@ -301,7 +301,9 @@ int drive_group(bpe_gpu_group *g) {
                 g->eager = true;
                 (void)hipGetLastError();
             }
-            if (g->graph) {
+            if (g->graph && fused && PIPE_ON) {
+                if ((r = replay_pipelined(g->cs[0], g->graph, C0.merges_done))) return r;
+            } else if (g->graph) {
                 HIPCHK(hipGraphLaunch(g->graph, g->st));
             } else {
                 for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++)
