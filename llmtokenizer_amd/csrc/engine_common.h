@@ -199,34 +199,52 @@ struct Halo {
     uint32_t HL[3], HR[3], hlrun, myidx;
 };
 
-__host__ __device__ inline void shard_halo(const uint32_t *rec, uint32_t nshards, uint32_t me, uint32_t a, Halo *h) {
+// 3-entry arrays indexed by value through selects only, so that a Halo kept
+// in registers stays there (a dynamic index puts it in scratch memory, and a
+// kernel with scratch dispatches its waves measurably later)
+__host__ __device__ inline void put3(uint32_t *A, uint32_t m, uint32_t v) {
+    A[0] = m == 0 ? v : A[0];
+    A[1] = m == 1 ? v : A[1];
+    A[2] = m == 2 ? v : A[2];
+}
+__host__ __device__ inline uint32_t get3(const uint32_t *A, uint32_t m) { return m == 0 ? A[0] : m == 1 ? A[1] : A[2]; }
+
+// ld(p) reads one record word (device: plain, or an L1/L2-coherent load when
+// the records were just published inside the same kernel)
+template <typename Ld>
+__host__ __device__ inline void shard_halo_ld(const uint32_t *rec, uint32_t nshards, uint32_t me, uint32_t a, Halo *h,
+                                              Ld ld) {
     for (int m = 0; m < 3; m++) h->HL[m] = h->HR[m] = 0xFFFFFFFFu;
     uint32_t m = 0;
     for (int s = (int)me - 1; s >= 0 && m < 3; s--) {
         const uint32_t *r = rec + (uint64_t)s * EDGE_WORDS;
-        const uint32_t c = r[ER_CNT] < 3 ? r[ER_CNT] : 3;
-        for (uint32_t t = 0; t < c && m < 3; t++) h->HL[m++] = r[ER_L + t];
+        const uint32_t c0 = ld(r + ER_CNT), c = c0 < 3 ? c0 : 3;
+        for (uint32_t t = 0; t < c && m < 3; t++) put3(h->HL, m++, ld(r + ER_L + t));
     }
     m = 0;
     for (uint32_t s = me + 1; s < nshards && m < 3; s++) {
         const uint32_t *r = rec + (uint64_t)s * EDGE_WORDS;
-        const uint32_t c = r[ER_CNT] < 3 ? r[ER_CNT] : 3;
-        for (uint32_t t = 0; t < c && m < 3; t++) h->HR[m++] = r[ER_F + t];
+        const uint32_t c0 = ld(r + ER_CNT), c = c0 < 3 ? c0 : 3;
+        for (uint32_t t = 0; t < c && m < 3; t++) put3(h->HR, m++, ld(r + ER_F + t));
     }
     // a==b runs that cross shard edges: how many a's precede my first token
     uint64_t run = 0;
     for (int s = (int)me - 1; s >= 0; s--) {
         const uint32_t *r = rec + (uint64_t)s * EDGE_WORDS;
-        if (r[ER_CNT] == 0) continue;
-        if (r[ER_L] != a) break;
-        run += r[ER_TRAIL];
-        if (!r[ER_ALL]) break;
+        if (ld(r + ER_CNT) == 0) continue;
+        if (ld(r + ER_L) != a) break;
+        run += ld(r + ER_TRAIL);
+        if (!ld(r + ER_ALL)) break;
     }
     h->hlrun = run > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)run;
     const uint32_t *r = rec + (uint64_t)me * EDGE_WORDS;
     uint64_t idx = 0;
-    if (r[ER_CNT] && r[ER_L] == a) idx = (uint64_t)r[ER_TRAIL] - 1 + (r[ER_ALL] ? run : 0);
+    if (ld(r + ER_CNT) && ld(r + ER_L) == a) idx = (uint64_t)ld(r + ER_TRAIL) - 1 + (ld(r + ER_ALL) ? run : 0);
     h->myidx = idx > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)idx;
+}
+
+__host__ __device__ inline void shard_halo(const uint32_t *rec, uint32_t nshards, uint32_t me, uint32_t a, Halo *h) {
+    shard_halo_ld(rec, nshards, me, a, h, [](const uint32_t *q) { return *q; });
 }
 
 __host__ __device__ inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }

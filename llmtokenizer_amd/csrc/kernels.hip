@@ -29,6 +29,9 @@ __device__ inline uint32_t lane_id() { return __lane_id(); }
 __device__ inline uint32_t aload(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ inline void astore(uint32_t *p, uint32_t v) {  // global_store sc1 (write-through to memory)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ inline unsigned long long aload64(const unsigned long long *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -44,6 +47,11 @@ __device__ inline uint32_t wave_append(bool pred, uint32_t *counter) {
     base = __shfl(base, leader);
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
+
+// a word of the sharded deltas: from a P2P mailbox (X) with a system-coherent
+// load (the pushes are system-coherent stores; no acquire fence), else from
+// the local exchange buffer (written before the kernel boundary)
+__device__ inline uint32_t xld(const P2P *X, const uint32_t *p) { return X ? sys_load(p) : *p; }
 
 // the sharded exchange buffer of delta parity P
 __device__ inline uint32_t *xbufp(const Eng *E, uint32_t P) { return E->xbuf + (uint64_t)P * E->xstride; }
@@ -100,7 +108,6 @@ __device__ inline void wait_records(const Eng *E, Ctl *C) {
         }
         __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 struct LazyHalo {
@@ -112,8 +119,12 @@ struct LazyHalo {
     Halo h;
     __device__ inline const Halo &get() {  // sharded contexts only (E->erec)
         if (!ready) {
-            if (wait) wait_records(E, C);
-            shard_halo(E->erec, E->nshards, E->shard, a, &h);
+            if (wait) {  // records published in this kernel: L2-coherent loads, no acquire fence
+                wait_records(E, C);
+                shard_halo_ld(E->erec, E->nshards, E->shard, a, &h, [](const uint32_t *q) { return aload(q); });
+            } else {
+                shard_halo(E->erec, E->nshards, E->shard, a, &h);
+            }
             ready = true;
         }
         return h;
@@ -122,8 +133,8 @@ struct LazyHalo {
 
 template <bool SH, typename HaloT>
 __device__ inline uint32_t id_at(const uint32_t *__restrict__ tok, HaloT &h, int64_t p, int64_t n) {
-    if (p < 0) return SH && p >= -3 ? h.get().HL[-1 - p] : HOLE;
-    if (p >= n) return SH && p - n < 3 ? h.get().HR[p - n] : HOLE;
+    if (p < 0) return SH && p >= -3 ? get3(h.get().HL, (uint32_t)(-1 - p)) : HOLE;
+    if (p >= n) return SH && p - n < 3 ? get3(h.get().HR, (uint32_t)(p - n)) : HOLE;
     return tok[p];
 }
 
@@ -710,7 +721,6 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
         const uint32_t seq = C->nx_seq0;  // the push k_fused_sh's block 1 makes
         const unsigned long long t0 = wall_clock64();
         if (threadIdx.x < X->W) p2p_wait(X, X->mb[X->rank] + MB_FLAG0 + 16 * threadIdx.x, seq, t0);
-        if (X->fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         __syncthreads();
         XW = X->W;
         xc0 = X->c0;
@@ -719,7 +729,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     uint32_t Rg = R;  // occurrences over all shards
     if (sh) {
         Rg = 0;
-        for (uint32_t r = 0; r < XW; r++) Rg += xbP[(uint64_t)r * xc0 + 4 * E->vcap];
+        for (uint32_t r = 0; r < XW; r++) Rg += xld(X, xbP + (uint64_t)r * xc0 + 4 * E->vcap);
     }
     if (!UNDO && sh && bid == roleA_blocks && threadIdx.x == 0) C->Rgp[P] = Rg;  // for k_select (xbuf is cleared)
     __shared__ uint32_t marks[MARK_CAP];
@@ -758,10 +768,10 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
         if (cat >= 0 && sh) {
             const uint32_t *xb = xbP, vc = E->vcap;
             for (uint32_t r = 0; r < XW; r++, xb += xc0) {  // (one pass: XW == 1)
-                vdr += u == b && v < vc ? xb[V_DR * vc + v] : 0;
-                vdl += v == a && u < vc ? xb[V_DL * vc + u] : 0;
-                vir += u == z && v < vc ? xb[V_IR * vc + v] : 0;
-                vil += v == z && u < vc ? xb[V_IL * vc + u] : 0;
+                vdr += u == b && v < vc ? xld(X, xb + V_DR * vc + v) : 0;
+                vdl += v == a && u < vc ? xld(X, xb + V_DL * vc + u) : 0;
+                vir += u == z && v < vc ? xld(X, xb + V_IR * vc + v) : 0;
+                vil += v == z && u < vc ? xld(X, xb + V_IL * vc + u) : 0;
             }
         } else if (cat >= 0) {
             vdr = u == b ? dval(E, P, V_DR, v) : 0;
@@ -1080,10 +1090,13 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec_sh(const Eng *__restrict
         C->nx_live = !S.stop;
     }
     if (S.stop) return;
+    ts_mark(E, S.z, TS_K1_IN, true);
+    ts_mark(E, S.z, TS_K1_LASTIN, false);
     const uint32_t nscan = gridDim.x - rblocks;  // scan blocks, the edge block included
     if (blockIdx.x == 0) {
         if (S.spec) {
             scan_body<true, true, true>(E, C, S, nscan - 1, nscan, X);
+            ts_mark(E, S.z, TS_K1_SCAN, false);
         } else {
             records_pull_block(E, C, X);
             scan_exit_stamp(E, 0);
@@ -1091,8 +1104,10 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec_sh(const Eng *__restrict
     } else if (blockIdx.x <= rblocks) {
         rescan1_body(E, C, S, blockIdx.x - 1, rblocks);
         scan_exit_stamp(E, blockIdx.x);
+        ts_mark(E, S.z, TS_K1_RESCAN, false);
     } else if (S.spec) {
         scan_body<true, true, true>(E, C, S, blockIdx.x - 1 - rblocks, nscan, X);
+        ts_mark(E, S.z, TS_K1_SCAN, false);
     } else {
         scan_exit_stamp(E, blockIdx.x);
     }
@@ -1425,7 +1440,10 @@ __global__ __launch_bounds__(1024) void k_fused_sh(const Eng *__restrict__ E, Ct
                                                    const P2P *__restrict__ X) {
     const uint32_t nap = gridDim.x - 3;  // apply blocks
     if (blockIdx.x == 0) {
+        const uint32_t z0 = C->z;  // the current merge (select moves on)
+        ts_mark(E, z0, TS_K2_IN, true);
         select_block(E, C, SEL_FUSED);
+        ts_mark(E, z0, TS_K2_SELECT, false);
         return;
     }
     if (!C->nx_live) return;  // K1 saw a stop: nothing was scanned or pulled
@@ -1441,7 +1459,9 @@ __global__ __launch_bounds__(1024) void k_fused_sh(const Eng *__restrict__ E, Ct
     if (!valid) return;
     const Snap S = snap_next(C);
     const uint32_t bid = blockIdx.x - 2;
+    ts_mark(E, S.z - 1, TS_K2_IN, true);
     apply_body<false>(E, C, S, bid, nap, roleA_blocks, X);
+    ts_mark(E, S.z - 1, bid < roleA_blocks ? TS_K2_APPLY_A : TS_K2_APPLY_B, false);
     if (bid < roleA_blocks) {  // spans written: the record block may read them
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1595,14 +1615,14 @@ __device__ void records_pull_block(const Eng *__restrict__ E, Ctl *__restrict__ 
     if (tid < W) p2p_wait(X, X->mb[me] + MB_FLAG1 + 16 * tid, seq, t0);
     if (X->fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     __syncthreads();
+    // system-coherent loads of the mailbox, L2-coherent (sc1) stores of erec
+    // drained before the flag: the other blocks read erec with sc1 loads, so
+    // no release / acquire fence (no L2 write-back or invalidate) is needed
     const uint32_t *src = X->mb[me] + MB_DATA1 + (uint64_t)par * P2P_MAXR * EDGE_WORDS;
-    if (tid < W * EDGE_WORDS) E->erec[tid] = src[tid];
+    if (tid < W * EDGE_WORDS) astore(E->erec + tid, sys_load(src + tid));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(&C->erec_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (tid == 0) __hip_atomic_store(&C->erec_ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Fused sharded step, k_fused_sh block 1: the deltas K1 accumulated in buf
@@ -1614,11 +1634,13 @@ __device__ void push_exchange_block(const P2P *__restrict__ X, const uint32_t *_
     const uint32_t W = X->W, me = X->rank, c0 = X->c0, tid = threadIdx.x, T = blockDim.x;
     const uint32_t par = seq & 1u;
     const uint32_t nv = count / 4;
-    for (uint32_t p = 0; p < W; p++) {
-        uint32_t *dst = X->mb[p] + MB_DATA0 + ((uint64_t)par * W + me) * c0;
-        for (uint32_t i = tid; i < nv; i += T)
-            reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(buf)[i];
-        for (uint32_t i = nv * 4 + tid; i < count; i += T) dst[i] = buf[i];
+    for (uint32_t i = tid; i < nv; i += T) {
+        const uint4 v = reinterpret_cast<const uint4 *>(buf)[i];
+        for (uint32_t p = 0; p < W; p++) sys_store4(X->mb[p] + MB_DATA0 + ((uint64_t)par * W + me) * c0 + 4 * i, v);
+    }
+    for (uint32_t i = nv * 4 + tid; i < count; i += T) {
+        const uint32_t v = buf[i];
+        for (uint32_t p = 0; p < W; p++) sys_store(X->mb[p] + MB_DATA0 + ((uint64_t)par * W + me) * c0 + i, v);
     }
     p2p_release_point();
     if (tid == 0) {
@@ -1655,7 +1677,7 @@ __device__ void records_push_block(const Eng *__restrict__ E, Ctl *__restrict__ 
     const uint32_t seq = X->xs[XS_SEQ1] + 1u, par = seq & 1u;
     if (tid < W * EDGE_WORDS) {
         const uint32_t p = tid / EDGE_WORDS, w = tid % EDGE_WORDS;
-        X->mb[p][MB_DATA1 + ((uint64_t)par * P2P_MAXR + me) * EDGE_WORDS + w] = rec[w];
+        sys_store(X->mb[p] + MB_DATA1 + ((uint64_t)par * P2P_MAXR + me) * EDGE_WORDS + w, rec[w]);
     }
     if (tid < EDGE_WORDS) E->myrec[tid] = rec[tid];
     p2p_release_point();

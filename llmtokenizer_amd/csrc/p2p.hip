@@ -46,6 +46,21 @@ __device__ inline uint32_t sys_load(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// system-coherent stores (global_store sc0 sc1: written through every cache
+// level, to the local or a peer's HBM): the mailbox payload is stored this way
+// and drained before the flag, and read back with sys_load, so the exchange
+// needs no system-scope release / acquire fence (a fence writes back or
+// invalidates the whole L2 of the XCD it runs on); P2P::fence adds them back
+__device__ inline void sys_store(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline void sys_store4(uint32_t *p, const uint4 &v) {
+    sys_store(p, v.x);
+    sys_store(p + 1, v.y);
+    sys_store(p + 2, v.z);
+    sys_store(p + 3, v.w);
+}
+
 // spin until *p reached want (wrapping compare); false (+ error words) on timeout
 __device__ inline bool p2p_wait(const P2P *X, const uint32_t *p, uint32_t want, unsigned long long t0) {
     while ((int32_t)(sys_load(p) - want) < 0) {
@@ -75,9 +90,8 @@ __global__ __launch_bounds__(256) void k_p2p_sum(const P2P *__restrict__ X, uint
     const uint32_t p = (me + blockIdx.x) % W;
     uint32_t *dst = X->mb[p] + MB_DATA0 + ((uint64_t)par * W + me) * c0;
     const uint32_t nv = count / 4;
-    for (uint32_t i = tid; i < nv; i += blockDim.x)
-        reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(buf)[i];
-    for (uint32_t i = nv * 4 + tid; i < count; i += blockDim.x) dst[i] = buf[i];
+    for (uint32_t i = tid; i < nv; i += blockDim.x) sys_store4(dst + 4 * i, reinterpret_cast<const uint4 *>(buf)[i]);
+    for (uint32_t i = nv * 4 + tid; i < count; i += blockDim.x) sys_store(dst + i, buf[i]);
     p2p_release_point();
     if (tid == 0) {
         if (X->fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
@@ -97,14 +111,14 @@ __global__ __launch_bounds__(256) void k_p2p_sum(const P2P *__restrict__ X, uint
     for (uint32_t i = lo + 4 * tid; i < hv; i += 4 * blockDim.x) {
         uint4 s = make_uint4(0, 0, 0, 0);
         for (uint32_t r = 0; r < W; r++) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(src + (uint64_t)r * c0 + i);
-            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            const uint32_t *q = src + (uint64_t)r * c0 + i;
+            s.x += sys_load(q); s.y += sys_load(q + 1); s.z += sys_load(q + 2); s.w += sys_load(q + 3);
         }
         *reinterpret_cast<uint4 *>(buf + i) = s;
     }
     for (uint32_t i = hv + tid; i < hi; i += blockDim.x) {
         uint32_t s = 0;
-        for (uint32_t r = 0; r < W; r++) s += src[(uint64_t)r * c0 + i];
+        for (uint32_t r = 0; r < W; r++) s += sys_load(src + (uint64_t)r * c0 + i);
         buf[i] = s;
     }
     // every block read seq before it pushed; block 0 passed the push count
@@ -118,7 +132,7 @@ __global__ __launch_bounds__(64) void k_p2p_gather(const P2P *__restrict__ X, co
     const uint32_t seq = X->xs[XS_SEQ1] + 1u, par = seq & 1u;
     const uint32_t v = tid < EDGE_WORDS ? src[tid] : 0;
     for (uint32_t p = 0; p < W; p++)
-        if (tid < EDGE_WORDS) X->mb[p][MB_DATA1 + ((uint64_t)par * P2P_MAXR + me) * EDGE_WORDS + tid] = v;
+        if (tid < EDGE_WORDS) sys_store(X->mb[p] + MB_DATA1 + ((uint64_t)par * P2P_MAXR + me) * EDGE_WORDS + tid, v);
     p2p_release_point();
     if (tid == 0) {
         if (X->fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -130,7 +144,7 @@ __global__ __launch_bounds__(64) void k_p2p_gather(const P2P *__restrict__ X, co
     if (X->fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     __syncthreads();
     const uint32_t *s = X->mb[me] + MB_DATA1 + (uint64_t)par * P2P_MAXR * EDGE_WORDS;
-    for (uint32_t t = tid; t < W * EDGE_WORDS; t += blockDim.x) dst[t] = s[t];
+    for (uint32_t t = tid; t < W * EDGE_WORDS; t += blockDim.x) dst[t] = sys_load(s + t);
     if (tid == 0) X->xs[XS_SEQ1] = seq;
 }
 

@@ -210,7 +210,10 @@ bool group_fused(const bpe_gpu_group *g) { return g->p2p && g->cs.size() == 1 &&
 
 void launch_group_fused(bpe_gpu_group *g) {
     bpe_gpu_ctx *c = g->cs[0];
-    k_rescan_spec_sh<<<1 + SPEC_RB + SPEC_SB, SCAN_T, 0, g->st>>>(c->dE, c->dC, SPEC_RB, g->d_p2p);
+    // the edge block takes one scan block's place: 1024-thread blocks are
+    // resident one per CU, so a grid above 256 leaves its last block to a
+    // second dispatch round (the last block entered ~6 us late)
+    k_rescan_spec_sh<<<SPEC_RB + std::max<uint32_t>(SPEC_SB, 2), SCAN_T, 0, g->st>>>(c->dE, c->dC, SPEC_RB, g->d_p2p);
     if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, g->st>>>(c->dE, c->dC);
     k_fused_sh<<<3 + FUSED_A + FUSED_B, 1024, 0, g->st>>>(c->dE, c->dC, FUSED_A, g->d_p2p);
 }
@@ -493,6 +496,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
                 "reduce %.2f merge %.2f tail %.2f\n", C.xdbg[0] / 100.0 / C.counters[7],
                 C.counters[9] / 100.0 / C.counters[0], C.counters[10] / 100.0 / C.counters[0],
                 C.counters[11] / 100.0 / C.counters[0]);
+    if (g->cs[0]->h.dbgts) print_timeline(g->cs[0], C.z);
     g->stats.spec_hits = C.counters[7];
     g->stats.spec_misses = C.counters[8];
     g->stats.ms_init = t1 - t0;
@@ -701,7 +705,7 @@ int bpe_gpu_group_create_p2p(int device, int nranks, int rank, long max_merges, 
     double tmo = 30.0;
     if (const char *t = getenv("BPE_P2P_TIMEOUT_S")) tmo = std::max(0.01, atof(t));
     g->hp.timeout = (unsigned long long)(tmo * 1000.0 * khz);
-    g->hp.fence = 1;
+    g->hp.fence = 0;  // system-coherent payload stores / loads instead (p2p.hip); BPE_P2P_FENCE=1 adds fences
     if (const char *f = getenv("BPE_P2P_FENCE")) g->hp.fence = atoi(f) != 0;
     bpe_gpu_ctx *c;
     if ((r = ctx_new(device, g->st, &c))) { bpe_gpu_group_destroy(g); return r; }
