@@ -17,7 +17,10 @@ namespace bpeamd {
 
 constexpr uint32_t HOLE = 0xFFFFFFFFu;
 constexpr uint32_t DENSE = 2048;         // ids aggregated in LDS / stored densely in delta vectors
-constexpr uint32_t REPL = 8;             // replicas of the dense delta accumulators
+#ifndef BPE_REPL
+#define BPE_REPL 8
+#endif
+constexpr uint32_t REPL = BPE_REPL;             // replicas of the dense delta accumulators
 constexpr uint32_t NTHR = 16;            // reference THREAD_NO (bpe.c:409)
 constexpr uint64_t CHUNK = 65536;        // reference CHUNK_SIZE (bpe.c:423)
 constexpr uint64_t DYN_LIMIT = CHUNK * NTHR;     // n >= this: chunked counting

@@ -710,7 +710,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     const uint32_t stride = nB * blockDim.x;
     uint32_t *const *lst = E->vlist[P];
     const bool sh = E->sharded;
-    const uint32_t W = sh ? E->vcap : DENSE;
+    const uint32_t W = sh ? E->vcap : min(DENSE, E->vcap);  // ids >= vcap never occur
     uint32_t nl[4];
     for (int v = 0; v < 4; v++) nl[v] = sh ? 0 : E->vnl[P][v];
     const uint32_t dense_end = 1 + 4 * W;
@@ -966,7 +966,9 @@ __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__r
             for (uint32_t x = tid; x < 4 * E->vcap + 2; x += stride) xb[x] = 0;
         } else {
             uint32_t *vd = E->vecd + (uint64_t)P * REPL * 4 * DENSE;
-            for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride) vd[x] = 0;
+            const uint32_t vc = E->vcap;  // ids >= vcap are never written
+            for (uint32_t x = tid; x < REPL * 4 * DENSE; x += stride)
+                if (x % DENSE < vc) vd[x] = 0;
             for (int vv = 0; vv < 4; vv++) {
                 const uint32_t nq = E->vnl[P][vv];
                 for (uint32_t t = tid; t < nq; t += stride) E->vec[P][vv][E->vlist[P][vv][t]] = 0;
@@ -1060,10 +1062,10 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ 
     if (blockIdx.x < rblocks) {
         rescan1_body(E, C, S, blockIdx.x, rblocks);
         scan_exit_stamp(E, blockIdx.x);
-        ts_mark(E, S.z, TS_K1_RESCAN, false);
+        ts_mark(E, S.z, TS_K1_RESCAN, false, true);
     } else if (S.spec) {
         scan_body<false, true>(E, C, S, blockIdx.x - rblocks, gridDim.x - rblocks);
-        ts_mark(E, S.z, TS_K1_SCAN, false);
+        ts_mark(E, S.z, TS_K1_SCAN, false, true);
     } else {
         scan_exit_stamp(E, blockIdx.x);
     }
@@ -1096,7 +1098,7 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec_sh(const Eng *__restrict
     if (blockIdx.x == 0) {
         if (S.spec) {
             scan_body<true, true, true>(E, C, S, nscan - 1, nscan, X);
-            ts_mark(E, S.z, TS_K1_SCAN, false);
+            ts_mark(E, S.z, TS_K1_SCAN, false, true);
         } else {
             records_pull_block(E, C, X);
             scan_exit_stamp(E, 0);
@@ -1104,10 +1106,10 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec_sh(const Eng *__restrict
     } else if (blockIdx.x <= rblocks) {
         rescan1_body(E, C, S, blockIdx.x - 1, rblocks);
         scan_exit_stamp(E, blockIdx.x);
-        ts_mark(E, S.z, TS_K1_RESCAN, false);
+        ts_mark(E, S.z, TS_K1_RESCAN, false, true);
     } else if (S.spec) {
         scan_body<true, true, true>(E, C, S, blockIdx.x - 1 - rblocks, nscan, X);
-        ts_mark(E, S.z, TS_K1_SCAN, false);
+        ts_mark(E, S.z, TS_K1_SCAN, false, true);
     } else {
         scan_exit_stamp(E, blockIdx.x);
     }
@@ -1415,14 +1417,14 @@ __global__ __launch_bounds__(1024) void k_fused(const Eng *__restrict__ E, Ctl *
         const uint32_t z0 = C->z;  // the current merge (select moves on)
         ts_mark(E, z0, TS_K2_IN, true);
         select_block(E, C, SEL_FUSED);
-        ts_mark(E, z0, TS_K2_SELECT, false);
+        ts_mark(E, z0, TS_K2_SELECT, false, true);
         return;
     }
     const Snap S = snap_next(C);
     if (S.stop) return;
     ts_mark(E, S.z - 1, TS_K2_IN, true);
     apply_body<false>(E, C, S, blockIdx.x - 1, gridDim.x - 1, roleA_blocks, X);
-    ts_mark(E, S.z - 1, blockIdx.x - 1 < roleA_blocks ? TS_K2_APPLY_A : TS_K2_APPLY_B, false);
+    ts_mark(E, S.z - 1, blockIdx.x - 1 < roleA_blocks ? TS_K2_APPLY_A : TS_K2_APPLY_B, false, true);
     if (blockIdx.x == 1 && threadIdx.x == 0) C->spec_z = S.z;
 }
 
@@ -1443,7 +1445,7 @@ __global__ __launch_bounds__(1024) void k_fused_sh(const Eng *__restrict__ E, Ct
         const uint32_t z0 = C->z;  // the current merge (select moves on)
         ts_mark(E, z0, TS_K2_IN, true);
         select_block(E, C, SEL_FUSED);
-        ts_mark(E, z0, TS_K2_SELECT, false);
+        ts_mark(E, z0, TS_K2_SELECT, false, true);
         return;
     }
     if (!C->nx_live) return;  // K1 saw a stop: nothing was scanned or pulled
@@ -1461,7 +1463,7 @@ __global__ __launch_bounds__(1024) void k_fused_sh(const Eng *__restrict__ E, Ct
     const uint32_t bid = blockIdx.x - 2;
     ts_mark(E, S.z - 1, TS_K2_IN, true);
     apply_body<false>(E, C, S, bid, nap, roleA_blocks, X);
-    ts_mark(E, S.z - 1, bid < roleA_blocks ? TS_K2_APPLY_A : TS_K2_APPLY_B, false);
+    ts_mark(E, S.z - 1, bid < roleA_blocks ? TS_K2_APPLY_A : TS_K2_APPLY_B, false, true);
     if (bid < roleA_blocks) {  // spans written: the record block may read them
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -2118,16 +2120,27 @@ __global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, co
     __syncthreads();
     const uint64_t n0 = E->n0;
     const uint64_t s = (uint64_t)t * tile, e = min(n0 - 1, s + tile);
-    // each thread takes SORT_PER = 8 consecutive positions per round (uint2 load + 1 byte)
+    // each thread takes SORT_PER = 8 consecutive positions per round (uint2 load
+    // + 1 byte); the next round's bytes are loaded before this round's LDS sort
+    auto fetch = [&](uint64_t p, uint2 *w, uint32_t *b8) {
+        *w = make_uint2(0, 0);
+        *b8 = 0;
+        if (p < e) {
+            *w = *reinterpret_cast<const uint2 *>(E->bytes + p);
+            *b8 = p + SORT_PER < n0 ? E->bytes[p + SORT_PER] : 0;
+        }
+    };
+    uint2 wn;
+    uint32_t bn;
+    fetch(s + threadIdx.x * SORT_PER, &wn, &bn);
     for (uint64_t p0 = s + threadIdx.x * SORT_PER; p0 - threadIdx.x * SORT_PER < e; p0 += SORT_CH) {
         uint32_t bins[SORT_PER], vals[SORT_PER];
-        uint32_t by[SORT_PER + 1] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (p0 < e) {
-            const uint2 w = *reinterpret_cast<const uint2 *>(E->bytes + p0);
+        uint32_t by[SORT_PER + 1];
+        const uint2 w = wn;
+        by[SORT_PER] = bn;
+        fetch(p0 + SORT_CH, &wn, &bn);
 #pragma unroll
-            for (uint32_t k = 0; k < 4; k++) { by[k] = (w.x >> (8 * k)) & 0xFF; by[4 + k] = (w.y >> (8 * k)) & 0xFF; }
-            by[SORT_PER] = p0 + SORT_PER < n0 ? E->bytes[p0 + SORT_PER] : 0;
-        }
+        for (uint32_t k = 0; k < 4; k++) { by[k] = (w.x >> (8 * k)) & 0xFF; by[4 + k] = (w.y >> (8 * k)) & 0xFF; }
 #pragma unroll
         for (uint32_t k = 0; k < SORT_PER; k++) {
             const bool in = p0 + k < e;
