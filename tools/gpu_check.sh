@@ -14,4 +14,6 @@ export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline --no-encode > $OUT/bench_prof_$TAG.json 2> $OUT/prof_$TAG.err || exit 1
 timeout -k 10 120 python3 tools/enc_prof.py train > $OUT/encprof_$TAG.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_enc_$TAG -o run -- python3 tools/enc_prof.py enc >> $OUT/encprof_$TAG.log 2>&1 || exit 1
+# the sharded step (one rank, P2P mailbox transport): what bench.py --gpus N runs per rank
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_sh_$TAG -o run -- python3 bench.py --sharded --no-cpu-baseline --no-encode > $OUT/bench_prof_sh_$TAG.json 2> $OUT/prof_sh_$TAG.err || exit 1
 echo done
