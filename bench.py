@@ -104,9 +104,13 @@ def encode_bench(args, rank, world, local, dist, barrier):
     tr.train(args.encode_merges)
     merges = tr.merges()
     tr.close()
-    total = args.encode_size
-    lo, hi = rank * (total // world), (total if rank == world - 1 else (rank + 1) * (total // world))
     per = 3 << 30  # bytes per shard context (u32 positions)
+    total = args.encode_size
+    if world > 1:
+        # one shard per rank across ranks: a rank's share must fit u32
+        # positions (10 GiB over 2 ranks does not; 4 and 8 ranks keep 10 GiB)
+        total = min(total, world * per)
+    lo, hi = rank * (total // world), (total if rank == world - 1 else (rank + 1) * (total // world))
     if world > 1:
         from llmtokenizer_amd import dist as bdist
         g = bdist.group(local, len(merges))
@@ -140,7 +144,7 @@ def encode_bench(args, rank, world, local, dist, barrier):
         n_out = int(t.item())
     w = 2 if 256 + len(merges) <= 65536 else 4
     alg = total + n_out * w  # input bytes + n_out * w
-    out = {"metric": "encode MB/s, 10 GiB stream through 32k merges", "value": round(total / 1e6 / el, 1),
+    out = {"metric": "encode MB/s, %g GiB stream through 32k merges" % (total / (1 << 30)), "value": round(total / 1e6 / el, 1),
            "unit": "MB/s", "ms": round(el * 1e3, 2), "n_gpus": world, "bytes": total, "merges": len(merges),
            "n_out": n_out, "shards": g.nshards, "batches": st["iterations"], "candidates": st["candidates"],
            "occurrences": st["occurrences"], "breakdown_ms": {"init": round(st["ms_init"], 2),
@@ -175,6 +179,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank flow on a one-GPU box: every rank on this device
+    if os.environ.get("BPE_BENCH_DEVICE") is not None:
+        local = int(os.environ["BPE_BENCH_DEVICE"])
     sharded = world > 1 or args.sharded
     dist = None
     if sharded:
