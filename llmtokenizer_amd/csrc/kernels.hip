@@ -956,6 +956,11 @@ __device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C
 // record (it only needs k_apply's span writes) beside the rescans
 // bid / nblk: this block's index among the launch's rescan blocks (any
 // block size: the work is one wave per dirty level-1 block)
+#ifndef BPE_RESCAN_PASSES
+#define BPE_RESCAN_PASSES 2
+#endif
+constexpr uint32_t RESCAN_PASSES = BPE_RESCAN_PASSES;
+
 __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__restrict__ C, const Snap &S, uint32_t bid,
                                              uint32_t nblk) {
     {   // k_apply has consumed this iteration's delta vectors: clear them
@@ -985,11 +990,11 @@ __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__r
     for (uint64_t w = wid; w < nwork; w += nwaves) {
         const uint32_t blk = full ? (uint32_t)w : E->l1list[(uint64_t)S.parity * E->l1cap + w];
         Top2 mine = top2_one(0, 0, ~0ull);
-        // two halves of 8 slots per lane, each half's counts and keys loaded
-        // together (one round trip per half; half the registers of one pass)
-        constexpr uint32_t HQ = L1W / 128;
+        // RESCAN_PASSES passes over the block's 16 slots per lane, each pass's
+        // counts and keys loaded together (one round trip per pass)
+        constexpr uint32_t HQ = L1W / 64 / RESCAN_PASSES;
 #pragma unroll
-        for (uint32_t h = 0; h < 2; h++) {
+        for (uint32_t h = 0; h < RESCAN_PASSES; h++) {
             uint32_t cnt[HQ];
             unsigned long long key[HQ];
 #pragma unroll

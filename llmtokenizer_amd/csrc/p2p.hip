@@ -54,11 +54,13 @@ __device__ inline uint32_t sys_load(const uint32_t *p) {
 __device__ inline void sys_store(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// 16 bytes in one system-coherent store (hipcc has no 128-bit atomic store;
+// the asm store is retired by the vmcnt(0) wait before the flag, and the
+// s_nop keeps hipcc from reusing its data registers before it reads them)
 __device__ inline void sys_store4(uint32_t *p, const uint4 &v) {
-    sys_store(p, v.x);
-    sys_store(p + 1, v.y);
-    sys_store(p + 2, v.z);
-    sys_store(p + 3, v.w);
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    const u4 d = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
 }
 
 // spin until *p reached want (wrapping compare); false (+ error words) on timeout
