@@ -1055,6 +1055,7 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
     // counting sort of pair positions by rank key
     const uint64_t npairs = c->n0 - 1;
     uint64_t tile = std::max<uint64_t>(1 << 16, (npairs + 1023) / 1024);
+    if (const char *t = getenv("BPE_SORT_TILE")) tile = std::max<uint64_t>(1 << 16, strtoull(t, nullptr, 0));  // tuning
     tile = (tile + 1023) & ~1023ull;  // kernels read 16-byte groups / 1-KB blocks (k_pair_hist_span)
     const uint32_t ntl = (uint32_t)((npairs + tile - 1) / tile);
     const uint32_t parts = (AA + HBINS - 1) / HBINS;
