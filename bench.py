@@ -281,7 +281,7 @@ def main():
         "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "bytes_per_launch": round(kbytes), "avg_ms": round(kms, 5), "launches": launches,
-                     "avg_ms_source": "device wall clock inside the timed run (block-0 entry to last block exit)",
+                     "avg_ms_source": "device wall clock inside the timed run (first block entry to the last block's retired memory operations)",
                      "avg_ms_hip_events": round(ev_ms, 5) if ev_n else None, "hip_event_launches": ev_n,
                      "note": "per-merge kernel is bound by dependent-load latency, not bandwidth; "
                              "event nodes add their own latency to the measured span"},

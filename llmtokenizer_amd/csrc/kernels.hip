@@ -218,7 +218,11 @@ __device__ inline void flush_list(uint32_t *list, uint16_t *ltag, uint32_t *lcou
 
 // in-kernel timing (bench.py's roofline): block 0 stamps the entry, every
 // block stamps its exit; k_select folds max(exit) - entry into Ctl
+// (taken once every wave of the block has retired its memory operations, so
+// the span ends where the block's work is complete, as the kernel's end does)
 __device__ inline void scan_exit_stamp(const Eng *E, uint32_t bid) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (threadIdx.x == 0) E->scan_tend[bid] = wall_clock64();
 }
 

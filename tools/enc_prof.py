@@ -24,7 +24,7 @@ def main():
         return
     m = np.load(PATH)
     total = 10 << 30
-    k = math.ceil(total / (3 << 30))
+    k = int(os.environ.get("ENC_SHARDS", "0")) or math.ceil(total / (3 << 30))
     g = api.ShardGroup(0, local_shards=k)
     step = total // k
     for q in range(k):
