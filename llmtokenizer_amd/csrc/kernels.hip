@@ -2044,7 +2044,10 @@ __device__ inline uint32_t tile_count(const uint32_t *hist, const uint32_t *tot,
 // consecutive addresses.  Pass A's entries are packed into 4 bytes: the
 // second byte's rank in the top 8 bits, the position relative to the tile
 // start in the low 24 (tile <= 2^24), so each pass moves 4 B per pair.
-constexpr uint32_t SORT_T = 1024, SORT_PER = 8, SORT_CH = SORT_T * SORT_PER;
+#ifndef BPE_SORT_T
+#define BPE_SORT_T 1024
+#endif
+constexpr uint32_t SORT_T = BPE_SORT_T, SORT_PER = 8, SORT_CH = SORT_T * SORT_PER;
 constexpr uint32_t SORT_LOCAL_BITS = 24;
 
 struct SortLds {
