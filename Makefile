@@ -27,7 +27,7 @@ $(BUILD)/%.o: $(PKG)/src/%.c $(wildcard include/*.h) | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(PKG)/libbpe_amd.so: $(BUILD)/engine.o $(COBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lm -ldl
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lm -ldl -lpthread
 
 tools/bpe_main: tools/bpe_main.c $(PKG)/libbpe_amd.so
 	$(CC) -O2 -Iinclude -o $@ $< -L$(PKG) -lbpe_amd -Wl,-rpath,'$$ORIGIN/../$(PKG)'

@@ -26,6 +26,19 @@ dyn_arr_t *compress_ex(const char *path, long max_merges, int device, uint32_t *
 dyn_arr_t *bpe_train_bytes(const uint8_t *bytes, size_t n, long max_merges, int device,
                            uint32_t **encoding, size_t *len);
 
+/* One training job over ndev devices in this process (rank r on devices[r];
+ * a device may repeat): contiguous shards, per-merge exchanges through P2P
+ * mailboxes, identical merges; the encoding is the shards' ids concatenated.
+ * Corpora below 2^20 bytes train on devices[0] alone (the sharded tie rule
+ * equals the reference's from there on); an unbounded
+ * run (max_merges < 0) over several devices stops at 2^22 merges.
+ * compress() takes this path when BPE_NUM_GPUS > 1 (devices BPE_DEVICE ..) or
+ * BPE_DEVICES="d0,d1,..." lists several devices (device count). */
+dyn_arr_t *bpe_train_bytes_devices(const uint8_t *bytes, size_t n, long max_merges, int ndev, const int *devices,
+                                   uint32_t **encoding, size_t *len);
+/* compress() over ngpu devices BPE_DEVICE, BPE_DEVICE + 1, ... */
+dyn_arr_t *compress_multi(const char *path, long max_merges, int ngpu, uint32_t **encoding, size_t *len);
+
 /* encode bytes with a trained merge list (dyn_arr_t from compress/read_pairs) */
 uint32_t *bpe_encode_bytes(const uint8_t *bytes, size_t n, dyn_arr_t *pair_arr, int device, size_t *len);
 

@@ -163,6 +163,14 @@ int bpe_gpu_group_create(int device, int local_shards, int nranks, int rank, con
 int bpe_gpu_group_create_p2p(int device, int nranks, int rank, long max_merges, uint8_t *handle, size_t cap,
                              bpe_gpu_group **out);
 int bpe_gpu_group_p2p_connect(bpe_gpu_group *g, const uint8_t *handles, size_t each);
+/* One process, several devices: nranks P2P groups (rank r on devices[r]; a
+ * device may repeat) connected through direct pointers to each other's
+ * mailboxes (peer access between distinct devices) instead of IPC handles.
+ * out[r] receives rank r's group (at most 3 ranks per device: ranks sharing
+ * a device need hardware queues of their own).  Each group must then be driven by a host
+ * thread of its own (the ranks' kernels wait for each other's pushes), e.g.
+ * bpe_train_bytes_devices (bpe_ex.h). */
+int bpe_gpu_group_create_local_p2p(int nranks, const int *devices, long max_merges, bpe_gpu_group **out);
 void bpe_gpu_group_destroy(bpe_gpu_group *g);
 int bpe_gpu_group_shards(bpe_gpu_group *g, int *local_shards, int *nshards, int *first_shard);
 /* shard k (local index) of the group */

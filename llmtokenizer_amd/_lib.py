@@ -20,6 +20,7 @@ EXPORTS = [
     "hash_table_search", "hash_table_clear", "hash_table_merge",
     # bpe_ex.h
     "compress_ex", "bpe_train_bytes", "bpe_encode_bytes", "bpe_last_stats",
+    "bpe_train_bytes_devices", "compress_multi",
     # bpe_gpu.h
     "bpe_gpu_device_count", "bpe_gpu_create", "bpe_gpu_destroy", "bpe_gpu_load", "bpe_gpu_synth",
     "bpe_gpu_train", "bpe_gpu_fetch_merges", "bpe_gpu_fetch_ids", "bpe_gpu_encode", "bpe_gpu_decode",
@@ -31,6 +32,7 @@ EXPORTS = [
     "bpe_gpu_group_load", "bpe_gpu_group_synth", "bpe_gpu_group_train", "bpe_gpu_group_encode", "bpe_gpu_group_fetch_merges",
     "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo", "bpe_gpu_group_kernel_profile",
     "bpe_gpu_group_create_p2p", "bpe_gpu_group_p2p_connect", "bpe_gpu_group_transport",
+    "bpe_gpu_group_create_local_p2p",
 ]
 
 
@@ -114,6 +116,13 @@ def load():
     L.compress_ex.restype = ctypes.POINTER(DynArr)
     L.bpe_train_bytes.argtypes = [vp, sz, ctypes.c_long, ctypes.c_int, ctypes.POINTER(u32p), ctypes.POINTER(sz)]
     L.bpe_train_bytes.restype = ctypes.POINTER(DynArr)
+    L.bpe_train_bytes_devices.argtypes = [vp, sz, ctypes.c_long, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(u32p), ctypes.POINTER(sz)]
+    L.bpe_train_bytes_devices.restype = ctypes.POINTER(DynArr)
+    L.compress_multi.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_int, ctypes.POINTER(u32p), ctypes.POINTER(sz)]
+    L.compress_multi.restype = ctypes.POINTER(DynArr)
+    L.bpe_gpu_group_create_local_p2p.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_long,
+                                                 ctypes.POINTER(vp)]
     L.bpe_encode_bytes.argtypes = [vp, sz, ctypes.POINTER(DynArr), ctypes.c_int, ctypes.POINTER(sz)]
     L.bpe_encode_bytes.restype = u32p
     L.decompress.argtypes = [u32p, sz, ctypes.POINTER(DynArr)]

@@ -65,7 +65,8 @@ def compress(path, max_merges=None, device=0):
     L = _lib.load()
     enc = _u32p()
     n = ctypes.c_size_t(0)
-    if max_merges is None and device == 0 and "BPE_MAX_MERGES" not in os.environ:
+    if max_merges is None and device == 0:
+        # the C entry point itself reads BPE_MAX_MERGES / BPE_DEVICE / BPE_NUM_GPUS / BPE_DEVICES
         arr = L.compress(os.fsencode(path), ctypes.byref(enc), ctypes.byref(n))
     else:
         mm = -1 if max_merges is None else int(max_merges)
@@ -89,6 +90,25 @@ def train_bytes(data: bytes, max_merges=-1, device=0):
                             ctypes.byref(enc), ctypes.byref(n))
     if not arr:
         raise BpeError("bpe_train_bytes failed")
+    try:
+        merges = _arr_to_merges(arr)
+    finally:
+        L.dyn_arr_free(arr)
+    return merges, _take_ids(enc, n.value)
+
+
+def train_bytes_devices(data: bytes, devices, max_merges=-1):
+    """One training job over len(devices) devices in this process (bpe_train_bytes_devices:
+    contiguous shards, one host thread per device; a device may repeat).  Returns (merges, ids)."""
+    L = _lib.load()
+    buf = np.frombuffer(data, dtype=np.uint8)
+    devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+    enc = _u32p()
+    n = ctypes.c_size_t(0)
+    arr = L.bpe_train_bytes_devices(buf.ctypes.data_as(ctypes.c_void_p), buf.size, int(max_merges), len(devices),
+                                    devs, ctypes.byref(enc), ctypes.byref(n))
+    if not arr:
+        raise BpeError("bpe_train_bytes_devices failed")
     try:
         merges = _arr_to_merges(arr)
     finally:

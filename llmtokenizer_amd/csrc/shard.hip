@@ -737,6 +737,53 @@ int bpe_gpu_group_p2p_connect(bpe_gpu_group *g, const uint8_t *handles, size_t e
     return 0;
 }
 
+int bpe_gpu_group_create_local_p2p(int nranks, const int *devices, long max_merges, bpe_gpu_group **out) {
+    if (!out || !devices || nranks < 1 || nranks > (int)P2P_MAXR) return BPE_GPU_EINVAL;
+    for (int r = 0; r < nranks; r++) out[r] = nullptr;
+    // the ranks' kernels wait for each other: ranks sharing a device need
+    // streams on distinct hardware queues (HIP's default: 4 per process, one
+    // of them taken by the runtime's own work; 4 ranks on one device measured
+    // a queue shared and the exchange timing out)
+    for (int r = 0; r < nranks; r++) {
+        int same = 0;
+        for (int p = 0; p < nranks; p++) same += devices[p] == devices[r];
+        if (same > 3) return fail(BPE_GPU_EINVAL, "more than 3 ranks on one device in one process");
+    }
+    int rc = 0;
+    uint8_t handle[BPE_GPU_P2P_HANDLE_BYTES];
+    for (int r = 0; r < nranks && !rc; r++)
+        rc = bpe_gpu_group_create_p2p(devices[r], nranks, r, max_merges, handle, sizeof handle, &out[r]);
+    // peer access between the distinct devices (both directions)
+    for (int r = 0; r < nranks && !rc; r++)
+        for (int p = 0; p < nranks && !rc; p++) {
+            if (devices[p] == devices[r]) continue;
+            int ok = 0;
+            if (hipDeviceCanAccessPeer(&ok, devices[r], devices[p]) != hipSuccess || !ok) {
+                rc = fail(BPE_GPU_EHIP, "no peer access between the devices");
+                break;
+            }
+            (void)hipSetDevice(devices[r]);
+            const hipError_t e = hipDeviceEnablePeerAccess(devices[p], 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) rc = fail(BPE_GPU_EHIP, "hipDeviceEnablePeerAccess", e);
+            (void)hipGetLastError();  // (already-enabled is not an error here)
+        }
+    for (int r = 0; r < nranks && !rc; r++) {
+        bpe_gpu_group *g = out[r];
+        for (int p = 0; p < nranks; p++) g->hp.mb[p] = out[p]->mailbox;
+        (void)hipSetDevice(g->dev);
+        hipError_t e = hipMemcpy(g->d_p2p, &g->hp, sizeof(P2P), hipMemcpyHostToDevice);
+        if (e != hipSuccess) rc = fail(BPE_GPU_EHIP, "p2p descriptor", e);
+        g->p2p_ready = true;
+    }
+    if (rc) {
+        for (int r = 0; r < nranks; r++) {
+            bpe_gpu_group_destroy(out[r]);
+            out[r] = nullptr;
+        }
+    }
+    return rc;
+}
+
 void bpe_gpu_group_destroy(bpe_gpu_group *g) {
     if (!g) return;
     (void)hipSetDevice(g->dev);

@@ -11,6 +11,7 @@
 #include "../../include/bpe_ex.h"
 #include "../../include/bpe_gpu.h"
 
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -265,6 +266,166 @@ fail:
     return NULL;
 }
 
+/* ------------------------------------------------- one process, N devices */
+/* One training job over ndev contiguous shards, rank r
+ * on devices[r], the ranks' per-merge exchanges pushed through each other's
+ * mailboxes; one host thread per rank drives its group. */
+struct rank_job {
+    bpe_gpu_group *g;
+    const uint8_t *bytes;
+    size_t n;
+    long max_merges;
+    int rc;
+    const char *what;
+    char msg[256];  /* the library's last error is per thread */
+};
+
+static void *rank_main(void *arg)
+{
+    struct rank_job *j = arg;
+    size_t k = 0;
+    j->what = "load";
+    if ((j->rc = bpe_gpu_group_load(j->g, 0, j->bytes, j->n))) {
+        snprintf(j->msg, sizeof j->msg, "%s", bpe_gpu_last_error());
+        return NULL;
+    }
+    j->what = "train";
+    j->rc = bpe_gpu_group_train(j->g, j->max_merges, &k);
+    if (j->rc) snprintf(j->msg, sizeof j->msg, "%s", bpe_gpu_last_error());
+    return NULL;
+}
+
+/* the sharded tie rule equals the single-GPU one from 2^20 tokens on
+ * (DESIGN.md section 6); smaller corpora train on one device */
+#define MULTI_MIN_BYTES (1u << 20)
+/* unbounded runs over several devices are capped here (the mailbox holds
+ * 4 words per id) */
+#define MULTI_DEFAULT_CAP (1l << 22)
+
+dyn_arr_t *bpe_train_bytes_devices(const uint8_t *bytes, size_t n, long max_merges, int ndev, const int *devices,
+                                   uint32_t **encoding, size_t *len)
+{
+    if (!bytes || !encoding || !len || ndev < 1 || !devices) return NULL;
+    if (ndev == 1 || n < MULTI_MIN_BYTES || (size_t)ndev > n / 2)
+        return bpe_train_bytes(bytes, n, max_merges, devices[0], encoding, len);
+    if (ndev > BPE_GPU_P2P_MAX_RANKS) {
+        fprintf(stderr, "bpe: at most %d devices\n", BPE_GPU_P2P_MAX_RANKS);
+        return NULL;
+    }
+    long cap = max_merges;
+    if (cap < 0) cap = (long)((n - 1) < (size_t)MULTI_DEFAULT_CAP ? (n - 1) : (size_t)MULTI_DEFAULT_CAP);
+    bpe_gpu_group *gs[BPE_GPU_P2P_MAX_RANKS] = {0};
+    struct rank_job jobs[BPE_GPU_P2P_MAX_RANKS];
+    pthread_t th[BPE_GPU_P2P_MAX_RANKS];
+    dyn_arr_t *arr = NULL;
+    uint32_t *pairs = NULL, *ids = NULL;
+    size_t k = 0, got = 0, total = 0;
+    int rc, started = 0;
+    if ((rc = bpe_gpu_group_create_local_p2p(ndev, devices, cap, gs))) {
+        report("multi-device group", rc);
+        goto out;
+    }
+    for (int r = 0; r < ndev; r++) {
+        const size_t lo = (size_t)r * (n / (size_t)ndev), hi = r == ndev - 1 ? n : (size_t)(r + 1) * (n / (size_t)ndev);
+        jobs[r] = (struct rank_job){gs[r], bytes + lo, hi - lo, cap, 0, "", ""};
+        if (pthread_create(&th[r], NULL, rank_main, &jobs[r])) {
+            fprintf(stderr, "bpe: pthread_create failed\n");
+            break;
+        }
+        started++;
+    }
+    for (int r = 0; r < started; r++) pthread_join(th[r], NULL);
+    if (started < ndev) goto out;
+    for (int r = 0; r < ndev; r++)
+        if (jobs[r].rc) {
+            fprintf(stderr, "bpe: rank %d %s failed: %s (%s)\n", r, jobs[r].what, bpe_gpu_strerror(jobs[r].rc),
+                    jobs[r].msg);
+            goto out;
+        }
+    if ((rc = bpe_gpu_group_fetch_merges(gs[0], NULL, 0, &k))) { report("fetch merges", rc); goto out; }
+    pairs = malloc((k ? k : 1) * 2 * sizeof(uint32_t));
+    if (!pairs || (rc = bpe_gpu_group_fetch_merges(gs[0], pairs, k, &got))) goto out;
+    for (int r = 0; r < ndev; r++) {
+        size_t m = 0;
+        if ((rc = bpe_gpu_group_fetch_ids(gs[r], 0, NULL, 0, &m))) { report("fetch ids", rc); goto out; }
+        total += m;
+    }
+    ids = malloc((total ? total : 1) * sizeof(uint32_t));
+    if (!ids) goto out;
+    total = 0;
+    for (int r = 0; r < ndev; r++) {
+        size_t m = 0;
+        if ((rc = bpe_gpu_group_fetch_ids(gs[r], 0, NULL, 0, &m)) ||
+            (rc = bpe_gpu_group_fetch_ids(gs[r], 0, ids + total, m, &m))) {
+            report("fetch ids", rc);
+            goto out;
+        }
+        total += m;
+    }
+    arr = pairs_to_arr(pairs, k);
+    if (arr) {
+        bpe_gpu_group_get_stats(gs[0], &g_last_stats);
+        *encoding = ids;
+        *len = total;
+        ids = NULL;
+    }
+out:
+    for (int r = 0; r < ndev; r++) bpe_gpu_group_destroy(gs[r]);
+    free(pairs);
+    free(ids);
+    if (!arr) {
+        *encoding = NULL;
+        *len = 0;
+    }
+    return arr;
+}
+
+/* BPE_DEVICES="0,1,..." (a device may repeat), else BPE_NUM_GPUS devices
+ * from BPE_DEVICE on; returns the count (0: bad value) */
+static int env_devices(int *devs)
+{
+    long dev, ng;
+    if (env_int("BPE_DEVICE", 0, &dev) || env_int("BPE_NUM_GPUS", 1, &ng)) return 0;
+    const char *list = getenv("BPE_DEVICES");
+    if (list && *list) {
+        int k = 0;
+        const char *p = list;
+        while (*p && k < BPE_GPU_P2P_MAX_RANKS) {
+            char *end;
+            const long v = strtol(p, &end, 10);
+            if (end == p || v < 0) return 0;
+            devs[k++] = (int)v;
+            p = *end == ',' ? end + 1 : end;
+            if (*end && *end != ',') return 0;
+        }
+        return k;
+    }
+    if (ng < 1 || ng > BPE_GPU_P2P_MAX_RANKS) return 0;
+    for (int r = 0; r < ng; r++) devs[r] = (int)dev + r;
+    return (int)ng;
+}
+
+dyn_arr_t *compress_multi(const char *path, long max_merges, int ngpu, uint32_t **encoding, size_t *len)
+{
+    if (!path || !encoding || !len || ngpu < 1 || ngpu > BPE_GPU_P2P_MAX_RANKS) return NULL;
+    long dev;
+    if (env_int("BPE_DEVICE", 0, &dev)) return NULL;
+    int devs[BPE_GPU_P2P_MAX_RANKS];
+    for (int r = 0; r < ngpu; r++) devs[r] = (int)dev + r;
+    char *buf = get_file(path);
+    if (!buf) return NULL;
+    size_t n = strlen(buf);
+    if (n < 2) {
+        printf("Error: File contains less than 2 characters\n");
+        fflush(stdout);
+        free(buf);
+        return NULL;
+    }
+    dyn_arr_t *arr = bpe_train_bytes_devices((const uint8_t *)buf, n, max_merges, ngpu, devs, encoding, len);
+    free(buf);
+    return arr;
+}
+
 dyn_arr_t *compress_ex(const char *path, long max_merges, int device, uint32_t **encoding, size_t *len)
 {
     if (!path || !encoding || !len) return NULL;
@@ -284,12 +445,27 @@ dyn_arr_t *compress_ex(const char *path, long max_merges, int device, uint32_t *
 
 dyn_arr_t *compress(const char *path, uint32_t **encoding, size_t *len)
 {
-    long maxm, dev;
-    if (env_int("BPE_MAX_MERGES", -1, &maxm) || env_int("BPE_DEVICE", 0, &dev)) {
-        fprintf(stderr, "bpe: BPE_MAX_MERGES / BPE_DEVICE must be integers\n");
+    long maxm;
+    int devs[BPE_GPU_P2P_MAX_RANKS];
+    const int nd = env_devices(devs);
+    if (env_int("BPE_MAX_MERGES", -1, &maxm) || nd < 1) {
+        fprintf(stderr, "bpe: BPE_MAX_MERGES / BPE_DEVICE / BPE_NUM_GPUS / BPE_DEVICES: bad value\n");
         return NULL;
     }
-    return compress_ex(path, maxm, (int)dev, encoding, len);
+    if (nd == 1) return compress_ex(path, maxm, devs[0], encoding, len);
+    if (!path || !encoding || !len) return NULL;
+    char *buf = get_file(path);
+    if (!buf) return NULL;
+    size_t n = strlen(buf);
+    if (n < 2) {
+        printf("Error: File contains less than 2 characters\n");
+        fflush(stdout);
+        free(buf);
+        return NULL;
+    }
+    dyn_arr_t *arr = bpe_train_bytes_devices((const uint8_t *)buf, n, maxm, nd, devs, encoding, len);
+    free(buf);
+    return arr;
 }
 
 uint32_t *bpe_encode_bytes(const uint8_t *bytes, size_t n, dyn_arr_t *pair_arr, int device, size_t *len)

@@ -1,0 +1,27 @@
+"""Repro probe 2: the test module's sequence, then the small tracked run 6 times vs the oracle."""
+import sys
+sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/tests")
+import numpy as np
+if "torch" in sys.argv:  # as tests/conftest.py does: torch initialises HIP first
+    import torch
+    print("torch cuda", torch.cuda.is_available(), flush=True)
+from llmtokenizer_amd import api
+from llmtokenizer_amd.synth import synth_bytes
+import oracle_lib as O
+
+for ranks, merges in [(2, 300), (3, 200)]:
+    data = synth_bytes(5, (3 << 20) + 12345)
+    api.train_bytes(data, merges, device=0)
+    api.train_bytes_devices(data, [0] * ranks, merges)
+try:
+    api.train_bytes_devices(synth_bytes(9, 1 << 20), [0] * 4, 10)
+except api.BpeError:
+    pass
+api.train_bytes_devices(synth_bytes(6, 1 << 20), [0, 0], 40)
+data = synth_bytes(7, 50000)
+om, oids, _ = O.train(data, 100, O.EMU)
+for k in range(6):
+    m, ids = api.train_bytes(data, 100, device=0)
+    same = m.shape == om.shape and bool((m == om).all()) and ids.size == oids.size and bool((ids == oids).all())
+    first = int(np.argmax((m != om).any(axis=1))) if m.shape == om.shape and not same else -1
+    print(k, "oracle-equal", same, "first diff merge", first, flush=True)
