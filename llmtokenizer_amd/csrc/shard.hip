@@ -660,10 +660,18 @@ int bpe_gpu_group_create(int device, int local_shards, int nranks, int rank, con
     return 0;
 }
 
+static int group_create_p2p(int device, int nranks, int rank, long max_merges, uint8_t *handle, bpe_gpu_group **out);
+
 int bpe_gpu_group_create_p2p(int device, int nranks, int rank, long max_merges, uint8_t *handle, size_t cap,
                              bpe_gpu_group **out) {
-    if (!out || !handle || cap < BPE_GPU_P2P_HANDLE_BYTES || nranks < 1 || nranks > (int)P2P_MAXR || rank < 0 ||
-        rank >= nranks || max_merges < 0 || max_merges > (1l << 24))
+    if (!out || !handle || cap < BPE_GPU_P2P_HANDLE_BYTES) return BPE_GPU_EINVAL;
+    return group_create_p2p(device, nranks, rank, max_merges, handle, out);
+}
+
+// handle == nullptr: an in-process group (no IPC export of the mailbox)
+static int group_create_p2p(int device, int nranks, int rank, long max_merges, uint8_t *handle, bpe_gpu_group **out) {
+    if (!out || nranks < 1 || nranks > (int)P2P_MAXR || rank < 0 || rank >= nranks || max_merges < 0 ||
+        max_merges > (1l << 24))
         return BPE_GPU_EINVAL;
     static_assert(sizeof(hipIpcMemHandle_t) <= BPE_GPU_P2P_HANDLE_BYTES, "IPC handle size");
     int n = 0;
@@ -689,13 +697,15 @@ int bpe_gpu_group_create_p2p(int device, int nranks, int rank, long max_merges, 
         bpe_gpu_group_destroy(g);
         return fail(BPE_GPU_EHIP, "p2p set-up", e);
     }
-    hipIpcMemHandle_t h;
-    if ((e = hipIpcGetMemHandle(&h, g->mailbox)) != hipSuccess) {
-        bpe_gpu_group_destroy(g);
-        return fail(BPE_GPU_EHIP, "hipIpcGetMemHandle", e);
+    if (handle) {
+        hipIpcMemHandle_t h;
+        if ((e = hipIpcGetMemHandle(&h, g->mailbox)) != hipSuccess) {
+            bpe_gpu_group_destroy(g);
+            return fail(BPE_GPU_EHIP, "hipIpcGetMemHandle", e);
+        }
+        memset(handle, 0, BPE_GPU_P2P_HANDLE_BYTES);
+        memcpy(handle, &h, sizeof h);
     }
-    memset(handle, 0, BPE_GPU_P2P_HANDLE_BYTES);
-    memcpy(handle, &h, sizeof h);
     g->hp.W = (uint32_t)nranks;
     g->hp.rank = (uint32_t)rank;
     g->hp.c0 = (uint32_t)c0;
@@ -750,9 +760,7 @@ int bpe_gpu_group_create_local_p2p(int nranks, const int *devices, long max_merg
         if (same > 3) return fail(BPE_GPU_EINVAL, "more than 3 ranks on one device in one process");
     }
     int rc = 0;
-    uint8_t handle[BPE_GPU_P2P_HANDLE_BYTES];
-    for (int r = 0; r < nranks && !rc; r++)
-        rc = bpe_gpu_group_create_p2p(devices[r], nranks, r, max_merges, handle, sizeof handle, &out[r]);
+    for (int r = 0; r < nranks && !rc; r++) rc = group_create_p2p(devices[r], nranks, r, max_merges, nullptr, &out[r]);
     // peer access between the distinct devices (both directions)
     for (int r = 0; r < nranks && !rc; r++)
         for (int p = 0; p < nranks && !rc; p++) {
