@@ -1,8 +1,12 @@
 """Repro probe 2: the test module's sequence, then the small tracked run 6 times vs the oracle."""
+import os
 import sys
 sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/tests")
 import numpy as np
-if "torch" in sys.argv:  # as tests/conftest.py does: torch initialises HIP first
+if "libfirst" in sys.argv:  # the library (and /opt/rocm's HIP runtime) before torch
+    from llmtokenizer_amd import _lib
+    _lib.load()
+if "torch" in sys.argv:  # torch initialises HIP (its own bundled runtime, unless the library came first)
     import torch
     print("torch cuda", torch.cuda.is_available(), flush=True)
 from llmtokenizer_amd import api
@@ -20,7 +24,8 @@ except api.BpeError:
 api.train_bytes_devices(synth_bytes(6, 1 << 20), [0, 0], 40)
 data = synth_bytes(7, 50000)
 om, oids, _ = O.train(data, 100, O.EMU)
-for k in range(6):
+reps = int(os.environ.get("REPS", "6"))
+for k in range(reps):
     m, ids = api.train_bytes(data, 100, device=0)
     same = m.shape == om.shape and bool((m == om).all()) and ids.size == oids.size and bool((ids == oids).all())
     first = int(np.argmax((m != om).any(axis=1))) if m.shape == om.shape and not same else -1
