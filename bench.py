@@ -104,6 +104,8 @@ def encode_bench(args, rank, world, local, dist, barrier):
     tr.train(args.encode_merges)
     merges = tr.merges()
     tr.close()
+    import hashlib
+    merges_md5 = hashlib.md5(merges.tobytes()).hexdigest()  # (the same on every rank and every N)
     per = 3 << 30  # bytes per shard context (u32 positions)
     total = args.encode_size
     if world > 1:
@@ -146,7 +148,8 @@ def encode_bench(args, rank, world, local, dist, barrier):
     alg = total + n_out * w  # input bytes + n_out * w
     out = {"metric": "encode MB/s, %g GiB stream through 32k merges" % (total / (1 << 30)), "value": round(total / 1e6 / el, 1),
            "unit": "MB/s", "ms": round(el * 1e3, 2), "n_gpus": world, "bytes": total, "merges": len(merges),
-           "n_out": n_out, "shards": g.nshards, "batches": st["iterations"], "candidates": st["candidates"],
+           "n_out": n_out, "merges_md5": merges_md5, "shards": g.nshards, "batches": st["iterations"],
+           "candidates": st["candidates"],
            "occurrences": st["occurrences"], "breakdown_ms": {"init": round(st["ms_init"], 2),
                                                              "replay": round(st["ms_train"], 2)},
            "roofline": {"bound": "hbm", "achieved": round(alg / el / 1e9, 1), "peak": HBM_PEAK_GBS,

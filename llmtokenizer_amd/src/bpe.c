@@ -284,11 +284,6 @@ static void *rank_main(void *arg)
 {
     struct rank_job *j = arg;
     size_t k = 0;
-    j->what = "load";
-    if ((j->rc = bpe_gpu_group_load(j->g, 0, j->bytes, j->n))) {
-        snprintf(j->msg, sizeof j->msg, "%s", bpe_gpu_last_error());
-        return NULL;
-    }
     j->what = "train";
     j->rc = bpe_gpu_group_train(j->g, j->max_merges, &k);
     if (j->rc) snprintf(j->msg, sizeof j->msg, "%s", bpe_gpu_last_error());
@@ -325,9 +320,18 @@ dyn_arr_t *bpe_train_bytes_devices(const uint8_t *bytes, size_t n, long max_merg
         report("multi-device group", rc);
         goto out;
     }
+    /* the shards are uploaded from this thread, one after the other (pageable
+     * host-to-device copies from several threads at once are avoided); only
+     * the training, whose ranks wait for each other, needs a thread per rank */
     for (int r = 0; r < ndev; r++) {
         const size_t lo = (size_t)r * (n / (size_t)ndev), hi = r == ndev - 1 ? n : (size_t)(r + 1) * (n / (size_t)ndev);
         jobs[r] = (struct rank_job){gs[r], bytes + lo, hi - lo, cap, 0, "", ""};
+        if ((rc = bpe_gpu_group_load(gs[r], 0, bytes + lo, hi - lo))) {
+            report("load", rc);
+            goto out;
+        }
+    }
+    for (int r = 0; r < ndev; r++) {
         if (pthread_create(&th[r], NULL, rank_main, &jobs[r])) {
             fprintf(stderr, "bpe: pthread_create failed\n");
             break;

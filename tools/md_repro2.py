@@ -13,15 +13,18 @@ from llmtokenizer_amd import api
 from llmtokenizer_amd.synth import synth_bytes
 import oracle_lib as O
 
+multi = not os.environ.get("NOMULTI")
 for ranks, merges in [(2, 300), (3, 200)]:
     data = synth_bytes(5, (3 << 20) + 12345)
     api.train_bytes(data, merges, device=0)
-    api.train_bytes_devices(data, [0] * ranks, merges)
-try:
-    api.train_bytes_devices(synth_bytes(9, 1 << 20), [0] * 4, 10)
-except api.BpeError:
-    pass
-api.train_bytes_devices(synth_bytes(6, 1 << 20), [0, 0], 40)
+    if multi:
+        api.train_bytes_devices(data, [0] * ranks, merges)
+if multi:
+    try:
+        api.train_bytes_devices(synth_bytes(9, 1 << 20), [0] * 4, 10)
+    except api.BpeError:
+        pass
+    api.train_bytes_devices(synth_bytes(6, 1 << 20), [0, 0], 40)
 data = synth_bytes(7, 50000)
 om, oids, _ = O.train(data, 100, O.EMU)
 reps = int(os.environ.get("REPS", "6"))
