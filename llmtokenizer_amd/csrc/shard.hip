@@ -689,7 +689,10 @@ static int group_create_p2p(int device, int nranks, int rank, long max_merges, u
     // words) and the set-up exchanges (byte-pair counts: up to 256^2 words)
     const uint64_t c0 = ((std::max<uint64_t>(65536, 4ull * (256 + (uint64_t)max_merges) + 2) + 3) / 4) * 4;
     const size_t bytes = ((size_t)MB_DATA0 + 2ull * nranks * c0) * 4;
-    e = hipExtMallocWithFlags((void **)&g->mailbox, bytes, hipDeviceMallocUncached);
+    // in-process groups (no handle) take a plain allocation: every mailbox
+    // access is a system-coherent load / store either way (p2p.hip)
+    e = handle ? hipExtMallocWithFlags((void **)&g->mailbox, bytes, hipDeviceMallocUncached)
+               : hipMalloc((void **)&g->mailbox, bytes);
     if (e != hipSuccess) { g->mailbox = nullptr; bpe_gpu_group_destroy(g); return fail(BPE_GPU_ENOMEM, "uncached mailbox", e); }
     if ((e = hipMemset(g->mailbox, 0, bytes)) != hipSuccess ||
         (e = hipMalloc(&g->xs, 64)) != hipSuccess || (e = hipMemset(g->xs, 0, 64)) != hipSuccess ||
