@@ -1,40 +1,48 @@
 #!/usr/bin/env python3
-"""Benchmark of the BPE merge-training loop on MI355X (BASELINE.json metric
-"corpus MB/s per merge iter").
+"""Benchmark of the BPE merge-training loop and encode pass on MI355X
+(BASELINE.json metric "corpus MB/s per merge iter (train) + encode MB/s").
 
-Workload (BASELINE.json configs[3], one GPU per rank): a 1 GiB synthetic
-random_text.txt-shaped corpus (seed 2, generated directly in HBM), trained
-for K merge iterations.  One "step" = one merge iteration over the corpus.
-The timed region is the WHOLE training job on resident input: the one-off
-pair counting sort + K iterations (count deltas -> argmax -> merge), ending
-with the final ids compacted in HBM.
+One STEP = one whole training job over the 1 GiB synthetic corpus (splitmix64
+seed 2, random_text.txt-shaped, generated in HBM before timing): the one-off
+pair counting sort, M merge iterations (count deltas -> argmax -> merge), the
+final ids compacted in HBM.  `--steps K` jobs are timed back to back after
+`--warmup W` untimed jobs; the merge count does not depend on K.
 
-value = n_gpus * corpus_MB * K / wall   (MB = 1e6 bytes)
+  N = 1  BASELINE configs[2]: 1 GiB x 8192 merges on one MI355X (the "HBM
+         roofline run").  Extra key `train_1024`: the same corpus at 1024
+         merges (configs[3] at N = 1, the north-star comparison point).
+  N > 1  BASELINE configs[3]: the SAME 1 GiB corpus cut into N contiguous
+         shards, one per rank (strong scaling), 1024 merges; per merge a sum
+         of count deltas + a gather of edge records over xGMI (P2P mailboxes,
+         or RCCL with --xport rccl).  Rank 0 first times the single-GPU job on
+         its own device, so the line carries the measured speed-up 1 -> N and
+         checks that merges and ids (checksum) equal the single-GPU run.
+         Extra key `weak`: N GiB (1 GiB per rank), one job.
 
-Multi-GPU (torchrun, one rank per GPU): ONE training job over an N GiB
-corpus cut into N contiguous 1 GiB shards (weak scaling).  Every merge sums
-the shards' count deltas and gathers their 16-word edge records: by default
-one push kernel per exchange over xGMI into the peers' IPC-mapped mailboxes
-(BPE_XPORT=rccl: RCCL collectives on libbpe_amd.so's own communicator);
-torch.distributed/gloo only carries the set-up handles, the barrier and the
-max over ranks.  The merges are
-checked identical on every rank.  value = N * 1073.7 MB * K / wall.
+value = corpus_MB * merges * K / wall  (MB = 1e6 bytes; whole job, max over ranks)
 
-The JSON line also carries
-  roofline     -- the dominant kernel of the loop (k_scan), its average span
-                  from the device wall clock inside the timed run, corroborated
-                  by HIP event nodes in a second run; algorithmic bytes =
-                  8 B/candidate + 20 B/occurrence;
-  roofline_count_pass -- the one corpus-wide streaming pass (k_pair_hist),
-                  timed with HIP events on the engine's stream;
-  cpu_baseline -- the unmodified reference (oracle/_ref/bpe_ref, 16 threads)
-                  timed on this host on a bounded sample (rank 0, N=1 only).
+The line also carries
+  roofline        the dominant per-merge kernel (k_rescan_spec): algorithmic
+                  bytes per launch (8 B/candidate + 20 B/occurrence + 12 B per
+                  dirty summary slot) and its average span from the
+                  device wall clock, both over the LAST timed job; the committed
+                  rocprofv3 summary and PMC traffic of this same command
+                  (profiles/r2_*) beside them;
+  roofline_count_pass  the corpus-wide pair-count pass, priced at SURVEY 8(d)
+                  widths (1 B/token read + 2 B/token id write while V <= 65536);
+  correctness     merges md5 + position-keyed ids checksum (bpe_gpu_ids_checksum)
+                  of the warm-up and the timed jobs: they must agree, else the
+                  line carries "error" and the process exits non-zero;
+  cpu_baseline    the unmodified reference (oracle/_ref/bpe_ref, 16 pthreads as
+                  it hard-codes) on a bounded sample, rank 0 at N = 1 only;
+  encode          BASELINE configs[4]: a 10 GiB seed-3 stream through the first
+                  32768 merges the trainer learns; ids checksum of the warm and
+                  timed runs must agree and n_out + occurrences == bytes.
 """
 import argparse
 import csv
-import glob
+import hashlib
 import json
-import re
 import os
 import subprocess
 import sys
@@ -45,6 +53,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+GIB = 1 << 30
+PROFILE_TAG = "r2"     # profiles/<tag>_bench_kernel_stats.csv, <tag>_pmc_traffic.json
 
 
 def cpu_baseline(seed, size, merges):
@@ -94,67 +104,238 @@ def cpu_encode_baseline(merges, seed, size):
                       f"sequential replace passes, {dt:.1f} s wall"}
 
 
-def encode_bench(args, rank, world, local, dist, barrier):
+class Ctx:
+    """rank / world / torch.distributed plumbing (gloo carries only set-up data,
+    barriers and the max over ranks; the per-merge exchange is in libbpe_amd)"""
+
+    def __init__(self, sharded):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # rehearsal of the N-rank flow on a one-GPU box: every rank on this device
+        if os.environ.get("BPE_BENCH_DEVICE") is not None:
+            self.local = int(os.environ["BPE_BENCH_DEVICE"])
+        self.dist = None
+        if sharded:
+            import torch
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            self.dist.barrier()
+
+    def allreduce(self, x, op="sum", dtype="float64"):
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=getattr(torch, dtype))
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX if op == "max" else self.dist.ReduceOp.SUM)
+        return t.item()
+
+    def allgather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+
+def group_checksum(cx, g):
+    """ids checksum of the whole corpus over the ranks' shard groups"""
+    s, n = g.ids_checksum(0)
+    counts = cx.allgather(n)
+    base = sum(counts[:cx.rank])
+    s, n = g.ids_checksum(base)
+    sums = cx.allgather(s)
+    return sum(sums) % (1 << 64), sum(counts)
+
+
+def timed_jobs(cx, run, k):
+    """k back-to-back jobs between barriers + device syncs; max over ranks"""
+    cx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        run()
+    t1 = time.perf_counter()
+    cx.barrier()
+    return cx.allreduce(t1 - t0, "max")
+
+
+def committed_profile(name):
+    """rocprof average (ms) of kernel `name` and PMC traffic per launch from
+    the committed summaries of this same command (profiles/<tag>_*)"""
+    out = {}
+    p = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_bench_kernel_stats.csv")
+    if os.path.exists(p):
+        with open(p) as f:
+            for r in csv.DictReader(f):
+                nm = r["Name"].split("(")[0].replace("bpeamd::", "").replace("void ", "").strip()
+                if nm.split("<")[0] == name:
+                    out["avg_ms_rocprof"] = round(float(r["AverageNs"]) / 1e6, 5)
+                    out["rocprof_calls"] = int(r["Calls"])
+                    out["rocprof_summary"] = os.path.relpath(p, ROOT)
+                    break
+    p = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_traffic.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            tr = json.load(f)
+        if name in tr:
+            out["traffic"] = tr[name]["traffic_bytes_per_launch"]
+            out["traffic_source"] = (os.path.relpath(p, ROOT) + ": FETCH_SIZE x %.1f + WRITE_SIZE, separate "
+                                     "--pmc passes of this command" % tr[name]["fetch_correction"])
+    return out
+
+
+def train_single(args, cx, out):
+    """N = 1: configs[2] (1 GiB x 8192 merges) + the 1024-merge figure"""
+    from llmtokenizer_amd import api
+    e = api.Engine(cx.local)
+    e.synth(args.seed, args.size)
+    merges = args.merges or 8192
+    for _ in range(args.warmup):
+        e.train(merges)
+    ref = None
+    if args.warmup:
+        ref = (hashlib.md5(e.merges().tobytes()).hexdigest(), e.ids_checksum())
+    done = []
+    el = timed_jobs(cx, lambda: done.append(e.train(merges)), args.steps)
+    got = (hashlib.md5(e.merges().tobytes()).hexdigest(), e.ids_checksum())
+    st = e.stats()
+    prof = e.kernel_profile()  # the last timed job: bytes per launch and span from one window
+    if any(k != merges for k in done):
+        out["error"] = f"a job stopped early: {sorted(set(done))} merges"
+    if ref is not None and ref != got:
+        out["error"] = f"warm-up and timed jobs differ: {ref} vs {got}"
+    extra = {}
+    if not args.no_extras:
+        e.train(1024)  # warm
+        t = timed_jobs(cx, lambda: e.train(1024), 1)
+        s2 = e.stats()
+        extra = {"train_1024": {"value": round(args.size / 1e6 * 1024 / t, 1), "ms": round(t * 1e3, 3),
+                                "workload": "configs[3] at N=1: 1 GiB x 1024 merges, one job",
+                                "breakdown_ms": {"init": round(s2["ms_init"], 3), "loop": round(s2["ms_train"], 3)},
+                                "ids_checksum": "%016x" % e.ids_checksum(),
+                                "merges_md5": hashlib.md5(e.merges().tobytes()).hexdigest()}}
+    e.close()
+    return el, merges, st, prof, got, extra
+
+
+def train_sharded(args, cx, out):
+    """N > 1 (or --sharded): configs[3], one 1 GiB corpus over N ranks"""
+    from llmtokenizer_amd import api
+    from llmtokenizer_amd import dist as bdist
+    merges = args.merges or 1024
+    single = None
+    if not args.no_extras and cx.world > 1:
+        # the 1-GPU reference point, on rank 0's device, same corpus and merges
+        if cx.rank == 0:
+            e = api.Engine(cx.local)
+            e.synth(args.seed, args.size)
+            e.train(merges)
+            t0 = time.perf_counter()
+            e.train(merges)
+            t1 = time.perf_counter()
+            single = (t1 - t0, hashlib.md5(e.merges().tobytes()).hexdigest(), e.ids_checksum())
+            e.close()
+        cx.barrier()
+    g = bdist.group(cx.local, merges, args.xport)
+    lo, hi = bdist.shard_range(args.size, cx.rank, cx.world)
+    g.synth(0, args.seed, hi - lo, lo)
+    for _ in range(args.warmup):
+        g.train(merges)
+    done = []
+    el = timed_jobs(cx, lambda: done.append(g.train(merges)), args.steps)
+    st = g.stats()
+    md5 = hashlib.md5(g.merges().tobytes()).hexdigest()
+    digests = cx.allgather(md5)
+    csum, n_ids = group_checksum(cx, g)
+    prof = g.kernel_profile(0)
+    transport = g.transport()
+    if any(k != merges for k in done):
+        out["error"] = f"a job stopped early: {sorted(set(done))} merges"
+    if len(set(digests)) != 1:
+        out["error"] = "merges differ across ranks"
+    extra = {"merges_identical_across_ranks": len(set(digests)) == 1, "transport": transport}
+    if single is not None:
+        t1 = single[0]
+        extra["single_gpu_1024"] = {"ms": round(t1 * 1e3, 3), "value": round(args.size / 1e6 * merges / t1, 1)}
+        extra["speedup_vs_1gpu"] = round(t1 / (el / args.steps), 3)
+        same = single[1] == md5 and single[2] == csum
+        extra["identical_to_1gpu"] = same
+        if not same:
+            out["error"] = "sharded merges/ids differ from the single-GPU run"
+    if not args.no_extras and cx.world > 1:
+        # weak scaling: 1 GiB per rank, one job
+        g.synth(0, args.seed, args.size, cx.rank * args.size)
+        g.train(merges)
+        t = timed_jobs(cx, lambda: g.train(merges), 1)
+        extra["weak"] = {"value": round(cx.world * args.size / 1e6 * merges / t, 1), "ms": round(t * 1e3, 3),
+                         "workload": f"{cx.world} GiB ({cx.world} x 1 GiB shards), {merges} merges, one job"}
+    g.close()
+    return el, merges, st, prof, (md5, csum), extra
+
+
+def encode_bench(args, cx):
     """BASELINE configs[4]: encode a 10 GiB seed-3 stream with the first 32768
     merges the GPU trainer learns on the 1 GiB seed-2 corpus.  Input resident
     in HBM; timed = the whole encode (pair sort + batched merge replay + ids)."""
     from llmtokenizer_amd import api
-    tr = api.Engine(local)  # same deterministic merges on every rank
+    tr = api.Engine(cx.local)  # same deterministic merges on every rank
     tr.synth(args.seed, args.size)
     tr.train(args.encode_merges)
     merges = tr.merges()
     tr.close()
-    import hashlib
     merges_md5 = hashlib.md5(merges.tobytes()).hexdigest()  # (the same on every rank and every N)
     per = 3 << 30  # bytes per shard context (u32 positions)
     total = args.encode_size
+    world = cx.world
     if world > 1:
-        # one shard per rank across ranks: a rank's share must fit u32
-        # positions (10 GiB over 2 ranks does not; 4 and 8 ranks keep 10 GiB)
-        total = min(total, world * per)
-    lo, hi = rank * (total // world), (total if rank == world - 1 else (rank + 1) * (total // world))
+        total = min(total, world * per)  # a rank's share must fit u32 positions
     if world > 1:
         from llmtokenizer_amd import dist as bdist
-        g = bdist.group(local, len(merges))
+        lo, hi = bdist.shard_range(total, cx.rank, world)
+        g = bdist.group(cx.local, len(merges), args.xport)
         g.synth(0, 3, hi - lo, lo)
     else:
         k = max(1, -(-total // per))
-        g = api.ShardGroup(local, local_shards=k)
+        g = api.ShardGroup(cx.local, local_shards=k)
         step = total // k
         for q in range(k):
             a = q * step
             b = total if q == k - 1 else a + step
             g.synth(q, 3, b - a, a)
     g.encode(merges)  # warm (pools, graphs)
-    barrier()
-    t0 = time.perf_counter()
-    g.encode(merges)
-    t1 = time.perf_counter()
-    barrier()
-    el = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    warm = group_checksum(cx, g)
+    el = timed_jobs(cx, lambda: g.encode(merges), 1)
     st = g.stats()
-    n_out = st["n_out"]
-    if dist is not None:
-        import torch
-        t = torch.tensor([n_out], dtype=torch.int64)
-        dist.all_reduce(t)
-        n_out = int(t.item())
+    got = group_checksum(cx, g)
+    n_out = int(cx.allreduce(st["n_out"], dtype="int64"))
+    occ = int(cx.allreduce(st["occurrences"], dtype="int64"))
     w = 2 if 256 + len(merges) <= 65536 else 4
     alg = total + n_out * w  # SURVEY 8(d): input bytes + n_out * w
-    out = {"metric": "encode MB/s, %g GiB stream through 32k merges" % (total / (1 << 30)), "value": round(total / 1e6 / el, 1),
+    out = {"metric": "encode MB/s, %g GiB stream through 32k merges" % (total / GIB), "value": round(total / 1e6 / el, 1),
            "unit": "MB/s", "ms": round(el * 1e3, 2), "n_gpus": world, "bytes": total, "merges": len(merges),
-           "n_out": n_out, "merges_md5": merges_md5, "shards": g.nshards, "batches": st["iterations"],
-           "candidates": st["candidates"],
-           "occurrences": st["occurrences"], "breakdown_ms": {"init": round(st["ms_init"], 2),
-                                                             "replay": round(st["ms_train"], 2)},
+           "n_out": n_out, "merges_md5": merges_md5, "ids_checksum": "%016x" % got[0],
+           "warm_ids_checksum": "%016x" % warm[0], "shards": g.nshards, "batches": st["iterations"],
+           "candidates": int(cx.allreduce(st["candidates"], dtype="int64")), "occurrences": occ,
+           "breakdown_ms": {"init": round(st["ms_init"], 2), "replay": round(st["ms_train"], 2)},
            "roofline": {"bound": "hbm", "achieved": round(alg / el / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 5),
                         "bytes": alg, "note": "whole-job algorithmic bytes (input + n_out*w) / wall"}}
+    errs = []
+    if warm != got:
+        errs.append("warm and timed encodes differ")
+    if n_out + occ != total or got[1] != n_out:
+        errs.append(f"n_out {n_out} + occurrences {occ} != bytes {total}")
+    if errs:
+        out["error"] = "; ".join(errs)
     g.close()
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_encode_baseline(merges, 3, args.cpu_encode_size)
@@ -164,176 +345,108 @@ def encode_bench(args, rank, world, local, dist, barrier):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1024, help="merge iterations timed")
-    ap.add_argument("--warmup", type=int, default=16, help="merge iterations of a throwaway run")
-    ap.add_argument("--size", type=int, default=1 << 30, help="corpus bytes per GPU")
+    ap.add_argument("--steps", type=int, default=3, help="training jobs timed")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed training jobs first")
+    ap.add_argument("--merges", type=int, default=None,
+                    help="merges per job (default: 8192 at N=1 = configs[2]; 1024 sharded = configs[3])")
+    ap.add_argument("--size", type=int, default=GIB, help="corpus bytes (the whole job, all ranks)")
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--xport", choices=("p2p", "rccl"), default=None, help="per-merge exchange (N > 1)")
+    ap.add_argument("--sharded", action="store_true", help="the sharded path even with one rank")
+    ap.add_argument("--no-extras", action="store_true", help="skip the 1024-merge / speed-up / weak legs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-size", type=int, default=64 << 20)
     ap.add_argument("--cpu-merges", type=int, default=16)
-    ap.add_argument("--sharded", action="store_true",
-                    help="use the sharded path even with one rank")
     ap.add_argument("--no-encode", action="store_true", help="skip the configs[4] encode measurement")
     ap.add_argument("--encode-size", type=int, default=10 << 30)
     ap.add_argument("--encode-merges", type=int, default=32768)
     ap.add_argument("--cpu-encode-size", type=int, default=256 << 10)
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal of the N-rank flow on a one-GPU box: every rank on this device
-    if os.environ.get("BPE_BENCH_DEVICE") is not None:
-        local = int(os.environ["BPE_BENCH_DEVICE"])
-    sharded = world > 1 or args.sharded
-    dist = None
+    sharded = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.sharded
+    cx = Ctx(sharded)
+    out = {}
     if sharded:
-        import torch
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29517")
-        torch.cuda.set_device(local)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-
-    from llmtokenizer_amd import api
-    if sharded:
-        from llmtokenizer_amd import dist as bdist
-        e = bdist.group(local, max(args.steps, args.warmup))
-        e.synth(0, args.seed, args.size, offset=rank * args.size)  # resident in HBM before timing
+        el, merges, st, prof, dig, extra = train_sharded(args, cx, out)
     else:
-        e = api.Engine(local)
-        e.synth(args.seed, args.size)
+        el, merges, st, prof, dig, extra = train_single(args, cx, out)
+    enc = None if args.no_encode else encode_bench(args, cx)
 
-    # warmup: a throwaway short run (kernels loaded, graphs captured, pools warm)
-    if args.warmup > 0:
-        e.train(args.warmup)
-
-    def barrier():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
-
-    barrier()
-    t0 = time.perf_counter()
-    k = e.train(args.steps)
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    same = True
-    if dist is not None:
-        import hashlib
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        digests = [None] * world
-        dist.all_gather_object(digests, hashlib.md5(e.merges().tobytes()).hexdigest())
-        same = len(set(digests)) == 1
-    st = e.stats()
-    transport = e.transport() if sharded else "none"
-    name, kms, kbytes, launches = e.kernel_profile()  # live, in-kernel wall clock
-    ev_ms, ev_n = 0.0, 0
-    if not sharded:
-        # corroboration with HIP events: event-record nodes spliced around every
-        # k_scan node of a second, shorter run (they add latency, so not in the timed run)
-        e.set_profile(True)
-        e.train(min(args.steps, 256))
-        ev_ms, ev_n = e.event_profile()
-        e.set_profile(False)
-    if dist is not None:
-        dist.barrier()
-    e.close()
-    enc = None
-    if not args.no_encode:
-        enc = encode_bench(args, rank, world, local, dist, barrier)
-
-    if rank != 0:
+    if cx.rank != 0:
         return
+    k = args.steps
     corpus_mb = args.size / 1e6
-    value = world * corpus_mb * k / elapsed
+    value = corpus_mb * merges * k / el
+    name, kms, kbytes, launches = prof
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    # count pass at SURVEY 8(d) widths: 1 B/token read (V = 256) + the fused
+    # initial id write at 2 B/token (V <= 65536); the engine stores u32 ids
+    V = 256 + merges
+    w_ids = 2 if V <= 65536 else 4
     cp_ms = st["ms_count_pass"]
-    cp_name = "k_pair_hist_span" if st["count_pass_span"] else "k_pair_hist"
-    # span form: the count pass also writes the initial u32 tokens (fused kernel:
-    # algorithmic bytes = 1 B/token read + 4 B/token write)
-    cp_bytes = args.size * (5 if st["count_pass_span"] else 1)
+    cp_bytes = args.size * (1 + w_ids) if st["count_pass_span"] else args.size
     cp_achieved = cp_bytes / (cp_ms * 1e-3) / 1e9 if cp_ms > 0 else 0.0
-    out = {
-        "metric": "corpus MB/s per merge iter (train), 1 GiB synthetic corpus per GPU",
+    world = cx.world
+    if sharded:
+        workload = (f"configs[3]: one 1 GiB corpus in {world} contiguous shards (one per rank), "
+                    f"{merges} merges per job, {k} jobs timed")
+    else:
+        workload = f"configs[2]: 1 GiB corpus, {merges} merges per job on one MI355X, {k} jobs timed"
+    out.update({
+        "metric": "corpus MB/s per merge iter (train), 1 GiB synthetic corpus",
         "value": round(value, 1),
         "unit": "corpus MB/s per merge iter",
         "n_gpus": world,
         "steps": k,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed * 1e3 / max(k, 1), 4),
+        "ms_per_step": round(el * 1e3 / max(k, 1), 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (random_text.txt-shaped, splitmix64 seed %d, generated in HBM)" % args.seed,
-        "config": {"workload": "configs[3]: 1 GiB corpus/GPU, %d merges" % args.steps,
-                   "corpus_bytes_per_gpu": args.size, "corpus_bytes_total": args.size * world, "merges": k,
-                   "parallelism": ("dp%d: one training job, %d contiguous corpus shards, per merge a sum of count "
-                                   "deltas + a gather of edge records over %s" %
-                                   (world, world, {"p2p": "xGMI P2P mailboxes", "rccl": "RCCL"}.get(transport, transport)))
-                   if sharded else "single GPU",
-                   "merges_identical_across_ranks": same},
-        # dominant kernel of the timed run: k_scan (latency-bound random gathers);
-        # algorithmic bytes per launch = 8 B/candidate + 20 B/occurrence
+        "config": {"workload": workload, "corpus_bytes": args.size, "merges_per_job": merges,
+                   "step": "one whole training job (count pass + merges + ids compaction)",
+                   "parallelism": (f"dp{world}: one training job over {world} contiguous corpus shards, per merge a "
+                                   "sum of count deltas + a gather of edge records") if sharded else "single GPU"},
+        "correctness": {"merges_md5": dig[0], "ids_checksum": "%016x" % dig[1],
+                        "checked": "warm-up job == timed jobs" if not sharded else "ranks agree"},
         "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "bytes_per_launch": round(kbytes), "avg_ms": round(kms, 5), "launches": launches,
-                     "avg_ms_source": "device wall clock inside the timed run (first block entry to the last block's retired memory operations)",
-                     "avg_ms_hip_events": round(ev_ms, 5) if ev_n else None, "hip_event_launches": ev_n,
-                     "note": "per-merge kernel is bound by dependent-load latency, not bandwidth; "
-                             "event nodes add their own latency to the measured span"},
-        # the one corpus-wide streaming pass (pair count over 1 B/token, V = 256)
-        "roofline_count_pass": {"kernel": cp_name, "bound": "hbm", "achieved": round(cp_achieved, 1),
-                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(cp_achieved / HBM_PEAK_GBS, 4),
+                     "window": "the last timed job (bytes and span from the same merges)",
+                     "avg_ms_source": "device wall clock (first block entry to the last block's retired "
+                                      "memory operations) inside the timed run",
+                     "note": "per-merge kernel: dependent random gathers, latency-bound"},
+        "roofline_count_pass": {"kernel": "k_pair_hist_span" if st["count_pass_span"] else "k_pair_hist",
+                                "bound": "hbm", "achieved": round(cp_achieved, 1), "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(cp_achieved / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": cp_bytes, "avg_ms": round(cp_ms, 4),
-                                "note": ("fused count pass + initial tok[] write: 1 B/token read + 4 B/token write"
-                                         if st["count_pass_span"] else "1 B/token read")},
+                                "note": f"SURVEY 8(d) widths: 1 B/token read + {w_ids} B/token fused id write "
+                                        "(the engine stores u32 ids: 5 B/token moved)"},
         "breakdown_ms": {"init": round(st["ms_init"], 3), "loop": round(st["ms_train"], 3),
-                         "total_engine": round(st["ms_total"], 3)},
+                         "total_engine": round(st["ms_total"], 3), "per_merge_us": round(st["ms_train"] * 1e3 / merges, 2)},
         "engine": {k2: st[k2] for k2 in ("n_out", "iterations", "distinct_pairs", "merged_buckets",
-                                          "tracked_iters", "tie_events", "edge_events", "rule_ties",
-                                          "table_grows", "keys", "l1_rescanned", "spec_hits",
+                                          "rule_ties", "table_grows", "keys", "l1_rescanned", "spec_hits",
                                           "spec_misses")},
-    }
-    # the committed rocprofv3 --kernel-trace --stats summary of this command
-    # (profiles/): its per-launch average includes dispatch and completion
-    # signalling, which the in-kernel span (first block entry -> last block
-    # exit) does not; both are reported
-    prof = sorted(glob.glob(os.path.join(ROOT, "profiles", "r1_v*_train_kernel_stats.csv")),
-                  key=lambda p: int(re.search(r"_v(\d+)_", p).group(1)))
-    if prof:
-        with open(prof[-1]) as f:
-            for r in csv.DictReader(f):
-                if r["Name"].split("(")[0].replace("bpeamd::", "").replace("void ", "").strip() == name:
-                    rp_ms = float(r["AverageNs"]) / 1e6
-                    out["roofline"]["avg_ms_rocprof"] = round(rp_ms, 5)
-                    out["roofline"]["frac_at_rocprof_avg"] = round(kbytes / (rp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                    out["roofline"]["rocprof_summary"] = os.path.relpath(prof[-1], ROOT)
-                    break
-    # HBM traffic per launch from the committed rocprofv3 PMC passes
-    # (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE in separate runs)
-    pmc = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            tr = json.load(f)
-        if name in tr:
-            out["roofline"]["traffic"] = tr[name]["traffic_bytes_per_launch"]
-            out["roofline"]["traffic_source"] = ("profiles/r1_pmc_traffic.json (FETCH_SIZE raw, uncalibrated for "
-                                                 "4-byte gathers, + WRITE_SIZE; 256-merge run)")
-        if cp_name in tr:
-            out["roofline_count_pass"]["traffic"] = tr[cp_name]["traffic_bytes_per_launch"]
+    })
+    out.update(extra)
+    cp = committed_profile(name)
+    out["roofline"].update({k2: v for k2, v in cp.items() if k2 != "traffic"})
+    if "traffic" in cp:
+        out["roofline"]["traffic"] = cp["traffic"]
+    if "avg_ms_rocprof" in cp:
+        out["roofline"]["frac_at_rocprof_avg"] = round(kbytes / (cp["avg_ms_rocprof"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.cpu_size, args.cpu_merges)
     if enc is not None:
         out["encode"] = enc
+        if "error" in enc:
+            out["error"] = (out.get("error", "") + "; encode: " + enc["error"]).lstrip("; ")
     print(json.dumps(out), flush=True)
+    if "error" in out:
+        print("bench: ERROR " + out["error"], file=sys.stderr, flush=True)
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -11,8 +11,8 @@
  *                         get_freq workers + hash_table_merge + flatten +
  *                         dyn_arr_max + replace pass
  *                         (bpe/src/bpe.c:428-527, 669-783;
- *                          hash_table/src/hash_table.c:147-345;
- *                          dyn_arr/src/dyn_arr.c:222-267)
+ *                          hash_table/src/hash_table.c:109-193, 195-307;
+ *                          dyn_arr/src/dyn_arr.c:136-181)
  *   bpe_gpu_fetch_ids  -- compress()'s *encoding output (bpe.c:785-794)
  *   bpe_gpu_encode     -- the replace pass (bpe.c:760-779) applied merge by
  *                         merge to new text (standalone encoder)
@@ -112,6 +112,12 @@ int bpe_gpu_decode(bpe_gpu_ctx *ctx, const uint32_t *ids, size_t len,
 
 int bpe_gpu_get_stats(bpe_gpu_ctx *ctx, bpe_gpu_stats *st);
 
+/* Position-keyed checksum of the ids of the last train / encode, computed in
+ * HBM: sum over i of mix64(mix64(base + i) ^ ids[i]) mod 2^64 (mix64 = the
+ * splitmix64 / murmur3 fmix64 finalizer).  A sequence held in pieces sums to
+ * the checksum of the whole when each piece passes its global start index. */
+int bpe_gpu_ids_checksum(bpe_gpu_ctx *ctx, uint64_t base, uint64_t *sum);
+
 /* device pointer of the loaded corpus bytes / ids (for in-HBM benchmarking) */
 int bpe_gpu_device_tokens(bpe_gpu_ctx *ctx, const void **dev_tok, size_t *n);
 
@@ -185,6 +191,9 @@ int bpe_gpu_group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merge
 int bpe_gpu_group_fetch_merges(bpe_gpu_group *g, uint32_t *pairs, size_t cap, size_t *count);
 int bpe_gpu_group_fetch_ids(bpe_gpu_group *g, int k, uint32_t *ids, size_t cap, size_t *len);
 int bpe_gpu_group_get_stats(bpe_gpu_group *g, bpe_gpu_stats *st);
+/* bpe_gpu_ids_checksum over the group's local shards in order (the first
+ * starting at global index `base`); *n_ids = the local ids counted */
+int bpe_gpu_group_ids_checksum(bpe_gpu_group *g, uint64_t base, uint64_t *sum, uint64_t *n_ids);
 /* bpe_gpu_kernel_profile of local shard k after a group train */
 int bpe_gpu_group_kernel_profile(bpe_gpu_group *g, int k, const char **name, double *avg_ms,
                                  double *bytes_per_launch, uint64_t *launches);

@@ -32,7 +32,7 @@ EXPORTS = [
     "bpe_gpu_group_load", "bpe_gpu_group_synth", "bpe_gpu_group_train", "bpe_gpu_group_encode", "bpe_gpu_group_fetch_merges",
     "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo", "bpe_gpu_group_kernel_profile",
     "bpe_gpu_group_create_p2p", "bpe_gpu_group_p2p_connect", "bpe_gpu_group_transport",
-    "bpe_gpu_group_create_local_p2p",
+    "bpe_gpu_group_create_local_p2p", "bpe_gpu_ids_checksum", "bpe_gpu_group_ids_checksum",
 ]
 
 
@@ -105,6 +105,9 @@ def load():
     L.bpe_gpu_encode.argtypes = [vp, vp, sz]
     L.bpe_gpu_decode.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats)]
+    L.bpe_gpu_ids_checksum.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    L.bpe_gpu_group_ids_checksum.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                             ctypes.POINTER(ctypes.c_uint64)]
     L.bpe_gpu_set_profile.argtypes = [vp, ctypes.c_int]
     L.bpe_gpu_event_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
     L.bpe_gpu_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]

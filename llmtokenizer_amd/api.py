@@ -240,6 +240,12 @@ class Engine:
         _lib.check(self.L.bpe_gpu_get_stats(self.ctx, ctypes.byref(st)), "stats")
         return st.as_dict()
 
+    def ids_checksum(self, base=0):
+        """position-keyed checksum of the ids in HBM (bpe_gpu_ids_checksum)"""
+        s = ctypes.c_uint64()
+        _lib.check(self.L.bpe_gpu_ids_checksum(self.ctx, int(base), ctypes.byref(s)), "ids_checksum")
+        return s.value
+
     def set_profile(self, on=True):
         _lib.check(self.L.bpe_gpu_set_profile(self.ctx, 1 if on else 0), "set_profile")
 
@@ -358,6 +364,13 @@ class ShardGroup:
         st = GpuStats()
         _lib.check(self.L.bpe_gpu_group_get_stats(self.g, ctypes.byref(st)), "stats")
         return st.as_dict()
+
+    def ids_checksum(self, base=0):
+        """(checksum, n_ids) of the local shards' ids, the first at global index base"""
+        s, n = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.check(self.L.bpe_gpu_group_ids_checksum(self.g, int(base), ctypes.byref(s), ctypes.byref(n)),
+                   "ids_checksum")
+        return s.value, n.value
 
     def kernel_profile(self, k=0):
         name = ctypes.c_char_p()

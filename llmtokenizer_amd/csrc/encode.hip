@@ -360,7 +360,6 @@ __global__ __launch_bounds__(256) void k_apply_batch(const Eng *__restrict__ E, 
             C->counters[5] += spre[nb];
             C->counters[6]++;  // batches
             C->n_live -= spre[nb];
-            C->ebp = p ^ 1;
             const uint32_t xl = SH ? C->xleft : HOLE;
             if (xl != HOLE) {
                 tok[xl] = HOLE;
@@ -398,7 +397,7 @@ __global__ __launch_bounds__(256) void k_apply_batch(const Eng *__restrict__ E, 
 template <bool SH>
 __global__ __launch_bounds__(256) void k_link_batch(const Eng *__restrict__ E, const Ctl *__restrict__ C) {
     if (C->stop) return;
-    const EncBatch *B = E->eb + (C->ebp ^ 1u);  // k_apply_batch already flipped to the next batch
+    const EncBatch *B = E->eb + C->ebp;
     const uint32_t nb = B->nbg;
     __shared__ uint32_t sseg[BMAX + 1], sz[BMAX], sR[BMAX], spre[BMAX + 1];
     const uint32_t tid = threadIdx.x;
@@ -422,6 +421,16 @@ __global__ __launch_bounds__(256) void k_link_batch(const Eng *__restrict__ E, c
         const int64_t k = i + E->tlen[sz[m]];
         E->occnb[e] = nb_tag(ps >= 0 ? tok[ps] : HOLE, k < n ? tok[k] : HOLE);
     }
+}
+
+// Switch to the descriptor k_apply_batch's last block formed.  A kernel of its
+// own: every block of scan / apply / link reads C->ebp on entry, and blocks of
+// one launch are dispatched over several XCDs in no fixed order, so a flip
+// inside any of them could be seen by a block that has not started yet (it
+// would then work on the next batch's descriptor with R = 0 and a stale nbg).
+__global__ void k_enc_flip(Ctl *__restrict__ C) {
+    if (C->stop) return;
+    if (threadIdx.x == 0) C->ebp ^= 1u;
 }
 
 }  // namespace bpeamd

@@ -602,6 +602,7 @@ int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint
             k_scan_batch<false><<<SCAN_BLOCKS, ESCAN_T, 0, c->st>>>(c->dE, c->dC);
             k_apply_batch<false><<<ENC_APPLY_BLOCKS + 1, 256, 0, c->st>>>(c->dE, c->dC);
             k_link_batch<false><<<ENC_APPLY_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+            k_enc_flip<<<1, 64, 0, c->st>>>(c->dC);
         } else {
             launch_iteration(c, tracked);
         }
@@ -1414,6 +1415,9 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
         c->stats.occurrences = c->hC->counters[5];
     }
     if ((r = compact_ids(c))) return r;
+    // every applied occurrence removes exactly one token
+    if (c->n0 >= 2 && n_merges && c->ids_len != c->n0 - c->hC->counters[5])
+        return fail(BPE_GPU_EINTERNAL, "encode: n_out != n_in - occurrences");
     const double t1 = now_ms();
     c->merges_done = 0;
     c->stats.n_out = c->ids_len;
@@ -1511,6 +1515,23 @@ int bpe_gpu_event_profile(bpe_gpu_ctx *c, double *avg_ms, uint64_t *launches) {
     if (!c || !avg_ms || !launches) return BPE_GPU_EINVAL;
     *avg_ms = c->event_ms;
     *launches = c->event_n;
+    return 0;
+}
+
+int bpe_gpu_ids_checksum(bpe_gpu_ctx *c, uint64_t base, uint64_t *sum) {
+    if (!c || !sum) return BPE_GPU_EINVAL;
+    if (!c->ids_ready) return fail(BPE_GPU_ESTATE, "no ids: train or encode first");
+    HIPCHK(hipSetDevice(c->dev));
+    unsigned long long *d = nullptr, h = 0;
+    HIPCHK(hipMalloc(&d, 8));
+    HIPCHK(hipMemsetAsync(d, 0, 8, c->st));
+    if (c->ids_len) k_ids_checksum<<<2048, 256, 0, c->st>>>(c->h.ids_out, c->ids_len, base, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(BPE_GPU_EHIP, "ids checksum", e);
+    *sum = h;
     return 0;
 }
 

@@ -287,7 +287,7 @@ __host__ __device__ inline uint64_t mix64(uint64_t x) {
 
 // B_final of the reference's merged table for D distinct keys: the table
 // starts at 65536 buckets and doubles at every insert call made while
-// num_of_nodes >= 0.3 * buckets (hash_table.c:286-292, evaluated in double).
+// num_of_nodes >= 0.3 * buckets (hash_table.c:248-254, evaluated in double).
 // *edge = 1 when D equals a threshold exactly, i.e. the last doubling depends
 // on whether another insert call followed the D-th new key.
 __host__ __device__ inline uint64_t bfinal_nominal(uint64_t D, uint32_t *edge) {

@@ -2547,6 +2547,21 @@ __global__ void k_synth(uint8_t *__restrict__ out, uint64_t n, uint64_t seed, ui
     }
 }
 
+// ------------------------------------------------------------------ checksum
+// Position-keyed checksum of an id sequence: sum over i of
+// mix64(mix64(base + i) ^ ids[i]) mod 2^64.  The sum commutes, so the result
+// does not depend on the block schedule, and a sequence cut into pieces sums
+// to the same value when each piece passes its global start as `base`
+// (tests/golden_lib.py ids_checksum is the numpy form).
+__global__ __launch_bounds__(256) void k_ids_checksum(const uint32_t *__restrict__ ids, uint64_t n, uint64_t base,
+                                                      unsigned long long *__restrict__ out) {
+    uint64_t s = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        s += mix64(mix64(base + i) ^ ids[i]);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)s);
+}
+
 // ------------------------------------------------------------------ decode
 // elen[id] = non-NUL byte count of id's expansion (the reference concatenates
 // C strings, so NUL bytes vanish: bpe.c:47-54, 76-77).  A record whose first

@@ -191,6 +191,7 @@ int launch_group_batch(bpe_gpu_group *g) {
     for (bpe_gpu_ctx *c : g->cs) k_scan_batch<true><<<SCAN_BLOCKS, ESCAN_T, 0, g->st>>>(c->dE, c->dC);
     for (bpe_gpu_ctx *c : g->cs) k_apply_batch<true><<<ENC_APPLY_BLOCKS + 1, 256, 0, g->st>>>(c->dE, c->dC);
     for (bpe_gpu_ctx *c : g->cs) k_link_batch<true><<<ENC_APPLY_BLOCKS, 256, 0, g->st>>>(c->dE, c->dC);
+    for (bpe_gpu_ctx *c : g->cs) k_enc_flip<<<1, 64, 0, g->st>>>(c->dC);
     for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 0);
     HIPCHK(hipGetLastError());
     return ex_records(g, g->d_ptrs);
@@ -593,6 +594,10 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
         g->stats.candidates += c->hC->counters[4];
         g->stats.occurrences += c->hC->counters[5];
     }
+    // every applied occurrence removes exactly one token (checkable here when
+    // the group holds every shard; across ranks the caller sums n_out)
+    if (K == g->nshards && nout != ntot - g->stats.occurrences)
+        return fail(BPE_GPU_EINTERNAL, "group encode: n_out != n_in - occurrences");
     g->stats.ms_init = t1 - t0;
     g->stats.ms_train = t2 - t1;
     g->stats.ms_total = t2 - t0;
@@ -857,6 +862,21 @@ int bpe_gpu_group_fetch_ids(bpe_gpu_group *g, int k, uint32_t *ids, size_t cap, 
     bpe_gpu_ctx *c = group_shard(g, k);
     if (!c) return BPE_GPU_EINVAL;
     return bpe_gpu_fetch_ids(c, ids, cap, len);
+}
+
+int bpe_gpu_group_ids_checksum(bpe_gpu_group *g, uint64_t base, uint64_t *sum, uint64_t *n_ids) {
+    if (!g || !sum) return BPE_GPU_EINVAL;
+    uint64_t tot = 0, n = 0;
+    for (bpe_gpu_ctx *c : g->cs) {
+        uint64_t s = 0;
+        int r;
+        if ((r = bpe_gpu_ids_checksum(c, base + n, &s))) return r;
+        tot += s;
+        n += c->ids_len;
+    }
+    *sum = tot;
+    if (n_ids) *n_ids = n;
+    return 0;
 }
 
 int bpe_gpu_group_get_stats(bpe_gpu_group *g, bpe_gpu_stats *st) {

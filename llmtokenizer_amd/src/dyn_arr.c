@@ -8,7 +8,7 @@
  *   - get() fails only when the page is missing (an unwritten slot inside an
  *     allocated page reads whatever the page holds, as in the reference);
  *   - max()/min() keep the FIRST extreme element (strict comparison), which
- *     is the merge tie rule of dyn_arr_max (dyn_arr.c:249-260);
+ *     is the merge tie rule of dyn_arr_max (dyn_arr.c:136-181, first strict max at :170);
  *   - sort() is a merge sort with the reference's split and tie rule.
  * Deliberate fixes (no effect on results): create(0, ...) initialises
  * last_index, and page-table growth never takes log2(0).
@@ -119,7 +119,7 @@ bool dyn_arr_min(dyn_arr_t *d, size_t start_index, size_t end_index, dyn_compare
 }
 
 /* Top-down merge sort over a flat copy.  Same split (mid = lo + (hi-lo)/2)
- * and merge rule as the reference (dyn_arr.c:316-479): the left element is
+ * and merge rule as the reference (dyn_arr.c:230-393): the left element is
  * taken iff compare(left, right), so equal elements may swap exactly as they
  * do there. */
 static void msort(char *a, char *tmp, size_t lo, size_t hi, size_t w, dyn_compare_t cmp)

@@ -84,25 +84,35 @@ def cases(big: bool):
     return c
 
 
-def run_ref(data: bytes, max_merges: int):
+# fixtures that also keep the reference's own dump_pairs file (bpe.c:243-278)
+# and main.c's stdout (print_text of the encoding, bpe.c:182-196)
+WITH_IO = ("prose", "synth_s1_4k", "aab_runs", "binary_5k", "nul_truncates")
+
+
+def run_ref(data: bytes, max_merges: int, with_io=False):
     with tempfile.TemporaryDirectory() as td:
         inp = os.path.join(td, "in.bin")
         with open(inp, "wb") as f:
             f.write(data)
-        mo, io_ = os.path.join(td, "m.txt"), os.path.join(td, "i.bin")
-        env = dict(os.environ, BPE_REF_MAX_MERGES=str(max_merges))
+        mo, io_, po = os.path.join(td, "m.txt"), os.path.join(td, "i.bin"), os.path.join(td, "p.bin")
+        env = dict(os.environ, BPE_REF_MAX_MERGES=str(max_merges), BPE_REF_PRINT="1" if with_io else "0")
         t0 = time.time()
-        p = subprocess.run([REF, inp, mo, io_], env=env, capture_output=True, text=True)
+        p = subprocess.run([REF, inp, mo, io_] + ([po] if with_io else []), env=env, capture_output=True)
         dt = time.time() - t0
         if p.returncode != 0:
-            return dict(error=True, stdout=p.stdout, seconds=dt)
+            return dict(error=True, stdout=p.stdout.decode(errors="replace"), seconds=dt)
         merges = []
         with open(mo) as f:
             for line in f:
                 i, a, b = line.split()
                 merges.append([int(a), int(b)])
         ids = np.fromfile(io_, dtype="<u4")
-        return dict(error=False, merges=merges, ids=ids, seconds=dt, stdout=p.stdout)
+        out = dict(error=False, merges=merges, ids=ids, seconds=dt)
+        if with_io:
+            with open(po, "rb") as f:
+                out["pairs_file"] = f.read()
+            out["print_text"] = p.stdout
+        return out
 
 
 def main():
@@ -119,7 +129,7 @@ def main():
         data = c.get("data")
         if data is None:
             data = synth_bytes(c["seed"], c["n"])
-        r = run_ref(data, c["max_merges"])
+        r = run_ref(data, c["max_merges"], with_io=c["name"] in WITH_IO)
         fx = dict(name=c["name"], max_merges=c["max_merges"], generator="oracle/make_goldens.py",
                   ref_seconds=round(r["seconds"], 3))
         if "data" in c:
@@ -136,6 +146,10 @@ def main():
             fx["ids_md5"] = hashlib.md5(ids.astype("<u4").tobytes()).hexdigest()
             if ids.size <= 4096:
                 fx["ids"] = ids.tolist()
+            if "pairs_file" in r:
+                fx["dump_pairs_b64"] = base64.b64encode(r["pairs_file"]).decode()
+                fx["print_text_md5"] = hashlib.md5(r["print_text"]).hexdigest()
+                fx["print_text_len"] = len(r["print_text"])
         with open(os.path.join(GOLD, c["name"] + ".json"), "w") as f:
             json.dump(fx, f, separators=(",", ":"))
         print(f"{c['name']}: merges={len(fx.get('merges', []))} ids_len={fx.get('ids_len')} "

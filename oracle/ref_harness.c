@@ -8,6 +8,11 @@
  *
  *   merges file : one line per merge, "id a b\n"  (ids 256..)
  *   ids file    : the final encoding as raw little-endian u32
+ *   pairs file  : (optional 4th argument) the merge list written by the
+ *                 reference's own dump_pairs (bpe.c:243-278), raw 8-byte
+ *                 records, final merge dropped, as the reference writes it
+ *   stdout      : with BPE_REF_PRINT=1, the reference's own print_text of the
+ *                 encoding (bpe.c:182-196) -- main.c's output (main.c:20)
  *
  * Merge cap without editing the reference: the build links this file with
  * -Wl,--wrap=hash_table_merge.  compress() calls hash_table_merge once per
@@ -17,7 +22,7 @@
  * environment variable BPE_REF_MAX_MERGES (unset / negative = uncapped, the
  * reference default).
  *
- * usage: bpe_ref <corpus> <merges_out> <ids_out>
+ * usage: bpe_ref <corpus> <merges_out> <ids_out> [<pairs_out>]
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -37,6 +42,8 @@ typedef bool (*ref_add_fn)(const void *, const void *, const void *);
 extern ref_dyn_arr_t *compress(const char *path, uint32_t **encoding, size_t *len);
 extern bool dyn_arr_get(ref_dyn_arr_t *arr, size_t index, void *out);
 extern void dyn_arr_free(ref_dyn_arr_t *arr);
+extern bool dump_pairs(const char *path, ref_dyn_arr_t *pair_arr);
+extern void print_text(const uint32_t *text, int length);
 extern void *hash_table_create(size_t nb, size_t ks, size_t vs);
 extern void *__real_hash_table_merge(void **tables, size_t len, ref_add_fn add,
                                      size_t ks, size_t vs, size_t nb);
@@ -89,6 +96,15 @@ int main(int argc, char **argv)
     if (len) fwrite(enc, sizeof(uint32_t), len, fi);
     fclose(fm);
     fclose(fi);
+    if (argc > 4 && !dump_pairs(argv[4], pairs)) {
+        fprintf(stderr, "dump_pairs failed\n");
+        return 1;
+    }
+    const char *pr = getenv("BPE_REF_PRINT");
+    if (pr && *pr == '1') {
+        print_text(enc, (int)len);
+        fflush(stdout);
+    }
     /* one machine-readable summary line on stderr: merges, len, seconds */
     fprintf(stderr, "REF merges=%zu len=%zu seconds=%.6f iterations=%ld\n",
             merges, len, secs, g_calls);

@@ -56,3 +56,23 @@ def check(fx, merges, ids):
     ids = np.asarray(ids, dtype=np.uint32)
     assert ids.size == fx["ids_len"], f"{fx['name']}: len {ids.size} vs {fx['ids_len']}"
     assert ids_md5(ids) == fx["ids_md5"], f"{fx['name']}: ids differ"
+
+
+def _mix64(x):
+    x = x ^ (x >> np.uint64(33))
+    x = x * np.uint64(0xFF51AFD7ED558CCD)
+    x = x ^ (x >> np.uint64(33))
+    x = x * np.uint64(0xC4CEB9FE1A85EC53)
+    return x ^ (x >> np.uint64(33))
+
+
+def ids_checksum(ids, base=0, chunk=1 << 24) -> int:
+    """numpy form of bpe_gpu_ids_checksum: sum_i mix64(mix64(base + i) ^ ids[i]) mod 2^64"""
+    ids = np.asarray(ids, dtype=np.uint32)
+    tot = 0
+    with np.errstate(over="ignore"):
+        for s in range(0, ids.size, chunk):
+            part = ids[s:s + chunk].astype(np.uint64)
+            pos = np.arange(base + s, base + s + part.size, dtype=np.uint64)
+            tot = (tot + int(_mix64(_mix64(pos) ^ part).sum(dtype=np.uint64))) & ((1 << 64) - 1)
+    return tot

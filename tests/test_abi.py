@@ -73,6 +73,56 @@ def test_dump_read_pairs_format(tmp_path):
     assert back.tolist() == merges[:3].tolist()
 
 
+IO_FIXTURES = ["prose", "synth_s1_4k", "aab_runs", "binary_5k", "nul_truncates"]
+
+
+@pytest.mark.parametrize("name", IO_FIXTURES)
+def test_dump_pairs_matches_reference_file(name, tmp_path):
+    """Merge-list files against ones the reference's own dump_pairs wrote
+    (bpe.c:243-278, fixture dump_pairs_b64 from oracle/_ref): our dump_pairs
+    writes the same bytes (last merge dropped, 8-byte LE records from id 256)
+    and our read_pairs (bpe.c:280-339) reads the reference's file back."""
+    import base64
+    import golden_lib as G
+    fx = G.load(name)
+    ref = base64.b64decode(fx["dump_pairs_b64"])
+    merges = np.asarray(fx["merges"], dtype=np.uint32).reshape(-1, 2)
+    assert len(ref) == 8 * (merges.shape[0] - 1)
+    p = tmp_path / "ours.bin"
+    api.dump_pairs(str(p), merges)
+    assert p.read_bytes() == ref
+    q = tmp_path / "ref.bin"
+    q.write_bytes(ref)
+    assert api.read_pairs(str(q)).tolist() == merges[:-1].tolist()
+
+
+@pytest.mark.parametrize("name", IO_FIXTURES)
+def test_print_text_matches_reference_stdout(name):
+    """print_text (bpe.c:182-196) of the reference's ids prints exactly what
+    the reference's main.c printed (fixture print_text_md5); host-only call."""
+    import hashlib
+    import sys
+    import golden_lib as G
+    import oracle_lib as O
+    fx = G.load(name)
+    ids = fx.get("ids")
+    if ids is None:  # (not inline: the oracle's replay, pinned to the reference by ids_md5)
+        ids = O.encode(O.effective_bytes(G.input_bytes(fx)), np.asarray(fx["merges"], dtype=np.uint32))
+        assert G.ids_md5(ids) == fx["ids_md5"]
+        ids = ids.tolist()
+    code = ("import ctypes,sys,json; sys.path.insert(0, %r); from llmtokenizer_amd import _lib; L=_lib.load(); "
+            "ids=json.loads(sys.stdin.read()); a=(ctypes.c_uint32*max(1,len(ids)))(*ids); "
+            "L.print_text(a, len(ids)); ctypes.CDLL(None).fflush(None)" % ROOT)
+    out = subprocess.run([sys.executable, "-c", code], input=json_dumps(ids), capture_output=True, check=True).stdout
+    assert len(out) == fx["print_text_len"]
+    assert hashlib.md5(out).hexdigest() == fx["print_text_md5"]
+
+
+def json_dumps(x):
+    import json
+    return json.dumps(x).encode()
+
+
 def test_hash_table_order_matches_reference_model():
     """Host hash_table: murmur buckets, head insertion, 0.3 doubling -- the
     iteration order a caller walking table->buckets would observe."""
@@ -135,7 +185,7 @@ def test_dyn_arr_max_first_strict_max():
                               ctypes.c_void_p]
     L.dyn_arr_max.restype = ctypes.c_bool
     assert L.dyn_arr_max(arr, 0, 3, ctypes.cast(L.is_less, ctypes.c_void_p), ctypes.cast(out, ctypes.c_void_p))
-    assert list(out) == [3, 4, 9]  # first of the two 9s, as dyn_arr.c:256 keeps
+    assert list(out) == [3, 4, 9]  # first of the two 9s, as dyn_arr.c:170 keeps
     assert arr.contents.last_index == 3
     L.dyn_arr_free(arr)
 

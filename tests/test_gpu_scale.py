@@ -1,0 +1,174 @@
+"""BASELINE configs at their full sizes on one MI355X (SURVEY.md 8(d) "parity
+at scale").  The oracle cannot train 1 GiB x 8192 merges end to end, so:
+
+  configs[2]  1 GiB x 8192 merges: spot checks -- the GPU's token array after
+              t merges is copied back and the CPU restatement recounts every
+              pair and picks the next merge (oracle_next_merge, RULE order =
+              the reference's own at >= 2^20 tokens); it must be merge t of the
+              GPU run, for t = 1024, 4096, 8191.  Plus: the standalone encoder
+              replaying the 8192 merges gives the training ids (checksums).
+  configs[3]  the 1 GiB corpus in 8 contiguous shards on one device == the
+              single engine at 1024 merges, and == the reference goldens
+              (1 GiB x 4 merges) at k = 8.
+  configs[4]  a 3 GiB stream through a 32k-merge list: one context, 2 shards
+              and 4 uneven shards give the same ids checksum and length; decode
+              of id windows gives the stream's bytes back; a 256 KiB chunk
+              encoded alone matches the oracle.
+Plus the reference CLI (main.c) run through tools/bpe_main: its stdout equals
+what the reference's main.c printed (fixture print_text_md5)."""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import golden_lib as G
+import oracle_lib as O
+from llmtokenizer_amd import api
+from llmtokenizer_amd.synth import synth_bytes
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GIB = 1 << 30
+
+
+def _elen(merges):
+    """byte length of every id's expansion (no NUL in the synthetic corpora)"""
+    V = 256 + merges.shape[0]
+    el = np.ones(V, dtype=np.int64)
+    for r, (a, b) in enumerate(merges.tolist()):
+        el[256 + r] = el[a] + el[b]
+    return el
+
+
+def test_device_checksum_is_the_numpy_form():
+    data = synth_bytes(12, 3 << 20)
+    e = api.Engine(0)
+    e.load(data)
+    e.train(300)
+    ids = e.ids()
+    assert e.ids_checksum() == G.ids_checksum(ids)
+    assert e.ids_checksum(base=12345) == G.ids_checksum(ids, base=12345)
+    g = api.ShardGroup(0, local_shards=3)
+    g.load_split(data, [0, 1000, 2 << 20, len(data)])
+    g.encode(e.merges())
+    s, n = g.ids_checksum()
+    assert n == ids.size and s == G.ids_checksum(ids)
+    e.close()
+    g.close()
+
+
+def test_config2_1g_8192_merges_spot_checks():
+    e = api.Engine(0)
+    e.synth(2, GIB)
+    k = e.train(8192)
+    assert k == 8192
+    M = e.merges()
+    st = e.stats()
+    csum = e.ids_checksum()
+    n_out = st["n_out"]
+    e.close()
+    # the encoder replaying the learned list lands on the training ids
+    x = api.Engine(0)
+    x.synth(2, GIB)
+    x.encode(M)
+    assert x.stats()["n_out"] == n_out
+    assert x.ids_checksum() == csum
+    x.close()
+    # spot checks: recount on the CPU after t merges -> merge t
+    t3 = api.Engine(0)
+    t3.synth(2, GIB)
+    for t in (1024, 4096, 8191):
+        assert t3.train(t) == t
+        assert (t3.merges() == M[:t]).all()  # prefix property
+        ids = t3.ids()
+        nm = O.next_merge(ids, 256 + t)
+        assert nm is not None, t
+        assert (nm[0], nm[1]) == tuple(M[t].tolist()), (t, nm, M[t])
+        del ids
+    t3.close()
+
+
+def test_config3_1g_eight_shards_equals_single_engine():
+    e = api.Engine(0)
+    e.synth(2, GIB)
+    assert e.train(1024) == 1024
+    M, csum, n_out = e.merges(), e.ids_checksum(), e.stats()["n_out"]
+    e.close()
+    g = api.ShardGroup(0, local_shards=8)
+    step = GIB // 8
+    for q in range(8):
+        g.synth(q, 2, step, q * step)
+    assert g.train(1024) == 1024
+    assert (g.merges() == M).all()
+    s, n = g.ids_checksum()
+    assert n == n_out and s == csum
+    g.close()
+
+
+def test_config3_reference_golden_at_eight_shards():
+    fx = G.load("synth_s2_1g")
+    g = api.ShardGroup(0, local_shards=8)
+    n = fx["synth"]["n"]
+    cuts = [0, 1, 77777777, n // 3, n // 2, n // 2 + 2, 3 * n // 4, n - 5, n]  # uneven, 1- and 2-byte shards
+    for q in range(8):
+        g.synth(q, fx["synth"]["seed"], cuts[q + 1] - cuts[q], cuts[q])
+    g.train(fx["max_merges"])
+    G.check(fx, g.merges(), g.all_ids())
+    g.close()
+
+
+def test_config4_encode_3g_through_32k_merges_cut_independent():
+    tr = api.Engine(0)
+    tr.synth(2, GIB)
+    assert tr.train(32768) == 32768
+    M = tr.merges()
+    tr.close()
+    n = 3 * GIB
+    one = api.Engine(0)
+    one.synth(3, n)
+    one.encode(M)
+    st = one.stats()
+    assert st["n_out"] == n - st["occurrences"]
+    want = one.ids_checksum()
+    ids = one.ids()
+    one.close()
+    assert ids.size == st["n_out"]
+    for cuts in ([0, GIB + 12345, n], [0, 1, GIB // 3, 2 * GIB + 7, n]):
+        g = api.ShardGroup(0, local_shards=len(cuts) - 1)
+        for q in range(len(cuts) - 1):
+            g.synth(q, 3, cuts[q + 1] - cuts[q], cuts[q])
+        g.encode(M)
+        gs = g.stats()
+        got, cnt = g.ids_checksum()
+        assert cnt == ids.size and gs["n_out"] == ids.size, cuts
+        assert got == want, cuts
+        g.close()
+    # decode(encode(x)) == x on windows of the ids
+    el = _elen(M)
+    starts = np.concatenate([[0], np.cumsum(el[ids], dtype=np.int64)])
+    d = api.Engine(0)
+    for s in (0, ids.size // 2, ids.size - (1 << 20)):
+        w = ids[s:s + (1 << 20)]
+        out = d.decode(w, M)
+        assert len(out) == starts[s + w.size] - starts[s]
+        assert out == synth_bytes(3, len(out), lo=int(starts[s]))
+    # a chunk encoded alone, against the oracle's sequential replace passes
+    chunk = synth_bytes(3, 256 << 10, lo=5 * (1 << 28))
+    assert (api.encode(chunk, M) == O.encode(chunk, M)).all()
+    d.close()
+
+
+@pytest.mark.parametrize("name", ["prose", "synth_s1_4k", "binary_5k", "nul_truncates"])
+def test_cli_matches_reference_main_stdout(name, tmp_path):
+    """tools/bpe_main (the reference's main.c contract, main.c:14-23) on the
+    GPU: stdout == the reference main.c's stdout on the same file."""
+    fx = G.load(name)
+    p = tmp_path / (name + ".txt")
+    p.write_bytes(G.input_bytes(fx))
+    out = subprocess.run([os.path.join(ROOT, "tools", "bpe_main"), str(p)], capture_output=True, check=True,
+                         timeout=60).stdout
+    assert len(out) == fx["print_text_len"]
+    assert hashlib.md5(out).hexdigest() == fx["print_text_md5"]

@@ -85,7 +85,7 @@ REF_FILES = {
 }
 
 
-@pytest.mark.parametrize("fname", ["testing.txt"])
+@pytest.mark.parametrize("fname", ["testing.txt", pytest.param("random_text.txt", marks=pytest.mark.slow)])
 def test_reference_corpus_hashes(fname):
     """Hashes of the reference run on its own corpora; only in
     the build container, where /root/reference exists."""
@@ -99,3 +99,34 @@ def test_reference_corpus_hashes(fname):
     txt = "".join(f"{256 + r} {a} {b}\n" for r, (a, b) in enumerate(merges.tolist()))
     assert hashlib.md5(txt.encode()).hexdigest() == m_md5
     assert G.ids_md5(ids) == i_md5
+
+
+def test_next_merge_matches_training():
+    """oracle_next_merge (one full recount + the RULE order) picks, on the ids
+    after t merges, exactly merge t of a RULE training run -- the spot check
+    tests/test_gpu_scale.py applies to long GPU runs.  Both count paths (dense
+    V x V and the open hash)."""
+    from llmtokenizer_amd.synth import synth_bytes
+    data = synth_bytes(11, (1 << 20) + 4096)  # >= 2^20 tokens: RULE == the reference's outcome
+    merges, _, _ = O.train(data, 12, O.RULE)
+    assert merges.shape[0] == 12
+    for t in (0, 1, 5, 11):
+        ids = O.encode(data, merges[:t])
+        for V in (256 + t, 20000):
+            got = O.next_merge(ids, V)
+            assert got is not None and (got[0], got[1]) == tuple(merges[t].tolist()), (t, V, got)
+    assert O.next_merge(np.arange(100, dtype=np.uint32), 100) is None  # every count 1: stop
+
+
+def test_ids_checksum_splits():
+    """The position-keyed checksum of a sequence equals the sum of its pieces'
+    (each piece at its global start), and moves when one id or position moves."""
+    rng = np.random.default_rng(3)
+    ids = rng.integers(0, 40000, 100003, dtype=np.uint32)
+    whole = G.ids_checksum(ids)
+    for cut in (1, 777, 50000, 100002):
+        assert (G.ids_checksum(ids[:cut]) + G.ids_checksum(ids[cut:], base=cut)) % (1 << 64) == whole
+    ids2 = ids.copy()
+    ids2[500] ^= 1
+    assert G.ids_checksum(ids2) != whole
+    assert G.ids_checksum(ids[1:]) != G.ids_checksum(ids[:-1])
