@@ -73,6 +73,13 @@ uint32_t SPEC_RB = 64, SPEC_SB = 192;
 uint32_t FUSED_A = 64, FUSED_B = 16;  // k_fused apply blocks (1024 threads): span rewrite, table update
 bool SPEC_ON = true;
 bool PIPE_ON = !getenv("BPE_PIPE") || atoi(getenv("BPE_PIPE")) != 0;  // pipelined graph replays (drive)
+// BPE_GRAPH=0: the 16-iteration "graphs" are launched kernel by kernel (for
+// profilers that do not follow graph replays; the device work is the same)
+bool GRAPH_ON = !getenv("BPE_GRAPH") || atoi(getenv("BPE_GRAPH")) != 0;
+// BPE_HOT=0: the level summaries instead of the hot-set argmax (A/B runs)
+bool HOT_ON = !getenv("BPE_HOT") || atoi(getenv("BPE_HOT")) != 0;
+enum : uintptr_t { NOGRAPH_PLAIN = 1, NOGRAPH_TRACKED = 2, NOGRAPH_ENCODE = 3 };
+inline bool real_graph(hipGraphExec_t g) { return (uintptr_t)g > NOGRAPH_ENCODE; }
 struct SpecInit {
     SpecInit() {
         if (const char *e = getenv("BPE_SPEC")) SPEC_ON = atoi(e) != 0;
@@ -228,6 +235,7 @@ struct bpe_gpu_ctx {
     uint32_t *d_tileoff = nullptr;
     uint32_t *d_enc_pairs = nullptr;
     hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr;
+    bool hot_fallback = false;  // the hot set was given up for the level summaries
     std::vector<hipGraphExec_t> retired;  // replaced graphs, destroyed with the run
     bpe_gpu_stats stats{};
     // profile of the dominant kernel: HIP events captured around every k_scan
@@ -291,10 +299,11 @@ void free_train(bpe_gpu_ctx *c, bool release = false) {
         c->pool.clear();
     }
     for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked, &c->g_encode}) {
-        if (*g) (void)hipGraphExecDestroy(*g);
+        if (real_graph(*g)) (void)hipGraphExecDestroy(*g);
         *g = nullptr;
     }
-    for (hipGraphExec_t g : c->retired) (void)hipGraphExecDestroy(g);
+    for (hipGraphExec_t g : c->retired)
+        if (real_graph(g)) (void)hipGraphExecDestroy(g);
     c->retired.clear();
     c->ids_ready = false;
 }
@@ -371,6 +380,22 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if (getenv("BPE_DEBUG_TS") && !encode && (r = dalloc(c, &h.dbgts, (size_t)TS_SLOTS * TS_N))) return r;
     h.spec_on = SPEC_ON && !encode && (!c->sharded || h.xfused);
     h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? 1 + SPEC_RB + SPEC_SB : 0);
+    // hot-set argmax: untracked one-shard training with the speculative graph
+    h.hot = HOT_ON && h.spec_on && !c->sharded && (c->fast || n0 >= TRACK_LIMIT) ? 1 : 0;
+    h.hot_parts = SPEC_RB;
+    h.hot_target = HOT_TARGET;
+    if (const char *t = getenv("BPE_HOT_TARGET")) h.hot_target = std::max(1, std::min(atoi(t), (int)HOT_TARGET));
+    h.hot_slot = h.hot_hist = h.hotp_tie = nullptr;
+    h.hotp_best = h.hotp_key = h.hotp_v2 = h.hotp_k2 = nullptr;
+    if (h.hot) {
+        if ((r = dalloc(c, &h.hot_slot, HOT_CAP, false))) return r;
+        if ((r = dalloc(c, &h.hot_hist, HOT_BINS))) return r;
+        if ((r = dalloc(c, &h.hotp_best, SPEC_RB))) return r;
+        if ((r = dalloc(c, &h.hotp_key, SPEC_RB))) return r;
+        if ((r = dalloc(c, &h.hotp_v2, SPEC_RB))) return r;
+        if ((r = dalloc(c, &h.hotp_k2, SPEC_RB))) return r;
+        if ((r = dalloc(c, &h.hotp_tie, SPEC_RB))) return r;
+    }
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
     if ((r = dalloc(c, &c->d_tileoff, h.ntiles + 1))) return r;
@@ -382,14 +407,17 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.sfirst, h.scap))) return r;
     // pair table
     if (!encode) {
-        // keys (distinct pairs ever seen) grow by up to ~1.2 k per merge on
-        // uniform text (1 GiB: 1.25 M after 1024 merges) and never exceed the
-        // positions: size for that under the half-full rule so that typical
-        // runs never regrow (a regrowth is a host round trip + rehash), capped
-        // where k_select stops reducing level 1 directly
-        const uint64_t keys = std::min<uint64_t>(n0, 65536 + 1536ull * mcap);
+        // keys (distinct pairs ever seen): merge t adds at most 2 (256 + t)
+        // (its (p, z) and (z, q) pairs), so after m merges at most
+        // 65536 + 512 m + m^2, and never more than the positions (uniform text,
+        // 1 GiB: 1.25 M after 1024 merges, 46 M after 8192).  Sized for that
+        // under the half-full rule, up to 2^28 slots (3 GiB), so that runs up
+        // to ~10 k merges never regrow (a regrowth is a host round trip, a
+        // rehash and a graph recapture)
+        const uint64_t mm = mcap;
+        const uint64_t keys = std::min<uint64_t>(n0, 65536 + 512 * mm + mm * mm);
         uint64_t want = std::max<uint64_t>(2 * keys, 4ull * (65536 + 16ull * (256 + std::min<uint64_t>(mcap, 4096))));
-        want = std::min<uint64_t>(want, (uint64_t)SELECT_L1_MAX * L1W);
+        want = std::min<uint64_t>(want, 1ull << 28);
         // BPE_TABLE_SLOTS: initial size override (tests drive the regrowth path with it)
         h.hcap = pow2_at_least(std::max<uint64_t>(want, 1ull << 17));
         if (const char *t = getenv("BPE_TABLE_SLOTS"))
@@ -509,6 +537,41 @@ void launch_summaries(bpe_gpu_ctx *c, bool edges = false) {
     if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
 }
 
+// Rebuild the hot set (rare: when its best falls below hot_T or it grew past
+// HOT_LIMIT; after a table regrowth moved the slots): histogram, threshold,
+// listing.  Falls back to the level summaries for the rest of the run when the
+// keys holding the top count alone would overfill the list.
+int hot_rebuild(bpe_gpu_ctx *c) {
+    if (!c->h.hot) return 0;
+    k_hot_hist<<<1024, 256, 0, c->st>>>(c->dE);
+    k_hot_pick<<<1, 1024, 0, c->st>>>(c->dE, c->dC);
+    HIPCHK(hipGetLastError());
+    uint32_t fill = 0;
+    HIPCHK(hipMemcpyAsync(&fill, &c->dC->hot_fill, 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    static const uint32_t fill_max = getenv("BPE_HOT_FILL") ? (uint32_t)atoi(getenv("BPE_HOT_FILL")) : HOT_LIMIT / 2;
+    if (fill > fill_max) {
+        c->h.hot = 0;
+        int r;
+        if ((r = push_desc(c))) return r;
+        static const uint32_t one = 1;  // the summaries start with a full rescan
+        HIPCHK(hipMemcpyAsync(&c->dC->full, &one, 4, hipMemcpyHostToDevice, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        c->hot_fallback = true;
+        return 0;
+    }
+    k_hot_collect<<<2048, 256, 0, c->st>>>(c->dE, c->dC);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// the argmax inputs k_select reads: level summaries (dirty blocks, or all of
+// them after a B change / rebuild) or the hot set's partials
+void launch_argmax_inputs(bpe_gpu_ctx *c) {
+    launch_summaries(c);
+    if (c->h.hot) k_hot_reduce<<<c->h.hot_parts, 1024, 0, c->st>>>(c->dE, c->dC);
+}
+
 void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
     if (c->h.spec_on && !tracked) {
         // fused speculative graph: entered with the current merge applied
@@ -589,7 +652,32 @@ int add_scan_events(bpe_gpu_ctx *c, hipGraph_t g, bool tracked) {
     return 0;
 }
 
+void launch_enc_batch(bpe_gpu_ctx *c) {
+    k_scan_batch<false><<<SCAN_BLOCKS, ESCAN_T, 0, c->st>>>(c->dE, c->dC);
+    k_apply_batch<false><<<ENC_APPLY_BLOCKS + 1, 256, 0, c->st>>>(c->dE, c->dC);
+    k_link_batch<false><<<ENC_APPLY_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+    k_enc_flip<<<1, 64, 0, c->st>>>(c->dC);
+}
+
+// replay a captured graph, or (BPE_GRAPH=0) launch the same kernels directly
+int glaunch(bpe_gpu_ctx *c, hipGraphExec_t g) {
+    if (real_graph(g)) {
+        HIPCHK(hipGraphLaunch(g, c->st));
+        return 0;
+    }
+    for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++) {
+        if ((uintptr_t)g == NOGRAPH_ENCODE) launch_enc_batch(c);
+        else launch_iteration(c, (uintptr_t)g == NOGRAPH_TRACKED);
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint32_t n_enc = 0) {
+    if (!GRAPH_ON) {
+        *out = (hipGraphExec_t)(encode ? NOGRAPH_ENCODE : tracked ? NOGRAPH_TRACKED : NOGRAPH_PLAIN);
+        return 0;
+    }
     hipGraph_t g;
     const bool prof = c->profile && !encode;
     if (prof)
@@ -599,10 +687,7 @@ int capture(bpe_gpu_ctx *c, hipGraphExec_t *out, bool tracked, bool encode, uint
     HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
     for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++) {
         if (encode) {
-            k_scan_batch<false><<<SCAN_BLOCKS, ESCAN_T, 0, c->st>>>(c->dE, c->dC);
-            k_apply_batch<false><<<ENC_APPLY_BLOCKS + 1, 256, 0, c->st>>>(c->dE, c->dC);
-            k_link_batch<false><<<ENC_APPLY_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
-            k_enc_flip<<<1, 64, 0, c->st>>>(c->dC);
+            launch_enc_batch(c);
         } else {
             launch_iteration(c, tracked);
         }
@@ -862,13 +947,14 @@ struct Resolver {
 // caller's pull_ctl synchronises).  Nothing is queued past the merge cap.
 int replay_pipelined(bpe_gpu_ctx *c, hipGraphExec_t g, uint64_t merges_done) {
     *c->hprobe = STOP_NONE;  // the stream is idle here (the caller pulled the control block)
-    HIPCHK(hipGraphLaunch(g, c->st));
+    int r;
+    if ((r = glaunch(c, g))) return r;
     uint64_t queued = merges_done + ITERS_PER_GRAPH;  // merges done once the queued replays end (at most)
     for (int q = 0;; q ^= 1) {
         HIPCHK(hipEventRecord(c->ev_probe[q], c->st));
         const bool ahead = queued < c->h.mcap;
         if (ahead) {
-            HIPCHK(hipGraphLaunch(g, c->st));
+            if ((r = glaunch(c, g))) return r;
             queued += ITERS_PER_GRAPH;
         }
         HIPCHK(hipEventSynchronize(c->ev_probe[q]));
@@ -924,7 +1010,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
                     break;
                 }
             }
-            HIPCHK(hipGraphLaunch(*g, c->st));
+            if ((r = glaunch(c, *g))) return r;
             break;
         }
         case STOP_DONE:
@@ -940,6 +1026,11 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             break;
         case STOP_MODE:
             C.stop = STOP_NONE;
+            if (c->h.hot) {  // tracked iterations select from the level summaries
+                c->h.hot = 0;
+                C.full = 1;
+                if ((r = push_desc(c))) return r;
+            }
             if ((r = push_ctl(c))) return r;
             launch_stats(c);
             launch_summaries(c);
@@ -951,13 +1042,23 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             C.full = 1;
             if ((r = push_ctl(c))) return r;
             if ((r = grow_table(c, c->h.hcap * 4))) return r;
+            if ((r = hot_rebuild(c))) return r;  // (slots moved)
             const bool tracked = !c->h.fast && C.n_live < TRACK_LIMIT;
-            launch_summaries(c);
+            launch_argmax_inputs(c);
             k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
             HIPCHK(hipGetLastError());
             need_scan = true;
             break;
         }
+        case STOP_HOT:
+            C.stop = STOP_NONE;
+            if ((r = push_ctl(c))) return r;
+            if ((r = hot_rebuild(c))) return r;
+            launch_argmax_inputs(c);
+            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, SEL_PLAIN);
+            HIPCHK(hipGetLastError());
+            need_scan = true;
+            break;
         case STOP_EVENT: {
             uint32_t u = 0, v = 0;
             if ((r = res.resolve(&u, &v))) return r;
@@ -1136,11 +1237,13 @@ void fill_profile(bpe_gpu_ctx *c) {
         // algorithmic bytes per merge: the scan reads 8 B per candidate (list
         // entry + token) and moves 20 B per occurrence; with the speculative
         // graph the span is k_rescan_spec's, which also reads 12 B per slot
-        // of every dirty level-1 block
+        // of every dirty level-1 block, or (hot set) 16 B per listed key
+        // (slot, count, key)
         const bool spec = c->h.spec_on && C.counters[7];
         c->prof_name = spec ? (c->h.xfused ? "k_rescan_spec_sh" : "k_rescan_spec") : "k_scan";
         c->prof_ms = khz > 0 ? (double)C.scan_ticks / C.scan_launches / khz : 0;
-        c->prof_bytes = (8.0 * C.counters[4] + 20.0 * C.counters[5] + (spec ? 12.0 * L1W * C.counters[6] : 0.0)) /
+        const double argmax_bytes = !spec ? 0.0 : 12.0 * L1W * C.counters[6] + 16.0 * C.hot_scanned;
+        c->prof_bytes = (8.0 * C.counters[4] + 20.0 * C.counters[5] + argmax_bytes) /
                         std::max<double>(1.0, C.counters[0]);
         c->prof_launches = C.scan_launches;
     }
@@ -1303,7 +1406,9 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     HIPCHK(hipGetLastError());
     const bool tracked = !c->fast && c->n0 < TRACK_LIMIT;
     if (tracked) launch_stats(c);
-    launch_summaries(c);
+    c->hot_fallback = false;
+    if ((r = hot_rebuild(c))) return r;
+    launch_argmax_inputs(c);
     k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));
@@ -1329,6 +1434,8 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.l1_rescanned = C.counters[6];
     c->stats.spec_hits = C.counters[7];
     c->stats.spec_misses = C.counters[8];
+    c->stats.hot_rebuilds = C.hot_rebuilds;
+    c->stats.hot_mode = c->h.hot ? 1 : c->hot_fallback ? 2 : 0;
     if (c->h.dbgts) print_timeline(c, C.z);
     if (getenv("BPE_DEBUG"))
         fprintf(stderr, "select phases (ticks/iter): reduce %.1f merge %.1f tail %.1f\n",
@@ -1503,7 +1610,7 @@ int bpe_gpu_set_profile(bpe_gpu_ctx *c, int on) {
     if (!c) return BPE_GPU_EINVAL;
     if (c->profile != (on != 0)) {
         for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked}) {
-            if (*g) (void)hipGraphExecDestroy(*g);
+            if (real_graph(*g)) (void)hipGraphExecDestroy(*g);
             *g = nullptr;
         }
     }

@@ -49,7 +49,33 @@ enum : uint32_t {
     STOP_ENC_END = 6,  // encode: merge list exhausted
     STOP_MODE = 7,     // n fell below 2^21: switch to the tracked iteration graph
     STOP_REDO = 8,     // speculative graph: the predicted next merge was wrong, host scans
+    STOP_HOT = 9,      // hot-set argmax: the set no longer holds the maximum (or grew): host rebuilds it
 };
+
+// Hot-set argmax (Eng::hot, untracked one-shard training): the keys whose count
+// is >= Ctl::hot_T are listed in Eng::hot_slot.  A key's count only rises in
+// the merge that creates the later of its two ids (every other delta is a
+// decrement), so a key enters the list at most once, when that merge lifts it
+// to >= hot_T, and every key outside the list stays below hot_T.  While the
+// list's best count is >= hot_T it is the table's argmax (ties included: a key
+// tied with it is >= hot_T, so it is listed too).  The list is rebuilt from a
+// full table pass when its best falls below hot_T or it grows past HOT_LIMIT.
+constexpr uint32_t HOT_TARGET = 16384;              // keys a rebuild aims to list
+constexpr uint32_t HOT_LIMIT = 65536;               // rebuild once the list grows past this
+constexpr uint32_t HOT_CAP = 1u << 20;              // list capacity (appends beyond are dropped; > HOT_LIMIT)
+constexpr uint32_t HOT_BINS = 2048 + 21 * 128;      // count histogram: exact below 2048, 1/128 octave above
+
+__host__ __device__ inline uint32_t hot_bin(uint32_t c) {
+    if (c < 2048) return c;
+    uint32_t e = 31;
+    while (!(c >> e)) e--;
+    return 2048 + (e - 11) * 128 + ((c >> (e - 7)) & 127u);
+}
+__host__ __device__ inline uint32_t hot_bin_lo(uint32_t b) {  // smallest count in bin b
+    if (b < 2048) return b;
+    const uint32_t e = 11 + (b - 2048) / 128, m = (b - 2048) % 128;
+    return (128u + m) << (e - 7);
+}
 
 // k_select's graph argument
 enum : uint32_t { SEL_PLAIN = 0, SEL_TRACKED = 1, SEL_FUSED = 2 };
@@ -134,6 +160,14 @@ struct Eng {
     const uint32_t *enc_pairs;  // [2 * n_enc]
     uint32_t n_enc;
     EncBatch *eb;         // [2] double-buffered batch descriptors
+    // hot-set argmax (see HOT_TARGET); hot == 0: the level summaries
+    uint32_t hot;
+    uint32_t hot_parts;   // partial results per launch (k_rescan_spec's rescan blocks)
+    uint32_t hot_target;  // keys a rebuild aims to list (HOT_TARGET; BPE_HOT_TARGET for tests)
+    uint32_t *hot_slot;   // [HOT_CAP] table slots of the listed keys
+    uint32_t *hot_hist;   // [HOT_BINS] rebuild scratch (zero between rebuilds)
+    unsigned long long *hotp_best, *hotp_key, *hotp_v2, *hotp_k2;  // [hot_parts] partial top-2
+    uint32_t *hotp_tie;
 };
 
 // Control block.  Everything up to Dp is owned by k_select, which stages it in
@@ -168,6 +202,7 @@ struct Ctl {
     // candidate list, armed flag; occurrences k_rescan_spec found, per parity
     uint32_t sa, sb, s_mode, s_off;
     uint32_t s_len, spec, sRp[2];
+    uint32_t hot_T, hot_fill, hot_pad0, hot_pad1;  // hot-set threshold; keys the last rebuild listed
     // ---- tail: written by k_apply / k_rescan_spec (see above)
     unsigned long long Dp[2];   // D delta of the merge applied with parity p (finish_iteration folds it)
     unsigned long long nkeys;   // pair-table slots in use
@@ -189,6 +224,9 @@ struct Ctl {
     uint32_t adone;                   // fused sharded step: k_fused_sh apply blocks done with the spans
     uint32_t nx_seq0, nx_live;        // fused sharded step: the delta exchange's sequence number; K1 ran
     unsigned long long xdbg[4];       // fused sharded step timing sums (BPE_DEBUG; wall-clock ticks)
+    uint32_t hot_n;                   // hot-set entries (role B appends while k_select runs)
+    uint32_t hot_rebuilds;
+    unsigned long long hot_scanned;   // hot-set entries reduced, summed over the merges (profiling)
 };
 constexpr uint32_t CTL_SELECT_WORDS = offsetof(Ctl, Dp) / 4;  // k_select's write-back
 

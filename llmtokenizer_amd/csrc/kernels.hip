@@ -260,6 +260,7 @@ __device__ inline void stage_one(uint32_t *list, uint16_t *ltag, uint32_t *lcoun
 // ones (Ctl lives in HBM between launches).
 struct Snap {
     uint32_t stop, a, b, z, parity, R, occ_top, mode, off, len, nl1, full, spec, sa, sb, s_mode, s_off, s_len;
+    uint32_t hotT;  // hot-set threshold (Eng::hot)
     unsigned long long D, B;  // D: distinct pairs after the merge applied last (base + its delta)
 };
 
@@ -271,6 +272,7 @@ __device__ inline Snap snap(const Ctl *C) {
     s.nl1 = C->nl1p[s.parity]; s.full = C->full;
     s.spec = C->spec; s.sa = C->sa; s.sb = C->sb; s.s_mode = C->s_mode; s.s_off = C->s_off; s.s_len = C->s_len;
     s.D = C->D + C->Dp[s.parity]; s.B = C->B;
+    s.hotT = C->hot_T;
     return s;
 }
 
@@ -281,6 +283,7 @@ __device__ inline Snap snap_next(const Ctl *C) {
     s.a = C->nx_a; s.b = C->nx_b; s.z = C->nx_z; s.parity = C->nx_P; s.occ_top = C->nx_occ;
     s.R = C->sRp[s.parity];
     s.B = C->nx_B;
+    s.hotT = C->hot_T;  // (k_select may write the head back meanwhile: same value)
     return s;
 }
 
@@ -742,12 +745,14 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     __syncthreads();
     long long dD = 0;
     uint32_t nins = 0;  // keys this thread inserted
+    const bool hot = E->hot != 0;
     unsigned long long tprobe = 0, tcount = 0;  // debug timeline (BPE_DEBUG_TS)
     const uint32_t base0 = (bid - roleA_blocks) * blockDim.x;
     for (uint32_t t0 = base0; t0 < total; t0 += stride) {  // uniform trip count per block
         const uint32_t t = t0 + threadIdx.x;
-        bool mark = false;
+        bool mark = false, hot_in = false;
         uint32_t blk = 0;
+        uint64_t hslot = 0;
         uint32_t u = 0, v = 0;
         int cat = -1;  // category of this entry
         uint32_t x = 0;
@@ -812,16 +817,28 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
                     const uint32_t nw = (uint32_t)((long long)old + d);
                     E->hcnt[slot] = nw;
                     dD += (long long)(nw != 0) - (long long)(old != 0);
-                    // the level-1 summary (best + runner-up) only changes if the
-                    // key reaches the block's runner-up before or after the
-                    // update; a B change rescans everything anyway
-                    const unsigned long long hi = pack_val(old > nw ? old : nw, u, v, S.B);
-                    mark = !UNDO && hi >= bv2;
+                    if (hot) {
+                        // a rise to >= hot_T lists the key (once: counts only rise
+                        // in the merge creating z; an undo's rises restore counts
+                        // of keys that were listed when they had them)
+                        hot_in = !UNDO && d > 0 && nw >= S.hotT && old < S.hotT;
+                        hslot = slot;
+                    } else {
+                        // the level-1 summary (best + runner-up) only changes if the
+                        // key reaches the block's runner-up before or after the
+                        // update; a B change rescans everything anyway
+                        const unsigned long long hi = pack_val(old > nw ? old : nw, u, v, S.B);
+                        mark = !UNDO && hi >= bv2;
+                    }
                 }
             }
         }
         const uint32_t p = wave_append(mark, &nmark);
         if (mark) marks[p] = blk;
+        if (hot) {
+            const uint32_t hp = wave_append(hot_in, &C->hot_n);
+            if (hot_in && hp < HOT_CAP) E->hot_slot[hp] = (uint32_t)hslot;
+        }
         __syncthreads();
         if (!UNDO) ts_mark(E, z - 1, TS_B_TABLE, false, true);
         if (!UNDO && E->dbgts) {  // the block's latest probe / count load
@@ -905,6 +922,7 @@ struct Best {
 __device__ inline Best best_merge(Best x, Best y) {
     if (y.v > x.v) return y;
     if (y.v < x.v) return x;
+    if (x.key == y.key) return x;  // the same key twice (hot set): one holder
     return Best{x.v, x.tie + y.tie, x.key < y.key ? x.key : y.key};
 }
 
@@ -925,7 +943,9 @@ __device__ inline Top2 top2_merge(Top2 x, Top2 y) {
     r.b = best_merge(x.b, y.b);
     // runner-up: the loser's first or the winner's second
     const bool xw = ahead(x.b.v, x.b.key, y.b.v, y.b.key);
-    const unsigned long long lv = xw ? y.b.v : x.b.v, lk = xw ? y.b.key : x.b.key;
+    const bool dup = x.b.key == y.b.key;  // (then the loser's own runner-up competes instead)
+    const unsigned long long lv = dup ? (xw ? y.v2 : x.v2) : xw ? y.b.v : x.b.v;
+    const unsigned long long lk = dup ? (xw ? y.k2 : x.k2) : xw ? y.b.key : x.b.key;
     const unsigned long long sv = xw ? x.v2 : y.v2, sk = xw ? x.k2 : y.k2;
     const bool l = ahead(lv, lk, sv, sk);
     r.v2 = l ? lv : sv;
@@ -984,6 +1004,7 @@ __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__r
             }
         }
     }
+    if (E->hot) return;  // (the hot set replaces the level summaries: hot_reduce_body)
     const uint64_t B = summary_B(S.D);
     const bool full = S.full || B != S.B;
     const uint64_t nL1 = E->hcap / L1W;
@@ -1024,6 +1045,103 @@ __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__r
             E->l1k2[blk] = r.k2;
             if (!full) E->l2list[w] = blk / L2W;  // duplicates are harmless
         }
+    }
+}
+
+// Hot-set argmax, partial: the top-2 over this block's share of the listed
+// keys (counts after the merge applied last, B_final of its D) into
+// hotp_*[bid]; k_select reduces the hot_parts partials.  No apply runs beside
+// it, so hot_n is stable.
+__device__ void hot_reduce_body(const Eng *__restrict__ E, Ctl *__restrict__ C, const Snap &S, uint32_t bid,
+                                uint32_t nblk) {
+    const uint64_t B = summary_B(S.D);
+    const uint32_t n = min(C->hot_n, HOT_CAP);
+    if (bid == 0 && threadIdx.x == 0) C->hot_scanned += n;
+    Top2 mine = top2_one(0, 0, ~0ull);
+    for (uint32_t i = bid * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
+        const uint32_t slot = E->hot_slot[i];
+        const uint32_t c = E->hcnt[slot];
+        const unsigned long long k = E->hkey[slot] - 1;
+        if (c) mine = top2_merge(mine, top2_one(pack_val(c, (uint32_t)(k >> 32), (uint32_t)k, B), 1, k));
+    }
+    mine = wave_top2(mine);
+    __shared__ Top2 hw[16];
+    if ((threadIdx.x & 63) == 0) hw[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Top2 r = hw[0];
+        for (uint32_t q = 1; q < blockDim.x / 64; q++) r = top2_merge(r, hw[q]);
+        E->hotp_best[bid] = r.b.v;
+        E->hotp_tie[bid] = r.b.v ? r.b.tie : 0;
+        E->hotp_key[bid] = r.b.key;
+        E->hotp_v2[bid] = r.v2;
+        E->hotp_k2[bid] = r.k2;
+    }
+}
+
+// host-launched hot reduce (before a k_select outside the speculative graph)
+__global__ __launch_bounds__(1024) void k_hot_reduce(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    if (!E->hot) return;
+    const Snap S = snap(C);
+    if (S.stop) return;
+    hot_reduce_body(E, C, S, blockIdx.x, gridDim.x);
+}
+
+// Rebuild, pass 1: histogram of the counts >= 2 (hot_bin) over the whole table
+__global__ __launch_bounds__(256) void k_hot_hist(const Eng *__restrict__ E) {
+    __shared__ uint32_t h[HOT_BINS];
+    for (uint32_t x = threadIdx.x; x < HOT_BINS; x += blockDim.x) h[x] = 0;
+    __syncthreads();
+    const uint64_t n4 = E->hcap / 4;
+    const uint4 *c4 = reinterpret_cast<const uint4 *>(E->hcnt);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 q = c4[i];
+        if (q.x >= 2) atomicAdd(&h[hot_bin(q.x)], 1u);
+        if (q.y >= 2) atomicAdd(&h[hot_bin(q.y)], 1u);
+        if (q.z >= 2) atomicAdd(&h[hot_bin(q.z)], 1u);
+        if (q.w >= 2) atomicAdd(&h[hot_bin(q.w)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < HOT_BINS; x += blockDim.x)
+        if (h[x]) atomicAdd(&E->hot_hist[x], h[x]);
+}
+
+// Rebuild, pass 2 (one block): the threshold -- the lowest bin edge that keeps
+// the listed keys within HOT_TARGET (or the top bin alone); hot_fill = keys
+// that will be listed (> HOT_LIMIT / 2: the host falls back to the level
+// summaries).  Zeroes the histogram for the next rebuild.
+__global__ __launch_bounds__(1024) void k_hot_pick(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    __shared__ uint32_t h[HOT_BINS];
+    for (uint32_t x = threadIdx.x; x < HOT_BINS; x += blockDim.x) {
+        h[x] = E->hot_hist[x];
+        E->hot_hist[x] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x) return;
+    uint32_t T = 0, cum = 0;
+    for (int b = (int)HOT_BINS - 1; b >= 2; b--) {
+        const uint32_t c = h[b];
+        if (!c) continue;
+        if (cum > 0 && cum + c > E->hot_target) break;
+        cum += c;
+        T = hot_bin_lo((uint32_t)b);
+    }
+    C->hot_T = T < 2 ? 2u : T;  // no count >= 2: an empty list, k_select stops (max <= 1)
+    C->hot_fill = cum;
+    C->hot_n = 0;
+    C->hot_rebuilds++;
+}
+
+// Rebuild, pass 3: list every key with count >= hot_T
+__global__ __launch_bounds__(256) void k_hot_collect(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    const uint32_t T = C->hot_T;
+    const uint64_t n = E->hcap;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t end = (n + stride - 1) / stride * stride;  // uniform trip count (wave_append)
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride) {
+        const bool in = i < n && E->hcnt[i] >= T;
+        const uint32_t p = wave_append(in, &C->hot_n);
+        if (in && p < HOT_CAP) E->hot_slot[p] = (uint32_t)i;
     }
 }
 
@@ -1070,6 +1188,7 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ 
     ts_mark(E, S.z, TS_K1_LASTIN, false);
     if (blockIdx.x < rblocks) {
         rescan1_body(E, C, S, blockIdx.x, rblocks);
+        if (E->hot) hot_reduce_body(E, C, S, blockIdx.x, rblocks);
         scan_exit_stamp(E, blockIdx.x);
         ts_mark(E, S.z, TS_K1_RESCAN, false, true);
     } else if (S.spec) {
@@ -1127,7 +1246,7 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec_sh(const Eng *__restrict
 // one wave per dirty level-2 entry (256 level-1 entries, 4 per lane); only
 // for tables too large for k_select to reduce level 1 directly
 __global__ __launch_bounds__(256) void k_rescan2(const Eng *__restrict__ E, Ctl *__restrict__ C) {
-    if (C->stop) return;
+    if (C->stop || E->hot) return;
     const uint64_t nL1 = E->hcap / L1W;
     if (nL1 <= SELECT_L1_MAX) return;
     const Snap S = snap(C);
@@ -1214,7 +1333,8 @@ __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Ctl *Cg, T
         C->scan_ticks += tend - C->scan_t0;
         C->scan_launches++;
     }
-    if (C->pend[P0]) C->counters[6] += (C->full || summary_B(C->D + C->Dp[P0]) != C->B) ? E->hcap / L1W : C->nl1p[P0];
+    if (C->pend[P0] && !E->hot)
+        C->counters[6] += (C->full || summary_B(C->D + C->Dp[P0]) != C->B) ? E->hcap / L1W : C->nl1p[P0];
     const uint32_t was_spec = graph == SEL_FUSED ? C->spec : 0;  // the prediction's scan ran since
     C->spec = 0;
     C->stop_z = C->z;
@@ -1231,6 +1351,9 @@ __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Ctl *Cg, T
     C->edge = edge;
     const uint32_t cnt = (uint32_t)(r.v >> 32);
     if (C->merges_done >= E->mcap) { C->stop = STOP_CAP; return; }
+    // hot set: its best is the argmax only while it is >= hot_T (hot_T == 2:
+    // every key with a count >= 2 is listed, so an empty list means max <= 1)
+    if (E->hot && ((cnt < C->hot_T && C->hot_T > 2) || Cg->hot_n > HOT_LIMIT)) { C->stop = STOP_HOT; return; }
     if (r.v == 0 || cnt <= 1) { C->stop = STOP_DONE; return; }
     if (C->nkeys + 4ull * (256ull + C->merges_done + 2) >= E->hcap / 2) { C->stop = STOP_GROW; return; }
     const bool tracked = !E->fast && C->n_live < DYN_LIMIT;  // deterministic (static) reference iteration
@@ -1366,9 +1489,11 @@ __device__ __forceinline__ void select_block(const Eng *__restrict__ E, Ctl *__r
     for (uint32_t x = tid; x < E->scan_blocks; x += blockDim.x) tend = max(tend, E->scan_tend[x]);
     const uint64_t nL1 = E->hcap / L1W;
     const bool lvl1 = nL1 <= SELECT_L1_MAX;
-    Top2 mine = summary_top2(lvl1 ? E->l1best : E->l2best, lvl1 ? E->l1tie : E->l2tie, lvl1 ? E->l1key : E->l2key,
-                             lvl1 ? E->l1v2 : E->l2v2, lvl1 ? E->l1k2 : E->l2k2,
-                             lvl1 ? nL1 : (nL1 + L2W - 1) / L2W);
+    const bool hot = E->hot != 0;
+    Top2 mine = hot ? summary_top2(E->hotp_best, E->hotp_tie, E->hotp_key, E->hotp_v2, E->hotp_k2, E->hot_parts)
+                    : summary_top2(lvl1 ? E->l1best : E->l2best, lvl1 ? E->l1tie : E->l2tie,
+                                   lvl1 ? E->l1key : E->l2key, lvl1 ? E->l1v2 : E->l2v2, lvl1 ? E->l1k2 : E->l2k2,
+                                   lvl1 ? nL1 : (nL1 + L2W - 1) / L2W);
     if (tid < CW) scw[tid] = cw_v;
     if (tid < 256) srank[tid] = rk_v;
     if (tid == 0) sc_t1 = wall_clock64();

@@ -300,7 +300,7 @@ int drive_group(bpe_gpu_group *g) {
                 need_scan = false;
                 ran_fused = true;
             }
-            if (!g->graph && !g->eager && capture_group(g)) {
+            if (!g->graph && !g->eager && (!GRAPH_ON || capture_group(g))) {
                 // collectives that refuse stream capture: launch eagerly
                 g->eager = true;
                 (void)hipGetLastError();
