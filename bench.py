@@ -223,8 +223,28 @@ def train_single(args, cx, out):
                                 "breakdown_ms": {"init": round(s2["ms_init"], 3), "loop": round(s2["ms_train"], 3)},
                                 "ids_checksum": "%016x" % e.ids_checksum(),
                                 "merges_md5": hashlib.md5(e.merges().tobytes()).hexdigest()}}
+        extra["ingest"] = ingest_rate(e)
     e.close()
     return el, merges, st, prof, got, extra
+
+
+def ingest_rate(e, size=GIB):
+    """get_file + strlen into HBM (bpe_gpu_load_fd, pinned double-buffered
+    staging) for a 1 GiB file in the page cache: the PCIe-inclusive rate
+    (never `value`: the timed jobs start from resident input)"""
+    import numpy as np
+    path = os.path.join(tempfile.gettempdir(), "bpe_bench_ingest.bin")
+    try:
+        np.random.default_rng(0).integers(32, 127, size, dtype=np.uint8).tofile(path)
+        e.load_file(path)  # warm (staging buffers)
+        t0 = time.perf_counter()
+        n = e.load_file(path)
+        t1 = time.perf_counter()
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
+    return {"bytes": n, "ms": round((t1 - t0) * 1e3, 2), "GB/s": round(n / (t1 - t0) / 1e9, 2),
+            "note": "file in the page cache -> HBM incl. the NUL scan, PCIe-inclusive; not part of value"}
 
 
 def train_sharded(args, cx, out):

@@ -16,7 +16,10 @@
  *   bpe_gpu_fetch_ids  -- compress()'s *encoding output (bpe.c:785-794)
  *   bpe_gpu_encode     -- the replace pass (bpe.c:760-779) applied merge by
  *                         merge to new text (standalone encoder)
- *   bpe_gpu_decode     -- decompress()/resolve_pair (bpe.c:23-92, 341-394)
+ *   bpe_gpu_decode     -- decompress()/resolve_pair (bpe.c:23-92, 341-394):
+ *                         expansion lengths, prefix sum and byte gather
+ *                         on the device
+ *   bpe_gpu_load_fd    -- get_file + strlen (bpe.c:130-180, 555), streamed
  */
 #ifndef BPE_GPU_H
 #define BPE_GPU_H
@@ -37,7 +40,8 @@ enum {
     BPE_GPU_ESTATE = -5,   /* call out of order (e.g. train before load)    */
     BPE_GPU_ERANGE = -6,   /* corpus larger than 2^32-2 bytes per device    */
     BPE_GPU_EDATA = -7,    /* unknown token id (decode) / corrupt merge list */
-    BPE_GPU_EINTERNAL = -8 /* engine invariant violated (reported, not hidden) */
+    BPE_GPU_EINTERNAL = -8,/* engine invariant violated (reported, not hidden) */
+    BPE_GPU_EIO = -9       /* file read error (errno is set)                */
 };
 
 typedef struct bpe_gpu_ctx bpe_gpu_ctx;
@@ -79,6 +83,13 @@ void bpe_gpu_destroy(bpe_gpu_ctx *ctx);
 /* Load a byte corpus (host memory) into HBM.  No NUL truncation is applied
  * here; compress() applies the reference's strlen semantics before calling. */
 int bpe_gpu_load(bpe_gpu_ctx *ctx, const uint8_t *bytes, size_t n);
+
+/* Stream the first `size` bytes of file descriptor fd (positional reads from
+ * offset 0) into HBM through pinned,
+ * double-buffered staging (disk reads overlap the host-to-device copies).  The
+ * corpus ends at the first NUL byte, as the reference's get_file + strlen
+ * (bpe/src/bpe.c:130-180, 555); *n_loaded receives its length. */
+int bpe_gpu_load_fd(bpe_gpu_ctx *ctx, int fd, size_t size, size_t *n_loaded);
 
 /* Generate bytes [offset, offset+n) of the seeded random_text.txt-shaped corpus
  * (llmtokenizer_amd/synth.py) directly in HBM. */

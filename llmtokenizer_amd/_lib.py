@@ -32,7 +32,7 @@ EXPORTS = [
     "bpe_gpu_group_load", "bpe_gpu_group_synth", "bpe_gpu_group_train", "bpe_gpu_group_encode", "bpe_gpu_group_fetch_merges",
     "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo", "bpe_gpu_group_kernel_profile",
     "bpe_gpu_group_create_p2p", "bpe_gpu_group_p2p_connect", "bpe_gpu_group_transport",
-    "bpe_gpu_group_create_local_p2p", "bpe_gpu_ids_checksum", "bpe_gpu_group_ids_checksum",
+    "bpe_gpu_group_create_local_p2p", "bpe_gpu_ids_checksum", "bpe_gpu_group_ids_checksum", "bpe_gpu_load_fd",
 ]
 
 
@@ -76,6 +76,7 @@ def load():
     L.bpe_gpu_destroy.restype = None
     L.bpe_gpu_load.argtypes = [vp, vp, sz]
     L.bpe_gpu_synth.argtypes = [vp, ctypes.c_uint64, sz, ctypes.c_uint64]
+    L.bpe_gpu_load_fd.argtypes = [vp, ctypes.c_int, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_train.argtypes = [vp, ctypes.c_long, ctypes.POINTER(sz)]
     L.bpe_gpu_train_ex.argtypes = [vp, ctypes.c_long, ctypes.c_uint, ctypes.POINTER(sz)]
     ip = ctypes.POINTER(ctypes.c_int)

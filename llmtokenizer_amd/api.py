@@ -193,6 +193,17 @@ class Engine:
         buf = np.frombuffer(data, dtype=np.uint8)
         _lib.check(self.L.bpe_gpu_load(self.ctx, buf.ctypes.data_as(ctypes.c_void_p), buf.size), "load")
 
+    def load_file(self, path):
+        """stream a file into HBM (bpe_gpu_load_fd: pinned double-buffered
+        staging, the corpus ends at the first NUL); returns the bytes loaded"""
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            n = ctypes.c_size_t(0)
+            _lib.check(self.L.bpe_gpu_load_fd(self.ctx, fd, os.fstat(fd).st_size, ctypes.byref(n)), "load_fd")
+        finally:
+            os.close(fd)
+        return n.value
+
     def synth(self, seed, n, offset=0):
         _lib.check(self.L.bpe_gpu_synth(self.ctx, int(seed), int(n), int(offset)), "synth")
 

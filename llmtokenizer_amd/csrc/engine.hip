@@ -4,6 +4,9 @@
 //
 // C-ABI: include/bpe_gpu.h.  One context = one device, one stream.
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
+#include <unistd.h>
+#include <cerrno>
 
 #include <algorithm>
 #include <chrono>
@@ -12,6 +15,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+
+#include <rocprim/rocprim.hpp>
 
 #include "../../include/bpe_gpu.h"
 #include "kernels.hip"
@@ -247,6 +252,12 @@ struct bpe_gpu_ctx {
     std::string prof_name;
     double prof_ms = 0, prof_bytes = 0;
     uint64_t prof_launches = 0;
+    // grow-only device scratch of decode (ids, pairs, elen, offsets, scan
+    // temporaries, output, error words) and the pinned staging of file loads
+    void *dscr[7] = {};
+    size_t dscr_cap[7] = {};
+    uint8_t *stage[2] = {};
+    hipEvent_t stage_ev[2] = {};
 };
 
 namespace {
@@ -1251,6 +1262,23 @@ void fill_profile(bpe_gpu_ctx *c) {
     c->event_n = c->scan_n;
 }
 
+// grow-only device scratch slot k of at least `bytes`
+int dscratch(bpe_gpu_ctx *c, int k, size_t bytes, void **out) {
+    if (bytes > c->dscr_cap[k]) {
+        if (c->dscr[k]) {
+            HIPCHK(hipStreamSynchronize(c->st));
+            (void)hipFree(c->dscr[k]);
+            c->dscr[k] = nullptr;
+            c->dscr_cap[k] = 0;
+        }
+        const size_t cap = std::max<size_t>(bytes, 1 << 16);
+        HIPCHK(hipMalloc(&c->dscr[k], cap));
+        c->dscr_cap[k] = cap;
+    }
+    *out = c->dscr[k];
+    return 0;
+}
+
 // a context on `device`; shared == nullptr creates its own stream
 int ctx_new(int device, hipStream_t shared, bpe_gpu_ctx **out) {
     bpe_gpu_ctx *c = new bpe_gpu_ctx();
@@ -1292,6 +1320,7 @@ const char *bpe_gpu_strerror(int code) {
     case BPE_GPU_ERANGE: return "corpus too large for one device (max 2^32-2 bytes)";
     case BPE_GPU_EDATA: return "unknown token id or corrupt merge list";
     case BPE_GPU_EINTERNAL: return "engine invariant violated";
+    case BPE_GPU_EIO: return "file read error (errno is set)";
     default: return "unknown error";
     }
 }
@@ -1328,6 +1357,12 @@ void bpe_gpu_destroy(bpe_gpu_ctx *c) {
     for (auto &e : c->ev_probe)
         if (e) (void)hipEventDestroy(e);
     if (c->d_enc_pairs) hipFree(c->d_enc_pairs);
+    for (void *p : c->dscr)
+        if (p) (void)hipFree(p);
+    for (int k = 0; k < 2; k++) {
+        if (c->stage[k]) (void)hipHostFree(c->stage[k]);
+        if (c->stage_ev[k]) (void)hipEventDestroy(c->stage_ev[k]);
+    }
     for (auto &a : c->ev)
         for (auto &b : a)
             for (auto &e : b)
@@ -1537,72 +1572,99 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
 int bpe_gpu_decode(bpe_gpu_ctx *c, const uint32_t *ids, size_t len, const uint32_t *pairs, size_t n_merges,
                    uint8_t *out, size_t cap, size_t *out_len) {
     if (!c || !out_len || (!ids && len) || (!pairs && n_merges)) return BPE_GPU_EINVAL;
+    if (n_merges > 0xFFFFFEFFull) return fail(BPE_GPU_ERANGE, "merge list too long");
     HIPCHK(hipSetDevice(c->dev));
-    // expansion lengths (non-NUL bytes) per id, memoized DFS with cycle check
-    const size_t V = 256 + n_merges;
-    std::vector<uint64_t> elen(V, 0);
-    std::vector<uint8_t> state(V, 0);  // 0 new, 1 in progress, 2 done
-    for (uint32_t x = 0; x < 256; x++) { elen[x] = x ? 1 : 0; state[x] = 2; }
-    for (size_t root = 256; root < V; root++) {
-        if (state[root] == 2) continue;
-        std::vector<size_t> stk{root};
-        while (!stk.empty()) {
-            size_t x = stk.back();
-            if (state[x] == 2) { stk.pop_back(); continue; }
-            const uint32_t a = pairs[2 * (x - 256)], b = pairs[2 * (x - 256) + 1];
-            if (a == x) {  // self-referencing record: the reference prints it as one char
-                elen[x] = (uint8_t)a ? 1 : 0;
-                state[x] = 2;
-                stk.pop_back();
-                continue;
-            }
-            if (a >= V || b >= V) return fail(BPE_GPU_EDATA, "merge references an unknown id");
-            state[x] = 1;
-            bool ready = true;
-            for (uint32_t y : {a, b}) {
-                if (state[y] == 1 && y != x) return fail(BPE_GPU_EDATA, "cyclic merge list");
-                if (state[y] == 0) { stk.push_back(y); ready = false; }
-            }
-            if (ready) {
-                elen[x] = elen[a] + elen[b];
-                state[x] = 2;
-                stk.pop_back();
-            }
-        }
-    }
+    // all on the device: expansion lengths per id (k_dec_elen), their prefix
+    // sum over the ids (rocprim scan), the byte gather (k_dec_expand)
+    const uint32_t V = (uint32_t)(256 + n_merges);
+    int r;
+    void *p[7];
+    if ((r = dscratch(c, 0, std::max<size_t>(len, 1) * 4, &p[0])) || (r = dscratch(c, 1, std::max<size_t>(n_merges, 1) * 8, &p[1])) ||
+        (r = dscratch(c, 2, (size_t)V * 8, &p[2])) || (r = dscratch(c, 3, (len + 1) * 8, &p[3])) ||
+        (r = dscratch(c, 6, 64, &p[6])))
+        return r;
+    uint32_t *d_ids = (uint32_t *)p[0], *d_pairs = (uint32_t *)p[1], *d_err = (uint32_t *)p[6];
+    uint64_t *d_elen = (uint64_t *)p[2], *d_off = (uint64_t *)p[3];
+    HIPCHK(hipMemsetAsync(d_err, 0, 8, c->st));
+    if (len) HIPCHK(hipMemcpyAsync(d_ids, ids, len * 4, hipMemcpyHostToDevice, c->st));
+    if (n_merges) HIPCHK(hipMemcpyAsync(d_pairs, pairs, n_merges * 8, hipMemcpyHostToDevice, c->st));
+    k_dec_elen<<<1, 1024, 0, c->st>>>(d_pairs, (uint32_t)n_merges, d_elen);
+    if (len) k_dec_check<<<1024, 256, 0, c->st>>>(d_ids, len, V, d_elen, d_err);
+    HIPCHK(hipGetLastError());
+    auto lens = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),
+                                                 DecLen{d_ids, d_elen, (uint64_t)len, V});
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, lens, d_off, (uint64_t)0, len + 1, rocprim::plus<uint64_t>(), c->st));
+    if ((r = dscratch(c, 4, tb, &p[4]))) return r;
+    HIPCHK(rocprim::exclusive_scan(p[4], tb, lens, d_off, (uint64_t)0, len + 1, rocprim::plus<uint64_t>(), c->st));
+    uint32_t err[2] = {0, 0};
     uint64_t total = 0;
-    std::vector<uint64_t> off(len + 1);
-    for (size_t i = 0; i < len; i++) {
-        if (ids[i] >= V) return fail(BPE_GPU_EDATA, "unknown token id");
-        off[i] = total;
-        total += elen[ids[i]];
-    }
-    off[len] = total;
+    HIPCHK(hipMemcpyAsync(err, d_err, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(&total, d_off + len, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (err[0] & 1) return fail(BPE_GPU_EDATA, "unknown token id");
+    if (err[0] & 2) return fail(BPE_GPU_EDATA, "a token's merge record names an unknown id or is cyclic");
     *out_len = total;
     if (!out) return 0;
     if (cap < total) return fail(BPE_GPU_EINVAL, "decode: output buffer too small");
     if (len == 0 || total == 0) return 0;
-    uint32_t *d_ids, *d_pairs;
-    uint64_t *d_elen, *d_off;
-    uint8_t *d_out;
-    HIPCHK(hipMalloc(&d_ids, len * 4));
-    HIPCHK(hipMalloc(&d_pairs, std::max<size_t>(n_merges, 1) * 8));
-    HIPCHK(hipMalloc(&d_elen, V * 8));
-    HIPCHK(hipMalloc(&d_off, (len + 1) * 8));
-    HIPCHK(hipMalloc(&d_out, total));
-    HIPCHK(hipMemcpyAsync(d_ids, ids, len * 4, hipMemcpyHostToDevice, c->st));
-    if (n_merges) HIPCHK(hipMemcpyAsync(d_pairs, pairs, n_merges * 8, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipMemcpyAsync(d_elen, elen.data(), V * 8, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipMemcpyAsync(d_off, off.data(), (len + 1) * 8, hipMemcpyHostToDevice, c->st));
-    k_dec_expand<<<1024, 256, 0, c->st>>>(d_ids, len, d_pairs, d_elen, d_off, d_out);
+    if ((r = dscratch(c, 5, total, &p[5]))) return r;
+    k_dec_expand<<<1024, 256, 0, c->st>>>(d_ids, len, d_pairs, d_elen, d_off, (uint8_t *)p[5]);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(out, d_out, total, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(out, p[5], total, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    hipFree(d_ids);
-    hipFree(d_pairs);
-    hipFree(d_elen);
-    hipFree(d_off);
-    hipFree(d_out);
+    return 0;
+}
+
+// Stream the first `size` bytes of fd (positional reads from offset 0; the
+// descriptor's own offset is not used) into HBM through two pinned staging buffers:
+// the read of chunk k+1 overlaps the copy of chunk k.  The corpus ends at the
+// first NUL (the reference trains on strlen of the file, bpe.c:130-180, 555).
+int bpe_gpu_load_fd(bpe_gpu_ctx *c, int fd, size_t size, size_t *n_loaded) {
+    if (!c || fd < 0 || !n_loaded) return BPE_GPU_EINVAL;
+    HIPCHK(hipSetDevice(c->dev));
+    int r;
+    if ((r = alloc_bytes(c, size))) return r;
+    constexpr size_t CH = 64u << 20;
+    for (int k = 0; k < 2; k++) {
+        if (!c->stage[k]) HIPCHK(hipHostMalloc((void **)&c->stage[k], CH, hipHostMallocDefault));
+        if (!c->stage_ev[k]) HIPCHK(hipEventCreateWithFlags(&c->stage_ev[k], hipEventDisableTiming));
+    }
+    size_t off = 0;
+    bool done = false;
+    for (uint64_t k = 0; off < size && !done; k++) {
+        uint8_t *buf = c->stage[k & 1];
+        if (k >= 2) HIPCHK(hipEventSynchronize(c->stage_ev[k & 1]));  // its previous copy is done
+        const size_t want = std::min(CH, size - off);
+        size_t got = 0;
+        while (got < want) {
+            const ssize_t q = pread(fd, buf + got, want - got, (off_t)(off + got));
+            if (q < 0 && errno == EINTR) continue;
+            if (q < 0) {
+                const int e = errno;
+                (void)hipStreamSynchronize(c->st);
+                c->n0 = 0;
+                const int rc = fail(BPE_GPU_EIO, "read");
+                errno = e;
+                return rc;
+            }
+            if (q == 0) { done = true; break; }  // the file shrank: stop at its end
+            got += (size_t)q;
+        }
+        const void *nul = memchr(buf, 0, got);
+        if (nul) {
+            got = (size_t)((const uint8_t *)nul - buf);
+            done = true;
+        }
+        if (got) {
+            HIPCHK(hipMemcpyAsync(c->h.bytes + off, buf, got, hipMemcpyHostToDevice, c->st));
+            HIPCHK(hipEventRecord(c->stage_ev[k & 1], c->st));
+        }
+        off += got;
+    }
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->n0 = off;
+    *n_loaded = off;
     return 0;
 }
 

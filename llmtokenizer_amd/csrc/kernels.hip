@@ -2695,6 +2695,72 @@ __device__ inline bool dec_leaf(uint32_t x, const uint32_t *pairs) {
     return x < 256 || pairs[2 * (x - 256)] == x;
 }
 
+constexpr uint64_t ELEN_UNK = ~0ull;
+
+// elen of every id of a merge list (one block; the list is small next to the
+// ids): leaves and self-referencing records first, then passes that resolve an
+// id once both halves are known, until a pass changes nothing.  A valid list
+// (halves created earlier) resolves in (tree depth) passes.  Records naming an
+// unknown id, and cycles, stay unresolved (ELEN_UNK): like the reference's
+// resolve_pair (bpe.c:23-92), which only fails when such a record is used.
+__global__ __launch_bounds__(1024) void k_dec_elen(const uint32_t *__restrict__ pairs, uint32_t nm,
+                                                    uint64_t *__restrict__ elen) {
+    const uint32_t V = 256 + nm;
+    __shared__ uint32_t changed;
+    for (uint32_t x = threadIdx.x; x < V; x += blockDim.x) {
+        if (x < 256) {
+            elen[x] = x ? 1 : 0;
+            continue;
+        }
+        const uint32_t a = pairs[2 * (x - 256)];
+        elen[x] = a == x ? ((uint8_t)a ? 1 : 0) : ELEN_UNK;  // self-reference: that one char (bpe.c:47-53)
+    }
+    __syncthreads();
+    for (;;) {
+        if (threadIdx.x == 0) changed = 0;
+        __syncthreads();
+        for (uint32_t x = 256 + threadIdx.x; x < V; x += blockDim.x) {
+            if (elen[x] != ELEN_UNK) continue;
+            const uint32_t a = pairs[2 * (x - 256)], b = pairs[2 * (x - 256) + 1];
+            if (a >= V || b >= V) continue;
+            const uint64_t ea = elen[a], eb = elen[b];
+            if (ea != ELEN_UNK && eb != ELEN_UNK) {
+                elen[x] = ea + eb;
+                changed = 1;
+            }
+        }
+        __syncthreads();
+        const uint32_t ch = changed;
+        __syncthreads();
+        if (!ch) break;
+    }
+}
+
+// ids outside the vocabulary (err bit 1) or naming an unresolvable record (bit 2)
+__global__ __launch_bounds__(256) void k_dec_check(const uint32_t *__restrict__ ids, uint64_t len, uint32_t V,
+                                                    const uint64_t *__restrict__ elen, uint32_t *__restrict__ err) {
+    uint32_t bad = 0;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < len; q += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t x = ids[q];
+        bad |= x >= V ? 1u : elen[x] == ELEN_UNK ? 2u : 0u;
+    }
+    for (int o = 32; o > 0; o >>= 1) bad |= __shfl_xor(bad, o);
+    if (bad && lane_id() == 0) atomicOr(err, bad);
+}
+
+// byte length of ids[i] (0 past the end: the scan's total lands at [len])
+struct DecLen {
+    const uint32_t *ids;
+    const uint64_t *elen;
+    uint64_t len;
+    uint32_t V;
+    __host__ __device__ uint64_t operator()(uint64_t i) const {
+        if (i >= len) return 0;
+        const uint32_t x = ids[i];
+        return x < V ? elen[x] : 0;
+    }
+};
+
 __global__ void k_dec_expand(const uint32_t *__restrict__ ids, uint64_t len, const uint32_t *__restrict__ pairs,
                              const uint64_t *__restrict__ elen, const uint64_t *__restrict__ off,
                              uint8_t *__restrict__ out) {

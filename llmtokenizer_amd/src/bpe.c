@@ -15,6 +15,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 static bpe_gpu_stats g_last_stats;
 
@@ -230,17 +231,13 @@ static uint32_t *arr_to_pairs(dyn_arr_t *arr, size_t *k)
     return pairs;
 }
 
-dyn_arr_t *bpe_train_bytes(const uint8_t *bytes, size_t n, long max_merges, int device, uint32_t **encoding,
-                           size_t *len)
+/* train on the corpus loaded into ctx, fetch merges + ids; destroys ctx */
+static dyn_arr_t *train_loaded(bpe_gpu_ctx *ctx, long max_merges, uint32_t **encoding, size_t *len)
 {
-    if (!bytes || !encoding || !len) return NULL;
-    bpe_gpu_ctx *ctx = NULL;
     dyn_arr_t *arr = NULL;
     uint32_t *pairs = NULL, *ids = NULL;
     size_t k = 0, n_ids = 0, got = 0;
     int rc;
-    if ((rc = open_engine(device, &ctx))) goto fail;
-    if ((rc = bpe_gpu_load(ctx, bytes, n))) { report("load", rc); goto fail; }
     if ((rc = bpe_gpu_train(ctx, max_merges, &k))) { report("train", rc); goto fail; }
     pairs = malloc((k ? k : 1) * 2 * sizeof(uint32_t));
     if (!pairs) goto fail;
@@ -264,6 +261,22 @@ fail:
     *encoding = NULL;
     *len = 0;
     return NULL;
+}
+
+dyn_arr_t *bpe_train_bytes(const uint8_t *bytes, size_t n, long max_merges, int device, uint32_t **encoding,
+                           size_t *len)
+{
+    if (!bytes || !encoding || !len) return NULL;
+    bpe_gpu_ctx *ctx = NULL;
+    int rc;
+    if ((rc = open_engine(device, &ctx)) || (rc = bpe_gpu_load(ctx, bytes, n))) {
+        if (ctx) report("load", rc);
+        bpe_gpu_destroy(ctx);
+        *encoding = NULL;
+        *len = 0;
+        return NULL;
+    }
+    return train_loaded(ctx, max_merges, encoding, len);
 }
 
 /* ------------------------------------------------- one process, N devices */
@@ -430,21 +443,57 @@ dyn_arr_t *compress_multi(const char *path, long max_merges, int ngpu, uint32_t 
     return arr;
 }
 
+/* get_file (bpe.c:130-180) + strlen (bpe.c:555) + compress on one device, the
+ * file streamed into HBM through pinned staging (bpe_gpu_load_fd) instead of
+ * a whole-file host buffer; same messages and NULL returns as the reference */
 dyn_arr_t *compress_ex(const char *path, long max_merges, int device, uint32_t **encoding, size_t *len)
 {
     if (!path || !encoding || !len) return NULL;
-    char *buf = get_file(path);
-    if (!buf) return NULL;
-    size_t n = strlen(buf); /* the reference trains on the text up to the first NUL */
-    if (n < 2) {
-        printf("Error: File contains less than 2 characters\n");
-        fflush(stdout);
-        free(buf);
+    FILE *f = fopen(path, "r");
+    if (!f) {
+        perror("fopen");
         return NULL;
     }
-    dyn_arr_t *arr = bpe_train_bytes((const uint8_t *)buf, n, max_merges, device, encoding, len);
-    free(buf);
-    return arr;
+    long size = -1;
+    if (fseek(f, 0, SEEK_END) == -1) {
+        perror("fseek");
+        fclose(f);
+        return NULL;
+    }
+    if ((size = ftell(f)) == -1) {
+        perror("ftell");
+        fclose(f);
+        return NULL;
+    }
+    rewind(f);
+    /* strlen < 2 needs only the first two bytes: the reference's message
+     * comes before any GPU work */
+    unsigned char head[2] = {0, 0};
+    const ssize_t h = size >= 2 ? pread(fileno(f), head, 2, 0) : 0;
+    if (h < 0) {
+        perror("fread");
+        fclose(f);
+        return NULL;
+    }
+    if (h < 2 || !head[0] || !head[1]) {
+        printf("Error: File contains less than 2 characters\n");
+        fflush(stdout);
+        fclose(f);
+        return NULL;
+    }
+    bpe_gpu_ctx *ctx = NULL;
+    size_t n = 0;
+    int rc = open_engine(device, &ctx);
+    if (!rc && (rc = bpe_gpu_load_fd(ctx, fileno(f), (size_t)size, &n))) {
+        if (rc == BPE_GPU_EIO) perror("fread");
+        else report("load", rc);
+    }
+    fclose(f);
+    if (rc) {
+        bpe_gpu_destroy(ctx);
+        return NULL;
+    }
+    return train_loaded(ctx, max_merges, encoding, len);
 }
 
 dyn_arr_t *compress(const char *path, uint32_t **encoding, size_t *len)

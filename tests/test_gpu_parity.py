@@ -157,3 +157,49 @@ def test_table_regrowth_matches_presized(monkeypatch):
     assert (e2.merges() == m0).all() and (e2.ids() == i0).all()
     om, oids, _ = O.train(data, 400, O.EMU)
     assert (m0 == om).all() and (i0 == oids).all()
+
+
+def test_decode_errors_and_self_reference():
+    """Device decode (k_dec_elen / k_dec_check): unknown ids, records naming
+    unknown ids and cyclic lists are errors; a record whose first element is
+    its own id decodes as that one char (reference resolve_pair, bpe.c:23-92)."""
+    e = api.Engine(0)
+    m = np.array([[104, 105], [256, 33]], dtype=np.uint32)  # 256 = "hi", 257 = "hi!"
+    assert e.decode(np.array([257, 32, 256], dtype=np.uint32), m) == b"hi! hi"
+    with pytest.raises(api.BpeError):
+        e.decode(np.array([258], dtype=np.uint32), m)            # id outside the vocabulary
+    bad = np.array([[300, 65]], dtype=np.uint32)  # a record naming an unknown id: an error only when used
+    assert e.decode(np.array([65], dtype=np.uint32), bad) == O.decode(np.array([65]), bad) == b"A"
+    with pytest.raises(api.BpeError):
+        e.decode(np.array([256], dtype=np.uint32), bad)
+    with pytest.raises(api.BpeError):
+        e.decode(np.array([256], dtype=np.uint32), np.array([[257, 65], [256, 66]], dtype=np.uint32))  # cycle
+    # self reference (bpe.c:47-53): that one char, (char)256 == NUL vanishes
+    self_ref = np.array([[256, 7], [321, 9]], dtype=np.uint32)  # (id 257 = [321, 9]: 321 unknown)
+    assert e.decode(np.array([256, 65], dtype=np.uint32), self_ref) == b"A"
+    # a deep chain (a-run merges: every id doubles the previous one)
+    chain = np.array([[97, 97]] + [[256 + r, 256 + r] for r in range(12)], dtype=np.uint32)
+    assert e.decode(np.array([256 + 12], dtype=np.uint32), chain) == b"a" * (1 << 13)
+    assert e.decode(np.zeros(0, dtype=np.uint32), chain) == b""
+
+
+def test_streaming_file_load(tmp_path):
+    """bpe_gpu_load_fd (pinned double-buffered staging, 64 MiB chunks) ==
+    the bytes themselves, and stops at the first NUL even several chunks in;
+    compress(path) on such a file == training on the truncated bytes."""
+    n = 150 << 20
+    data = bytearray(synth_bytes(31, n))
+    cut = (100 << 20) + 7
+    data[cut] = 0
+    p = tmp_path / "big.txt"
+    p.write_bytes(bytes(data))
+    e = api.Engine(0)
+    assert e.load_file(str(p)) == cut
+    e.train(0)
+    got = e.ids()
+    assert got.size == cut and got.astype(np.uint8).tobytes() == bytes(data[:cut])
+    merges, ids = api.compress(str(p), max_merges=4)
+    ref = api.Engine(0)
+    ref.load(bytes(data[:cut]))
+    ref.train(4)
+    assert (merges == ref.merges()).all() and (ids == ref.ids()).all()
