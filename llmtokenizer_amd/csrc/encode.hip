@@ -241,7 +241,6 @@ __global__ __launch_bounds__(ESCAN_T) void k_scan_batch(const Eng *__restrict__ 
     __syncthreads();
     const uint64_t n = E->n0;
     const uint32_t *__restrict__ tok = E->tok;
-    const uint32_t *__restrict__ dist = E->dist;
     uint32_t *scratch = E->ids_out;
     for (uint32_t t0 = blockIdx.x * ESCAN_T; t0 < total; t0 += gridDim.x * ESCAN_T) {
         const uint32_t t = t0 + tid;
@@ -254,7 +253,7 @@ __global__ __launch_bounds__(ESCAN_T) void k_scan_batch(const Eng *__restrict__ 
             if (md == 2) {
                 j = E->occ[soff[m] + q];
                 if (tag_ok(E->occnb[soff[m] + q] >> 8, a) && tok[j] == b) {
-                    i = v_left<SH>(tok, dist, j);
+                    i = v_left<SH>(tok, j);
                     ok = i >= 0 && tok[i] == a;  // i < 0: the left shard's pair
                 }
             } else {
@@ -268,7 +267,7 @@ __global__ __launch_bounds__(ESCAN_T) void k_scan_batch(const Eng *__restrict__ 
             if (ok && a == b) {
                 // only the run's first token walks it, pairing 0-1, 2-3, ...; a run
                 // entering from the left shard continues its parity
-                const int64_t ps = v_left<SH>(tok, dist, i);
+                const int64_t ps = v_left<SH>(tok, i);
                 const uint32_t p = ps >= 0 ? tok[ps] : (SH ? sh.HL[0] : HOLE);
                 if (p == a) {
                     if (ps >= 0) ok = false;
@@ -346,7 +345,7 @@ __global__ __launch_bounds__(256) void k_apply_batch(const Eng *__restrict__ E, 
     block_exscan256(sR, spre, nb);
     const uint32_t occ_base = B->occ_base;
     const uint64_t n = E->n0;
-    uint32_t *tok = E->tok, *dist = E->dist;
+    uint32_t *tok = E->tok;
     if (blockIdx.x == gridDim.x - 1) {
         // bookkeeping of this batch, my retired first token, then the next
         // batch into the other descriptor
@@ -362,9 +361,13 @@ __global__ __launch_bounds__(256) void k_apply_batch(const Eng *__restrict__ E, 
             C->n_live -= spre[nb];
             const uint32_t xl = SH ? C->xleft : HOLE;
             if (xl != HOLE) {
-                tok[xl] = HOLE;
                 const uint64_t end = (uint64_t)xl + C->xleft_lb;
-                if (end - 1 < n) dist[end - 1] = MARK;
+                if (end - 1 == xl) {
+                    tok[xl] = MARKV;
+                } else {
+                    tok[xl] = HOLE;
+                    if (end - 1 < n) tok[end - 1] = MARKV;
+                }
                 C->F1 = (uint32_t)(end < n ? end : n);
             }
         }
@@ -384,8 +387,12 @@ __global__ __launch_bounds__(256) void k_apply_batch(const Eng *__restrict__ E, 
         const uint64_t j = i + sla[m], k = j + slb[m];
         tok[i] = sz[m];
         if (!SH || j < n) {  // else: b starts in a later shard, which retires it
-            tok[j] = HOLE;
-            if (!SH || k - 1 < n) dist[k - 1] = (uint32_t)(k - 1 - i);
+            if (k - 1 == j) {
+                tok[j] = end_code(k - 1 - i);
+            } else {
+                tok[j] = HOLE;
+                if (!SH || k - 1 < n) tok[k - 1] = end_code(k - 1 - i);
+            }
             if (SH && j == L1) C->L1new = (uint32_t)i;
         }
         E->occ[occ_base + spre[m] + q] = (uint32_t)i;
@@ -410,14 +417,14 @@ __global__ __launch_bounds__(256) void k_link_batch(const Eng *__restrict__ E, c
     block_exscan256(sR, spre, nb);
     const uint32_t total = sseg[nb], occ_base = B->occ_base;
     const int64_t n = (int64_t)E->n0;
-    const uint32_t *tok = E->tok, *dist = E->dist;
+    const uint32_t *tok = E->tok;
     for (uint32_t t = blockIdx.x * blockDim.x + tid; t < total; t += gridDim.x * blockDim.x) {
         const uint32_t m = seg_of(sseg, nb, t);
         const uint32_t q = t - sseg[m];
         if (q >= sR[m]) continue;
         const uint32_t e = occ_base + spre[m] + q;
         const int64_t i = E->occ[e];
-        const int64_t ps = v_left<SH>(tok, dist, i);
+        const int64_t ps = v_left<SH>(tok, i);
         const int64_t k = i + E->tlen[sz[m]];
         E->occnb[e] = nb_tag(ps >= 0 ? tok[ps] : HOLE, k < n ? tok[k] : HOLE);
     }

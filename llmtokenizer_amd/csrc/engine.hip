@@ -350,7 +350,6 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     const uint64_t n0 = c->n0;
     int r;
     if ((r = dalloc(c, &h.tok, n0 + 8, false))) return r;  // + 8: k_scan's 2x16-byte windows
-    if ((r = dalloc(c, &h.dist, n0, false))) return r;  // read only where written (left_start)
     if ((r = dalloc(c, &h.tlen, h.vcap))) return r;
     if ((r = dalloc(c, &h.rank, 256))) return r;
     if ((r = dalloc(c, &h.plist, n0, false))) return r;
@@ -1029,7 +1028,8 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
         case STOP_ENC_END:
             return 0;
         case STOP_ERROR:
-            return fail(BPE_GPU_EINTERNAL, C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : "thread-stat table full");
+            return fail(C.err == 5 ? BPE_GPU_ERANGE : BPE_GPU_EINTERNAL,
+                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than 2^31 - 3 bytes" : "thread-stat table full");
         case STOP_REDO:  // missed prediction: k_select committed the real merge
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;

@@ -1,13 +1,15 @@
 // engine_common.h -- shared device-side definitions of the gfx950 BPE engine.
 //
 // Token representation in HBM ("position space"): the corpus keeps its
-// original byte positions 0..n0-1 for the whole run.  A token covering bytes
-// [s, e) stores its id at tok[s]; every other slot of the span holds HOLE.
-// dist[e-1] = e-1-s lets the token to the RIGHT of a span find the span's
-// start (its left neighbour) in O(1); the right neighbour of a token at s is
-// simply s + tlen[id].  Merging two adjacent tokens is therefore three word
-// writes, and no compaction pass is needed during training (the reference
-// rewrites the whole u32 array per merge, bpe/src/bpe.c:760-777).
+// original byte positions 0..n0-1 for the whole run, in ONE u32 array tok[].
+// A token covering bytes [s, e) stores its id at tok[s]; a token of two or
+// more slots stores END_FLAG | (e-1-s) at its end slot tok[e-1], so the token
+// to the RIGHT of a span finds the span's start (its left neighbour) from the
+// one slot before it; interior slots hold HOLE (or a stale end code, never
+// read).  The right neighbour of a token at s is simply s + tlen[id].  Merging
+// two adjacent tokens writes two or three words, all inside the new span (one
+// or two 64-byte sectors), and no compaction pass is needed during training
+// (the reference rewrites the whole u32 array per merge, bpe/src/bpe.c:760-777).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -15,7 +17,12 @@
 
 namespace bpeamd {
 
-constexpr uint32_t HOLE = 0xFFFFFFFFu;
+constexpr uint32_t HOLE = 0xFFFFFFFFu;     // interior slot of a token (and "no id")
+constexpr uint32_t END_FLAG = 0x80000000u; // tok[] end slot of a multi-slot token: END_FLAG | (end - start)
+constexpr uint32_t MARKV = 0xFFFFFFFEu;    // tok[] end slot of a token that starts in an earlier shard
+constexpr uint64_t END_MAX = 0x7FFFFFFDull; // longest end distance an end code holds
+__host__ __device__ inline bool is_id(uint32_t v) { return v < END_FLAG; }  // a token start
+__host__ __device__ inline uint32_t end_code(uint64_t d) { return END_FLAG | (uint32_t)d; }
 constexpr uint32_t DENSE = 2048;         // ids aggregated in LDS / stored densely in delta vectors
 #ifndef BPE_REPL
 #define BPE_REPL 8
@@ -29,7 +36,6 @@ constexpr uint64_t MERGED_B0 = 65536;    // reference MERGED_TABLE_BUCKET_NUM (b
 constexpr uint64_t THREAD_B0 = 256;      // reference PER_THREAD_TABLE_BUCKET_NUM (bpe.c:610)
 constexpr uint32_t L1W = 1024;           // slots per level-1 summary block
 constexpr uint32_t L2W = 256;            // level-1 entries per level-2 summary
-constexpr uint32_t MARK = 0xFFFFFFFFu;   // dist[] of an end slot whose token starts in an earlier shard
 constexpr uint32_t EDGE_WORDS = 16;      // words per shard edge record
 constexpr uint32_t TS_SLOTS = 4096;      // merges kept by the debug block timeline
 // debug timeline slots (wall clock; entries stored complemented so that
@@ -103,8 +109,7 @@ struct Eng {
     uint32_t A;           // distinct bytes in the corpus
     uint32_t encode;      // 1: encode mode (no counting)
     uint8_t *bytes;
-    uint32_t *tok;
-    uint32_t *dist;
+    uint32_t *tok;        // ids at token starts, end codes at end slots (see above)
     uint32_t *tlen;       // byte length of each id
     uint32_t *rank;       // [256] byte -> dense rank (HOLE if absent)
     uint32_t *plist;      // byte-pair positions grouped by rank key (counting sort)

@@ -138,18 +138,23 @@ __device__ inline uint32_t id_at(const uint32_t *__restrict__ tok, HaloT &h, int
     return tok[p];
 }
 
-// start of the token left of the token starting at p.  A single-slot token is
-// its own end slot (tok != HOLE there); a longer one stored its start distance
-// in dist[end] when it was created, or MARK when it starts in an earlier
-// shard -- so dist never needs initialising.
+// start of the token whose end slot is e, from the word there: a single-slot
+// token is its own end slot (an id), a longer one left its start distance
+// (end code), MARKV when it starts in an earlier shard (-1: the halo)
 template <bool SH = true>
-__device__ inline int64_t v_left(const uint32_t *__restrict__ tok, const uint32_t *__restrict__ dist, int64_t p) {
+__device__ inline int64_t start_of_end(uint32_t v, int64_t e) {
+    if (is_id(v)) return e;
+    if (SH && v == MARKV) return -1;
+    const int64_t d = v & ~END_FLAG;
+    if (!SH) return e - d;  // one shard: every end code is a real distance
+    return d > e ? -1 : e - d;
+}
+
+// start of the token left of the token starting at p: one load, tok[p-1]
+template <bool SH = true>
+__device__ inline int64_t v_left(const uint32_t *__restrict__ tok, int64_t p) {
     if (p <= 0) return p - 1;
-    const int64_t e = p - 1;
-    if (tok[e] != HOLE) return e;
-    const uint32_t d = dist[e];
-    if (!SH) return e - (int64_t)d;  // one shard: every dist[] is a real distance
-    return (int64_t)d > e ? -1 : e - (int64_t)d;
+    return start_of_end<SH>(tok[p - 1], p - 1);
 }
 
 // start of the token after the token of length len starting at p (p >= 0)
@@ -320,7 +325,6 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
     uint32_t *const Rc = SPEC ? &C->sRp[S.parity ^ 1u] : &C->R;
     const int64_t n = (int64_t)E->n0;
     const uint32_t *__restrict__ tok = E->tok;
-    const uint32_t *__restrict__ dist = E->dist;
     const uint32_t la = E->tlen[a], lb = E->tlen[b];
     const bool count = !E->encode;
     const uint32_t obase = SPEC ? S.occ_top + S.R : S.occ_top;
@@ -352,19 +356,19 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
         bool ok = false;
         int64_t i = 0, j = 0;
         // Everything a candidate needs that depends only on its position is
-        // loaded in ONE round trip (the token, its partner, the left slot and
-        // its dist, the right neighbour of the pair): the scan is a chain of
-        // dependent gathers, so round trips, not bytes, set its time.
-        uint32_t tl = HOLE, dl = 0, tr = HOLE;
+        // loaded in ONE round trip (the token, its partner, the left slot --
+        // an id, or the end code that gives the left token's start -- and the
+        // right neighbour of the pair): the scan is a chain of dependent
+        // gathers, so round trips, not bytes, set its time.
+        uint32_t tl = HOLE, tr = HOLE;
         if (e < len) {
             if (mode == 2) {
                 j = E->occ[off + e];
                 if (tag_ok(E->occnb[off + e] >> 8, want) && tok[j] == b) {
-                    i = v_left<SH>(tok, dist, j);
+                    i = v_left<SH>(tok, j);
                     ok = i >= 0 && tok[i] == a;  // i < 0: the pair is the left shard's
                     if (ok) {
                         tl = i > 0 ? tok[i - 1] : HOLE;
-                        dl = i > 0 ? dist[i - 1] : 0;
                         tr = j + lb < n ? tok[j + lb] : HOLE;
                     }
                 }
@@ -379,7 +383,6 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
                     tl = i > 0 ? W.at(i - 1) : HOLE;
                     tr = kk >= n ? HOLE : W.has(kk) ? W.at(kk) : tok[kk];
                     ok = t0 == a && t1 == b && j < n;
-                    if (ok && i > 0 && tl == HOLE) dl = dist[i - 1];  // left token spans slots
                 }
             }
         }
@@ -388,15 +391,11 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
             if (ok) {
                 list[slot] = (uint32_t)i;
                 // left neighbour from the preloaded slot i-1 (v_left without reloading)
-                int64_t ps;
-                if (i == 0) ps = -1;
-                else if (tl != HOLE) ps = i - 1;
-                else if (SH && (int64_t)dl > i - 1) ps = -1;
-                else ps = i - 1 - (int64_t)dl;
-                const uint32_t p = (i > 0 && tl != HOLE) ? tl : id_at<SH>(tok, h, ps, n);
+                const int64_t ps = i == 0 ? -1 : start_of_end<SH>(tl, i - 1);
+                const uint32_t p = (i > 0 && is_id(tl)) ? tl : id_at<SH>(tok, h, ps, n);
                 bool cov = false;
                 if (p != HOLE) {
-                    if (p == b) cov = id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a;
+                    if (p == b) cov = id_at<SH>(tok, h, v_left<SH>(tok, ps), n) == a;
                     if (!cov && count) {
                         vadd<SH>(s, E, P, V_DL, p);
                         vadd<SH>(s, E, P, V_IL, p);
@@ -418,7 +417,7 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
             // a == b: only the thread holding a run's first token walks it,
             // pairing tokens 0-1, 2-3, ... (greedy left-to-right).  A run that
             // enters from the left shard continues its parity (hlrun a's precede).
-            const int64_t ps = v_left<SH>(tok, dist, i);
+            const int64_t ps = v_left<SH>(tok, i);
             const uint32_t p = id_at<SH>(tok, h, ps, n);
             bool start = true, left = p != HOLE;
             int64_t pos = i;
@@ -467,10 +466,10 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
                 if (hh.HL[0] == a && tok[F1] == b && (a != b || (hh.hlrun & 1))) xl = (uint32_t)F1;
                 const int64_t i = C->L1;
                 if (tok[i] == a && hh.HR[0] == b && (a != b || !(hh.myidx & 1))) {
-                    const int64_t ps = v_left<SH>(tok, dist, i);
+                    const int64_t ps = v_left<SH>(tok, i);
                     const uint32_t p = id_at<SH>(tok, h, ps, n);
                     bool cov = p == HOLE;
-                    if (!cov) cov = a != b ? (p == b && id_at<SH>(tok, h, v_left<SH>(tok, dist, ps), n) == a) : p == a;
+                    if (!cov) cov = a != b ? (p == b && id_at<SH>(tok, h, v_left<SH>(tok, ps), n) == a) : p == a;
                     const uint32_t q = hh.HR[1];
                     const bool nocc = q == a && hh.HR[2] == b;
                     stage_one(list, ltag, &lcount, Rc, occz, tagz, (uint32_t)i,
@@ -656,25 +655,30 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
         const uint32_t la = E->tlen[a], lb = E->tlen[b];
         const uint32_t *occz = E->occ + S.occ_top;
         uint32_t *tok = E->tok;
-        uint32_t *dist = E->dist;
         const uint64_t n = E->n0;
         const bool sh = E->sharded;
         const uint64_t L1 = C->L1;
         for (uint32_t e = bid * blockDim.x + threadIdx.x; e < R; e += roleA_blocks * blockDim.x) {
             const uint64_t i = occz[e];
             const uint64_t j = i + la, k = j + lb;
-            if (UNDO) {  // b's end slot had its own start distance (j >= n: b is a later shard's)
+            if (UNDO) {  // b's end slot had its own start distance (j >= n: b is a later shard's);
+                         // a's end slot was never rewritten
                 tok[i] = a;
                 if (j < n) {
                     tok[j] = b;
-                    if (lb > 1 && k - 1 < n) dist[k - 1] = lb - 1;
+                    if (lb > 1 && k - 1 < n) tok[k - 1] = end_code(lb - 1);
                 }
                 continue;
             }
             tok[i] = z;
             if (j < n) {  // else: b starts in a later shard, which retires it
-                tok[j] = HOLE;
-                if (k - 1 < n) dist[k - 1] = (uint32_t)(k - 1 - i);  // k-1 >= j: never a token start now
+                if (k - 1 - i > END_MAX) C->err = 5;  // (a token longer than an end code holds)
+                if (k - 1 == j) {
+                    tok[j] = end_code(k - 1 - i);
+                } else {
+                    tok[j] = HOLE;
+                    if (k - 1 < n) tok[k - 1] = end_code(k - 1 - i);  // k-1 > j: never a token start now
+                }
                 if (sh && j == L1) C->L1new = (uint32_t)i;
             }
         }
@@ -685,9 +689,13 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
             if (E->spec_on) E->tlen[z] = (a < z && b < z) ? la + lb : 1;  // (the fused k_select does not)
             const uint32_t xl = sh ? C->xleft : HOLE;
             if (xl != HOLE) {  // my first token is the b of the left shard's pair
-                tok[xl] = HOLE;
                 const uint64_t end = (uint64_t)xl + lb;
-                if (end - 1 < n) dist[end - 1] = MARK;
+                if (end - 1 == xl) {
+                    tok[xl] = MARKV;
+                } else {
+                    tok[xl] = HOLE;
+                    if (end - 1 < n) tok[end - 1] = MARKV;
+                }
                 C->F1 = (uint32_t)(end < n ? end : n);
             }
             if (sh) C->erec_ready = 0;  // the tokens at my edges may have changed
@@ -699,7 +707,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
             if (xl != HOLE) {
                 tok[xl] = b;
                 const uint64_t end = (uint64_t)xl + lb;
-                if (lb > 1 && end - 1 < n) dist[end - 1] = lb - 1;
+                if (lb > 1 && end - 1 < n) tok[end - 1] = end_code(lb - 1);
                 C->F1 = xl;
             }
             C->L1new = HOLE;
@@ -1670,7 +1678,7 @@ __device__ inline uint32_t block_prefix256(bool pred, uint32_t *total) {
 }
 
 // This shard's edge record into rec (LDS), by the first 256 threads of the
-// block (every thread calls it).  Token starts are exactly the non-HOLE slots
+// block (every thread calls it).  Token starts are exactly the id slots
 // of [F1, L1], so the first / last tokens are found with block-wide ballots
 // over 256-slot windows (one round trip when tokens are short) instead of a
 // dependent walk.
@@ -1699,8 +1707,8 @@ __device__ void edge_record_compute(const Eng *__restrict__ E, Ctl *__restrict__
             const int64_t p = base + tid;
             const uint32_t v = act && p <= L1 ? aload(&tok[p]) : HOLE;
             uint32_t tot;
-            const uint32_t r = found + block_prefix256(v != HOLE, &tot);
-            if (v != HOLE && r < 3) rec[ER_F + r] = v;
+            const uint32_t r = found + block_prefix256(is_id(v), &tot);
+            if (is_id(v) && r < 3) rec[ER_F + r] = v;
             found += tot;
         }
         if (tid == 0) slast = aload(&tok[L1]);
@@ -1712,9 +1720,9 @@ __device__ void edge_record_compute(const Eng *__restrict__ E, Ctl *__restrict__
             const int64_t p = top - (int64_t)tid;  // rank from the end grows with tid
             const uint32_t v = act && p >= F1 ? aload(&tok[p]) : HOLE;
             uint32_t tot;
-            const uint32_t r = foundL + block_prefix256(v != HOLE, &tot);
-            if (v != HOLE && r < 3) rec[ER_L + r] = v;
-            if (v != HOLE && v != last) atomicMin(&firstdiff, r);
+            const uint32_t r = foundL + block_prefix256(is_id(v), &tot);
+            if (is_id(v) && r < 3) rec[ER_L + r] = v;
+            if (is_id(v) && v != last) atomicMin(&firstdiff, r);
             __syncthreads();
             done = firstdiff != HOLE;
             foundL += tot;
@@ -2370,7 +2378,7 @@ __global__ void k_rehash(const Eng *__restrict__ E, Ctl *__restrict__ C, const u
 }
 
 // ------------------------------------------------------------- compaction
-// Live tokens (tok != HOLE) in position order -> ids (mode 0) or the
+// Live tokens (id slots of tok) in position order -> ids (mode 0) or the
 // compacted-index -> position map used by the tracked statistics (mode 1).
 // Tiles of CTILE positions; 256 threads read one uint4 (4 positions) each per
 // round, so loads and the order-preserving writes are both contiguous.
@@ -2387,7 +2395,7 @@ __device__ inline uint32_t live4(const uint32_t *tok, uint64_t p, uint64_t n0, u
         out->z = p + 2 < n0 ? tok[p + 2] : HOLE;
         out->w = HOLE;
     }
-    return (out->x != HOLE) + (out->y != HOLE) + (out->z != HOLE) + (out->w != HOLE);
+    return is_id(out->x) + is_id(out->y) + is_id(out->z) + is_id(out->w);
 }
 
 __global__ __launch_bounds__(256) void k_live_count(const Eng *__restrict__ E, const Ctl *__restrict__ C, int guard) {
@@ -2452,7 +2460,7 @@ __global__ __launch_bounds__(256) void k_live_write(const Eng *__restrict__ E, c
             const uint32_t x4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                if (x4[q] != HOLE) out[o++] = mode == 0 ? x4[q] : (uint32_t)(p + q);
+                if (is_id(x4[q])) out[o++] = mode == 0 ? x4[q] : (uint32_t)(p + q);
             base += ws[0] + ws[1] + ws[2] + ws[3];
             __syncthreads();
         }
@@ -2491,7 +2499,7 @@ __global__ __launch_bounds__(LC_T) void k_live_compact(const Eng *__restrict__ E
     const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (uint32_t r = 0; r < LC_R; r++) {
-        const uint32_t c = (v[r].x != HOLE) + (v[r].y != HOLE) + (v[r].z != HOLE) + (v[r].w != HOLE);
+        const uint32_t c = is_id(v[r].x) + is_id(v[r].y) + is_id(v[r].z) + is_id(v[r].w);
         // c in 0..4: prefix and total from three ballots
         const unsigned long long b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
         pre[r] = (uint32_t)__popcll(b0 & lt) + 2u * (uint32_t)__popcll(b1 & lt) + 4u * (uint32_t)__popcll(b2 & lt);
@@ -2545,7 +2553,7 @@ __global__ __launch_bounds__(LC_T) void k_live_compact(const Eng *__restrict__ E
         uint32_t o = pre[r];
 #pragma unroll
         for (int q = 0; q < 4; q++)
-            if (x4[q] != HOLE) sg[o++] = x4[q];
+            if (is_id(x4[q])) sg[o++] = x4[q];
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's staging stores landed
         __builtin_amdgcn_wave_barrier();
         const uint32_t cnt = __shfl(o, 63);  // lane 63's end = the wave's total this round
