@@ -448,7 +448,7 @@ def main():
                          "total_engine": round(st["ms_total"], 3), "per_merge_us": round(st["ms_train"] * 1e3 / merges, 2)},
         "engine": {k2: st[k2] for k2 in ("n_out", "iterations", "distinct_pairs", "merged_buckets",
                                           "rule_ties", "table_grows", "keys", "l1_rescanned", "spec_hits",
-                                          "spec_misses", "candidates", "occurrences", "hot_rebuilds", "hot_mode")},
+                                          "spec_misses", "candidates", "occurrences", "hot_rebuilds", "hot_mode", "hot_scanned")},
     })
     out.update(extra)
     cp = committed_profile(name)

@@ -71,6 +71,7 @@ typedef struct {
     uint64_t count_pass_span; /* 1: the count pass ran in span form (k_pair_hist_span) */
     uint64_t hot_rebuilds;    /* hot-set argmax: full-table rebuilds of the listed keys */
     uint64_t hot_mode;        /* 0 level summaries, 1 hot set, 2 hot set given up mid-run */
+    uint64_t hot_scanned;     /* hot-set entries reduced, summed over the merges */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */

@@ -1097,8 +1097,9 @@ void print_timeline(bpe_gpu_ctx *c, uint32_t zlast) {
                                    "K2 select out", "K2 applyA out", "K2 applyB out", "K1 last in",
                                    "scan cands done", "scan list flushed", "scan deltas flushed",
                                    "B deltas loaded", "B table updated", "B marks listed",
-                                   "B last insert done", "B last find done"};
-    for (uint32_t z = 257; z < zlast && z < TS_SLOTS; z++) {
+                                   "B last insert done", "B last find done", "K1 rescan blocks cleared"};
+    const uint32_t zfrom = getenv("BPE_DEBUG_TS_FROM") ? (uint32_t)atoi(getenv("BPE_DEBUG_TS_FROM")) : 257;
+    for (uint32_t z = std::max<uint32_t>(257, zfrom); z < zlast && z < TS_SLOTS; z++) {
         const unsigned long long *r = &t[(size_t)z * TS_N];
         bool ok = true;
         for (int k = 0; k < TS_N; k++) ok = ok && r[k] != 0;
@@ -1470,6 +1471,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.spec_hits = C.counters[7];
     c->stats.spec_misses = C.counters[8];
     c->stats.hot_rebuilds = C.hot_rebuilds;
+    c->stats.hot_scanned = C.hot_scanned;
     c->stats.hot_mode = c->h.hot ? 1 : c->hot_fallback ? 2 : 0;
     if (c->h.dbgts) print_timeline(c, C.z);
     if (getenv("BPE_DEBUG"))

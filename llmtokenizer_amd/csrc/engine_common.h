@@ -37,11 +37,12 @@ constexpr uint64_t THREAD_B0 = 256;      // reference PER_THREAD_TABLE_BUCKET_NU
 constexpr uint32_t L1W = 1024;           // slots per level-1 summary block
 constexpr uint32_t L2W = 256;            // level-1 entries per level-2 summary
 constexpr uint32_t EDGE_WORDS = 16;      // words per shard edge record
-constexpr uint32_t TS_SLOTS = 4096;      // merges kept by the debug block timeline
+constexpr uint32_t TS_SLOTS = 16384;     // merges kept by the debug block timeline
 // debug timeline slots (wall clock; entries stored complemented so that
 // atomicMax keeps the earliest): K1 = k_rescan_spec, K2 = k_fused
 enum { TS_K1_IN = 0, TS_K1_RESCAN, TS_K1_SCAN, TS_K2_IN, TS_K2_SELECT, TS_K2_APPLY_A, TS_K2_APPLY_B, TS_K1_LASTIN,
-       TS_S_CAND, TS_S_LIST, TS_S_DELTA, TS_B_DVAL, TS_B_TABLE, TS_B_MARKS, TS_B_PROBE, TS_B_COUNT, TS_N };
+       TS_S_CAND, TS_S_LIST, TS_S_DELTA, TS_B_DVAL, TS_B_TABLE, TS_B_MARKS, TS_B_PROBE, TS_B_COUNT, TS_K1_CLEARED,
+       TS_N };
 
 enum { V_DL = 0, V_DR = 1, V_IL = 2, V_IR = 3 };
 

@@ -1196,6 +1196,7 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ 
     ts_mark(E, S.z, TS_K1_LASTIN, false);
     if (blockIdx.x < rblocks) {
         rescan1_body(E, C, S, blockIdx.x, rblocks);
+        ts_mark(E, S.z, TS_K1_CLEARED, false, true);
         if (E->hot) hot_reduce_body(E, C, S, blockIdx.x, rblocks);
         scan_exit_stamp(E, blockIdx.x);
         ts_mark(E, S.z, TS_K1_RESCAN, false, true);
