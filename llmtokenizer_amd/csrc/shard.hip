@@ -83,6 +83,8 @@ struct bpe_gpu_group {
     // mailboxes mapped here, the counters and the descriptor the kernels read
     bool p2p = false, p2p_ready = false;
     uint32_t *mailbox = nullptr;
+    size_t mailbox_bytes = 0;
+    bool mailbox_uc = false;          // from the process-lifetime uncached cache
     uint32_t *xs = nullptr;
     P2P hp{};
     P2P *d_p2p = nullptr;
@@ -93,7 +95,49 @@ struct bpe_gpu_group {
     bpe_gpu_stats stats{};
 };
 
+#include <pthread.h>
+
 namespace {
+
+// Uncached mailboxes are never handed back to the HIP allocator: a freed
+// uncached range is given out again by plain hipMalloc in the same process
+// (tools/uc_reuse: same virtual addresses), and runs on buffers placed there
+// after a multi-rank run went wrong (tools/md_repro2.py: deterministic wrong
+// merges under ROCm 7.2, an illegal access under torch's bundled 7.0; exact
+// with the ranges kept out of circulation).  A released mailbox waits here
+// for the next group on its device that fits in it.
+struct UcBlock {
+    int dev;
+    void *p;
+    size_t bytes;
+};
+std::vector<UcBlock> g_uc_cache;
+pthread_mutex_t g_uc_mu = PTHREAD_MUTEX_INITIALIZER;
+
+hipError_t uc_take(int dev, size_t bytes, void **out, size_t *got) {
+    pthread_mutex_lock(&g_uc_mu);
+    size_t best = g_uc_cache.size();
+    for (size_t k = 0; k < g_uc_cache.size(); k++)
+        if (g_uc_cache[k].dev == dev && g_uc_cache[k].bytes >= bytes &&
+            (best == g_uc_cache.size() || g_uc_cache[k].bytes < g_uc_cache[best].bytes))
+            best = k;
+    if (best < g_uc_cache.size()) {
+        *out = g_uc_cache[best].p;
+        *got = g_uc_cache[best].bytes;
+        g_uc_cache.erase(g_uc_cache.begin() + best);
+        pthread_mutex_unlock(&g_uc_mu);
+        return hipSuccess;
+    }
+    pthread_mutex_unlock(&g_uc_mu);
+    *got = bytes;
+    return hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached);
+}
+
+void uc_give(int dev, void *p, size_t bytes) {
+    pthread_mutex_lock(&g_uc_mu);
+    g_uc_cache.push_back({dev, p, bytes});
+    pthread_mutex_unlock(&g_uc_mu);
+}
 
 // one device: the exchange is a sum / gather kernel over pointer tables
 bool local_mode(const bpe_gpu_group *g) { return !g->rccl && !g->p2p; }
@@ -694,10 +738,13 @@ static int group_create_p2p(int device, int nranks, int rank, long max_merges, u
     // words) and the set-up exchanges (byte-pair counts: up to 256^2 words)
     const uint64_t c0 = ((std::max<uint64_t>(65536, 4ull * (256 + (uint64_t)max_merges) + 2) + 3) / 4) * 4;
     const size_t bytes = ((size_t)MB_DATA0 + 2ull * nranks * c0) * 4;
-    // in-process groups (no handle) take a plain allocation: every mailbox
-    // access is a system-coherent load / store either way (p2p.hip)
-    e = handle ? hipExtMallocWithFlags((void **)&g->mailbox, bytes, hipDeviceMallocUncached)
-               : hipMalloc((void **)&g->mailbox, bytes);
+    // uncached (peers on other devices write it while my kernels poll it);
+    // kept out of the allocator after use (uc_take / uc_give).
+    // BPE_P2P_LOCAL_UNCACHED=0: in-process groups take plain memory (A/B)
+    static const bool local_uc = !getenv("BPE_P2P_LOCAL_UNCACHED") || atoi(getenv("BPE_P2P_LOCAL_UNCACHED"));
+    g->mailbox_uc = handle || local_uc;
+    e = g->mailbox_uc ? uc_take(device, bytes, (void **)&g->mailbox, &g->mailbox_bytes)
+                      : hipMalloc((void **)&g->mailbox, bytes);
     if (e != hipSuccess) { g->mailbox = nullptr; bpe_gpu_group_destroy(g); return fail(BPE_GPU_ENOMEM, "uncached mailbox", e); }
     if ((e = hipMemset(g->mailbox, 0, bytes)) != hipSuccess ||
         (e = hipMalloc(&g->xs, 64)) != hipSuccess || (e = hipMemset(g->xs, 0, 64)) != hipSuccess ||
@@ -810,7 +857,8 @@ void bpe_gpu_group_destroy(bpe_gpu_group *g) {
     if (g->d_ptrs_tmp) hipFree(g->d_ptrs_tmp);
     if (g->comm) (void)g->rccl->commDestroy(g->comm);
     for (void *p : g->opened) (void)hipIpcCloseMemHandle(p);
-    if (g->mailbox) hipFree(g->mailbox);
+    if (g->mailbox && g->mailbox_uc) uc_give(g->dev, g->mailbox, g->mailbox_bytes);
+    else if (g->mailbox) hipFree(g->mailbox);
     if (g->xs) hipFree(g->xs);
     if (g->d_p2p) hipFree(g->d_p2p);
     if (g->st) (void)hipStreamDestroy(g->st);
