@@ -54,7 +54,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 GIB = 1 << 30
-PROFILE_TAG = "r2"     # profiles/<tag>_bench_kernel_stats.csv, <tag>_pmc_traffic.json
+PROFILE_TAG = "r2"     # profiles/<tag>_train_kernel_stats.csv, <tag>_pmc_traffic.json (tools/gpu_profile.sh)
 
 
 def cpu_baseline(seed, size, merges):
@@ -172,7 +172,7 @@ def committed_profile(name):
     """rocprof average (ms) of kernel `name` and PMC traffic per launch from
     the committed summaries of this same command (profiles/<tag>_*)"""
     out = {}
-    p = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_bench_kernel_stats.csv")
+    p = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_train_kernel_stats.csv")
     if os.path.exists(p):
         with open(p) as f:
             for r in csv.DictReader(f):

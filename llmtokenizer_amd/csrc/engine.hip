@@ -568,6 +568,10 @@ int hot_rebuild(bpe_gpu_ctx *c) {
         HIPCHK(hipMemcpyAsync(&c->dC->full, &one, 4, hipMemcpyHostToDevice, c->st));
         HIPCHK(hipStreamSynchronize(c->st));
         c->hot_fallback = true;
+        for (hipGraphExec_t *gp : {&c->g_plain, &c->g_tracked}) {  // recaptured with the level-2 pass
+            if (*gp) c->retired.push_back(*gp);
+            *gp = nullptr;
+        }
         return 0;
     }
     k_hot_collect<<<2048, 256, 0, c->st>>>(c->dE, c->dC);
@@ -587,7 +591,8 @@ void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
         // fused speculative graph: entered with the current merge applied
         // (by the previous k_fused, or the host after a stop)
         k_rescan_spec<<<SPEC_RB + SPEC_SB, SCAN_T, 0, c->st>>>(c->dE, c->dC, SPEC_RB);
-        if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
+        // (the hot set needs no level-2 pass; a fall-back recaptures the graph)
+        if (c->h.hcap / L1W > SELECT_L1_MAX && !c->h.hot) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
         k_fused<<<1 + FUSED_A + FUSED_B, 1024, 0, c->st>>>(c->dE, c->dC, FUSED_A, nullptr);
         return;
     }
