@@ -224,6 +224,24 @@ def train_single(args, cx, out):
                                 "ids_checksum": "%016x" % e.ids_checksum(),
                                 "merges_md5": hashlib.md5(e.merges().tobytes()).hexdigest()}}
         extra["ingest"] = ingest_rate(e)
+        # configs[1]: a 1 MiB random_text.txt-shaped corpus (seed 1), 1024 merges,
+        # the reference's static 16-thread tie emulation (tracked iterations)
+        c1 = api.Engine(cx.local)
+        c1.synth(1, 1 << 20)
+        c1.train(1024)
+        t = timed_jobs(cx, lambda: c1.train(1024), 1)
+        extra["config1"] = {"value": round((1 << 20) / 1e6 * 1024 / t, 1), "ms": round(t * 1e3, 3),
+                            "workload": "configs[1]: 1 MiB seed-1 random_text.txt-shaped corpus, 1024 merges, "
+                                        "one job (tie order: the reference's static-schedule emulation)",
+                            "merges_md5": hashlib.md5(c1.merges().tobytes()).hexdigest()}
+        gold = os.path.join(ROOT, "tests", "golden", "synth_s1_1m.json")  # the reference's own merges
+        if os.path.exists(gold):
+            import numpy as np
+            with open(gold) as f:
+                gm = np.asarray(json.load(f)["merges"], dtype=np.uint32).reshape(-1, 2)
+            extra["config1"]["equals_reference_golden"] = bool(hashlib.md5(gm.tobytes()).hexdigest() ==
+                                                               extra["config1"]["merges_md5"])
+        c1.close()
     e.close()
     return el, merges, st, prof, got, extra
 
