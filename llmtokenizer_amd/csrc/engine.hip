@@ -21,6 +21,7 @@
 #include "../../include/bpe_gpu.h"
 #include "kernels.hip"
 #include "encode.hip"
+#include "encode_win.hip"
 
 using namespace bpeamd;
 
@@ -253,9 +254,11 @@ struct bpe_gpu_ctx {
     double prof_ms = 0, prof_bytes = 0;
     uint64_t prof_launches = 0;
     // grow-only device scratch of decode (ids, pairs, elen, offsets, scan
-    // temporaries, output, error words) and the pinned staging of file loads
-    void *dscr[7] = {};
-    size_t dscr_cap[7] = {};
+    // temporaries, output, error words; slots 0-6), of the window encoder
+    // (tables, halo bytes; 7-8), and the pinned staging of file loads
+    void *dscr[9] = {};
+    size_t dscr_cap[9] = {};
+    std::vector<uint32_t> ew_stage;  // host image of the window encoder's tables (outlives the upload)
     uint8_t *stage[2] = {};
     hipEvent_t stage_ev[2] = {};
 };
@@ -1310,6 +1313,181 @@ int ctx_new(int device, hipStream_t shared, bpe_gpu_ctx **out) {
     return 0;
 }
 
+// ------------------------------------------------ window encoder (encode_win.hip)
+
+int getenv_int(const char *k, int dflt) {
+    const char *v = getenv(k);
+    return v && *v ? atoi(v) : dflt;
+}
+
+// Batches of the commuting rule (encode.hip form_batch, without its scratch
+// cap) and the window encoder's lookup tables, as one host image:
+//   bp[65536] | ht[H] {key, value} | roles[V][2][8] (per id: batches using it left / right) | beq[nb] (bytes)
+struct EwPlan {
+    bool ok = false;
+    uint32_t nb = 0, H = 0;  // H: hash slots
+    size_t off_ht = 0, off_roles = 0, off_beq = 0, words = 0;
+};
+
+EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
+    EwPlan P;
+    if (m > EW_MAX_MERGES || getenv_int("BPE_ENC_WIN", 1) == 0) return P;
+    const uint32_t V = 256 + (uint32_t)m;
+    uint32_t H = 64;  // hash slots, at most half full
+    while (H < 2 * m) H <<= 1;
+    std::vector<uint32_t> bp(65536, ~0u), hkey(H, 0), hval(H, ~0u), batch(m);
+    std::vector<uint8_t> fl(V, 0), eq;
+    std::vector<uint32_t> touched;
+    auto slot = [&](uint32_t key) {
+        uint32_t s = (uint32_t)mix64(key) & (H - 1);
+        while (hkey[s] != 0 && hkey[s] != key) s = (s + 1) & (H - 1);
+        return s;
+    };
+    uint32_t b0 = 0, nb = 0;
+    for (uint32_t r = 0; r < m; r++) {
+        const uint32_t u = pairs[2 * r], v = pairs[2 * r + 1], z = 256 + r;
+        const bool valid = u < z && v < z, byte = u < 256 && v < 256;
+        uint32_t *first = nullptr;  // the key's first rank | batch << 16 (~0: new key)
+        if (valid) {
+            if (byte) {
+                first = &bp[(u << 8) | v];
+            } else {
+                const uint32_t key = ((u << 16) | v) + 1u, s = slot(key);
+                hkey[s] = key;
+                first = &hval[s];
+            }
+        }
+        if (r > b0) {
+            const uint8_t fu = valid ? fl[u] : 0, fv = valid ? fl[v] : 0;
+            const bool dep = ((fu | fv) & (UF_Z | UF_EQ)) || (fu & UF_R) || (fv & UF_L) || (u == v && (fu | fv)) ||
+                             (first && *first != ~0u && (*first & 0xFFFFu) >= b0);
+            if (dep) {
+                for (uint32_t id : touched) fl[id] = 0;
+                touched.clear();
+                nb++;
+                b0 = r;
+            }
+        }
+        if (valid) {
+            fl[u] |= UF_L | (u == v ? UF_EQ : 0);
+            fl[v] |= UF_R;
+            touched.push_back(u);
+            touched.push_back(v);
+            if (*first == ~0u) *first = r | (nb << 16);
+        }
+        fl[z] |= UF_Z;
+        touched.push_back(z);
+        batch[r] = nb;
+    }
+    if (m) nb++;
+    if (nb > EW_MAX_BATCHES) return P;
+    P.nb = nb;
+    P.H = H;
+    P.off_ht = 65536;
+    P.off_roles = P.off_ht + 2ull * H;  // (16-byte aligned: H >= 64)
+    P.off_beq = P.off_roles + (size_t)V * 16;
+    P.words = P.off_beq + (nb + 3) / 4 + 1;
+    img.assign(P.words, 0);
+    memcpy(img.data(), bp.data(), 65536 * 4);
+    for (uint32_t k = 0; k < H; k++) {
+        img[P.off_ht + 2 * k] = hkey[k];
+        img[P.off_ht + 2 * k + 1] = hval[k];
+    }
+    uint32_t *roles = img.data() + P.off_roles;
+    uint8_t *beq = (uint8_t *)(img.data() + P.off_beq);
+    for (uint32_t r = 0; r < m; r++) {
+        const uint32_t u = pairs[2 * r], v = pairs[2 * r + 1], z = 256 + r;
+        if (!(u < z && v < z)) continue;
+        const uint32_t b = batch[r];
+        roles[(size_t)u * 16 + (b >> 5)] |= 1u << (b & 31);
+        roles[(size_t)v * 16 + 8 + (b >> 5)] |= 1u << (b & 31);
+        if (u == v) beq[batch[r]] = 1;
+    }
+    P.ok = true;
+    return P;
+}
+
+// halo bytes each side of a window (the core is the rest of EW_W)
+uint32_t ew_halo() { return (uint32_t)std::max(16, std::min(getenv_int("BPE_EW_HALO", 256), (int)(EW_W / 2 - 256))); }
+
+// Encode c's bytes (halo bytes lh / rh around them, on c's device) by
+// windows into c's ids; *ok = false when a window's core was not certain.
+int ew_run(bpe_gpu_ctx *c, const EwPlan &P, const uint32_t *d_img, const uint8_t *lh, uint32_t lav, bool lmore,
+           const uint8_t *rh, uint32_t rav, bool rmore, bool *ok) {
+    const uint32_t halo = ew_halo(), core = EW_W - 2 * halo;
+    const uint64_t n = c->n0, nwin = (n + core - 1) / core;
+    int r;
+    uint32_t *ids, *cnt;
+    uint16_t *stage;
+    unsigned long long *off;
+    if ((r = dalloc(c, &ids, std::max<uint64_t>(n, 1), false))) return r;
+    if ((r = dalloc(c, &stage, std::max<uint64_t>(nwin * core, 1), false))) return r;
+    if ((r = dalloc(c, &cnt, nwin + 4))) return r;  // zeroed: counts (+ a 0 after the last), ticket, fail
+    if ((r = dalloc(c, &off, nwin + 1, false))) return r;
+    c->h.ids_out = ids;
+    EncWinArgs A{};
+    A.bytes = c->h.bytes;
+    A.lh = lh;
+    A.rh = rh;
+    A.n = n;
+    A.lav = lav;
+    A.rav = rav;
+    A.lmore = lmore;
+    A.rmore = rmore;
+    A.core = core;
+    A.halo = halo;
+    A.nwin = nwin;
+    A.nb = P.nb;
+    A.bp = d_img;
+    A.ht = (const unsigned long long *)(d_img + P.off_ht);
+    A.hmask = P.H - 1;
+    A.roles = d_img + P.off_roles;
+    A.beq = (const uint8_t *)(d_img + P.off_beq);
+    A.stage = stage;
+    A.cnt = cnt;
+    A.ticket = cnt + nwin + 2;
+    A.fail = cnt + nwin + 3;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nwin, (uint64_t)getenv_int("BPE_EW_GRID", 2048));
+    const bool prof = getenv_int("BPE_EW_PROF", 0) != 0;
+    if (prof) {
+        if ((r = dalloc(c, &A.prof, 8 + 512))) return r;
+    }
+    if (nwin) k_enc_win<<<grid, EW_T, 0, c->st>>>(A);
+    HIPCHK(hipGetLastError());
+    // window offsets (exclusive scan of the counts; off[nwin] = total), gather
+    size_t tb = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, tb, cnt, off, 0ull, nwin + 1, rocprim::plus<unsigned long long>(), c->st));
+    void *tmp;
+    if ((r = dscratch(c, 4, tb, &tmp))) return r;
+    HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, 0ull, nwin + 1, rocprim::plus<unsigned long long>(), c->st));
+    if (nwin)
+        k_ew_gather<<<(uint32_t)std::min<uint64_t>(nwin, 8192), 256, 0, c->st>>>(stage, cnt, off, nwin, core, ids);
+    HIPCHK(hipGetLastError());
+    if (prof) {
+        unsigned long long h[8 + 512];
+        HIPCHK(hipMemcpyAsync(h, A.prof, sizeof h, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        const double wn = (double)std::max(1ull, h[5]);
+        if (getenv_int("BPE_EW_PROF", 0) > 1)
+            for (uint32_t b = 0; b < P.nb; b++)
+                fprintf(stderr, "enc_win batch %u: merges %.2f us lookups %.2f us per window\n", b, h[8 + b] / wn / 100.0,
+                        h[8 + 256 + b] / wn / 100.0);
+        fprintf(stderr, "enc_win: %llu windows, per window (us): init %.2f batches %.2f (merges %.2f, lookups %.2f) "
+                "output %.2f; batches with work %.1f of %u; lookup-list overflows %llu\n", h[5], h[0] / wn / 100.0,
+                h[1] / wn / 100.0, h[3] / wn / 100.0, h[7] / wn / 100.0, h[2] / wn / 100.0, h[4] / wn, P.nb, h[6]);
+    }
+    uint32_t fl = 0;
+    unsigned long long total = 0;
+    HIPCHK(hipMemcpyAsync(&fl, A.fail, 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(&total, off + nwin, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    *ok = fl == 0;
+    c->ids_len = total;
+    c->ids_ready = *ok;
+    c->stats.enc_windows = nwin;
+    return 0;
+}
+
 }  // namespace
 
 // ===================================================================== C-ABI
@@ -1528,6 +1706,31 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
     c->nshards = 1;
     const double t0 = now_ms();
     int r;
+    // window-local replay (encode_win.hip); the global batched replay below
+    // when the list does not fit it or a window's core came out uncertain
+    if (c->n0 >= 2) {
+        const EwPlan P = ew_plan(pairs, n_merges, c->ew_stage);
+        if (P.ok) {
+            void *d_img;
+            if ((r = dscratch(c, 7, P.words * 4, &d_img))) return r;
+            HIPCHK(hipMemcpyAsync(d_img, c->ew_stage.data(), P.words * 4, hipMemcpyHostToDevice, c->st));
+            free_train(c);
+            bool ok = false;
+            if ((r = ew_run(c, P, (const uint32_t *)d_img, nullptr, 0, false, nullptr, 0, false, &ok))) return r;
+            if (ok) {
+                const double t1 = now_ms();
+                c->merges_done = 0;
+                c->stats.enc_path = 1;
+                c->stats.n_out = c->ids_len;
+                c->stats.merges = n_merges;
+                c->stats.iterations = P.nb;
+                c->stats.occurrences = c->n0 - c->ids_len;
+                c->stats.ms_train = t1 - t0;
+                c->stats.ms_total = t1 - t0;
+                return 0;
+            }
+        }
+    }
     if ((r = setup_run(c, (uint32_t)n_merges, true))) return r;
     if (c->d_enc_pairs) hipFree(c->d_enc_pairs);
     HIPCHK(hipMalloc(&c->d_enc_pairs, std::max<size_t>(n_merges, 1) * 8));
@@ -1537,6 +1740,7 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
         c->ids_ready = true;
         return 0;
     }
+    c->stats.enc_path = 2;
     std::vector<uint32_t> unrank;
     uint32_t *d_tot;
     if (c->n0 >= 2) {

@@ -556,6 +556,19 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
 // (encode.hip), the same batch on every shard (cut = min of the shards'
 // proposals, carried in the edge records), pairs across edges owned by the
 // left shard as in training.
+// bytes [a, a + len) of the group's stream (shard k holds [start[k], start[k + 1])) into dst, on the device
+int group_copy_bytes(bpe_gpu_group *g, const std::vector<uint64_t> &start, uint64_t a, uint64_t len, uint8_t *dst) {
+    for (size_t j = 0; j < g->cs.size() && len; j++) {
+        if (a >= start[j + 1]) continue;
+        const uint64_t take = std::min<uint64_t>(len, start[j + 1] - a);
+        HIPCHK(hipMemcpyAsync(dst, g->cs[j]->h.bytes + (a - start[j]), take, hipMemcpyDeviceToDevice, g->st));
+        dst += take;
+        a += take;
+        len -= take;
+    }
+    return 0;
+}
+
 int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
     int r;
     const uint32_t K = (uint32_t)g->cs.size();
@@ -569,6 +582,57 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
     uint64_t ntot;
     if ((r = group_total(g, &ntot))) return r;
     g->stats.n_in = ntot;
+    // window-local replay (encode_win.hip) of every shard, with halo bytes
+    // from its neighbours; the global batched replay below when the list does
+    // not fit it or a window's core came out uncertain
+    if (local_mode(g) && K == g->nshards) {
+        bpe_gpu_ctx *c0 = g->cs[0];
+        const EwPlan P = ew_plan(pairs, n_merges, c0->ew_stage);
+        if (P.ok) {
+            void *d_img;
+            if ((r = dscratch(c0, 7, P.words * 4, &d_img))) return r;
+            HIPCHK(hipMemcpyAsync(d_img, c0->ew_stage.data(), P.words * 4, hipMemcpyHostToDevice, g->st));
+            const uint32_t halo = ew_halo();
+            std::vector<uint64_t> start(K + 1, 0);
+            for (uint32_t k = 0; k < K; k++) start[k + 1] = start[k] + g->cs[k]->n0;
+            bool all = true;
+            uint64_t nout = 0, nwin = 0;
+            for (uint32_t k = 0; k < K && all; k++) {
+                bpe_gpu_ctx *c = g->cs[k];
+                c->stats = bpe_gpu_stats{};
+                c->merges_done = 0;
+                free_train(c);
+                const uint32_t lav = (uint32_t)std::min<uint64_t>(halo, start[k]);
+                const uint32_t rav = (uint32_t)std::min<uint64_t>(halo, ntot - start[k + 1]);
+                void *hb;
+                if ((r = dscratch(c, 8, lav + rav + 16, &hb))) return r;
+                uint8_t *lh = (uint8_t *)hb, *rh = lh + lav;
+                if ((r = group_copy_bytes(g, start, start[k] - lav, lav, lh))) return r;
+                if ((r = group_copy_bytes(g, start, start[k + 1], rav, rh))) return r;
+                bool ok = false;
+                if ((r = ew_run(c, P, (const uint32_t *)d_img, lh, lav, start[k] > lav, rh, rav,
+                                start[k + 1] + rav < ntot, &ok)))
+                    return r;
+                all = ok;
+                nout += c->ids_len;
+                nwin += c->stats.enc_windows;
+            }
+            if (all) {
+                const double t1 = now_ms();
+                g->merges_done = 0;
+                g->stats.enc_path = 1;
+                g->stats.enc_windows = nwin;
+                g->stats.n_out = nout;
+                g->stats.merges = n_merges;
+                g->stats.iterations = P.nb;
+                g->stats.occurrences = ntot - nout;
+                g->stats.ms_train = t1 - t0;
+                g->stats.ms_total = t1 - t0;
+                return 0;
+            }
+        }
+    }
+    g->stats.enc_path = 2;
     for (uint32_t k = 0; k < K; k++) {
         bpe_gpu_ctx *c = g->cs[k];
         c->stats = bpe_gpu_stats{};

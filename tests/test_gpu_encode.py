@@ -1,5 +1,7 @@
-"""GPU standalone encoder (batched merge replay) against the oracle's
-sequential replace passes (reference bpe.c:760-779 applied merge by merge).
+"""GPU standalone encoder against the oracle's sequential replace passes
+(reference bpe.c:760-779 applied merge by merge), through both replays: the
+window-local one (encode_win.hip, the default) and the global batched one
+(encode.hip; BPE_ENC_WIN=0, also the window path's fallback).
 
 Bit-exact bar: identical ids.  Merge lists: trained by the engine itself,
 random valid lists over tiny alphabets (dense dependencies, a==b runs),
@@ -14,6 +16,12 @@ from llmtokenizer_amd import api
 from llmtokenizer_amd.synth import synth_bytes
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["window", "global"], autouse=True)
+def replay(request, monkeypatch):
+    monkeypatch.setenv("BPE_ENC_WIN", "1" if request.param == "window" else "0")
+    return request.param
 
 
 def _engine_encode(data, merges):
