@@ -28,10 +28,11 @@
 // [Lu, Ru); otherwise the window FAILED and the host replays the stream
 // globally (encode.hip).
 //
-// LDS per position (5.1 B): id (u16, valid at token starts), cached rank of
-// the pair starting there (u16), its batch (u8 `bi`; EW_NONE: no merge), one
-// start bit.  Ids and ranks fit 16 bits: the host takes this path for merge
-// lists of <= EW_MAX_MERGES merges in <= EW_MAX_BATCHES batches.
+// LDS per position (4.1 B): id (u16, valid at token starts), cached rank of
+// the pair starting there (u16; a batch is a rank range, so the scan of batch
+// b is a range test), one start bit.  Ids and ranks fit 16 bits: the host
+// takes this path for merge lists of <= EW_MAX_MERGES merges in <=
+// EW_MAX_BATCHES batches.
 //
 // Latency is what a window costs (one workgroup walks ~80 batches), so every
 // batch keeps its global round trips to one: the pairs whose rank changed are
@@ -43,23 +44,24 @@
 namespace bpeamd {
 
 constexpr uint32_t EW_T = 256;             // threads per workgroup
-constexpr uint32_t EW_PER = 16;            // positions per thread in the batch scans (one uint4 of bi)
+constexpr uint32_t EW_PER = 16;            // positions per thread in the batch scans (two uint4 of rk)
 constexpr uint32_t EW_W = EW_T * EW_PER;   // LDS positions (core + 2 * halo)
-constexpr uint32_t EW_MAX_MERGES = 65279;  // ids and ranks in 16 bits
-constexpr uint32_t EW_MAX_BATCHES = 250;   // batch indices stay below the bi marks
-constexpr uint8_t EW_RUNC = 0xFC;          // bi: first token of an a == a run, certain
-constexpr uint8_t EW_RUNU = 0xFD;          //     ... uncertain
-constexpr uint8_t EW_PEND = 0xFE;          //     pair changed this batch: look its rank up
-constexpr uint8_t EW_NONE = 0xFF;          //     no merge (or not a token start)
+constexpr uint32_t EW_MAX_MERGES = 65279;  // ids and ranks in 16 bits, below the rk marks
+constexpr uint32_t EW_MAX_BATCHES = 256;   // bits of the per-id batch masks
+constexpr uint16_t EW_PEND = 0xFFFEu;      // rk: pair changed this batch, look its rank up
+constexpr uint16_t EW_NONE = 0xFFFFu;      //     no merge (or not a token start)
 constexpr uint32_t EW_NOPOS = 0xFFFFFFFFu;
 #ifndef EW_PROF  // per-phase wall-clock accounting (tools/ew_time.py; a build of its own: it costs registers)
 #define EW_PROF 0
 #endif
 #define EW_PROF_ON (EW_PROF && A.prof)
 #ifndef EW_WAVES
-#define EW_WAVES 6                          // waves per SIMD (workgroups per CU): caps the VGPRs
+#define EW_WAVES 8                          // waves per SIMD (workgroups per CU): caps the VGPRs
 #endif
-constexpr uint32_t EW_PENDCAP = 2048;      // pairs to look up per batch (beyond: scan of the bi bytes)
+#ifndef EW_PENDCAP_
+#define EW_PENDCAP_ 1024
+#endif
+constexpr uint32_t EW_PENDCAP = EW_PENDCAP_;  // pairs to look up per batch (beyond: a scan of rk)
 
 struct EncWinArgs {
     const uint8_t *bytes;   // this shard's bytes [0, n)
@@ -71,6 +73,7 @@ struct EncWinArgs {
     uint32_t core, halo;
     uint64_t nwin;
     uint32_t nb;                 // batches
+    const uint32_t *bstart;      // [nb + 1] first rank of each batch
     const uint32_t *bp;          // [65536] byte pair -> rank | batch << 16 (~0: none)
     const unsigned long long *ht;  // (a << 16 | b) + 1 (0 = empty) | (rank | batch << 16) << 32
     uint32_t hmask;
@@ -140,50 +143,48 @@ __device__ inline uint32_t ew_from(const uint32_t *sb, uint32_t p) {
     return p >= EW_W ? EW_W : ew_is_start(sb, p) ? p : ew_next(sb, p);
 }
 
-// bit 7 of every byte of x equal to the byte in c4 (c * 0x01010101), exactly
-__device__ inline uint32_t ew_eq4(uint32_t x, uint32_t c4) {
-    x ^= c4;
-    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+// bit k set: rank k of the 16 (two uint4 of u16) lies in [r0, r1)
+__device__ inline uint32_t ew_in(const uint4 &a, const uint4 &c, uint32_t r0, uint32_t r1) {
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) {
+        const uint32_t lo = w[j] & 0xFFFFu, hi = w[j] >> 16;
+        m |= (uint32_t)(lo - r0 < r1 - r0) << (2 * j);
+        m |= (uint32_t)(hi - r0 < r1 - r0) << (2 * j + 1);
+    }
+    return m;
 }
-
-// does any of the 16 bytes equal c
-__device__ inline bool ew_has(uint4 v, uint32_t c) {
-    const uint32_t c4 = c * 0x01010101u;
-    return (ew_eq4(v.x, c4) | ew_eq4(v.y, c4) | ew_eq4(v.z, c4) | ew_eq4(v.w, c4)) != 0;
-}
-
-__device__ inline uint32_t ew_word(const uint4 &v, uint32_t j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
 
 // mark p's pair for a rank lookup after the batch
-__device__ inline void ew_pend(uint8_t *bi, uint16_t *pend, uint32_t *npend, uint32_t p) {
-    bi[p] = EW_PEND;
+__device__ inline void ew_pend(uint16_t *rk, uint16_t *pend, uint32_t *npend, uint32_t p) {
+    rk[p] = EW_PEND;
     const uint32_t k = atomicAdd(npend, 1u);
     if (k < EW_PENDCAP) pend[k] = (uint16_t)p;
 }
 
-// rank of the pair starting at p (post-batch state) into rk / bi
-__device__ inline void ew_relook(const EncWinArgs &A, const uint16_t *tok, uint16_t *rk, uint8_t *bi, const uint32_t *sb,
-                                 uint32_t p, uint32_t W) {
+// rank of the pair starting at p (post-batch state) into rk
+__device__ inline void ew_relook(const EncWinArgs &A, const uint16_t *tok, uint16_t *rk, const uint32_t *sb, uint32_t p,
+                                 uint32_t W) {
     uint32_t r = ~0u;
     if (ew_is_start(sb, p)) {
         const uint32_t q = ew_next(sb, p);
         if (q < W) r = ew_info(A, tok[p], tok[q]);
     }
     rk[p] = (uint16_t)r;
-    bi[p] = (uint8_t)(r >> 16);
 }
 
 __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 8))) void k_enc_win(EncWinArgs A) {
     __shared__ __align__(16) uint16_t tok[EW_W];
     __shared__ __align__(16) uint16_t rk[EW_W];
-    __shared__ __align__(16) uint8_t bi[EW_W];
     __shared__ uint32_t sb[EW_W / 32];
     __shared__ uint16_t s_pend[EW_PENDCAP];
     __shared__ uint32_t s_win, s_Lu, s_Ru, s_runend, s_npend;
     __shared__ uint32_t s_lid, s_rid, s_lm[8], s_rm[8];  // edge tokens' ids and batch masks
     __shared__ uint32_t s_wcnt[EW_T / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    uint8_t *mybi = bi + tid * EW_PER;
+    const uint32_t p0 = tid * EW_PER;
+    uint16_t *myrk = rk + p0;
     uint32_t *tok32 = (uint32_t *)tok;
     for (;;) {
         if (tid == 0) s_win = atomicAdd(A.ticket, 1u);
@@ -228,30 +229,25 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
             s_lid = s_rid = EW_NOPOS;
         }
         __syncthreads();
-        {
-            // byte-pair ranks: independent lookups, 8 at a time
-            const uint32_t p0 = tid * EW_PER;
+        // byte-pair ranks: independent lookups, 8 at a time
 #pragma unroll
-            for (uint32_t h = 0; h < EW_PER; h += 8) {
-                uint32_t r[8];
+        for (uint32_t h = 0; h < EW_PER; h += 8) {
+            uint32_t r[8];
 #pragma unroll
-                for (uint32_t k = 0; k < 8; k++) {
-                    const uint32_t p = p0 + h + k;
-                    r[k] = p + 1 < W ? A.bp[((uint32_t)tok[p] << 8) | tok[p + 1]] : ~0u;
-                }
-                *(uint4 *)(rk + p0 + h) = make_uint4((r[0] & 0xFFFFu) | (r[1] << 16), (r[2] & 0xFFFFu) | (r[3] << 16),
-                                                    (r[4] & 0xFFFFu) | (r[5] << 16), (r[6] & 0xFFFFu) | (r[7] << 16));
-                *(uint2 *)(mybi + h) =
-                    make_uint2(((r[0] >> 16) & 0xFFu) | (((r[1] >> 16) & 0xFFu) << 8) | (((r[2] >> 16) & 0xFFu) << 16) |
-                                   (((r[3] >> 16) & 0xFFu) << 24),
-                               ((r[4] >> 16) & 0xFFu) | (((r[5] >> 16) & 0xFFu) << 8) | (((r[6] >> 16) & 0xFFu) << 16) |
-                                   (((r[7] >> 16) & 0xFFu) << 24));
+            for (uint32_t k = 0; k < 8; k++) {
+                const uint32_t p = p0 + h + k;
+                r[k] = p + 1 < W ? A.bp[((uint32_t)tok[p] << 8) | tok[p + 1]] : ~0u;
             }
+            *(uint4 *)(myrk + h) = make_uint4((r[0] & 0xFFFFu) | (r[1] << 16), (r[2] & 0xFFFFu) | (r[3] << 16),
+                                              (r[4] & 0xFFFFu) | (r[5] << 16), (r[6] & 0xFFFFu) | (r[7] << 16));
         }
         unsigned long long tp1 = EW_PROF_ON ? wall_clock64() : 0;
         for (uint32_t b = 0; b < A.nb; b++) {
-            uint4 v = *(const uint4 *)mybi;  // this thread's 16 bi bytes (no other thread writes them before phase A)
-            const bool has = __syncthreads_or(ew_has(v, b));
+            const uint32_t r0 = A.bstart[b], r1 = A.bstart[b + 1];
+            // this thread's 16 ranks (no other thread writes them before phase A)
+            uint4 va = ((const uint4 *)myrk)[0], vc = ((const uint4 *)myrk)[1];
+            uint32_t mine = ew_in(va, vc, r0, r1);
+            const bool has = __syncthreads_or(mine != 0);
             const uint32_t Lu = s_Lu, Ru = s_Ru;
             // the edge tokens' roles in this batch (pre-batch state): per-id
             // batch masks, fetched when the edge token changes
@@ -287,59 +283,44 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
             }
             nhas++;
             if (EW_PROF_ON) tq = wall_clock64();
-            const uint32_t cb4 = b * 0x01010101u;
-            const bool eq = A.beq[b] != 0;
-            if (eq) {
-                // a == a runs, from the pre-batch state: first tokens marked,
-                // the others dropped from the scan (their run's walk takes them)
-                for (uint32_t j = 0; j < 4; j++) {
-                    for (uint32_t m = ew_eq4(ew_word(v, j), cb4); m; m &= m - 1) {
-                        const uint32_t k = j * 4 + ((uint32_t)__builtin_ctz(m) >> 3);
-                        const uint32_t p = tid * EW_PER + k;
-                        const uint32_t x = tok[p];
-                        if (tok[ew_next(sb, p)] != x) continue;
-                        const uint32_t lp = ew_prev(sb, p);
-                        if (lp != EW_NOPOS && tok[lp] == x) {
-                            mybi[k] = EW_NONE;
-                        } else {
-                            const bool unc = p < Lu || (p == Lu && (lunk || Lu > 0));
-                            mybi[k] = unc ? EW_RUNU : EW_RUNC;
-                        }
+            if (A.beq[b]) {
+                // a == a runs, from the pre-batch state: a run's tokens after
+                // its first drop out of the scan (the first token's walk takes them)
+                for (uint32_t m = mine; m; m &= m - 1) {
+                    const uint32_t k = (uint32_t)__builtin_ctz(m), p = p0 + k;
+                    const uint32_t x = tok[p];
+                    if (tok[ew_next(sb, p)] != x) continue;
+                    const uint32_t lp = ew_prev(sb, p);
+                    if (lp != EW_NOPOS && tok[lp] == x) {
+                        myrk[k] = EW_NONE;
+                        mine &= ~(1u << k);
                     }
                 }
                 __syncthreads();
-                v = *(const uint4 *)mybi;
             }
-            for (uint32_t j = 0; j < 4; j++) {
-                const uint32_t wd = ew_word(v, j);
-                const uint32_t mrun = eq ? ew_eq4(wd, EW_RUNC * 0x01010101u) | ew_eq4(wd, EW_RUNU * 0x01010101u) : 0u;
-                for (uint32_t m = ew_eq4(wd, cb4) | mrun; m; m &= m - 1) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(m);
-                    const uint32_t k = j * 4 + (bit >> 3);
-                    const uint32_t cb = (wd >> (bit & 24)) & 0xFFu;
-                    const uint32_t p = tid * EW_PER + k;
-                    const uint32_t x = tok[p];
-                    const uint16_t z = (uint16_t)(256u + rk[p]);
-                    const uint32_t lp = ew_prev(sb, p);
-                    if (lp != EW_NOPOS) ew_pend(bi, s_pend, &s_npend, lp);  // its right neighbour changes
-                    uint32_t cur = p;
-                    for (;;) {
-                        const uint32_t q = ew_next(sb, cur);  // the pair's right token
-                        tok[cur] = z;
-                        atomicAnd(&sb[q >> 5], ~(1u << (q & 31)));
-                        bi[q] = EW_NONE;
-                        ew_pend(bi, s_pend, &s_npend, cur);
-                        if (cb == b) break;  // x != y: one pair
-                        cur = ew_next(sb, cur);
-                        if (cur >= W || tok[cur] != x) break;  // the run ends after a pair
-                        const uint32_t q2 = ew_next(sb, cur);
-                        if (q2 >= W || tok[q2] != x) {  // odd token out
-                            cur = q2;
-                            break;
-                        }
+            for (uint32_t m = mine; m; m &= m - 1) {
+                const uint32_t p = p0 + (uint32_t)__builtin_ctz(m);
+                const uint32_t x = tok[p];
+                const uint16_t z = (uint16_t)(256u + rk[p]);
+                const uint32_t lp = ew_prev(sb, p);
+                if (lp != EW_NOPOS) ew_pend(rk, s_pend, &s_npend, lp);  // its right neighbour changes
+                uint32_t cur = p, q = ew_next(sb, p);  // the pair's right token
+                const bool run = tok[q] == x;           // (a run's first token: the others were dropped)
+                for (;;) {
+                    tok[cur] = z;
+                    atomicAnd(&sb[q >> 5], ~(1u << (q & 31)));
+                    rk[q] = EW_NONE;
+                    ew_pend(rk, s_pend, &s_npend, cur);
+                    if (!run) break;
+                    cur = ew_next(sb, cur);
+                    if (cur >= W || tok[cur] != x) break;  // the run ends after a pair
+                    q = ew_next(sb, cur);
+                    if (q >= W || tok[q] != x) {  // odd token out
+                        cur = q;
+                        break;
                     }
-                    if (cb == EW_RUNU) atomicMax(&s_runend, min(cur, W));
                 }
+                if (run && (p < Lu || (p == Lu && (lunk || Lu > 0)))) atomicMax(&s_runend, min(cur, W));
             }
             __syncthreads();
             if (EW_PROF_ON) {
@@ -348,17 +329,17 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
                 if (tid == 0) atomicAdd(&A.prof[8 + b], t - tq);
                 tq = t;
             }
-            // new pairs' ranks: the listed positions, one per thread (the bi
-            // scan when the list overflowed); a position listed twice gets
+            // new pairs' ranks: the listed positions, one per thread (a scan
+            // of rk when the list overflowed); a position listed twice gets
             // the same value twice, one no longer a token start gets none
             const uint32_t np = s_npend;
             if (np <= EW_PENDCAP) {
-                for (uint32_t i = tid; i < np; i += EW_T) ew_relook(A, tok, rk, bi, sb, s_pend[i], W);
+                for (uint32_t i = tid; i < np; i += EW_T) ew_relook(A, tok, rk, sb, s_pend[i], W);
             } else {
-                v = *(const uint4 *)mybi;
-                for (uint32_t j = 0; j < 4; j++)
-                    for (uint32_t m = ew_eq4(ew_word(v, j), EW_PEND * 0x01010101u); m; m &= m - 1)
-                        ew_relook(A, tok, rk, bi, sb, tid * EW_PER + j * 4 + ((uint32_t)__builtin_ctz(m) >> 3), W);
+                va = ((const uint4 *)myrk)[0];
+                vc = ((const uint4 *)myrk)[1];
+                for (uint32_t m = ew_in(va, vc, EW_PEND, EW_PEND + 1); m; m &= m - 1)
+                    ew_relook(A, tok, rk, sb, p0 + (uint32_t)__builtin_ctz(m), W);
                 if (EW_PROF_ON && tid == 0) atomicAdd(&A.prof[6], 1ull);
             }
             if (tid == 0) {

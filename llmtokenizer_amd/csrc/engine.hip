@@ -1322,11 +1322,12 @@ int getenv_int(const char *k, int dflt) {
 
 // Batches of the commuting rule (encode.hip form_batch, without its scratch
 // cap) and the window encoder's lookup tables, as one host image:
-//   bp[65536] | ht[H] {key, value} | roles[V][2][8] (per id: batches using it left / right) | beq[nb] (bytes)
+//   bp[65536] | ht[H] {key, value} | roles[V][2][8] (per id: batches using it left / right) | bstart[nb + 1] |
+//   beq[nb] (bytes)
 struct EwPlan {
     bool ok = false;
     uint32_t nb = 0, H = 0;  // H: hash slots
-    size_t off_ht = 0, off_roles = 0, off_beq = 0, words = 0;
+    size_t off_ht = 0, off_roles = 0, off_bstart = 0, off_beq = 0, words = 0;
 };
 
 EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
@@ -1385,7 +1386,8 @@ EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
     P.H = H;
     P.off_ht = 65536;
     P.off_roles = P.off_ht + 2ull * H;  // (16-byte aligned: H >= 64)
-    P.off_beq = P.off_roles + (size_t)V * 16;
+    P.off_bstart = P.off_roles + (size_t)V * 16;
+    P.off_beq = P.off_bstart + nb + 1;
     P.words = P.off_beq + (nb + 3) / 4 + 1;
     img.assign(P.words, 0);
     memcpy(img.data(), bp.data(), 65536 * 4);
@@ -1394,6 +1396,9 @@ EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
         img[P.off_ht + 2 * k + 1] = hval[k];
     }
     uint32_t *roles = img.data() + P.off_roles;
+    uint32_t *bst = img.data() + P.off_bstart;
+    for (uint32_t r = m; r-- > 0;) bst[batch[r]] = r;  // first rank of each batch
+    bst[nb] = (uint32_t)m;
     uint8_t *beq = (uint8_t *)(img.data() + P.off_beq);
     for (uint32_t r = 0; r < m; r++) {
         const uint32_t u = pairs[2 * r], v = pairs[2 * r + 1], z = 256 + r;
@@ -1442,6 +1447,7 @@ int ew_run(bpe_gpu_ctx *c, const EwPlan &P, const uint32_t *d_img, const uint8_t
     A.ht = (const unsigned long long *)(d_img + P.off_ht);
     A.hmask = P.H - 1;
     A.roles = d_img + P.off_roles;
+    A.bstart = d_img + P.off_bstart;
     A.beq = (const uint8_t *)(d_img + P.off_beq);
     A.stage = stage;
     A.cnt = cnt;

@@ -7,14 +7,22 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+import numpy as np
+
 from llmtokenizer_amd import api
 
 GIB = 1 << 30
-tr = api.Engine(0)
-tr.synth(2, GIB)
-tr.train(32768)
-M = tr.merges()
-tr.close()
+CACHE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "m32k_s2_1g.npy")  # (not committed)
+if os.path.exists(CACHE):
+    M = np.load(CACHE)
+else:
+    tr = api.Engine(0)
+    tr.synth(2, GIB)
+    tr.train(32768)
+    M = tr.merges()
+    tr.close()
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.save("gpurun_out/m32k_s2_1g.npy", M)
 total = int(float(os.environ.get("EW_GIB", "10")) * GIB)
 k = max(1, -(-total // (3 << 30)))
 g = api.ShardGroup(0, local_shards=k)
@@ -22,12 +30,13 @@ step = total // k
 for q in range(k):
     a = q * step
     g.synth(q, 3, (total if q == k - 1 else a + step) - a, a)
+REPS = int(os.environ.get("EW_REPS", "3"))
 for spec in sys.argv[1:] or ["-"]:
     env = {} if spec == "-" else dict(kv.split("=") for kv in spec.split(","))
     old = {n: os.environ.get(n) for n in env}
     os.environ.update(env)
     best = 1e9
-    for _ in range(3):
+    for _ in range(REPS):
         t = time.perf_counter()
         g.encode(M)
         best = min(best, time.perf_counter() - t)
