@@ -72,7 +72,8 @@ typedef struct {
     uint64_t hot_rebuilds;    /* hot-set argmax: full-table rebuilds of the listed keys */
     uint64_t hot_mode;        /* 0 level summaries, 1 hot set, 2 hot set given up mid-run */
     uint64_t hot_scanned;     /* hot-set entries reduced, summed over the merges */
-    uint64_t enc_path;        /* encode: 1 window-local replay, 2 global batched replay */
+    uint64_t enc_path;        /* encode: 1 window-local replay, 3 the same after its wide-halo
+                                 retry, 2 global batched replay                 */
     uint64_t enc_windows;     /* encode: windows replayed (window path)           */
 } bpe_gpu_stats;
 

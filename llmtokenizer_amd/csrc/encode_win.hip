@@ -43,7 +43,10 @@
 
 namespace bpeamd {
 
-constexpr uint32_t EW_T = 256;             // threads per workgroup
+#ifndef EW_T_
+#define EW_T_ 256
+#endif
+constexpr uint32_t EW_T = EW_T_;           // threads per workgroup
 constexpr uint32_t EW_PER = 16;            // positions per thread in the batch scans (two uint4 of rk)
 constexpr uint32_t EW_W = EW_T * EW_PER;   // LDS positions (core + 2 * halo)
 constexpr uint32_t EW_MAX_MERGES = 65279;  // ids and ranks in 16 bits, below the rk marks

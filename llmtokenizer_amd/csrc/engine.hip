@@ -1413,13 +1413,16 @@ EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
 }
 
 // halo bytes each side of a window (the core is the rest of EW_W)
-uint32_t ew_halo() { return (uint32_t)std::max(16, std::min(getenv_int("BPE_EW_HALO", 256), (int)(EW_W / 2 - 256))); }
+// (first pass; a window whose core comes out uncertain makes the whole
+// stream go again with EW_HALO_WIDE, and only then to the global replay)
+constexpr uint32_t EW_HALO_WIDE = EW_W / 4;
+uint32_t ew_halo() { return (uint32_t)std::max(16, std::min(getenv_int("BPE_EW_HALO", 64), (int)EW_HALO_WIDE)); }
 
 // Encode c's bytes (halo bytes lh / rh around them, on c's device) by
 // windows into c's ids; *ok = false when a window's core was not certain.
-int ew_run(bpe_gpu_ctx *c, const EwPlan &P, const uint32_t *d_img, const uint8_t *lh, uint32_t lav, bool lmore,
-           const uint8_t *rh, uint32_t rav, bool rmore, bool *ok) {
-    const uint32_t halo = ew_halo(), core = EW_W - 2 * halo;
+int ew_run(bpe_gpu_ctx *c, const EwPlan &P, const uint32_t *d_img, uint32_t halo, const uint8_t *lh, uint32_t lav,
+           bool lmore, const uint8_t *rh, uint32_t rav, bool rmore, bool *ok) {
+    const uint32_t core = EW_W - 2 * halo;
     const uint64_t n = c->n0, nwin = (n + core - 1) / core;
     int r;
     uint32_t *ids, *cnt;
@@ -1720,13 +1723,17 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
             void *d_img;
             if ((r = dscratch(c, 7, P.words * 4, &d_img))) return r;
             HIPCHK(hipMemcpyAsync(d_img, c->ew_stage.data(), P.words * 4, hipMemcpyHostToDevice, c->st));
-            free_train(c);
             bool ok = false;
-            if ((r = ew_run(c, P, (const uint32_t *)d_img, nullptr, 0, false, nullptr, 0, false, &ok))) return r;
+            int pass = 0;
+            for (; pass < 2 && !ok; pass++) {
+                free_train(c);
+                const uint32_t halo = pass ? EW_HALO_WIDE : ew_halo();
+                if ((r = ew_run(c, P, (const uint32_t *)d_img, halo, nullptr, 0, false, nullptr, 0, false, &ok))) return r;
+            }
             if (ok) {
                 const double t1 = now_ms();
                 c->merges_done = 0;
-                c->stats.enc_path = 1;
+                c->stats.enc_path = pass == 1 ? 1 : 3;
                 c->stats.n_out = c->ids_len;
                 c->stats.merges = n_merges;
                 c->stats.iterations = P.nb;

@@ -592,35 +592,41 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
             void *d_img;
             if ((r = dscratch(c0, 7, P.words * 4, &d_img))) return r;
             HIPCHK(hipMemcpyAsync(d_img, c0->ew_stage.data(), P.words * 4, hipMemcpyHostToDevice, g->st));
-            const uint32_t halo = ew_halo();
             std::vector<uint64_t> start(K + 1, 0);
             for (uint32_t k = 0; k < K; k++) start[k + 1] = start[k] + g->cs[k]->n0;
-            bool all = true;
+            bool all = false;
+            int pass = 0;
             uint64_t nout = 0, nwin = 0;
-            for (uint32_t k = 0; k < K && all; k++) {
-                bpe_gpu_ctx *c = g->cs[k];
-                c->stats = bpe_gpu_stats{};
-                c->merges_done = 0;
-                free_train(c);
-                const uint32_t lav = (uint32_t)std::min<uint64_t>(halo, start[k]);
-                const uint32_t rav = (uint32_t)std::min<uint64_t>(halo, ntot - start[k + 1]);
-                void *hb;
-                if ((r = dscratch(c, 8, lav + rav + 16, &hb))) return r;
-                uint8_t *lh = (uint8_t *)hb, *rh = lh + lav;
-                if ((r = group_copy_bytes(g, start, start[k] - lav, lav, lh))) return r;
-                if ((r = group_copy_bytes(g, start, start[k + 1], rav, rh))) return r;
-                bool ok = false;
-                if ((r = ew_run(c, P, (const uint32_t *)d_img, lh, lav, start[k] > lav, rh, rav,
-                                start[k + 1] + rav < ntot, &ok)))
-                    return r;
-                all = ok;
-                nout += c->ids_len;
-                nwin += c->stats.enc_windows;
+            for (; pass < 2 && !all; pass++) {
+                const uint32_t halo = pass ? EW_HALO_WIDE : ew_halo();
+                all = true;
+                nout = nwin = 0;
+                for (uint32_t k = 0; k < K && all; k++) {
+                    bpe_gpu_ctx *c = g->cs[k];
+                    c->stats = bpe_gpu_stats{};
+                    c->merges_done = 0;
+                    free_train(c);
+                    // halo bytes from the neighbours (as many as the wide pass needs)
+                    const uint32_t lav = (uint32_t)std::min<uint64_t>(EW_HALO_WIDE, start[k]);
+                    const uint32_t rav = (uint32_t)std::min<uint64_t>(EW_HALO_WIDE, ntot - start[k + 1]);
+                    void *hb;
+                    if ((r = dscratch(c, 8, lav + rav + 16, &hb))) return r;
+                    uint8_t *lh = (uint8_t *)hb, *rh = lh + lav;
+                    if ((r = group_copy_bytes(g, start, start[k] - lav, lav, lh))) return r;
+                    if ((r = group_copy_bytes(g, start, start[k + 1], rav, rh))) return r;
+                    bool ok = false;
+                    if ((r = ew_run(c, P, (const uint32_t *)d_img, halo, lh, lav, start[k] > lav, rh, rav,
+                                    start[k + 1] + rav < ntot, &ok)))
+                        return r;
+                    all = ok;
+                    nout += c->ids_len;
+                    nwin += c->stats.enc_windows;
+                }
             }
             if (all) {
                 const double t1 = now_ms();
                 g->merges_done = 0;
-                g->stats.enc_path = 1;
+                g->stats.enc_path = pass == 1 ? 1 : 3;
                 g->stats.enc_windows = nwin;
                 g->stats.n_out = nout;
                 g->stats.merges = n_merges;

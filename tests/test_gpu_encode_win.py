@@ -59,6 +59,18 @@ def test_window_edges_any_halo(halo, monkeypatch):
         assert 1 in paths
 
 
+def test_long_runs_across_windows():
+    """a == a runs far longer than any halo: their windows are uncertain, the
+    wide-halo pass or the global replay must take over, exactly"""
+    rng = random.Random(5)
+    merges = _random_merges(rng, sorted(set(b"ab ")), 300, eq=0.3)
+    merges = np.vstack([np.array([[97, 97], [98, 98]], dtype=np.uint32), merges])
+    text = b"ab " * 3000 + b"a" * 20001 + b" b" * 2000 + b"b" * 5000 + b"ba " * 3000
+    ids, st = _encode(text, merges)
+    assert st["enc_path"] in (2, 3)
+    assert (ids == O.encode(text, merges)).all()
+
+
 def test_window_path_taken_on_trained_list():
     merges, _ = api.train_bytes(synth_bytes(500, 1 << 20), 4000)
     text = synth_bytes(501, 2 << 20)
