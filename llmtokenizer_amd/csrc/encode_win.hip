@@ -384,9 +384,14 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
             before += k < wv ? s_wcnt[k] : 0u;
             agg += s_wcnt[k];
         }
-        uint16_t *dst = A.stage + w * A.core + before + incl - cnt;
+        // compact into LDS (rk is free now), then whole-line stores to the slot
+        // (per-thread 2-byte stores would reach HBM as partial-line writes)
+        uint16_t *cmp = rk + before + incl - cnt;
         for (uint32_t p = lo; p < hi; p++)
-            if (ew_is_start(sb, p)) __builtin_nontemporal_store(tok[p], dst++);
+            if (ew_is_start(sb, p)) *cmp++ = tok[p];
+        __syncthreads();
+        uint4 *dst = (uint4 *)(A.stage + w * A.core);  // (core * 2 bytes is a multiple of 16)
+        for (uint32_t k = tid; k * 8 < agg; k += EW_T) dst[k] = ((const uint4 *)rk)[k];
         if (tid == 0) A.cnt[w] = agg;
         if (EW_PROF_ON && tid == 0) {
             const unsigned long long tp3 = wall_clock64();

@@ -1416,7 +1416,7 @@ EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
 // (first pass; a window whose core comes out uncertain makes the whole
 // stream go again with EW_HALO_WIDE, and only then to the global replay)
 constexpr uint32_t EW_HALO_WIDE = EW_W / 4;
-uint32_t ew_halo() { return (uint32_t)std::max(16, std::min(getenv_int("BPE_EW_HALO", 64), (int)EW_HALO_WIDE)); }
+uint32_t ew_halo() { return (uint32_t)std::max(16, std::min(getenv_int("BPE_EW_HALO", 64), (int)EW_HALO_WIDE)) & ~7u; }
 
 // Encode c's bytes (halo bytes lh / rh around them, on c's device) by
 // windows into c's ids; *ok = false when a window's core was not certain.
