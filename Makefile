@@ -40,3 +40,12 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# Host C library under AddressSanitizer + UBSan (device calls stubbed:
+# tests/asan/gpu_stub.c); run by tests/test_asan_host.py
+tests/asan/asan_host: tests/asan/asan_host.c tests/asan/gpu_stub.c $(CSRC) $(wildcard include/*.h)
+	$(CC) -O1 -g -std=c11 -D_GNU_SOURCE -fno-omit-frame-pointer -fsanitize=address,undefined \
+	    -fno-sanitize-recover=undefined -Iinclude -o $@ tests/asan/asan_host.c tests/asan/gpu_stub.c $(CSRC) -lm -lpthread
+
+asan-host: tests/asan/asan_host
+.PHONY: asan-host
