@@ -183,7 +183,7 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
     __shared__ uint32_t sb[EW_W / 32];
     __shared__ uint16_t s_pend[EW_PENDCAP];
     __shared__ uint32_t s_win, s_Lu, s_Ru, s_runend, s_npend;
-    __shared__ uint32_t s_lid, s_rid, s_lm[8], s_rm[8];  // edge tokens' ids and batch masks
+    __shared__ uint32_t s_lid, s_rid, s_lm[8], s_rm[8], s_lact, s_ract, s_tpos;  // edge tokens and their batch masks
     __shared__ uint32_t s_wcnt[EW_T / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t p0 = tid * EW_PER;
@@ -244,6 +244,30 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
             *(uint4 *)(myrk + h) = make_uint4((r[0] & 0xFFFFu) | (r[1] << 16), (r[2] & 0xFFFFu) | (r[3] << 16),
                                               (r[4] & 0xFFFFu) | (r[5] << 16), (r[6] & 0xFFFFu) | (r[7] << 16));
         }
+        // Edge snapshot (thread 0, taken where no thread writes tok / sb): the
+        // ids at the certain range's edges and their per-id batch masks (the
+        // rules of the header apply in batch b when mask bit b is set); a mask
+        // is fetched only when its edge token changes.
+        auto snapshot = [&](uint32_t Lu, uint32_t Ru) {
+            s_lact = (lunk || Lu > 0) && Lu < Ru;
+            if (s_lact && tok[Lu] != s_lid) {
+                s_lid = tok[Lu];
+                ew_mask(A, s_lid, 1, s_lm);
+            }
+            s_ract = 0;
+            if ((runk || Ru < W) && Ru > Lu) {
+                const uint32_t tp = ew_prev(sb, Ru);
+                if (tp != EW_NOPOS) {
+                    s_ract = 1;
+                    s_tpos = tp;
+                    if (tok[tp] != s_rid) {
+                        s_rid = tok[tp];
+                        ew_mask(A, s_rid, 0, s_rm);
+                    }
+                }
+            }
+        };
+        if (tid == 0) snapshot(0, W);  // (tok is complete: the init barrier)
         unsigned long long tp1 = EW_PROF_ON ? wall_clock64() : 0;
         for (uint32_t b = 0; b < A.nb; b++) {
             const uint32_t r0 = A.bstart[b], r1 = A.bstart[b + 1];
@@ -252,35 +276,19 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
             uint32_t mine = ew_in(va, vc, r0, r1);
             const bool has = __syncthreads_or(mine != 0);
             const uint32_t Lu = s_Lu, Ru = s_Ru;
-            // the edge tokens' roles in this batch (pre-batch state): per-id
-            // batch masks, fetched when the edge token changes
+            // the edge tokens' roles in this batch, from the snapshot taken
+            // when no thread was writing (other threads may already be merging)
             bool lmove = false, rmove = false;
-            uint32_t tpos = EW_NOPOS;
             if (tid == 0) {
-                if ((lunk || Lu > 0) && Lu < Ru) {
-                    const uint32_t id = tok[Lu];
-                    if (id != s_lid) {
-                        ew_mask(A, id, 1, s_lm);
-                        s_lid = id;
-                    }
-                    lmove = (s_lm[b >> 5] >> (b & 31)) & 1u;
-                }
-                if ((runk || Ru < W) && Ru > Lu) {
-                    tpos = ew_prev(sb, Ru);
-                    if (tpos != EW_NOPOS) {
-                        const uint32_t id = tok[tpos];
-                        if (id != s_rid) {
-                            ew_mask(A, id, 0, s_rm);
-                            s_rid = id;
-                        }
-                        rmove = (s_rm[b >> 5] >> (b & 31)) & 1u;
-                    }
-                }
+                lmove = s_lact && ((s_lm[b >> 5] >> (b & 31)) & 1u);
+                rmove = s_ract && ((s_rm[b >> 5] >> (b & 31)) & 1u);
             }
             if (!has) {
-                if (tid == 0) {
-                    if (lmove) s_Lu = ew_next(sb, Lu);
-                    if (rmove) s_Ru = tpos;
+                if (tid == 0 && (lmove || rmove)) {  // (no thread writes tok / sb in this batch)
+                    const uint32_t lu = lmove ? ew_next(sb, Lu) : Lu, ru = rmove ? s_tpos : Ru;
+                    s_Lu = lu;
+                    s_Ru = ru;
+                    snapshot(lu, ru);
                 }
                 continue;  // the next batch's barrier orders these stores
             }
@@ -345,10 +353,11 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
                     ew_relook(A, tok, rk, sb, p0 + (uint32_t)__builtin_ctz(m), W);
                 if (EW_PROF_ON && tid == 0) atomicAdd(&A.prof[6], 1ull);
             }
-            if (tid == 0) {
-                const uint32_t lu = lmove ? ew_next(sb, Lu) : Lu;
-                s_Lu = max(lu, s_runend);
-                if (rmove) s_Ru = tpos;
+            if (tid == 0) {  // (phase B: no thread writes tok / sb)
+                const uint32_t lu = max(lmove ? ew_next(sb, Lu) : Lu, s_runend), ru = rmove ? s_tpos : Ru;
+                s_Lu = lu;
+                s_Ru = ru;
+                snapshot(lu, ru);
             }
             __syncthreads();
             if (EW_PROF_ON) {
