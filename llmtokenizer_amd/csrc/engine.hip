@@ -255,9 +255,9 @@ struct bpe_gpu_ctx {
     uint64_t prof_launches = 0;
     // grow-only device scratch of decode (ids, pairs, elen, offsets, scan
     // temporaries, output, error words; slots 0-6), of the window encoder
-    // (tables, halo bytes; 7-8), and the pinned staging of file loads
-    void *dscr[9] = {};
-    size_t dscr_cap[9] = {};
+    // (tables, halo bytes, rank exchange; 7-9), and the pinned staging of file loads
+    void *dscr[10] = {};
+    size_t dscr_cap[10] = {};
     std::vector<uint32_t> ew_stage;  // host image of the window encoder's tables (outlives the upload)
     uint8_t *stage[2] = {};
     hipEvent_t stage_ev[2] = {};

@@ -569,6 +569,110 @@ int group_copy_bytes(bpe_gpu_group *g, const std::vector<uint64_t> &start, uint6
     return 0;
 }
 
+// Sum of count u32 words over the ranks, in place on the device (every rank
+// contributes disjoint words when it is a gather).
+int rank_sum(bpe_gpu_group *g, uint32_t *d, size_t count) {
+    int r;
+    if ((r = ex_allreduce(g, nullptr, {d}, count))) return r;
+    return 0;
+}
+
+// Window encode of a one-shard-per-rank group.  Every rank's size and first /
+// last EW_HALO_WIDE bytes are gathered by a sum over disjoint slots (the
+// group's own exchange: P2P mailboxes or RCCL); each rank builds its halos,
+// runs the window replay, and the ranks sum their fail flags so that all take
+// the same next step (wide-halo pass, then the global replay).  *done = 0:
+// the caller runs the global replay (collectively: the decision is the same
+// on every rank).
+int group_encode_window_ranks(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges, uint64_t ntot, double t0,
+                              int *done) {
+    *done = 0;
+    bpe_gpu_ctx *c = g->cs[0];
+    const EwPlan P = ew_plan(pairs, n_merges, c->ew_stage);
+    const uint32_t HB = EW_HALO_WIDE, HW = HB / 4, SLOT = 2 + 2 * HW, NR = g->nshards, me = g->shard0;
+    const size_t count = (size_t)NR * SLOT;
+    if (!P.ok || (g->p2p && count + 1 > g->hp.c0)) return 0;  // (the same on every rank)
+    int r;
+    void *d_img, *xb, *hb;
+    if ((r = dscratch(c, 7, P.words * 4, &d_img))) return r;
+    HIPCHK(hipMemcpyAsync(d_img, c->ew_stage.data(), P.words * 4, hipMemcpyHostToDevice, g->st));
+    if ((r = dscratch(c, 9, (count + 1) * 4, &xb))) return r;
+    uint32_t *x = (uint32_t *)xb;
+    HIPCHK(hipMemsetAsync(x, 0, count * 4, g->st));
+    const uint64_t n = c->n0;
+    const uint32_t sz[2] = {(uint32_t)n, (uint32_t)(n >> 32)};
+    uint32_t *mine = x + (size_t)me * SLOT;
+    HIPCHK(hipMemcpyAsync(mine, sz, 8, hipMemcpyHostToDevice, g->st));
+    const uint64_t hn = std::min<uint64_t>(n, HB);
+    if (hn) {
+        HIPCHK(hipMemcpyAsync(mine + 2, c->h.bytes, hn, hipMemcpyDeviceToDevice, g->st));
+        HIPCHK(hipMemcpyAsync(mine + 2 + HW, c->h.bytes + (n - hn), hn, hipMemcpyDeviceToDevice, g->st));
+    }
+    if ((r = rank_sum(g, x, count))) return r;
+    std::vector<uint32_t> hx(count);
+    HIPCHK(hipMemcpyAsync(hx.data(), x, count * 4, hipMemcpyDeviceToHost, g->st));
+    HIPCHK(hipStreamSynchronize(g->st));
+    if ((r = p2p_check(g))) return r;
+    std::vector<uint64_t> size(NR), start(NR + 1, 0);
+    for (uint32_t k = 0; k < NR; k++) {
+        size[k] = (uint64_t)hx[(size_t)k * SLOT] | ((uint64_t)hx[(size_t)k * SLOT + 1] << 32);
+        start[k + 1] = start[k] + size[k];
+    }
+    // halos: the tails of the ranks before me, the heads of the ranks after me
+    const uint32_t lav = (uint32_t)std::min<uint64_t>(HB, start[me]);
+    const uint32_t rav = (uint32_t)std::min<uint64_t>(HB, ntot - start[me + 1]);
+    std::vector<uint8_t> halo(lav + rav + 16, 0);
+    for (uint32_t i = 0; i < lav; i++) {  // byte start[me] - lav + i of the stream
+        const uint64_t gpos = start[me] - lav + i;
+        uint32_t k = me;
+        while (gpos < start[k]) k--;
+        const uint64_t tn = std::min<uint64_t>(size[k], HB), off = gpos - (start[k + 1] - tn);  // in k's tail
+        halo[i] = ((const uint8_t *)&hx[(size_t)k * SLOT + 2 + HW])[off];
+    }
+    for (uint32_t i = 0; i < rav; i++) {
+        const uint64_t gpos = start[me + 1] + i;
+        uint32_t k = me + 1;
+        while (gpos >= start[k + 1]) k++;
+        halo[lav + i] = ((const uint8_t *)&hx[(size_t)k * SLOT + 2])[gpos - start[k]];  // in k's head
+    }
+    if ((r = dscratch(c, 8, halo.size(), &hb))) return r;
+    HIPCHK(hipMemcpyAsync(hb, halo.data(), halo.size(), hipMemcpyHostToDevice, g->st));
+    HIPCHK(hipStreamSynchronize(g->st));  // (halo is a host vector)
+    const uint8_t *lh = (const uint8_t *)hb, *rh = lh + lav;
+    int pass = 0;
+    bool all = false;
+    for (; pass < 2 && !all; pass++) {
+        c->stats = bpe_gpu_stats{};
+        c->merges_done = 0;
+        free_train(c);
+        bool ok = false;
+        if ((r = ew_run(c, P, (const uint32_t *)d_img, pass ? EW_HALO_WIDE : ew_halo(), lh, lav, start[me] > lav, rh,
+                        rav, start[me + 1] + rav < ntot, &ok)))
+            return r;
+        const uint32_t bad = ok ? 0u : 1u;  // every rank's verdict
+        HIPCHK(hipMemcpyAsync(x + count, &bad, 4, hipMemcpyHostToDevice, g->st));
+        if ((r = rank_sum(g, x + count, 1))) return r;
+        uint32_t nbad = 0;
+        HIPCHK(hipMemcpyAsync(&nbad, x + count, 4, hipMemcpyDeviceToHost, g->st));
+        HIPCHK(hipStreamSynchronize(g->st));
+        if ((r = p2p_check(g))) return r;
+        all = nbad == 0;
+    }
+    if (!all) return 0;
+    const double t1 = now_ms();
+    g->merges_done = 0;
+    g->stats.enc_path = pass == 1 ? 1 : 3;
+    g->stats.enc_windows = c->stats.enc_windows;
+    g->stats.n_out = c->ids_len;
+    g->stats.merges = n_merges;
+    g->stats.iterations = P.nb;
+    g->stats.occurrences = n - c->ids_len;
+    g->stats.ms_train = t1 - t0;
+    g->stats.ms_total = t1 - t0;
+    *done = 1;
+    return 0;
+}
+
 int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
     int r;
     const uint32_t K = (uint32_t)g->cs.size();
@@ -637,6 +741,13 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
                 return 0;
             }
         }
+    }
+    // one shard per rank (P2P / RCCL groups): the same window replay, the
+    // neighbouring ranks' halo bytes gathered through the group's exchange
+    if (!local_mode(g) && K == 1) {
+        int done = 0;
+        if ((r = group_encode_window_ranks(g, pairs, n_merges, ntot, t0, &done))) return r;
+        if (done) return 0;
     }
     g->stats.enc_path = 2;
     for (uint32_t k = 0; k < K; k++) {

@@ -35,7 +35,7 @@ def main():
     else:
         merges = np.load(sys.argv[9])["merges"]
         g.encode(merges)
-        np.savez(out, ids=g.ids(0))
+        np.savez(out, ids=g.ids(0), path=np.array([g.stats()["enc_path"]]))
     dist.barrier()
     g.close()
     dist.destroy_process_group()

@@ -159,3 +159,28 @@ def test_p2p_ranks_small_vs_oracle_and_encode(tmp_path):
     text = synth_bytes(984, 5000)
     enc = _run_ranks(tmp_path, 3, "encode", "synth:984:5000", 200, [0, 2000, 2001, 5000], extra=(mfile,))
     assert (np.concatenate([r["ids"] for r in enc]) == O.encode(text, om)).all()
+    assert all(int(r["path"][0]) in (1, 3) for r in enc)  # window replay, halos gathered across ranks
+
+
+def test_p2p_ranks_window_encode_vs_oracle(tmp_path):
+    """one shard per rank, window replay with the neighbours' halo bytes
+    gathered through the mailboxes (ranks shorter than the halo included);
+    and the global replay when the window path is switched off"""
+    train = synth_bytes(985, 1 << 20)
+    om, _ = api.train_bytes(train, 1200)
+    mfile = str(tmp_path / "m.npz")
+    np.savez(mfile, merges=om)
+    n = 200000
+    text = synth_bytes(986, n)
+    want = O.encode(text, om)
+    for cuts in ([0, 90001, n], [0, 700, 1300, 1500, n]):
+        enc = _run_ranks(tmp_path, len(cuts) - 1, "encode", f"synth:986:{n}", 1200, cuts, extra=(mfile,))
+        assert (np.concatenate([r["ids"] for r in enc]) == want).all(), cuts
+        assert all(int(r["path"][0]) == 1 for r in enc), cuts
+    os.environ["BPE_ENC_WIN"] = "0"
+    try:
+        enc = _run_ranks(tmp_path, 2, "encode", f"synth:986:{n}", 1200, [0, 77777, n], extra=(mfile,))
+    finally:
+        del os.environ["BPE_ENC_WIN"]
+    assert (np.concatenate([r["ids"] for r in enc]) == want).all()
+    assert all(int(r["path"][0]) == 2 for r in enc)
