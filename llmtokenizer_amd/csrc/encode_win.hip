@@ -249,6 +249,10 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
         // rules of the header apply in batch b when mask bit b is set); a mask
         // is fetched only when its edge token changes.
         auto snapshot = [&](uint32_t Lu, uint32_t Ru) {
+#ifdef EW_TIMING_NOEDGE  // (timing experiment only: no edge tracking, results may differ)
+            s_lact = s_ract = 0;
+            return;
+#endif
             s_lact = (lunk || Lu > 0) && Lu < Ru;
             if (s_lact && tok[Lu] != s_lid) {
                 s_lid = tok[Lu];
