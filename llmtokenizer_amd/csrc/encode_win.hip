@@ -49,6 +49,8 @@ namespace bpeamd {
 constexpr uint32_t EW_T = EW_T_;           // threads per workgroup
 constexpr uint32_t EW_PER = 16;            // positions per thread in the batch scans (two uint4 of rk)
 constexpr uint32_t EW_W = EW_T * EW_PER;   // LDS positions (core + 2 * halo)
+constexpr uint32_t EW_EDGE_T = EW_T - 64;  // keeps the edge state: first lane of the last wave (the
+                                           // one with the fewest pair lookups after a batch)
 constexpr uint32_t EW_MAX_MERGES = 65279;  // ids and ranks in 16 bits, below the rk marks
 constexpr uint32_t EW_MAX_BATCHES = 256;   // bits of the per-id batch masks
 constexpr uint16_t EW_PEND = 0xFFFEu;      // rk: pair changed this batch, look its rank up
@@ -97,7 +99,15 @@ __device__ inline uint8_t ew_byte(const EncWinArgs &A, int64_t g) {
 // rank | batch << 16 of the pair (x, y); ~0 when the list has no such merge
 __device__ inline uint32_t ew_info(const EncWinArgs &A, uint32_t x, uint32_t y) {
     if (x < 256 && y < 256) return A.bp[(x << 8) | y];
-    const uint32_t key = ((x << 16) | y) + 1u;
+    uint32_t key = ((x << 16) | y) + 1u;
+#ifdef EW_TIMING_DOUBLE  // (timing experiment only: a second, dependent lookup of the same key)
+    {
+        uint32_t s = (uint32_t)mix64(key) & A.hmask;
+        unsigned long long e = A.ht[s];
+        while ((uint32_t)e != key && (uint32_t)e != 0) e = A.ht[s = (s + 1) & A.hmask];
+        key += (uint32_t)(e >> 32) == 0xDEADBEEFu;
+    }
+#endif
     uint32_t s = (uint32_t)mix64(key) & A.hmask;
     for (;;) {
         const unsigned long long e = A.ht[s];  // key and value in ONE 8-byte load
@@ -271,7 +281,7 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
                 }
             }
         };
-        if (tid == 0) snapshot(0, W);  // (tok is complete: the init barrier)
+        if (tid == EW_EDGE_T) snapshot(0, W);  // (tok is complete: the init barrier)
         unsigned long long tp1 = EW_PROF_ON ? wall_clock64() : 0;
         for (uint32_t b = 0; b < A.nb; b++) {
             const uint32_t r0 = A.bstart[b], r1 = A.bstart[b + 1];
@@ -283,12 +293,12 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
             // the edge tokens' roles in this batch, from the snapshot taken
             // when no thread was writing (other threads may already be merging)
             bool lmove = false, rmove = false;
-            if (tid == 0) {
+            if (tid == EW_EDGE_T) {
                 lmove = s_lact && ((s_lm[b >> 5] >> (b & 31)) & 1u);
                 rmove = s_ract && ((s_rm[b >> 5] >> (b & 31)) & 1u);
             }
             if (!has) {
-                if (tid == 0 && (lmove || rmove)) {  // (no thread writes tok / sb in this batch)
+                if (tid == EW_EDGE_T && (lmove || rmove)) {  // (no thread writes tok / sb in this batch)
                     const uint32_t lu = lmove ? ew_next(sb, Lu) : Lu, ru = rmove ? s_tpos : Ru;
                     s_Lu = lu;
                     s_Ru = ru;
@@ -357,7 +367,7 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
                     ew_relook(A, tok, rk, sb, p0 + (uint32_t)__builtin_ctz(m), W);
                 if (EW_PROF_ON && tid == 0) atomicAdd(&A.prof[6], 1ull);
             }
-            if (tid == 0) {  // (phase B: no thread writes tok / sb)
+            if (tid == EW_EDGE_T) {  // (phase B: no thread writes tok / sb)
                 const uint32_t lu = max(lmove ? ew_next(sb, Lu) : Lu, s_runend), ru = rmove ? s_tpos : Ru;
                 s_Lu = lu;
                 s_Ru = ru;
