@@ -44,7 +44,7 @@
 namespace bpeamd {
 
 #ifndef EW_T_
-#define EW_T_ 256
+#define EW_T_ 128
 #endif
 constexpr uint32_t EW_T = EW_T_;           // threads per workgroup
 constexpr uint32_t EW_PER = 16;            // positions per thread in the batch scans (two uint4 of rk)
@@ -64,7 +64,7 @@ constexpr uint32_t EW_NOPOS = 0xFFFFFFFFu;
 #define EW_WAVES 8                          // waves per SIMD (workgroups per CU): caps the VGPRs
 #endif
 #ifndef EW_PENDCAP_
-#define EW_PENDCAP_ 1024
+#define EW_PENDCAP_ 512
 #endif
 constexpr uint32_t EW_PENDCAP = EW_PENDCAP_;  // pairs to look up per batch (beyond: a scan of rk)
 

@@ -1416,7 +1416,7 @@ EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
 // (first pass; a window whose core comes out uncertain makes the whole
 // stream go again with EW_HALO_WIDE, and only then to the global replay)
 constexpr uint32_t EW_HALO_WIDE = EW_W / 4;
-uint32_t ew_halo() { return (uint32_t)std::max(16, std::min(getenv_int("BPE_EW_HALO", 64), (int)EW_HALO_WIDE)) & ~7u; }
+uint32_t ew_halo() { return (uint32_t)std::max(16, std::min(getenv_int("BPE_EW_HALO", 48), (int)EW_HALO_WIDE)) & ~7u; }
 
 // Encode c's bytes (halo bytes lh / rh around them, on c's device) by
 // windows into c's ids; *ok = false when a window's core was not certain.
@@ -1456,7 +1456,7 @@ int ew_run(bpe_gpu_ctx *c, const EwPlan &P, const uint32_t *d_img, uint32_t halo
     A.cnt = cnt;
     A.ticket = cnt + nwin + 2;
     A.fail = cnt + nwin + 3;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(nwin, (uint64_t)getenv_int("BPE_EW_GRID", 2048));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nwin, (uint64_t)getenv_int("BPE_EW_GRID", 2048 * 256 / EW_T));
     const bool prof = getenv_int("BPE_EW_PROF", 0) != 0;
     if (prof) {
         if ((r = dalloc(c, &A.prof, 8 + 512))) return r;
