@@ -1334,8 +1334,11 @@ EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
     EwPlan P;
     if (m > EW_MAX_MERGES || getenv_int("BPE_ENC_WIN", 1) == 0) return P;
     const uint32_t V = 256 + (uint32_t)m;
-    uint32_t H = 64;  // hash slots, at most half full
-    while (H < 2 * m) H <<= 1;
+    // hash slots: at most 1/8 full, so that a lookup (most of them misses:
+    // pairs a merge creates that the list does not hold) is ~1.1 dependent probes
+    uint32_t H = 64;
+    const uint64_t hscale = (uint64_t)std::max(2, getenv_int("BPE_EW_HSCALE", 8));
+    while (H < hscale * m) H <<= 1;
     std::vector<uint32_t> bp(65536, ~0u), hkey(H, 0), hval(H, ~0u), batch(m);
     std::vector<uint8_t> fl(V, 0), eq;
     std::vector<uint32_t> touched;
