@@ -75,6 +75,7 @@ typedef struct {
     uint64_t enc_path;        /* encode: 1 window-local replay, 3 the same after its wide-halo
                                  retry, 2 global batched replay                 */
     uint64_t enc_windows;     /* encode: windows replayed (window path)           */
+    uint64_t relists;         /* training: byte-pair position lists rebuilt       */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */

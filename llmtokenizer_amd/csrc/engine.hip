@@ -242,6 +242,7 @@ struct bpe_gpu_ctx {
     uint32_t *d_enc_pairs = nullptr;
     hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr;
     bool hot_fallback = false;  // the hot set was given up for the level summaries
+    uint32_t relists = 0;       // byte-pair list rebuilds of the current run
     std::vector<hipGraphExec_t> retired;  // replaced graphs, destroyed with the run
     bpe_gpu_stats stats{};
     // profile of the dominant kernel: HIP events captured around every k_scan
@@ -395,6 +396,14 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? 1 + SPEC_RB + SPEC_SB : 0);
     // hot-set argmax: untracked one-shard training with the speculative graph
     h.hot = HOT_ON && h.spec_on && !c->sharded && (c->fast || n0 >= TRACK_LIMIT) ? 1 : 0;
+    // byte-pair list rebuilds (STOP_RELIST, opt-in with BPE_RELIST=1): they
+    // cut configs[2]'s scanned candidates from 974 M to 0.48-0.53 G with
+    // identical merges, but the late merges did not get faster
+    h.relist_stale = 0;
+    if (!encode && !c->sharded && n0 >= (1ull << 24) && getenv("BPE_RELIST") && atoi(getenv("BPE_RELIST"))) {
+        const char *t = getenv("BPE_RELIST_STALE");
+        h.relist_stale = t ? (uint32_t)std::max(1L, atol(t)) : (32u << 20);
+    }
     h.hot_parts = SPEC_RB;
     h.hot_target = HOT_TARGET;
     if (const char *t = getenv("BPE_HOT_TARGET")) h.hot_target = std::max(1, std::min(atoi(t), (int)HOT_TARGET));
@@ -963,6 +972,34 @@ struct Resolver {
 // stops (Eng::hprobe); a replay queued behind a stop finds the stop set and
 // every kernel in it exits at once.  Returns with the stream still busy (the
 // caller's pull_ctl synchronises).  Nothing is queued past the merge cap.
+int dscratch(bpe_gpu_ctx *c, int k, size_t bytes, void **out);
+
+// Rebuild the byte-pair position lists from the live tokens (k_relist_hist,
+// the init sort's column scans, k_relist_scatter); the stream is idle here
+// (a stop), so no scan or apply runs beside it.
+int relist(bpe_gpu_ctx *c) {
+    Eng &h = c->h;
+    const uint32_t AA = h.A * h.A;
+    const uint64_t npairs = c->n0 - 1;
+    const uint64_t tile = 1ull << 20;
+    const uint32_t ntl = (uint32_t)((npairs + tile - 1) / tile);
+    const uint32_t per = (ntl + COLSCAN_GROUPS - 1) / COLSCAN_GROUPS;
+    const uint32_t ngr = (ntl + per - 1) / per;
+    void *p;
+    int r;
+    if ((r = dscratch(c, 9, ((size_t)ntl * AA + (size_t)ngr * AA + AA + 1) * 4, &p))) return r;
+    uint32_t *d_hist = (uint32_t *)p, *d_gsum = d_hist + (size_t)ntl * AA, *d_tot = d_gsum + (size_t)ngr * AA;
+    k_relist_hist<<<ntl, RELIST_T, AA * 4, c->st>>>(c->dE, d_hist, tile);
+    const dim3 cgrid((AA + 255) / 256, ngr);
+    k_pair_colsum<<<cgrid, 256, 0, c->st>>>(d_hist, d_gsum, AA, ntl, per);
+    k_pair_colscan<<<cgrid, 256, 0, c->st>>>(d_hist, d_gsum, d_tot, AA, ntl, per);
+    k_scan_single<<<1, 1024, 0, c->st>>>(d_tot, h.poff, AA);
+    k_relist_scatter<<<ntl, RELIST_T, AA * 4, c->st>>>(c->dE, d_hist, tile);
+    HIPCHK(hipGetLastError());
+    c->relists++;
+    return 0;
+}
+
 int replay_pipelined(bpe_gpu_ctx *c, hipGraphExec_t g, uint64_t merges_done) {
     *c->hprobe = STOP_NONE;  // the stream is idle here (the caller pulled the control block)
     int r;
@@ -1069,6 +1106,17 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             need_scan = true;
             break;
         }
+        case STOP_RELIST:
+            C.stop = STOP_NONE;
+            C.relist_c0 = (uint32_t)C.counters[4];
+            C.relist_o0 = (uint32_t)C.counters[5];
+            if ((r = push_ctl(c))) return r;
+            if ((r = relist(c))) return r;
+            launch_argmax_inputs(c);
+            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, SEL_PLAIN);
+            HIPCHK(hipGetLastError());
+            need_scan = true;
+            break;
         case STOP_HOT:
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;
@@ -1168,6 +1216,7 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
     for (uint32_t x = 0; x < 256; x++)
         if (bh[x]) { rank[x] = (uint32_t)unrank.size(); unrank.push_back(x); }
     h.A = (uint32_t)unrank.size();
+    if (h.A * h.A > RELIST_MAXAA) h.relist_stale = 0;  // (the rebuild's LDS histogram)
     HIPCHK(hipMemcpyAsync(h.rank, rank.data(), 1024, hipMemcpyHostToDevice, c->st));
     std::vector<uint32_t> tl(h.vcap, 1);
     HIPCHK(hipMemcpyAsync(h.tlen, tl.data(), 4ull * h.vcap, hipMemcpyHostToDevice, c->st));
@@ -1638,6 +1687,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     const bool tracked = !c->fast && c->n0 < TRACK_LIMIT;
     if (tracked) launch_stats(c);
     c->hot_fallback = false;
+    c->relists = 0;
     if ((r = hot_rebuild(c))) return r;
     launch_argmax_inputs(c);
     k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
@@ -1668,6 +1718,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.hot_rebuilds = C.hot_rebuilds;
     c->stats.hot_scanned = C.hot_scanned;
     c->stats.hot_mode = c->h.hot ? 1 : c->hot_fallback ? 2 : 0;
+    c->stats.relists = c->relists;
     if (c->h.dbgts) print_timeline(c, C.z);
     if (getenv("BPE_DEBUG"))
         fprintf(stderr, "select phases (ticks/iter): reduce %.1f merge %.1f tail %.1f\n",

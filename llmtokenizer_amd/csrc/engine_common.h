@@ -57,6 +57,7 @@ enum : uint32_t {
     STOP_MODE = 7,     // n fell below 2^21: switch to the tracked iteration graph
     STOP_REDO = 8,     // speculative graph: the predicted next merge was wrong, host scans
     STOP_HOT = 9,      // hot-set argmax: the set no longer holds the maximum (or grew): host rebuilds it
+    STOP_RELIST = 10,  // the byte-pair position lists went stale: host rebuilds them (k_relist_*)
 };
 
 // Hot-set argmax (Eng::hot, untracked one-shard training): the keys whose count
@@ -170,6 +171,9 @@ struct Eng {
     uint32_t hot;
     uint32_t hot_parts;   // partial results per launch (k_rescan_spec's rescan blocks)
     uint32_t hot_target;  // keys a rebuild aims to list (HOT_TARGET; BPE_HOT_TARGET for tests)
+    // byte-pair list rebuild: stale candidates scanned since the last rebuild
+    // that trigger the next one (0: never; see k_relist_hist)
+    uint32_t relist_stale;
     uint32_t *hot_slot;   // [HOT_CAP] table slots of the listed keys
     uint32_t *hot_hist;   // [HOT_BINS] rebuild scratch (zero between rebuilds)
     unsigned long long *hotp_best, *hotp_key, *hotp_v2, *hotp_k2;  // [hot_parts] partial top-2
@@ -208,7 +212,8 @@ struct Ctl {
     // candidate list, armed flag; occurrences k_rescan_spec found, per parity
     uint32_t sa, sb, s_mode, s_off;
     uint32_t s_len, spec, sRp[2];
-    uint32_t hot_T, hot_fill, hot_pad0, hot_pad1;  // hot-set threshold; keys the last rebuild listed
+    uint32_t hot_T, hot_fill;         // hot-set threshold; keys the last rebuild listed
+    uint32_t relist_c0, relist_o0;    // counters[4] / [5] (low words) at the last byte-pair list rebuild
     // ---- tail: written by k_apply / k_rescan_spec (see above)
     unsigned long long Dp[2];   // D delta of the merge applied with parity p (finish_iteration folds it)
     unsigned long long nkeys;   // pair-table slots in use

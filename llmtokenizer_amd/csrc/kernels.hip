@@ -1363,6 +1363,12 @@ __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Ctl *Cg, T
     // hot set: its best is the argmax only while it is >= hot_T (hot_T == 2:
     // every key with a count >= 2 is listed, so an empty list means max <= 1)
     if (E->hot && ((cnt < C->hot_T && C->hot_T > 2) || Cg->hot_n > HOT_LIMIT)) { C->stop = STOP_HOT; return; }
+    // byte-pair lists: rebuild them once enough stale candidates were scanned
+    // (low words: the differences stay exact across a wrap)
+    if (E->relist_stale) {
+        const uint32_t cs = (uint32_t)C->counters[4] - C->relist_c0, os = (uint32_t)C->counters[5] - C->relist_o0;
+        if (cs > os && cs - os >= E->relist_stale) { C->stop = STOP_RELIST; return; }
+    }
     if (r.v == 0 || cnt <= 1) { C->stop = STOP_DONE; return; }
     if (C->nkeys + 4ull * (256ull + C->merges_done + 2) >= E->hcap / 2) { C->stop = STOP_GROW; return; }
     const bool tracked = !E->fast && C->n_live < DYN_LIMIT;  // deterministic (static) reference iteration
@@ -2118,6 +2124,56 @@ __global__ __launch_bounds__(256) void k_pair_colscan(uint32_t *__restrict__ his
         }
     }
     if (g == gridDim.y - 1) tot[k] = run;
+}
+
+// ------------------------------------------------- byte-pair list rebuild
+// A byte pair's position list (plist, built once by the counting sort) keeps
+// every original position of the pair; positions whose bytes were merged into
+// longer tokens since stay in it as stale candidates, and late merges scan
+// mostly those (configs[2]: 12 % of the candidates of merges 6144..8192 are
+// still pairs).  A rebuild streams tok[] (a position is a live byte pair iff
+// tok[i] and tok[i + 1] are both byte ids: every other slot holds an id
+// >= 256 or a HOLE / end code >= 2^31) and counting-sorts the live positions
+// by rank key again: the same pass shape as the init sort, one random line
+// per stale candidate traded for a streaming read.  Bytes never re-form, so
+// the rebuilt lists hold every future occurrence of every byte pair.
+constexpr uint32_t RELIST_MAXAA = 12288;  // keys per LDS histogram (A <= 110)
+constexpr uint32_t RELIST_T = 1024;
+
+__global__ __launch_bounds__(RELIST_T) void k_relist_hist(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
+                                                          uint64_t tile) {
+    extern __shared__ uint32_t rh[];  // [A * A]
+    __shared__ uint32_t srank[256];
+    const uint32_t A = E->A, AA = A * A;
+    for (uint32_t k = threadIdx.x; k < AA; k += RELIST_T) rh[k] = 0;
+    if (threadIdx.x < 256) srank[threadIdx.x] = E->rank[threadIdx.x];
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * tile, hi = min(E->n0 - 1, lo + tile);
+    const uint32_t *__restrict__ tok = E->tok;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += RELIST_T) {
+        const uint32_t x = tok[i], y = tok[i + 1];
+        if (x < 256 && y < 256) atomicAdd(&rh[srank[x] * A + srank[y]], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < AA; k += RELIST_T) hist[(uint64_t)blockIdx.x * AA + k] = rh[k];
+}
+
+// hist[t][key] = live positions with `key` in tiles < t (k_pair_colscan), poff the key offsets
+__global__ __launch_bounds__(RELIST_T) void k_relist_scatter(const Eng *__restrict__ E,
+                                                             const uint32_t *__restrict__ hist, uint64_t tile) {
+    extern __shared__ uint32_t cur[];  // [A * A]
+    __shared__ uint32_t srank[256];
+    const uint32_t A = E->A, AA = A * A;
+    for (uint32_t k = threadIdx.x; k < AA; k += RELIST_T) cur[k] = E->poff[k] + hist[(uint64_t)blockIdx.x * AA + k];
+    if (threadIdx.x < 256) srank[threadIdx.x] = E->rank[threadIdx.x];
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * tile, hi = min(E->n0 - 1, lo + tile);
+    const uint32_t *__restrict__ tok = E->tok;
+    uint32_t *__restrict__ plist = E->plist;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += RELIST_T) {
+        const uint32_t x = tok[i], y = tok[i + 1];
+        if (x < 256 && y < 256) plist[atomicAdd(&cur[srank[x] * A + srank[y]], 1u)] = (uint32_t)i;
+    }
 }
 
 // exclusive scan of in[0..n) into out[0..n], out[n] = total; one block of

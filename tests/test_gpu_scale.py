@@ -172,3 +172,22 @@ def test_cli_matches_reference_main_stdout(name, tmp_path):
                          timeout=60).stdout
     assert len(out) == fx["print_text_len"]
     assert hashlib.md5(out).hexdigest() == fx["print_text_md5"]
+
+
+def test_byte_pair_list_rebuilds_keep_the_merges(monkeypatch):
+    """BPE_RELIST (opt-in): rebuilding the byte-pair position lists from the
+    live tokens mid-run changes only how many stale candidates are scanned"""
+    data_seed, n, m = 5, 48 << 20, 4000
+    runs = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("BPE_RELIST", flag)
+        monkeypatch.setenv("BPE_RELIST_STALE", "300000")
+        e = api.Engine(0)
+        e.synth(data_seed, n)
+        assert e.train(m) == m
+        st = e.stats()
+        runs[flag] = (e.merges(), e.ids_checksum(), st["relists"], st["candidates"], st["occurrences"])
+        e.close()
+    off, on = runs["0"], runs["1"]
+    assert (off[0] == on[0]).all() and off[1] == on[1] and off[4] == on[4]
+    assert off[2] == 0 and on[2] >= 1 and on[3] < off[3]
