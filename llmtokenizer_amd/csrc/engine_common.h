@@ -23,7 +23,10 @@ constexpr uint32_t MARKV = 0xFFFFFFFEu;    // tok[] end slot of a token that sta
 constexpr uint64_t END_MAX = 0x7FFFFFFDull; // longest end distance an end code holds
 __host__ __device__ inline bool is_id(uint32_t v) { return v < END_FLAG; }  // a token start
 __host__ __device__ inline uint32_t end_code(uint64_t d) { return END_FLAG | (uint32_t)d; }
-constexpr uint32_t DENSE = 2048;         // ids aggregated in LDS / stored densely in delta vectors
+#ifndef BPE_DENSE
+#define BPE_DENSE 8192
+#endif
+constexpr uint32_t DENSE = BPE_DENSE;    // ids aggregated in LDS / stored densely in delta vectors
 #ifndef BPE_REPL
 #define BPE_REPL 8
 #endif
