@@ -475,6 +475,19 @@ def main():
         out["roofline"]["traffic"] = cp["traffic"]
     if "avg_ms_rocprof" in cp:
         out["roofline"]["frac_at_rocprof_avg"] = round(kbytes / (cp["avg_ms_rocprof"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    # the other per-merge kernel (apply + select; the larger share of the loop's
+    # kernel time once the scan's deltas stay in LDS): rocprof average and PMC
+    # traffic from the same committed profile, priced at 12 B per occurrence
+    fz = committed_profile("k_fused")
+    if "avg_ms_rocprof" in fz and merges:
+        fb = 12.0 * st["occurrences"] / merges
+        fa = fb / (fz["avg_ms_rocprof"] * 1e-3) / 1e9
+        out["roofline_k_fused"] = {"kernel": "k_fused", "bound": "hbm", "achieved": round(fa, 1), "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": round(fa / HBM_PEAK_GBS, 4), "traffic": fz.get("traffic"),
+                                   "bytes_per_launch": round(fb), "avg_ms_rocprof": fz["avg_ms_rocprof"],
+                                   "rocprof_summary": fz.get("rocprof_summary"),
+                                   "note": "12 B x occurrences per merge (the span rewrite); dependent table "
+                                           "updates, latency-bound"}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.cpu_size, args.cpu_merges)
     if enc is not None:
