@@ -76,7 +76,10 @@ constexpr uint32_t ENC_APPLY_BLOCKS = 1024;
 // then the predicted merge's scan blocks.  BPE_SPEC=0 disables it;
 // BPE_SPEC_GRID="rescan,scan" overrides the split for tuning runs.
 uint32_t SPEC_RB = 64, SPEC_SB = 192;
-uint32_t FUSED_A = 64, FUSED_B = 16;  // k_fused apply blocks (1024 threads): span rewrite, table update
+// k_fused apply blocks (1024 threads): role A rewrites the spans, role B updates the
+// table, one owner thread per entry of 1 + 4 x DENSE dense ids + the listed ids >= DENSE:
+// 34 blocks take them in one round (16 took two, +7.5 us per late merge)
+uint32_t FUSED_A = 64, FUSED_B = 34;
 bool SPEC_ON = true;
 bool PIPE_ON = !getenv("BPE_PIPE") || atoi(getenv("BPE_PIPE")) != 0;  // pipelined graph replays (drive)
 // BPE_GRAPH=0: the 16-iteration "graphs" are launched kernel by kernel (for
