@@ -339,8 +339,12 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
     __shared__ uint32_t list[SCAN_T];
     __shared__ uint16_t ltag[SCAN_T];
     __shared__ uint32_t lcount, gbase, bR;
+    // ids <= z occur in this merge's deltas (its neighbours and z itself): the
+    // accumulators are cleared and flushed up to lim only (ids < 1281 at 1024 merges)
+    const uint32_t lim = min(DENSE, z + 1);
     if (count)
-        for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) (&s[0][0])[x] = 0;
+        for (uint32_t v = 0; v < 4; v++)
+            for (uint32_t x = threadIdx.x; x < lim; x += SCAN_T) s[v][x] = 0;
     if (threadIdx.x == 0) lcount = bR = 0;
     __syncthreads();
     if (XW && edge_block) {
@@ -493,21 +497,22 @@ __device__ __forceinline__ void scan_body(const Eng *__restrict__ E, Ctl *__rest
     if (count && !SH) {
         // flush into replica (block % REPL): ~REPL x fewer same-address atomics
         uint32_t *rep = E->vecd + (uint64_t)(P * REPL + bid % REPL) * 4 * DENSE;
-        for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) {
-            const uint32_t c = (&s[0][0])[x];
-            if (c) atomicAdd(&rep[x], c);  // result unused: no-return atomic
-        }
+        for (uint32_t v = 0; v < 4; v++)
+            for (uint32_t x = threadIdx.x; x < lim; x += SCAN_T) {
+                const uint32_t c = s[v][x];
+                if (c) atomicAdd(&rep[v * DENSE + x], c);  // result unused: no-return atomic
+            }
         __syncthreads();
     } else if (count) {
         // sharded: flush straight into the dense exchange buffer the shards
         // allreduce next (zeroed by the previous k_rescan1); no pack pass
         const uint32_t vc = E->vcap;
         uint32_t *xb = xbufp(E, P);
-        for (uint32_t x = threadIdx.x; x < 4 * DENSE; x += SCAN_T) {
-            const uint32_t c = (&s[0][0])[x];
-            const uint32_t v = x / DENSE, id = x % DENSE;
-            if (c && id < vc) atomicAdd(&xb[v * vc + id], c);
-        }
+        for (uint32_t v = 0; v < 4; v++)
+            for (uint32_t id = threadIdx.x; id < lim; id += SCAN_T) {
+                const uint32_t c = s[v][id];
+                if (c && id < vc) atomicAdd(&xb[v * vc + id], c);
+            }
         if (threadIdx.x == 0 && bR) atomicAdd(&xb[4 * vc], bR);  // this shard's R, summed
         __syncthreads();
     }
@@ -725,7 +730,8 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     const uint32_t stride = nB * blockDim.x;
     uint32_t *const *lst = E->vlist[P];
     const bool sh = E->sharded;
-    const uint32_t W = sh ? E->vcap : min(DENSE, E->vcap);  // ids >= vcap never occur
+    // ids > z never occur in this merge's deltas (nor ids >= vcap)
+    const uint32_t W = sh ? E->vcap : min(min(DENSE, E->vcap), z + 1);
     uint32_t nl[4];
     for (int v = 0; v < 4; v++) nl[v] = sh ? 0 : E->vnl[P][v];
     const uint32_t dense_end = 1 + 4 * W;
