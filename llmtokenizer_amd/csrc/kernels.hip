@@ -730,8 +730,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
     const uint32_t stride = nB * blockDim.x;
     uint32_t *const *lst = E->vlist[P];
     const bool sh = E->sharded;
-    // ids > z never occur in this merge's deltas (nor ids >= vcap)
-    const uint32_t W = sh ? E->vcap : min(min(DENSE, E->vcap), z + 1);
+    const uint32_t W = sh ? E->vcap : min(DENSE, E->vcap);  // ids >= vcap never occur
     uint32_t nl[4];
     for (int v = 0; v < 4; v++) nl[v] = sh ? 0 : E->vnl[P][v];
     const uint32_t dense_end = 1 + 4 * W;
@@ -1431,7 +1430,7 @@ __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Ctl *Cg, T
 // values alone (8 B per entry) give the wave's second-largest best M2 (with
 // multiplicity); only entries whose best reaches M2 can hold the wave's best
 // or runner-up, so only those few load their key / tie / runner-up.
-__device__ inline Top2 summary_top2(const unsigned long long *best, const uint32_t *tie,
+__device__ __forceinline__ Top2 summary_top2(const unsigned long long *best, const uint32_t *tie,
                                     const unsigned long long *key, const unsigned long long *v2,
                                     const unsigned long long *k2, uint64_t n) {
     constexpr uint32_t PER = SELECT_L1_MAX / 1024;
@@ -1511,10 +1510,15 @@ __device__ __forceinline__ void select_block(const Eng *__restrict__ E, Ctl *__r
     const uint64_t nL1 = E->hcap / L1W;
     const bool lvl1 = nL1 <= SELECT_L1_MAX;
     const bool hot = E->hot != 0;
-    Top2 mine = hot ? summary_top2(E->hotp_best, E->hotp_tie, E->hotp_key, E->hotp_v2, E->hotp_k2, E->hot_parts)
-                    : summary_top2(lvl1 ? E->l1best : E->l2best, lvl1 ? E->l1tie : E->l2tie,
-                                   lvl1 ? E->l1key : E->l2key, lvl1 ? E->l1v2 : E->l2v2, lvl1 ? E->l1k2 : E->l2k2,
-                                   lvl1 ? nL1 : (nL1 + L2W - 1) / L2W);
+    // one inlined reduction over the selected summary arrays: a second call
+    // site made the compiler outline it, and the call frame gave k_select /
+    // k_fused a scratch segment (late wave dispatch)
+    Top2 mine = summary_top2(hot ? E->hotp_best : lvl1 ? E->l1best : E->l2best,
+                             hot ? E->hotp_tie : lvl1 ? E->l1tie : E->l2tie,
+                             hot ? E->hotp_key : lvl1 ? E->l1key : E->l2key,
+                             hot ? E->hotp_v2 : lvl1 ? E->l1v2 : E->l2v2,
+                             hot ? E->hotp_k2 : lvl1 ? E->l1k2 : E->l2k2,
+                             hot ? E->hot_parts : lvl1 ? nL1 : (nL1 + L2W - 1) / L2W);
     if (tid < CW) scw[tid] = cw_v;
     if (tid < 256) srank[tid] = rk_v;
     if (tid == 0) sc_t1 = wall_clock64();

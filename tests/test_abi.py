@@ -200,3 +200,27 @@ def test_reference_main_links_against_library(tmp_path):
     subprocess.check_call(["gcc", "-O1", main, "-o", str(exe), "-L" + os.path.dirname(_lib.LIB_PATH),
                            "-lbpe_amd", "-Wl,-rpath," + os.path.dirname(_lib.LIB_PATH)])
     assert exe.exists()
+
+
+def test_per_merge_kernels_have_no_scratch_segment():
+    """The per-merge kernels run 10^3-10^4 times per job: a scratch (private)
+    segment delays their wave dispatch.  Round 2 found
+    k_fused / k_select / k_fused_sh with a 184-byte call frame from an
+    outlined summary reduction; read the gfx950 kernel descriptors of the
+    built library and keep every per-merge kernel at zero."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("kernel_scratch", os.path.join(ROOT, "tools", "kernel_scratch.py"))
+    ks = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ks)
+    lib = os.environ.get("BPE_LIB") or os.path.join(ROOT, "llmtokenizer_amd", "libbpe_amd.so")
+    kd = ks.scan(lib)
+    assert len(kd) > 20, "no gfx950 kernel descriptors found"
+    per_merge = ("k_fused", "k_fused_sh", "k_select", "k_rescan_spec", "k_rescan_spec_sh", "k_scan", "k_apply",
+                 "k_undo", "k_rescan1", "k_hot_reduce")
+    found = {}
+    for name, (lds, scratch) in kd.items():
+        for k in per_merge:
+            if re.search(r"\d%s(E|I)" % k, name):
+                found[k] = scratch
+    assert set(found) == set(per_merge), sorted(set(per_merge) - set(found))
+    assert all(v == 0 for v in found.values()), found
