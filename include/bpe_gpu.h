@@ -76,6 +76,9 @@ typedef struct {
                                  retry, 2 global batched replay                 */
     uint64_t enc_windows;     /* encode: windows replayed (window path)           */
     uint64_t relists;         /* training: byte-pair position lists rebuilt       */
+    uint64_t batches;         /* training: merge batches (several merges per scan/apply pair) */
+    uint64_t batch_dropped;   /* training: batch members that failed the verification */
+    uint64_t batch_retries;   /* training: batches formed again (shorter) after a failed member */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */

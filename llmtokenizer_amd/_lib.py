@@ -43,7 +43,8 @@ class GpuStats(ctypes.Structure):
         [(n, ctypes.c_double) for n in ("ms_init", "ms_train", "ms_total", "ms_count_pass")] + \
         [(n, ctypes.c_uint64) for n in ("candidates", "occurrences", "l1_rescanned", "spec_hits", "spec_misses",
                                                      "count_pass_span", "hot_rebuilds", "hot_mode", "hot_scanned",
-                                                     "enc_path", "enc_windows", "relists")]
+                                                     "enc_path", "enc_windows", "relists", "batches",
+                                                     "batch_dropped", "batch_retries")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1,0 +1,826 @@
+// batch.hip -- batched training: several merges per scan / apply kernel pair.
+//
+// The reference commits one merge per pass over the corpus (count, serial
+// table merge, argmax, replace: bpe/src/bpe.c:669-783).  The one-merge engine
+// (kernels.hip) already touches only what a merge changes, but every merge
+// still costs a fixed chain of dependent round trips.  Here one chain commits
+// a whole batch of merges:
+//
+//   k_bsel   the hot set's keys in argmax order (TOPK of them, each reduce
+//            block sorts its share with wave bitonic networks, the last block
+//            to finish merges the partial lists) -> the batch: the longest
+//            prefix of that order whose pairs commute (no id is the left id of
+//            one member and the right id of another; an a == b pair only
+//            alone), each member after the first strictly ahead of the next
+//            key in the order
+//   k_bscan  every member's occurrences in the PRE-batch tokens (commuting
+//            members never share a token, so these are exactly the
+//            occurrences the sequential replace passes would find), the exact
+//            count deltas of the whole batch (the pair between two adjacent
+//            occurrences belongs to the left one), and per member a bound on
+//            the count of any key it creates
+//   k_bapply verification, then role A (token spans, occurrence lists) and
+//            role B (the deltas into the pair table) for the verified prefix
+//
+// Verification.  Member j is the reference's argmax after members 0..j-1:
+// its own count is untouched by them (commuting), every other old key only
+// loses counts and was behind it (in the same tie order: the select requires
+// member j's count above the next key's unless no member can move B_final),
+// and a key a member i < j creates holds at most bound[i] (its occurrences
+// with one given neighbour id), which must be below member j's count.  Member
+// 0 is the exact argmax with the tie order, as in the one-merge engine.  A
+// batch whose member j fails is applied not at all (the pair between adjacent
+// occurrences of two members is counted once, by the left one, so a member's
+// deltas assume its neighbours' members merge too) and formed again with j
+// members; nothing changed in between, so the selection repeats.
+#pragma once
+#include "engine_common.h"
+
+namespace bpeamd {
+
+static_assert(TOPK == 32, "wave merges hold two 32-entry lists");
+static_assert(BRB == 2 * (1024 / 64), "the select's 16 waves merge two partial lists each");
+static_assert(BK < 32, "member masks are 32-bit");
+
+// ------------------------------------------------------------ sorted lists
+struct KV {
+    unsigned long long v, k;  // packed value (count << 32 | ~bucket), key (a << 32 | b)
+};
+__device__ inline KV kv_empty() { return KV{0ull, ~0ull}; }
+__device__ inline bool kv_ahead(const KV &x, const KV &y) { return x.v > y.v || (x.v == y.v && x.k < y.k); }
+__device__ inline KV kv_shfl(const KV &x, int src) { return KV{__shfl(x.v, src), __shfl(x.k, src)}; }
+
+// bitonic sort of the wave's 64 entries (one per lane): lane 0 holds the first
+// in argmax order
+__device__ inline KV wave_sort64(KV x) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            const KV y = kv_shfl(x, (int)(lane ^ j));
+            const bool desc = (lane & k) == 0, lower = (lane & j) == 0;
+            if (lower == desc ? kv_ahead(y, x) : kv_ahead(x, y)) x = y;
+        }
+    }
+    return x;
+}
+
+// lanes 0..31 one sorted list, lanes 32..63 another in reverse: a bitonic
+// sequence; after the merge the lanes hold the union sorted (0..31 its top)
+__device__ inline KV wave_merge64(KV x) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (uint32_t j = 32; j > 0; j >>= 1) {
+        const KV y = kv_shfl(x, (int)(lane ^ j));
+        if ((lane & j) == 0 ? kv_ahead(y, x) : kv_ahead(x, y)) x = y;
+    }
+    return x;
+}
+
+// tree of the block's wave lists in part[w] (sorted, TOPK each): part[0] = top TOPK
+__device__ inline void block_list_tree(KV (*part)[TOPK], uint32_t nw) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t s = 1; s < nw; s <<= 1) {
+        if (w % (2 * s) == 0 && w + s < nw) {
+            KV x = lane < 32 ? part[w][lane] : part[w + s][63 - lane];
+            x = wave_merge64(x);
+            if (lane < 32) part[w][lane] = x;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ k_bsel
+// this block's share of the hot set (counts after the batch applied last,
+// buckets under B_final of its D) as a sorted top-TOPK list in out (LDS)
+__device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bsz, KV *out) {
+    __shared__ KV part[16][TOPK];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    KV run = kv_empty();
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t base = blockIdx.x * blockDim.x + w * 64; base < n; base += stride) {  // uniform per wave
+        const uint32_t i = base + lane;
+        KV x = kv_empty();
+        if (i < n) {
+            const uint32_t slot = E->hot_slot[i];
+            const uint32_t c = E->hcnt[slot];
+            const unsigned long long key = E->hkey[slot] - 1;
+            if (c) x = KV{pack_val(c, (uint32_t)(key >> 32), (uint32_t)key, Bsz), key};
+        }
+        x = wave_sort64(x);
+        const KV r = kv_shfl(run, (int)(63 - lane));
+        if (lane >= 32) x = r;
+        run = wave_merge64(x);
+    }
+    if (lane < TOPK) part[w][lane] = run;
+    __syncthreads();
+    block_list_tree(part, nw);
+    if (threadIdx.x < TOPK) out[threadIdx.x] = part[0][threadIdx.x];
+    __syncthreads();
+}
+
+constexpr uint32_t BAT_HEAD_WORDS = offsetof(Bat, pv) / 4;
+
+// The selection (the last reduce block): folds the batch applied last into the
+// control block, runs the reference's stop rules on the argmax, forms the next
+// batch.  Control block and batch head are staged in LDS and written back whole
+// (no other block of the launch touches them any more).
+struct alignas(16) BatHead {  // the words of Bat up to the partial lists
+    uint32_t w[BAT_HEAD_WORDS];
+};
+
+__device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, Bat *__restrict__ Bg, uint32_t nhot) {
+    __shared__ Ctl sc;
+    __shared__ BatHead sbh;
+    __shared__ KV part[16][TOPK];
+    __shared__ uint32_t srank[256];
+    __shared__ uint32_t clear_k, nmem;
+    __shared__ uint32_t ctl[BK];
+    constexpr uint32_t CW = sizeof(Ctl) / 4;
+    static_assert(CW <= 1024 && BAT_HEAD_WORDS <= 1024, "staged one word per thread");
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t *scw = reinterpret_cast<uint32_t *>(&sc);
+    uint32_t *sbw = sbh.w;
+    const uint32_t *cgw = reinterpret_cast<const uint32_t *>(Cg);
+    const uint32_t *bgw = reinterpret_cast<const uint32_t *>(Bg);
+    // partial lists 2w and 2w+1 (published by the other blocks: L2-coherent loads)
+    KV x;
+    {
+        const uint32_t src = lane < 32 ? (2 * w) * TOPK + lane : (2 * w + 1) * TOPK + (63 - lane);
+        x.v = aload64(&Bg->pv[src]);
+        x.k = aload64(&Bg->pk[src]);
+    }
+    const uint32_t cv = tid < CW ? aload(cgw + tid) : 0u;
+    const uint32_t bv = tid < BAT_HEAD_WORDS ? aload(bgw + tid) : 0u;
+    const uint32_t rk = tid < 256 ? E->rank[tid] : 0u;
+    x = wave_merge64(x);
+    if (lane < 32) part[w][lane] = x;
+    if (tid < CW) scw[tid] = cv;
+    if (tid < BAT_HEAD_WORDS) sbw[tid] = bv;
+    if (tid < 256) srank[tid] = rk;
+    if (tid == 0) clear_k = nmem = 0;
+    __syncthreads();
+    block_list_tree(part, blockDim.x >> 6);
+    Bat *B = reinterpret_cast<Bat *>(&sbh);  // (head fields only)
+    // Wave 0 decides, one list entry per lane; every lane reads the staged
+    // words itself (no lane waits on another's LDS store); lane 0 writes the
+    // scalar results, lane q member q's
+    if (tid < 64) {
+        Ctl *C = &sc;
+        // ---- the batch applied last, folded
+        const bool applied = B->applied != 0;
+        const uint32_t jst = applied ? B->jstar : 0, kpr = applied ? B->k : 0;
+        const uint32_t retry = applied ? B->retry : 0;  // the last batch failed at member `retry`
+        // (read before the lanes overwrite the member fields)
+        const uint32_t olda = jst ? B->a[jst - 1] : 0, oldb = jst ? B->b[jst - 1] : 0, oldz0 = B->z0;
+        const uint32_t oldsum = B->sumlen;
+        unsigned long long rs = lane < jst ? B->R[lane] : 0ull;
+        for (int o = 32; o > 0; o >>= 1) rs += __shfl_xor(rs, o);
+        const unsigned long long D = C->D + (applied ? B->dD : 0ull);
+        const uint32_t md = C->merges_done + jst;
+        const unsigned long long n_live = C->n_live - rs;
+        // ---- the list, one entry per lane
+        const KV e = lane < TOPK ? part[0][lane] : kv_empty();
+        const unsigned long long kprev = __shfl(e.k, (int)(lane ? lane - 1 : 0));
+        const uint32_t nl = (uint32_t)__popcll(__ballot(lane < TOPK && e.v != 0));  // non-empty (sorted first)
+        const bool truncated = nl == TOPK;  // more keys may follow the list
+        const unsigned long long v0 = __shfl(e.v, 0), k0 = __shfl(e.k, 0);
+        const uint32_t cnt0 = (uint32_t)(v0 >> 32);
+        const uint32_t ties =
+            (uint32_t)__popcll(__ballot(lane < nl && e.v == v0 && (lane == 0 || e.k != kprev)));
+        uint32_t edge;
+        const uint64_t Bn = bfinal_nominal(D, &edge);
+        const uint64_t Bsz = edge ? 2 * Bn : Bn;
+        const uint32_t hotT = C->hot_T;
+        uint32_t stop = STOP_NONE;
+        if (C->err) stop = STOP_ERROR;
+        else if (!E->fast && n_live < TRACK_LIMIT) stop = STOP_MODE;
+        else if (md >= E->mcap) stop = STOP_CAP;
+        else if ((cnt0 < hotT && hotT > 2) || C->hot_n > HOT_LIMIT) stop = STOP_HOT;
+        else if (v0 == 0 || cnt0 <= 1) stop = STOP_DONE;
+        else if (C->nkeys + 4ull * (256ull + md + 2) >= E->hcap / 2) stop = STOP_GROW;
+        // ---- the batch: the longest prefix of the list whose entries qualify
+        uint32_t k = 0;
+        if (stop == STOP_NONE) {
+            const uint32_t u = (uint32_t)(e.k >> 32), v = (uint32_t)e.k, c = (uint32_t)(e.v >> 32);
+            const uint32_t u0 = (uint32_t)(k0 >> 32), w0 = (uint32_t)k0;
+            // ties with the next key keep their pre-batch order when the members
+            // before it cannot move B_final: a member adds or zeroes at most
+            // 2 min(ids, count) + 1 keys (its neighbours' pairs and its own)
+            const uint32_t cprev = (uint32_t)(__shfl(e.v, (int)(lane ? lane - 1 : 0)) >> 32);
+            unsigned long long span = lane > 0 && lane <= nl ? min(2ull * (256ull + md + BK), 2ull * cprev) + 1 : 0ull;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned long long y = __shfl_up(span, o);
+                if ((int)lane >= o) span += y;
+            }
+            const bool stable = summary_B(D > span ? D - span : 0) == Bsz && summary_B(D + span) == Bsz;
+            const uint32_t cnext = __shfl(c, (int)(lane < 63 ? lane + 1 : 63));
+            uint32_t why = 0;  // 0: qualifies
+            if (lane >= nl || lane >= BK) why = 8;  // past the list (reported as "list")
+            else if (lane > 0) {
+                if (e.k == kprev) why = 3;  // the same key listed twice (the one-merge engine's undo): end here
+                else if (md + lane >= E->mcap || c <= 1 || (hotT > 2 && c < hotT)) why = 1;
+                else if (u == v || u0 == w0) why = 2;  // a == b pairs alone
+                else if (!stable && ((lane + 1 >= nl && truncated) || !(c > (lane + 1 < nl ? cnext : 0u)))) why = 4;
+                else if (C->nkeys + 4ull * (256ull + md + lane + 2) * (lane + 1) >= E->hcap / 2) why = 6;
+            }
+            // commuting: no earlier entry uses my left id on its right or my right id on its left
+#pragma unroll
+            for (uint32_t p = 0; p < BK; p++) {
+                const uint32_t up = __builtin_amdgcn_readlane((int)u, (int)p), vp = __builtin_amdgcn_readlane((int)v, (int)p);
+                if (!why && p < lane && (u == vp || v == up)) why = 5;
+            }
+            const unsigned long long badm = __ballot(why != 0);
+            k = badm ? (uint32_t)__ffsll(badm) - 1 : 64;  // lane 0 always qualifies
+            if (retry && retry < k) k = retry;  // the last batch failed there (nothing changed since)
+            const uint32_t endwhy = __shfl(why, (int)(k < 64 ? k : 0));
+            // candidate lists and token lengths, one lane per member
+            uint32_t mode = 1, off = 0, len = 0, tl = 0;
+            if (lane < k) {
+                cand_of(E, u, v, true, srank, E->poff, &mode, &off, &len);
+                tl = E->tlen[u] + E->tlen[v];
+            }
+            // the members' candidates fit the occurrence staging (ids_out, n0 positions)
+            unsigned long long pre = len;  // inclusive prefix
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned long long y = __shfl_up(pre, o);
+                if ((int)lane >= o) pre += y;
+            }
+            const unsigned long long over = __ballot(lane > 0 && lane < k && pre > E->n0);
+            uint32_t why_end = endwhy == 8 ? 0 : endwhy;
+            if (over) {
+                k = (uint32_t)__ffsll(over) - 1;
+                why_end = 7;
+            }
+            const unsigned long long sumlen = __shfl(pre, (int)(k - 1));
+            // scan blocks in proportion to the candidate lists (>= 1 each), the
+            // rest to the largest member
+            const uint32_t nb = lane < k ? 1 + (uint32_t)(sumlen ? (uint64_t)(BSB - k) * len / sumlen : 0) : 0;
+            uint32_t bpre = nb;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(bpre, o);
+                if ((int)lane >= o) bpre += y;
+            }
+            const uint32_t used = __shfl(bpre, (int)(k - 1));
+            unsigned long long big = lane < k ? ((unsigned long long)len << 8) | (255u - lane) : 0ull;
+            for (int o = 32; o > 0; o >>= 1) big = max(big, (unsigned long long)__shfl_xor(big, o));
+            const uint32_t bigm = 255u - (uint32_t)(big & 255u);
+            const uint32_t extra = BSB - used;
+            if (lane < k) {
+                B->a[lane] = u;
+                B->b[lane] = v;
+                B->cnt[lane] = c;
+                B->mode[lane] = mode;
+                B->off[lane] = off;
+                B->len[lane] = len;
+                B->sbase[lane] = (uint32_t)(pre - len);
+                B->R[lane] = 0;
+                B->bound[lane] = 0;
+                B->blk0[lane] = bpre - nb + (lane > bigm ? extra : 0);
+                ctl[lane] = tl;
+            }
+            if (lane == 0) {
+                B->sbase[k] = (uint32_t)sumlen;
+                B->blk0[k] = BSB;
+                B->sumlen = (uint32_t)sumlen;
+                B->why[why_end]++;
+                if (ties > 1) C->counters[2]++;
+            }
+        }
+        if (lane == 0) {
+            if (applied) {
+                C->merges_done = md;
+                C->occ_top += (uint32_t)rs;
+                C->n_live = n_live;
+                C->D = D;
+                C->counters[0] += jst;
+                C->counters[4] += oldsum;
+                C->counters[5] += rs;
+                if (jst) {
+                    C->a = olda;
+                    C->b = oldb;
+                    C->z = oldz0 + jst - 1;
+                }
+                if (retry) {
+                    B->nretry++;
+                    B->ndrop += kpr - retry;
+                } else {
+                    B->nbatch++;
+                }
+                B->retry = 0;
+                B->applied = 0;
+                B->dD = 0;
+            }
+            clear_k = kpr;
+            C->hot_scanned += nhot;
+            C->stop_z = C->z;
+            C->B = Bsz;
+            C->full = 0;
+            C->W = v0;
+            C->edge = edge;
+            C->ties = ties;
+            C->stop = stop;
+            B->ticket = 0;
+            B->k = k;
+            B->z0 = 256 + md;
+            nmem = k;
+        }
+    }
+    __syncthreads();
+    if (tid < nmem) E->tlen[256 + sc.merges_done + tid] = ctl[tid];
+    for (uint32_t q = tid; q < CW; q += blockDim.x) reinterpret_cast<uint32_t *>(Cg)[q] = scw[q];
+    for (uint32_t q = tid; q < BAT_HEAD_WORDS; q += blockDim.x) reinterpret_cast<uint32_t *>(Bg)[q] = sbw[q];
+    for (uint32_t q = tid; q < clear_k * 4; q += blockDim.x) E->bvnl[q] = 0;
+    if (tid == 0 && sc.stop != STOP_NONE && E->hprobe) {
+        __hip_atomic_store(E->hprobe, sc.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    }
+}
+
+// Reduce (every block: its share of the hot set, sorted) + select (the last
+// block to finish).  Grid BRB x 1024.
+__global__ __launch_bounds__(1024) void k_bsel(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    if (C->stop) return;
+    Bat *B = E->bat;
+    const uint64_t Bsz = summary_B(C->D + B->dD);  // D after the batch applied last
+    const uint32_t n = min(C->hot_n, HOT_CAP);
+    __shared__ KV top[TOPK];
+    __shared__ uint32_t last;
+    bat_block_top(E, n, Bsz, top);
+    if (threadIdx.x < TOPK) {
+        B->pv[blockIdx.x * TOPK + threadIdx.x] = top[threadIdx.x].v;
+        B->pk[blockIdx.x * TOPK + threadIdx.x] = top[threadIdx.x].k;
+    }
+    // publish: stores drained, release, ticket; the last block acquires
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t = __hip_atomic_fetch_add(&B->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == gridDim.x - 1;
+        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (!last) return;
+    bselect_block(E, C, B, n);
+}
+
+// ----------------------------------------------------------------- k_bscan
+constexpr uint32_t RH = 128;  // LDS role table: member ids -> (left-member mask, right-member mask)
+__device__ inline uint32_t rh_hash(uint32_t id) { return (id * 2654435761u) >> 25; }
+
+struct RoleTab {
+    uint32_t id[RH], lm[RH], rm[RH];
+    __device__ inline void put(uint32_t x, bool right, uint32_t m) {
+        uint32_t s = rh_hash(x);
+        for (;;) {
+            const uint32_t prev = atomicCAS(&id[s], HOLE, x);
+            if (prev == HOLE || prev == x) {
+                atomicOr(right ? &rm[s] : &lm[s], 1u << m);
+                return;
+            }
+            s = (s + 1) & (RH - 1);
+        }
+    }
+    __device__ inline void get(uint32_t x, uint32_t *l, uint32_t *r) const {
+        uint32_t s = rh_hash(x);
+        for (;;) {  // at most 2 BK < RH / 2 ids
+            const uint32_t v = id[s];
+            if (v == x) { *l = lm[s]; *r = rm[s]; return; }
+            if (v == HOLE) { *l = *r = 0; return; }
+            s = (s + 1) & (RH - 1);
+        }
+    }
+};
+
+// member delta m, vector v, neighbour id x (LDS below DENSE, else global + list)
+__device__ inline void vadd_b(uint32_t (*s)[DENSE], const Eng *E, uint32_t m, int v, uint32_t x, uint32_t *gcnt) {
+    if (x < DENSE) {
+        atomicAdd(&s[v][x], 1u);
+        return;
+    }
+    const uint64_t base = ((uint64_t)m * 4 + v) * E->bvs;
+    const uint32_t old = atomicAdd(&E->bvec[base + (x - DENSE)], 1u);
+    if (old == 0) {
+        const uint32_t p = atomicAdd(&E->bvnl[m * 4 + v], 1u);
+        E->bvlist[base + p] = x;
+    }
+    if (v == V_DL || v == V_DR) atomicAdd(&gcnt[v], 1u);
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, const Ctl *__restrict__ C) {
+    if (C->stop) return;
+    Bat *B = E->bat;
+    __shared__ uint32_t s[4][DENSE];
+    __shared__ uint32_t list[SCAN_T];
+    __shared__ uint16_t ltag[SCAN_T];
+    __shared__ uint32_t lcount, gbase, bR, covc, sm, sk, sz0;
+    __shared__ uint32_t gcnt[2];
+    __shared__ uint32_t sa[BK], sb[BK], sla[BK];
+    __shared__ RoleTab rt;
+    __shared__ uint32_t wmx[2][16];
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {
+        sm = BK;
+        lcount = bR = covc = 0;
+        gcnt[0] = gcnt[1] = 0;
+        sk = B->k;
+        sz0 = B->z0;
+    }
+    for (uint32_t q = tid; q < RH; q += SCAN_T) {
+        rt.id[q] = HOLE;
+        rt.lm[q] = rt.rm[q] = 0;
+    }
+    if (tid < BK) {
+        const uint32_t lo = B->blk0[tid], hi = B->blk0[tid + 1];
+        const uint32_t ma = B->a[tid];
+        sa[tid] = ma;
+        sb[tid] = B->b[tid];
+        sla[tid] = E->tlen[ma];
+        if (blockIdx.x >= lo && blockIdx.x < hi && tid < B->k) sm = tid;
+    }
+    __syncthreads();
+    const uint32_t k = sk, m = sm, z0 = sz0;
+    if (m >= k) return;  // block-uniform: no member for this block
+    if (tid < k) {
+        rt.put(sa[tid], false, tid);
+        rt.put(sb[tid], true, tid);
+    }
+    const uint32_t a = sa[m], b = sb[m], z = z0 + m, la = sla[m];
+    const uint32_t lb = E->tlen[b];
+    const uint32_t mode = B->mode[m], off = B->off[m], len = B->len[m];
+    const uint32_t bid = blockIdx.x - B->blk0[m], nblk = B->blk0[m + 1] - B->blk0[m];
+    const uint32_t sbase = B->sbase[m];
+    uint32_t *occz = E->ids_out + sbase;
+    uint16_t *tagz = E->btag + sbase;
+    uint32_t *Rm = &B->R[m];
+    const int64_t n = (int64_t)E->n0;
+    const uint32_t *__restrict__ tok = E->tok;
+    const uint32_t want = mode == 2 ? a : b;
+    // ids < z0 + k occur in this batch's deltas
+    const uint32_t lim = min(DENSE, z0 + k);
+    for (uint32_t v = 0; v < 4; v++)
+        for (uint32_t x = tid; x < lim; x += SCAN_T) s[v][x] = 0;
+    __syncthreads();
+    auto tok_at = [&](int64_t p) -> uint32_t { return (p < 0 || p >= n) ? HOLE : tok[p]; };
+
+    for (uint32_t e0 = bid * SCAN_T; e0 < len; e0 += nblk * SCAN_T) {
+        const uint32_t e = e0 + tid;
+        bool ok = false;
+        int64_t i = 0, j = 0;
+        uint32_t tl = HOLE, tr = HOLE;
+        if (e < len) {
+            if (mode == 2) {
+                j = E->occ[off + e];
+                if (tag_ok(E->occnb[off + e] >> 8, want) && tok[j] == b) {
+                    i = v_left<false>(tok, j);
+                    ok = i >= 0 && tok[i] == a;
+                    if (ok) {
+                        tl = i > 0 ? tok[i - 1] : HOLE;
+                        tr = j + lb < n ? tok[j + lb] : HOLE;
+                    }
+                }
+            } else {
+                i = (mode == 0) ? E->plist[off + e] : E->occ[off + e];
+                if (mode == 0 || tag_ok(E->occnb[off + e] & 0xFFu, want)) {
+                    j = i + la;
+                    const TokWin W = tok_window(tok, i);
+                    const int64_t kk = j + lb;
+                    const uint32_t t0 = W.at(i);
+                    const uint32_t t1 = j >= n ? HOLE : W.has(j) ? W.at(j) : tok[j];
+                    tl = i > 0 ? W.at(i - 1) : HOLE;
+                    tr = kk >= n ? HOLE : W.has(kk) ? W.at(kk) : tok[kk];
+                    ok = t0 == a && t1 == b && j < n;
+                }
+            }
+        }
+        if (a != b) {
+            const uint32_t slot = wave_append(ok, &lcount);
+            if (ok) {
+                list[slot] = (uint32_t)i;
+                // left neighbour: covered when it is the b of an occurrence of
+                // a member (that occurrence owns the pair between the two)
+                const int64_t ps = i == 0 ? -1 : start_of_end<false>(tl, i - 1);
+                const uint32_t p = (i > 0 && is_id(tl)) ? tl : tok_at(ps);
+                uint32_t lfin = p;
+                if (p != HOLE) {
+                    uint32_t lmk, rmk;
+                    rt.get(p, &lmk, &rmk);
+                    bool cov = false;
+                    if (rmk) {
+                        const uint32_t pp = tok_at(v_left<false>(tok, ps));
+                        for (uint32_t q = rmk; q; q &= q - 1) {
+                            const uint32_t mm = __ffs(q) - 1;
+                            if (sa[mm] == pp) {
+                                cov = true;
+                                lfin = z0 + mm;
+                            }
+                        }
+                    }
+                    if (cov) {
+                        atomicAdd(&covc, 1u);
+                    } else {
+                        vadd_b(s, E, m, V_DL, p, gcnt);
+                        vadd_b(s, E, m, V_IL, p, gcnt);
+                    }
+                }
+                // right neighbour: the a of a member's occurrence -> that id
+                const int64_t kq = v_right(j, lb, n);
+                const uint32_t q = kq < n ? tr : HOLE;
+                uint32_t rfin = q;
+                if (q != HOLE) {
+                    uint32_t lmk, rmk;
+                    rt.get(q, &lmk, &rmk);
+                    if (lmk) {
+                        const uint32_t qq = tok_at(v_right(kq, sla[__ffs(lmk) - 1], n));
+                        for (uint32_t t = lmk; t; t &= t - 1) {
+                            const uint32_t mm = __ffs(t) - 1;
+                            if (sb[mm] == qq) rfin = z0 + mm;
+                        }
+                    }
+                    vadd_b(s, E, m, V_DR, q, gcnt);
+                    vadd_b(s, E, m, V_IR, rfin, gcnt);
+                }
+                ltag[slot] = nb_tag(lfin, rfin);
+            }
+        } else if (ok) {
+            // a == b (a batch of its own): the thread holding a run's first
+            // token walks it, pairing tokens 0-1, 2-3, ... (greedy left-to-right)
+            const int64_t ps = v_left<false>(tok, i);
+            const uint32_t p = tok_at(ps);
+            bool start = true, left = p != HOLE;
+            int64_t pos = i;
+            if (p == a) {
+                start = false;
+                left = false;
+            }
+            for (uint32_t mi = 0; start; mi++) {
+                const int64_t jj = pos + la;
+                if (jj >= n || tok[jj] != a) break;
+                const int64_t kq = v_right(jj, la, n);
+                const uint32_t q = tok_at(kq);
+                const bool knext = q == a;
+                const bool nocc = knext && tok_at(v_right(kq, la, n)) == a;
+                const uint32_t pfin = mi > 0 ? z : (left ? p : (p == HOLE ? HOLE : z));
+                stage_one(list, ltag, &lcount, Rm, occz, tagz, (uint32_t)pos, nb_tag(pfin, nocc ? z : q), &bR);
+                if (mi == 0 && left) {
+                    vadd_b(s, E, m, V_DL, p, gcnt);
+                    vadd_b(s, E, m, V_IL, p, gcnt);
+                }
+                if (q != HOLE) {
+                    vadd_b(s, E, m, V_DR, q, gcnt);
+                    vadd_b(s, E, m, V_IR, nocc ? z : q, gcnt);
+                }
+                if (!knext || kq >= n) break;
+                pos = kq;
+            }
+        }
+        flush_list(list, ltag, &lcount, &gbase, Rm, occz, tagz, &bR);
+    }
+    // deltas into replica (block % BREPL) of the member's accumulators, and the
+    // member's new-key bound: per block max over ids (+ covered left
+    // neighbours, + every add that bypassed LDS), summed over blocks
+    uint32_t *rep = E->bvecd + (uint64_t)(m * BREPL + bid % BREPL) * 4 * DENSE;
+    uint32_t mxl = 0, mxr = 0;
+    for (uint32_t v = 0; v < 4; v++)
+        for (uint32_t x = tid; x < lim; x += SCAN_T) {
+            const uint32_t c = s[v][x];
+            if (c) atomicAdd(&rep[v * DENSE + x], c);
+            if (v == V_DL) mxl = max(mxl, c);
+            if (v == V_DR) mxr = max(mxr, c);
+        }
+    if (k > 1) {
+        for (int o = 32; o > 0; o >>= 1) {
+            mxl = max(mxl, (uint32_t)__shfl_xor(mxl, o));
+            mxr = max(mxr, (uint32_t)__shfl_xor(mxr, o));
+        }
+        if ((tid & 63) == 0) {
+            wmx[0][tid >> 6] = mxl;
+            wmx[1][tid >> 6] = mxr;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t l = 0, r = 0;
+            for (uint32_t q = 0; q < SCAN_T / 64; q++) {
+                l = max(l, wmx[0][q]);
+                r = max(r, wmx[1][q]);
+            }
+            atomicAdd(&B->bound[m], max(l + gcnt[V_DL] + covc, r + gcnt[V_DR]));
+        }
+    }
+}
+
+// ---------------------------------------------------------------- k_bapply
+__device__ inline uint64_t hinsert_c(const Eng *E, uint32_t u, uint32_t v, uint32_t *nins) {
+    const unsigned long long key = (((unsigned long long)u << 32) | v) + 1ull;
+    const uint64_t msk = E->hcap - 1;
+    uint64_t s = mix64(key) & msk;
+    for (uint64_t p = 0; p <= msk; p++) {
+        const unsigned long long prev = atomicCAS(&E->hkey[s], 0ull, key);
+        if (prev == 0) {
+            *nins += 1;
+            return s;
+        }
+        if (prev == key) return s;
+        s = (s + 1) & msk;
+    }
+    return ~0ull;
+}
+
+// Verification, then role A (blocks [0, roleA_blocks): token spans of the
+// verified members' occurrences, occurrence lists copied into the pool) and
+// role B (the rest: every member's delta entries are read and cleared; the
+// verified members' go into the pair table with atomics -- a key touched by
+// several members or vectors takes each contribution separately, and since
+// within a batch old keys only fall and new keys only rise, D and the hot set
+// follow from each atomic's old value).
+__global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl *__restrict__ C,
+                                                 uint32_t roleA_blocks) {
+    if (C->stop) return;
+    Bat *B = E->bat;
+    __shared__ uint32_t sa[BK], sb[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], snl[BK * 4 + 1];
+    __shared__ uint32_t sk, sj, sz0;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t k = B->k;
+    if (tid < k) {
+        const uint32_t ma = B->a[tid], mb = B->b[tid];
+        sa[tid] = ma;
+        sb[tid] = mb;
+        sla[tid] = E->tlen[ma];
+        slb[tid] = E->tlen[mb];
+        sR[tid] = B->R[tid];
+        ssb[tid] = B->sbase[tid];
+    }
+    __shared__ uint32_t scnt[BK], sbnd[BK];
+    __shared__ unsigned long long slive;
+    __shared__ uint32_t sdt;
+    if (tid < k) {
+        scnt[tid] = B->cnt[tid];
+        sbnd[tid] = B->bound[tid];
+    }
+    if (tid < k * 4) snl[tid + 1] = E->bvnl[tid];
+    if (tid == 0) {
+        sk = k;
+        sz0 = B->z0;
+        slive = C->n_live;
+        sdt = B->drop_test;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        // the verified prefix: member j is the argmax after members < j when
+        // its count beats every key they can create, and the run is still
+        // untracked when it would be selected
+        uint32_t js = k ? 1 : 0, pm = 0;
+        unsigned long long live = slive - (k ? sR[0] : 0);
+        for (uint32_t q = 1; q < k; q++) {
+            pm = max(pm, sbnd[q - 1]);
+            if (!(pm < scnt[q])) break;
+            if (sdt && (sz0 + q) % sdt == 0) break;  // (tests: forced failures)
+            if (!E->fast && live < TRACK_LIMIT) break;
+            live -= sR[q];
+            js = q + 1;
+        }
+        if (js < k) {  // re-form the batch with the verified prefix; apply nothing
+            B->retry = js;
+            js = 0;
+        }
+        sj = js;
+        spre[0] = 0;
+        for (uint32_t q = 0; q < k; q++) spre[q + 1] = spre[q] + sR[q];
+        snl[0] = 0;
+        for (uint32_t q = 0; q < k * 4; q++) snl[q + 1] += snl[q];
+    }
+    __syncthreads();
+    const uint32_t js = sj, z0 = sz0;
+    if (blockIdx.x < roleA_blocks) {
+        uint32_t *tok = E->tok;
+        const uint64_t n = E->n0;
+        const uint32_t top = C->occ_top;
+        const uint32_t tot = spre[js];
+        for (uint32_t e = blockIdx.x * blockDim.x + tid; e < tot; e += roleA_blocks * blockDim.x) {
+            uint32_t m = 0;
+            while (e >= spre[m + 1]) m++;
+            const uint32_t loc = ssb[m] + (e - spre[m]);
+            const uint64_t i = E->ids_out[loc];
+            const uint16_t tg = E->btag[loc];
+            const uint64_t j = i + sla[m], kq = j + slb[m];
+            tok[i] = z0 + m;
+            if (kq - 1 - i > END_MAX) C->err = 5;
+            if (kq - 1 == j) {
+                tok[j] = end_code(kq - 1 - i);
+            } else {
+                tok[j] = HOLE;
+                if (kq - 1 < n) tok[kq - 1] = end_code(kq - 1 - i);
+            }
+            E->occ[top + e] = (uint32_t)i;
+            E->occnb[top + e] = tg;
+        }
+        if (blockIdx.x == 0 && tid == 0) {
+            const uint32_t md = C->merges_done;
+            for (uint32_t m = 0; m < js; m++) {
+                E->merges[2 * (md + m)] = sa[m];
+                E->merges[2 * (md + m) + 1] = sb[m];
+                E->occ_off[z0 + m] = top + spre[m];
+                E->occ_len[z0 + m] = sR[m];
+            }
+            B->jstar = js;
+            B->applied = 1;
+        }
+        return;
+    }
+    // role B
+    const uint32_t nB = gridDim.x - roleA_blocks, bidB = blockIdx.x - roleA_blocks;
+    const uint32_t Wd = min(DENSE, z0 + k);
+    const uint32_t per = 1 + 4 * Wd;
+    const uint32_t dense_total = k * per;
+    const uint32_t total = dense_total + snl[k * 4];
+    const uint32_t hotT = C->hot_T;
+    const bool hot = E->hot != 0;
+    long long dD = 0;
+    uint32_t nins = 0;
+    for (uint32_t t0 = bidB * blockDim.x; t0 < total; t0 += nB * blockDim.x) {  // uniform per block
+        const uint32_t t = t0 + tid;
+        uint32_t m = BK, cat = 0, x = 0, val = 0;
+        if (t < dense_total) {
+            m = t / per;
+            const uint32_t r = t % per;
+            if (r == 0) {
+                cat = 4;
+                val = sR[m];
+            } else {
+                cat = (r - 1) / Wd;
+                x = (r - 1) % Wd;
+                uint32_t *p0 = E->bvecd + ((uint64_t)(m * BREPL) * 4 + cat) * DENSE + x;
+#pragma unroll
+                for (uint32_t rr = 0; rr < BREPL; rr++) {
+                    uint32_t *pr = p0 + (uint64_t)rr * 4 * DENSE;
+                    const uint32_t c = *pr;
+                    val += c;
+                    if (c) *pr = 0;
+                }
+            }
+        } else if (t < total) {
+            const uint32_t q = t - dense_total;
+            uint32_t mv = 0;
+            while (q >= snl[mv + 1]) mv++;
+            m = mv / 4;
+            cat = mv % 4;
+            const uint64_t base = (uint64_t)mv * E->bvs;
+            x = E->bvlist[base + (q - snl[mv])];
+            val = E->bvec[base + (x - DENSE)];
+            E->bvec[base + (x - DENSE)] = 0;
+        }
+        bool hot_in = false;
+        uint32_t hslot = 0;
+        if (m < js && val != 0) {
+            const uint32_t a = sa[m], b = sb[m], z = z0 + m;
+            uint32_t u, v;
+            long long d;
+            if (cat == 4) { u = a; v = b; d = -(long long)val; }
+            else if (cat == V_DL) { u = x; v = a; d = -(long long)val; }
+            else if (cat == V_DR) { u = b; v = x; d = -(long long)val; }
+            else if (cat == V_IL) { u = x; v = z; d = val; }
+            else { u = z; v = x; d = val; }
+            const uint64_t slot = d > 0 ? hinsert_c(E, u, v, &nins) : hfind(E, u, v);
+            if (slot == ~0ull) {
+                C->err = d > 0 ? 2 : 1;
+            } else {
+                const uint32_t old = atomicAdd(&E->hcnt[slot], (uint32_t)d);
+                const uint32_t nw = old + (uint32_t)d;
+                dD += (long long)(nw != 0) - (long long)(old != 0);
+                hot_in = hot && d > 0 && nw >= hotT && old < hotT;
+                hslot = (uint32_t)slot;
+            }
+        }
+        if (hot) {
+            const uint32_t hp = wave_append(hot_in, &C->hot_n);
+            if (hot_in && hp < HOT_CAP) E->hot_slot[hp] = hslot;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        dD += __shfl_xor(dD, o);
+        nins += __shfl_xor(nins, o);
+    }
+    __shared__ long long sd[16];
+    __shared__ uint32_t si[16];
+    if ((tid & 63) == 0) {
+        sd[tid >> 6] = dD;
+        si[tid >> 6] = nins;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        long long t = 0;
+        unsigned long long ni = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) {
+            t += sd[w];
+            ni += si[w];
+        }
+        if (t != 0) atomicAdd(&B->dD, (unsigned long long)t);
+        if (ni != 0) atomicAdd(&C->nkeys, ni);
+    }
+}
+
+}  // namespace bpeamd

@@ -20,6 +20,7 @@
 
 #include "../../include/bpe_gpu.h"
 #include "kernels.hip"
+#include "batch.hip"
 #include "encode.hip"
 #include "encode_win.hip"
 
@@ -87,8 +88,27 @@ bool PIPE_ON = !getenv("BPE_PIPE") || atoi(getenv("BPE_PIPE")) != 0;  // pipelin
 bool GRAPH_ON = !getenv("BPE_GRAPH") || atoi(getenv("BPE_GRAPH")) != 0;
 // BPE_HOT=0: the level summaries instead of the hot-set argmax (A/B runs)
 bool HOT_ON = !getenv("BPE_HOT") || atoi(getenv("BPE_HOT")) != 0;
-enum : uintptr_t { NOGRAPH_PLAIN = 1, NOGRAPH_TRACKED = 2, NOGRAPH_ENCODE = 3 };
-inline bool real_graph(hipGraphExec_t g) { return (uintptr_t)g > NOGRAPH_ENCODE; }
+// BPE_BATCH=0: one merge per kernel pair (the speculative graph) instead of batches
+bool BATCH_ON = !getenv("BPE_BATCH") || atoi(getenv("BPE_BATCH")) != 0;
+// k_bapply blocks of 1024 threads: role A (spans, lists), role B (table);
+// BPE_BGRID="a,b" overrides them for tuning runs
+uint32_t BAPPLY_A = 64, BAPPLY_B = 192;
+constexpr uint32_t BATCHES_PER_GRAPH = 8;
+// ids >= DENSE of the batch delta vectors: per (member, vector) one slot per
+// id, so runs with a larger vocabulary cap than this stay on one merge per pair
+constexpr uint64_t BATCH_VCAP_MAX = 1ull << 18;
+struct BatchInit {
+    BatchInit() {
+        if (const char *g = getenv("BPE_BGRID")) {
+            unsigned a = 0, b = 0;
+            if (sscanf(g, "%u,%u", &a, &b) == 2 && a >= 1 && b >= 1 && a + b <= 2048) {
+                BAPPLY_A = a; BAPPLY_B = b;
+            }
+        }
+    }
+} batch_init;
+enum : uintptr_t { NOGRAPH_PLAIN = 1, NOGRAPH_TRACKED = 2, NOGRAPH_ENCODE = 3, NOGRAPH_BATCH = 4 };
+inline bool real_graph(hipGraphExec_t g) { return (uintptr_t)g > NOGRAPH_BATCH; }
 struct SpecInit {
     SpecInit() {
         if (const char *e = getenv("BPE_SPEC")) SPEC_ON = atoi(e) != 0;
@@ -243,7 +263,7 @@ struct bpe_gpu_ctx {
     std::vector<std::pair<void *, size_t>> pool;          // released buffers, reused by size
     uint32_t *d_tileoff = nullptr;
     uint32_t *d_enc_pairs = nullptr;
-    hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr;
+    hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr, g_batch = nullptr;
     bool hot_fallback = false;  // the hot set was given up for the level summaries
     uint32_t relists = 0;       // byte-pair list rebuilds of the current run
     std::vector<hipGraphExec_t> retired;  // replaced graphs, destroyed with the run
@@ -316,7 +336,7 @@ void free_train(bpe_gpu_ctx *c, bool release = false) {
         for (auto &q : c->pool) (void)hipFree(q.first);
         c->pool.clear();
     }
-    for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked, &c->g_encode}) {
+    for (hipGraphExec_t *g : {&c->g_plain, &c->g_tracked, &c->g_encode, &c->g_batch}) {
         if (real_graph(*g)) (void)hipGraphExecDestroy(*g);
         *g = nullptr;
     }
@@ -341,6 +361,8 @@ int push_ctl(bpe_gpu_ctx *c) {
     HIPCHK(hipMemcpyAsync(c->dC, c->hC, sizeof(Ctl), hipMemcpyHostToDevice, c->st));
     return 0;
 }
+
+int getenv_int(const char *k, int dflt);
 
 // allocate the per-run structures (sizes depend on the merge cap)
 int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
@@ -420,6 +442,25 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         if ((r = dalloc(c, &h.hotp_v2, SPEC_RB))) return r;
         if ((r = dalloc(c, &h.hotp_k2, SPEC_RB))) return r;
         if ((r = dalloc(c, &h.hotp_tie, SPEC_RB))) return r;
+    }
+    // batched training (batch.hip): the hot set's one-shard runs
+    h.batch = BATCH_ON && h.hot && h.vcap <= BATCH_VCAP_MAX ? 1 : 0;
+    h.bat = nullptr;
+    h.btag = nullptr;
+    h.bvecd = h.bvec = h.bvlist = h.bvnl = nullptr;
+    h.bvs = h.vcap > DENSE ? h.vcap - DENSE : 1;
+    if (h.batch) {
+        if ((r = dalloc(c, &h.bat, 1))) return r;
+        if ((r = dalloc(c, &h.btag, n0, false))) return r;
+        if ((r = dalloc(c, &h.bvecd, (size_t)BK * BREPL * 4 * DENSE))) return r;
+        if ((r = dalloc(c, &h.bvec, (size_t)BK * 4 * h.bvs))) return r;
+        if ((r = dalloc(c, &h.bvlist, (size_t)BK * 4 * h.bvs, false))) return r;
+        if ((r = dalloc(c, &h.bvnl, (size_t)BK * 4))) return r;
+        // BPE_BATCH_DROP_TEST=d: the verification drops members j >= 1 of id
+        // z = 0 mod d (tests drive the drop path with it)
+        const uint32_t dt = (uint32_t)getenv_int("BPE_BATCH_DROP_TEST", 0);
+        if (dt) HIPCHK(hipMemcpyAsync(&h.bat->drop_test, &dt, 4, hipMemcpyHostToDevice, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));  // (dt is on the stack)
     }
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
@@ -577,6 +618,7 @@ int hot_rebuild(bpe_gpu_ctx *c) {
     static const uint32_t fill_max = getenv("BPE_HOT_FILL") ? (uint32_t)atoi(getenv("BPE_HOT_FILL")) : HOT_LIMIT / 2;
     if (fill > fill_max) {
         c->h.hot = 0;
+        c->h.batch = 0;  // (batches select from the hot set)
         int r;
         if ((r = push_desc(c))) return r;
         static const uint32_t one = 1;  // the summaries start with a full rescan
@@ -599,6 +641,13 @@ int hot_rebuild(bpe_gpu_ctx *c) {
 void launch_argmax_inputs(bpe_gpu_ctx *c) {
     launch_summaries(c);
     if (c->h.hot) k_hot_reduce<<<c->h.hot_parts, 1024, 0, c->st>>>(c->dE, c->dC);
+}
+
+// one batch: scan, verify + apply, select the next (batch.hip)
+void launch_batch(bpe_gpu_ctx *c) {
+    k_bscan<<<BSB, SCAN_T, 0, c->st>>>(c->dE, c->dC);
+    k_bapply<<<BAPPLY_A + BAPPLY_B, 1024, 0, c->st>>>(c->dE, c->dC, BAPPLY_A);
+    k_bsel<<<BRB, 1024, 0, c->st>>>(c->dE, c->dC);
 }
 
 void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
@@ -695,11 +744,30 @@ int glaunch(bpe_gpu_ctx *c, hipGraphExec_t g) {
         HIPCHK(hipGraphLaunch(g, c->st));
         return 0;
     }
-    for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++) {
-        if ((uintptr_t)g == NOGRAPH_ENCODE) launch_enc_batch(c);
-        else launch_iteration(c, (uintptr_t)g == NOGRAPH_TRACKED);
+    if ((uintptr_t)g == NOGRAPH_BATCH) {
+        for (uint32_t k = 0; k < BATCHES_PER_GRAPH; k++) launch_batch(c);
+    } else {
+        for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++) {
+            if ((uintptr_t)g == NOGRAPH_ENCODE) launch_enc_batch(c);
+            else launch_iteration(c, (uintptr_t)g == NOGRAPH_TRACKED);
+        }
     }
     HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// the batch graph: BATCHES_PER_GRAPH x (k_bscan, k_bapply, k_bsel)
+int capture_batch(bpe_gpu_ctx *c, hipGraphExec_t *out) {
+    if (!GRAPH_ON) {
+        *out = (hipGraphExec_t)NOGRAPH_BATCH;
+        return 0;
+    }
+    hipGraph_t g;
+    HIPCHK(hipStreamBeginCapture(c->st, hipStreamCaptureModeThreadLocal));
+    for (uint32_t k = 0; k < BATCHES_PER_GRAPH; k++) launch_batch(c);
+    HIPCHK(hipStreamEndCapture(c->st, &g));
+    HIPCHK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+    HIPCHK(hipGraphDestroy(g));
     return 0;
 }
 
@@ -1003,17 +1071,31 @@ int relist(bpe_gpu_ctx *c) {
     return 0;
 }
 
-int replay_pipelined(bpe_gpu_ctx *c, hipGraphExec_t g, uint64_t merges_done) {
+// per_replay: merges one replay commits at least (batch graphs: one per batch)
+// after a host-side stop (or at the start): the next selection, as a batch
+// (k_bsel forms one) or one merge (k_select commits it; the caller scans it)
+int select_next(bpe_gpu_ctx *c, bool tracked) {
+    if (c->h.batch) {
+        k_bsel<<<BRB, 1024, 0, c->st>>>(c->dE, c->dC);
+    } else {
+        launch_argmax_inputs(c);
+        k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
+    }
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int replay_pipelined(bpe_gpu_ctx *c, hipGraphExec_t g, uint64_t merges_done, uint32_t per_replay = ITERS_PER_GRAPH) {
     *c->hprobe = STOP_NONE;  // the stream is idle here (the caller pulled the control block)
     int r;
     if ((r = glaunch(c, g))) return r;
-    uint64_t queued = merges_done + ITERS_PER_GRAPH;  // merges done once the queued replays end (at most)
+    uint64_t queued = merges_done + per_replay;  // merges done once the queued replays end (at least)
     for (int q = 0;; q ^= 1) {
         HIPCHK(hipEventRecord(c->ev_probe[q], c->st));
         const bool ahead = queued < c->h.mcap;
         if (ahead) {
             if ((r = glaunch(c, g))) return r;
-            queued += ITERS_PER_GRAPH;
+            queued += per_replay;
         }
         HIPCHK(hipEventSynchronize(c->ev_probe[q]));
         if (*c->hprobe != STOP_NONE || !ahead) return 0;
@@ -1056,6 +1138,14 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             hipGraphExec_t *g;
             if (encode) {
                 g = &c->g_encode;
+            } else if (c->h.batch) {
+                if (!c->g_batch && (r = capture_batch(c, &c->g_batch))) return r;
+                if (PIPE_ON && !c->profile) {
+                    if ((r = replay_pipelined(c, c->g_batch, C.merges_done, BATCHES_PER_GRAPH))) return r;
+                } else if ((r = glaunch(c, c->g_batch))) {
+                    return r;
+                }
+                break;
             } else {
                 const bool tracked = !c->h.fast && C.n_live < TRACK_LIMIT;
                 g = tracked ? &c->g_tracked : &c->g_plain;
@@ -1087,6 +1177,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             C.stop = STOP_NONE;
             if (c->h.hot) {  // tracked iterations select from the level summaries
                 c->h.hot = 0;
+                c->h.batch = 0;
                 C.full = 1;
                 if ((r = push_desc(c))) return r;
             }
@@ -1102,11 +1193,8 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             if ((r = push_ctl(c))) return r;
             if ((r = grow_table(c, c->h.hcap * 4))) return r;
             if ((r = hot_rebuild(c))) return r;  // (slots moved)
-            const bool tracked = !c->h.fast && C.n_live < TRACK_LIMIT;
-            launch_argmax_inputs(c);
-            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
-            HIPCHK(hipGetLastError());
-            need_scan = true;
+            if ((r = select_next(c, !c->h.fast && C.n_live < TRACK_LIMIT))) return r;
+            need_scan = !c->h.batch;
             break;
         }
         case STOP_RELIST:
@@ -1124,10 +1212,8 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;
             if ((r = hot_rebuild(c))) return r;
-            launch_argmax_inputs(c);
-            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, SEL_PLAIN);
-            HIPCHK(hipGetLastError());
-            need_scan = true;
+            if ((r = select_next(c, false))) return r;
+            need_scan = !c->h.batch;
             break;
         case STOP_EVENT: {
             uint32_t u = 0, v = 0;
@@ -1692,9 +1778,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->hot_fallback = false;
     c->relists = 0;
     if ((r = hot_rebuild(c))) return r;
-    launch_argmax_inputs(c);
-    k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
-    HIPCHK(hipGetLastError());
+    if ((r = select_next(c, tracked))) return r;
     HIPCHK(hipStreamSynchronize(c->st));
     const double t1 = now_ms();
     if ((r = drive(c, false, 0))) return r;
@@ -1722,6 +1806,17 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.hot_scanned = C.hot_scanned;
     c->stats.hot_mode = c->h.hot ? 1 : c->hot_fallback ? 2 : 0;
     c->stats.relists = c->relists;
+    if (c->h.bat) {
+        Bat hb;
+        HIPCHK(hipMemcpy(&hb, c->h.bat, offsetof(Bat, pv), hipMemcpyDeviceToHost));
+        c->stats.batches = hb.nbatch;
+        c->stats.batch_dropped = hb.ndrop;
+        c->stats.batch_retries = hb.nretry;
+        if (getenv("BPE_DEBUG"))
+            fprintf(stderr, "batches %llu, dropped %llu, re-formed %llu; formation ended by: list %llu, cap/count/hot_T %llu, a==b %llu, "
+                    "duplicate %llu, tie %llu, conflict %llu, table margin %llu, staging %llu\n", hb.nbatch, hb.ndrop, hb.nretry,
+                    hb.why[0], hb.why[1], hb.why[2], hb.why[3], hb.why[4], hb.why[5], hb.why[6], hb.why[7]);
+    }
     if (c->h.dbgts) print_timeline(c, C.z);
     if (getenv("BPE_DEBUG"))
         fprintf(stderr, "select phases (ticks/iter): reduce %.1f merge %.1f tail %.1f\n",

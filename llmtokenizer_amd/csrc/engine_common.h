@@ -105,6 +105,34 @@ struct EncBatch {
 };
 
 
+// Batched training (batch.hip): several merges per scan / apply kernel pair.
+// k_bsel lists the top TOPK keys of the hot set in argmax order and takes the
+// longest prefix whose pairs commute (no id is a left id of one member and a
+// right id of another; a == b pairs only alone); k_bscan finds every member's
+// occurrences in the pre-batch tokens; k_bapply applies the prefix of members
+// that are provably the argmax in turn (count above every key the earlier
+// members can create) and drops the rest, which the next selection sees again.
+constexpr uint32_t TOPK = 32;   // sorted list length (partials and the merged list)
+constexpr uint32_t BK = 31;     // members per batch (one list entry stays for the strictness test)
+constexpr uint32_t BRB = 32;    // k_bsel reduce blocks (partial lists)
+constexpr uint32_t BREPL = 2;   // replicas of a member's dense delta accumulators
+constexpr uint32_t BSB = 256;   // k_bscan blocks (1024 threads, one per CU)
+
+struct Bat {
+    uint32_t k, z0, applied, jstar;   // members; id of member 0; an apply ran (the select folds it); applied prefix
+    uint32_t ticket, retry, sumlen, pad0;  // reduce blocks done; > 0: re-form the batch with this many members; candidates
+    unsigned long long dD;            // distinct-pair delta of the applied batch
+    unsigned long long nbatch, ndrop, nretry;  // batches applied; members dropped by the verification; batches re-formed
+    unsigned long long why[8];        // what ended each batch's formation (BPE_DEBUG report)
+    uint32_t drop_test, pad1, pad2, pad3;  // > 0: members j >= 1 with (z0 + j) % drop_test == 0 fail (tests)
+    uint32_t a[BK], b[BK], cnt[BK], mode[BK], off[BK], len[BK];
+    uint32_t blk0[BK + 1];            // k_bscan block range of each member
+    uint32_t sbase[BK + 1];           // member's slice of the occurrence staging area (prefix of len)
+    uint32_t R[BK];                   // occurrences found (k_bscan, atomic)
+    uint32_t bound[BK];               // bound on the count any key made by the member can reach (atomic)
+    unsigned long long pv[BRB * TOPK], pk[BRB * TOPK];  // k_bsel partial lists: packed value, key
+};
+
 // Device-resident descriptor: every kernel takes a pointer to it, so tables can
 // be regrown without re-capturing the iteration graph.
 struct Eng {
@@ -181,6 +209,15 @@ struct Eng {
     uint32_t *hot_hist;   // [HOT_BINS] rebuild scratch (zero between rebuilds)
     unsigned long long *hotp_best, *hotp_key, *hotp_v2, *hotp_k2;  // [hot_parts] partial top-2
     uint32_t *hotp_tie;
+    // batched training (batch.hip; occurrence positions staged in ids_out)
+    uint32_t batch;       // 1: the batch kernels drive the run
+    uint32_t bvs;         // ids >= DENSE per (member, vector) in bvec / bvlist
+    Bat *bat;
+    uint16_t *btag;       // [n0] neighbour tags of the staged occurrences
+    uint32_t *bvecd;      // [BK][BREPL][4][DENSE] members' dense delta accumulators
+    uint32_t *bvec;       // [BK][4][bvs] ids >= DENSE (x - DENSE), listed on first touch in bvlist
+    uint32_t *bvlist;     // [BK][4][bvs]
+    uint32_t *bvnl;       // [BK][4] list lengths
 };
 
 // Control block.  Everything up to Dp is owned by k_select, which stages it in

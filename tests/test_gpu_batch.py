@@ -1,0 +1,141 @@
+"""Batched training (csrc/batch.hip): several merges per scan / apply pair.
+
+Every untracked one-shard run goes through the batch kernels (BPE_GPU_FAST on
+any corpus, or >= 2^21 tokens).  The batch must commit exactly the merges the
+reference's one-merge-per-pass loop commits (bpe/src/bpe.c:669-783), in the
+same order, with the same final ids: checked against the oracle's RULE order
+on corpora that stress each rule of the batch -- small alphabets (members
+sharing left or right ids, adjacent occurrences of different members, a == b
+runs that must stay alone), text-shaped and uniform corpora (long batches),
+and caps that end a run inside a batch.  The tests also require that batches
+of more than one merge actually ran and that the verification dropped members
+somewhere (new pairs overtaking later members)."""
+import os
+import random
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from llmtokenizer_amd import api
+from llmtokenizer_amd.synth import synth_bytes
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _train(data, mm):
+    e = api.Engine(0)
+    e.load(data)
+    e.train(mm, fast=True)
+    m, ids, st = e.merges(), e.ids(), e.stats()
+    e.close()
+    return m, ids, st
+
+
+def _check(data, mm):
+    m, ids, st = _train(data, mm)
+    om, oi, _ = O.train(data, mm, O.RULE)
+    assert m.shape == om.shape and (m == om).all(), (len(data), mm, "merges differ", m.shape, om.shape)
+    assert ids.size == oi.size and (ids == oi).all(), (len(data), mm, "ids differ")
+    return st
+
+
+def _small_cases():
+    rng = random.Random(777)
+    out = []
+    for _ in range(40):
+        alpha = rng.choice([b"ab", b"abc", b"aab", b"abcd", b"a b", bytes(range(97, 105)), bytes(range(32, 127)),
+                            b"aaab", b"xyxyz"])
+        n = rng.randint(100, 30000)
+        out.append((bytes(rng.choice(alpha) for _ in range(n)), rng.choice([-1, 40, 300, 1000])))
+    # repeated patterns: adjacent occurrences of different members in every batch
+    out.append((b"abcdabcdabcd" * 1000, -1))
+    out.append((b"xyzzyx" * 2000 + b"q" * 3001, 500))
+    out.append((b"a" * 5001 + b"ab" * 2000, 200))
+    return out
+
+
+def test_batches_match_oracle_small_alphabets():
+    batches = merges = dropped = 0
+    for data, mm in _small_cases():
+        st = _check(data, mm)
+        batches += st["batches"]
+        merges += st["merges"]
+        dropped += st["batch_dropped"]
+    assert batches > 0 and merges > batches, (batches, merges)  # some batches held several merges
+
+
+def test_dropped_members_match_oracle():
+    """BPE_BATCH_DROP_TEST=3: the verification drops every member after the
+    first whose id is 0 mod 3 (and everything after it) -- scanned occurrence
+    lists and delta vectors that are never applied must leave no trace"""
+    os.environ["BPE_BATCH_DROP_TEST"] = "3"
+    try:
+        dropped = 0
+        cases = _small_cases()[::3] + [(synth_bytes(505, 200000), 600)]
+        for data, mm in cases:
+            dropped += _check(data, mm)["batch_dropped"]
+    finally:
+        del os.environ["BPE_BATCH_DROP_TEST"]
+    assert dropped > 0
+
+
+@pytest.mark.parametrize("seed,n,mm", [(501, 1 << 20, 500), (502, 300000, 2000), (503, 60000, -1)])
+def test_batches_match_oracle_uniform(seed, n, mm):
+    data = synth_bytes(seed, n)
+    st = _check(data, mm)
+    assert st["batches"] > 0 and st["merges"] >= 2 * st["batches"], st
+
+
+def test_batches_match_oracle_text():
+    words = [b"the", b"of", b"and", b"to", b"in", b"is", b"that", b"for", b"it", b"as", b"was", b"with", b"be",
+             b"by", b"on", b"not", b"he", b"this", b"are", b"or", b"his", b"from", b"at", b"which", b"but"]
+    rng = random.Random(5)
+    data = b" ".join(rng.choice(words) for _ in range(40000))
+    st = _check(data, 1500)
+    assert st["batches"] > 0
+
+
+def test_cap_inside_a_batch():
+    """a merge cap that ends the run in the middle of a batch"""
+    data = synth_bytes(504, 256 << 10)
+    full = _check(data, 300)
+    for cap in (1, 2, 3, 7, 97, 301):
+        m, ids, st = _train(data, cap)
+        om, oi, _ = O.train(data, cap, O.RULE)
+        assert (m == om).all() and (ids == oi).all(), cap
+    assert full["merges"] == 300
+
+
+WORKER = r"""
+import sys
+sys.path.insert(0, %r)
+from llmtokenizer_amd import api
+from llmtokenizer_amd.synth import synth_bytes
+e = api.Engine(0)
+e.synth(int(sys.argv[1]), int(sys.argv[2]))
+e.train(int(sys.argv[3]))
+st = e.stats()
+print(e.ids_checksum(), e.merges().tobytes().hex()[:64], st["batches"], st["merges"])
+import hashlib
+print(hashlib.md5(e.merges().tobytes()).hexdigest())
+""" % ROOT
+
+
+def test_batch_equals_one_merge_engine_64m():
+    """64 MiB x 1500 merges: the batch engine == the one-merge speculative engine
+    (BPE_BATCH=0), merges and ids, bit for bit"""
+    outs = []
+    for flag in ("1", "0"):
+        env = dict(os.environ, BPE_BATCH=flag)
+        p = subprocess.run([sys.executable, "-c", WORKER, "77", str(64 << 20), "1500"], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-2000:]
+        lines = p.stdout.split("\n")
+        cs, _, nb, nm = lines[0].split()
+        outs.append((cs, lines[1], int(nb), int(nm)))
+    assert outs[0][0] == outs[1][0] and outs[0][1] == outs[1][1], outs
+    assert outs[0][2] > 0 and outs[1][2] == 0 and outs[0][3] == 1500, outs
