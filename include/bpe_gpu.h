@@ -38,7 +38,8 @@ enum {
     BPE_GPU_ENOMEM = -3,   /* device allocation failed                      */
     BPE_GPU_ENODEV = -4,   /* no GPU / device index out of range            */
     BPE_GPU_ESTATE = -5,   /* call out of order (e.g. train before load)    */
-    BPE_GPU_ERANGE = -6,   /* corpus larger than 2^32-2 bytes per device    */
+    BPE_GPU_ERANGE = -6,   /* corpus larger than 2^32-2 bytes per device, or a
+                              token longer than 2^31-3 bytes (its end code)   */
     BPE_GPU_EDATA = -7,    /* unknown token id (decode) / corrupt merge list */
     BPE_GPU_EINTERNAL = -8,/* engine invariant violated (reported, not hidden) */
     BPE_GPU_EIO = -9       /* file read error (errno is set)                */

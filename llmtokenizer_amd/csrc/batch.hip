@@ -41,6 +41,15 @@ namespace bpeamd {
 static_assert(TOPK == 32, "wave merges hold two 32-entry lists");
 static_assert(BRB == 2 * (1024 / 64), "the select's 16 waves merge two partial lists each");
 static_assert(BK < 32, "member masks are 32-bit");
+constexpr uint32_t SU = 4;  // candidates (k_bscan) / occurrences (rewrite) per thread per round
+
+// debug timeline of a batch (BPE_DEBUG_TS; E->dbgts rows indexed by batch)
+enum { BT_SCAN_IN = 0, BT_SCAN_CAND, BT_SCAN_OUT, BT_APPLY_IN, BT_APPLY_PRO, BT_APPLY_A, BT_APPLY_B, BT_SEL_IN,
+       BT_SEL_RED, BT_SEL_LIST, BT_SEL_OUT, BT_N };
+static_assert(BT_N <= TS_N, "batch stamps fit a timeline row");
+__device__ inline uint32_t bat_idx(const Eng *E) {
+    return E->dbgts ? (uint32_t)(E->bat->nbatch + E->bat->nretry) : 0u;
+}
 
 // ------------------------------------------------------------ sorted lists
 struct KV {
@@ -130,7 +139,8 @@ struct alignas(16) BatHead {  // the words of Bat up to the partial lists
     uint32_t w[BAT_HEAD_WORDS];
 };
 
-__device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, Bat *__restrict__ Bg, uint32_t nhot) {
+__device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, Bat *__restrict__ Bg, uint32_t nhot,
+                              uint32_t bi) {
     __shared__ Ctl sc;
     __shared__ BatHead sbh;
     __shared__ KV part[16][TOPK];
@@ -162,6 +172,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
     if (tid == 0) clear_k = nmem = 0;
     __syncthreads();
     block_list_tree(part, blockDim.x >> 6);
+    ts_mark(E, bi, BT_SEL_LIST, false);
     Bat *B = reinterpret_cast<Bat *>(&sbh);  // (head fields only)
     // Wave 0 decides, one list entry per lane; every lane reads the staged
     // words itself (no lane waits on another's LDS store); lane 0 writes the
@@ -175,6 +186,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         // (read before the lanes overwrite the member fields)
         const uint32_t olda = jst ? B->a[jst - 1] : 0, oldb = jst ? B->b[jst - 1] : 0, oldz0 = B->z0;
         const uint32_t oldsum = B->sumlen;
+        const uint32_t raerr = aload(&Bg->ra_err);  // a token too long for an end code (rewrite blocks)
         unsigned long long rs = lane < jst ? B->R[lane] : 0ull;
         for (int o = 32; o > 0; o >>= 1) rs += __shfl_xor(rs, o);
         const unsigned long long D = C->D + (applied ? B->dD : 0ull);
@@ -193,18 +205,25 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         const uint64_t Bn = bfinal_nominal(D, &edge);
         const uint64_t Bsz = edge ? 2 * Bn : Bn;
         const uint32_t hotT = C->hot_T;
+        // byte-pair lists gone stale (opt-in, BPE_RELIST): the host rebuilds them
+        bool relist_due = false;
+        if (E->relist_stale) {
+            const uint32_t cs = (uint32_t)(C->counters[4] + (applied ? oldsum : 0u)) - C->relist_c0;
+            const uint32_t os = (uint32_t)(C->counters[5] + rs) - C->relist_o0;
+            relist_due = cs > os && cs - os >= E->relist_stale;
+        }
         uint32_t stop = STOP_NONE;
-        if (C->err) stop = STOP_ERROR;
+        if (C->err || raerr) stop = STOP_ERROR;
         else if (!E->fast && n_live < TRACK_LIMIT) stop = STOP_MODE;
         else if (md >= E->mcap) stop = STOP_CAP;
         else if ((cnt0 < hotT && hotT > 2) || C->hot_n > HOT_LIMIT) stop = STOP_HOT;
+        else if (relist_due) stop = STOP_RELIST;
         else if (v0 == 0 || cnt0 <= 1) stop = STOP_DONE;
         else if (C->nkeys + 4ull * (256ull + md + 2) >= E->hcap / 2) stop = STOP_GROW;
         // ---- the batch: the longest prefix of the list whose entries qualify
         uint32_t k = 0;
         if (stop == STOP_NONE) {
             const uint32_t u = (uint32_t)(e.k >> 32), v = (uint32_t)e.k, c = (uint32_t)(e.v >> 32);
-            const uint32_t u0 = (uint32_t)(k0 >> 32), w0 = (uint32_t)k0;
             // ties with the next key keep their pre-batch order when the members
             // before it cannot move B_final: a member adds or zeroes at most
             // 2 min(ids, count) + 1 keys (its neighbours' pairs and its own)
@@ -221,7 +240,6 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             else if (lane > 0) {
                 if (e.k == kprev) why = 3;  // the same key listed twice (the one-merge engine's undo): end here
                 else if (md + lane >= E->mcap || c <= 1 || (hotT > 2 && c < hotT)) why = 1;
-                else if (u == v || u0 == w0) why = 2;  // a == b pairs alone
                 else if (!stable && ((lane + 1 >= nl && truncated) || !(c > (lane + 1 < nl ? cnext : 0u)))) why = 4;
                 else if (C->nkeys + 4ull * (256ull + md + lane + 2) * (lane + 1) >= E->hcap / 2) why = 6;
             }
@@ -321,6 +339,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             C->edge = edge;
             C->ties = ties;
             C->stop = stop;
+            if (raerr && !C->err) C->err = raerr;
             B->ticket = 0;
             B->k = k;
             B->z0 = 256 + md;
@@ -336,13 +355,105 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         __hip_atomic_store(E->hprobe, sc.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
+    ts_mark(E, bi, BT_SEL_OUT, false, true);
 }
 
 // Reduce (every block: its share of the hot set, sorted) + select (the last
 // block to finish).  Grid BRB x 1024.
+// Role A of the batch k_bapply applied last (blocks [BRB, grid)): its
+// members' spans in tok[], their occurrence lists copied into the pool.
+// Nothing the selection reads depends on it; the next k_bscan does.
+__device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat *__restrict__ B) {
+    __shared__ uint32_t sz[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], ablk[BK + 1];
+    __shared__ uint32_t sk, stop_, am, last;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t nA = gridDim.x - BRB, bid = blockIdx.x - BRB;
+    if (tid < 64) {
+        const uint32_t k = aload(&B->ra_k);
+        const bool in = lane < k;
+        const uint32_t R = in ? B->ra_R[lane] : 0u;
+        const uint32_t tot = k ? B->ra_pre[k] : 0u;
+        // blocks in proportion to the occurrences (>= 1 per member)
+        const uint32_t nb = in ? 1 + (uint32_t)(tot ? (uint64_t)(nA - k) * R / tot : 0) : 0;
+        uint32_t nbp = nb;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(nbp, o);
+            if ((int)lane >= o) nbp += y;
+        }
+        if (in) {
+            sz[lane] = B->ra_z[lane];
+            sla[lane] = B->ra_la[lane];
+            slb[lane] = B->ra_lb[lane];
+            sR[lane] = R;
+            ssb[lane] = B->ra_sbase[lane];
+            spre[lane] = B->ra_pre[lane];
+            ablk[lane] = nbp - nb;
+        }
+        if (lane == 0) {
+            sk = k;
+            stop_ = B->ra_top;
+            ablk[k] = nA;
+            am = BK;
+        }
+    }
+    __syncthreads();
+    const uint32_t k = sk;
+    if (k == 0) return;  // nothing pending (block-uniform)
+    if (tid < k && bid >= ablk[tid] && bid < ablk[tid + 1]) am = tid;
+    __syncthreads();
+    const uint32_t m = am;
+    if (m < k) {
+        uint32_t *tok = E->tok;
+        const uint64_t n = E->n0;
+        const uint32_t z = sz[m], la = sla[m], lb = slb[m], Rm = sR[m], base = ssb[m], obase = stop_ + spre[m];
+        const uint32_t bidm = bid - ablk[m], nbm = ablk[m + 1] - ablk[m];
+        for (uint32_t e0 = bidm * blockDim.x * SU; e0 < Rm; e0 += nbm * blockDim.x * SU) {
+            uint32_t pos[SU];
+            uint16_t tg[SU];
+#pragma unroll
+            for (uint32_t u = 0; u < SU; u++) {
+                const uint32_t e = e0 + u * blockDim.x + tid;
+                pos[u] = e < Rm ? E->ids_out[base + e] : 0u;
+                tg[u] = e < Rm ? E->btag[base + e] : (uint16_t)0;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < SU; u++) {
+                const uint32_t e = e0 + u * blockDim.x + tid;
+                if (e >= Rm) continue;
+                const uint64_t i = pos[u], j = i + la, kq = j + lb;
+                tok[i] = z;
+                if (kq - 1 - i > E->end_max) B->ra_err = 5;  // (the select's staged control block would drop C->err)
+                if (kq - 1 == j) {
+                    tok[j] = end_code(kq - 1 - i);
+                } else {
+                    tok[j] = HOLE;
+                    if (kq - 1 < n) tok[kq - 1] = end_code(kq - 1 - i);
+                }
+                E->occ[obase + e] = (uint32_t)i;
+                E->occnb[obase + e] = tg[u];
+            }
+        }
+    }
+    // the last block to finish marks the rewrite done (a k_bsel launched again
+    // after a stop has nothing to redo)
+    __syncthreads();
+    if (tid == 0) last = atomicAdd(&B->ra_done, 1u) == nA - 1;
+    __syncthreads();
+    if (last && tid == 0) {
+        B->ra_k = 0;
+        B->ra_done = 0;
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_bsel(const Eng *__restrict__ E, Ctl *__restrict__ C) {
-    if (C->stop) return;
     Bat *B = E->bat;
+    if (blockIdx.x >= BRB) {  // (whether or not this selection stops)
+        bat_rewrite(E, C, B);
+        return;
+    }
+    if (C->stop) return;
+    const uint32_t bi = bat_idx(E);
+    ts_mark(E, bi, BT_SEL_IN, true);
     const uint64_t Bsz = summary_B(C->D + B->dD);  // D after the batch applied last
     const uint32_t n = min(C->hot_n, HOT_CAP);
     __shared__ KV top[TOPK];
@@ -355,17 +466,18 @@ __global__ __launch_bounds__(1024) void k_bsel(const Eng *__restrict__ E, Ctl *_
     // publish: stores drained, release, ticket; the last block acquires
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    ts_mark(E, bi, BT_SEL_RED, false);
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t t = __hip_atomic_fetch_add(&B->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == gridDim.x - 1;
+        last = t == BRB - 1;
         if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     if (!last) return;
-    bselect_block(E, C, B, n);
+    bselect_block(E, C, B, n, bi);
 }
 
 // ----------------------------------------------------------------- k_bscan
@@ -411,13 +523,54 @@ __device__ inline void vadd_b(uint32_t (*s)[DENSE], const Eng *E, uint32_t m, in
     if (v == V_DL || v == V_DR) atomicAdd(&gcnt[v], 1u);
 }
 
+// The member whose occurrence covers the token p starting at ps (p is that
+// member's b and the token before it its a), or BK.  For an a == b member the
+// run of p ending at ps decides: greedy pairing from the run's first token
+// (bpe.c:760-772) makes p the second token of a pair iff the run is even.
+__device__ inline uint32_t cover_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const uint32_t *sa,
+                                    const uint32_t *sb, uint32_t p, int64_t ps) {
+    uint32_t lmk, rmk;
+    rt.get(p, &lmk, &rmk);
+    if (!rmk) return BK;
+    const int64_t pps = v_left<false>(tok, ps);
+    const uint32_t pp = pps < 0 ? HOLE : tok[pps];
+    for (uint32_t q = rmk; q; q &= q - 1) {
+        const uint32_t mm = __ffs(q) - 1;
+        if (sa[mm] != pp) continue;
+        if (sa[mm] != sb[mm]) return mm;
+        uint32_t L = 2;  // p and pp; then the rest of the run leftwards
+        for (int64_t x = v_left<false>(tok, pps); x >= 0 && tok[x] == p; x = v_left<false>(tok, x)) L++;
+        return (L & 1) ? BK : mm;
+    }
+    return BK;
+}
+
+// The member whose occurrence starts at the token q at kq (q is its a and the
+// token after it its b: for a != b always an occurrence; for a == b q starts
+// a run -- the token before it is an occurrence's b -- so it pairs), or BK.
+__device__ inline uint32_t starts_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const uint32_t *sb,
+                                     const uint32_t *sla, uint32_t q, int64_t kq, int64_t n) {
+    uint32_t lmk, rmk;
+    rt.get(q, &lmk, &rmk);
+    if (!lmk) return BK;
+    const int64_t kn = v_right(kq, sla[__ffs(lmk) - 1], n);
+    const uint32_t qq = kn < n ? tok[kn] : HOLE;
+    for (uint32_t t = lmk; t; t &= t - 1) {
+        const uint32_t mm = __ffs(t) - 1;
+        if (sb[mm] == qq) return mm;
+    }
+    return BK;
+}
+
 __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, const Ctl *__restrict__ C) {
     if (C->stop) return;
     Bat *B = E->bat;
+    const uint32_t bi = bat_idx(E);
+    ts_mark(E, bi, BT_SCAN_IN, true);
     __shared__ uint32_t s[4][DENSE];
-    __shared__ uint32_t list[SCAN_T];
-    __shared__ uint16_t ltag[SCAN_T];
-    __shared__ uint32_t lcount, gbase, bR, covc, sm, sk, sz0;
+    __shared__ uint32_t list[SCAN_T * SU];  // this round's occurrences (position, tag), flushed per round
+    __shared__ uint16_t ltag[SCAN_T * SU];
+    __shared__ uint32_t lcount, gbase, list_n, covc, sm, sk, sz0;
     __shared__ uint32_t gcnt[2];
     __shared__ uint32_t sa[BK], sb[BK], sla[BK];
     __shared__ RoleTab rt;
@@ -425,7 +578,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     const uint32_t tid = threadIdx.x;
     if (tid == 0) {
         sm = BK;
-        lcount = bR = covc = 0;
+        covc = lcount = 0;
         gcnt[0] = gcnt[1] = 0;
         sk = B->k;
         sz0 = B->z0;
@@ -467,119 +620,202 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     __syncthreads();
     auto tok_at = [&](int64_t p) -> uint32_t { return (p < 0 || p >= n) ? HOLE : tok[p]; };
 
-    for (uint32_t e0 = bid * SCAN_T; e0 < len; e0 += nblk * SCAN_T) {
-        const uint32_t e = e0 + tid;
-        bool ok = false;
-        int64_t i = 0, j = 0;
-        uint32_t tl = HOLE, tr = HOLE;
-        if (e < len) {
-            if (mode == 2) {
-                j = E->occ[off + e];
+    if (a != b) {
+        // SU candidates per thread per round, in stages, so that their chains of
+        // dependent gathers overlap; the round's occurrences are staged in LDS
+        // and leave with one global atomic per block
+        for (uint32_t e0 = bid * SCAN_T * SU; e0 < len; e0 += nblk * SCAN_T * SU) {  // uniform trip count
+            uint32_t ent[SU];
+            uint16_t etg[SU];
+            bool val[SU];
+#pragma unroll
+            for (uint32_t u = 0; u < SU; u++) {
+                const uint32_t e = e0 + u * SCAN_T + tid;
+                val[u] = e < len;
+                ent[u] = 0;
+                etg[u] = 0xFFFFu;
+                if (val[u]) {
+                    ent[u] = mode == 0 ? E->plist[off + e] : E->occ[off + e];
+                    if (mode) etg[u] = E->occnb[off + e];
+                }
+            }
+            int64_t ii[SU], jj[SU];
+            TokWin W[SU];
+#pragma unroll
+            for (uint32_t u = 0; u < SU; u++) {
+                if (mode == 2) {
+                    val[u] = val[u] && tag_ok(etg[u] >> 8, want);
+                    jj[u] = ent[u];
+                    ii[u] = 0;
+                    if (val[u]) W[u] = tok_window(tok, jj[u]);
+                } else {
+                    val[u] = val[u] && (mode == 0 || tag_ok(etg[u] & 0xFFu, want));
+                    ii[u] = ent[u];
+                    jj[u] = ii[u] + la;
+                    if (val[u]) W[u] = tok_window(tok, ii[u]);
+                }
+            }
+            bool ok[SU];
+            uint32_t tl[SU], tr[SU];
+#pragma unroll
+            for (uint32_t u = 0; u < SU; u++) {
+                ok[u] = false;
+                tl[u] = tr[u] = HOLE;
+                if (!val[u]) continue;
+                const int64_t j = jj[u];
+                if (mode == 2) {
+                    // the b at j (its list), the a left of it from the end slot j-1
+                    const uint32_t wl = j > 0 ? W[u].at(j - 1) : HOLE;
+                    const int64_t i = j > 0 ? start_of_end<false>(wl, j - 1) : -1;
+                    ii[u] = i;
+                    if (W[u].at(j) != b || i < 0) continue;
+                    const uint32_t ti = W[u].has(i) ? W[u].at(i) : tok[i];
+                    tl[u] = i > 0 ? (W[u].has(i - 1) ? W[u].at(i - 1) : tok[i - 1]) : HOLE;
+                    const int64_t kk = j + lb;
+                    tr[u] = kk < n ? (W[u].has(kk) ? W[u].at(kk) : tok[kk]) : HOLE;
+                    ok[u] = ti == a;
+                } else {
+                    const int64_t i = ii[u], kk = j + lb;
+                    const uint32_t t1 = j >= n ? HOLE : W[u].has(j) ? W[u].at(j) : tok[j];
+                    tl[u] = i > 0 ? W[u].at(i - 1) : HOLE;
+                    tr[u] = kk >= n ? HOLE : W[u].has(kk) ? W[u].at(kk) : tok[kk];
+                    ok[u] = W[u].at(i) == a && t1 == b && j < n;
+                }
+            }
+            // left neighbours: the id at the start of the left token
+            int64_t ps[SU];
+            uint32_t pv[SU];
+#pragma unroll
+            for (uint32_t u = 0; u < SU; u++) {
+                const int64_t i = ii[u];
+                ps[u] = i <= 0 ? -1 : start_of_end<false>(tl[u], i - 1);
+                pv[u] = (ok[u] && i > 0) ? (is_id(tl[u]) ? tl[u] : tok[ps[u]]) : HOLE;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < SU; u++) {
+                const int64_t i = ii[u], j = jj[u];
+                uint32_t lfin = HOLE, rfin = HOLE;
+                if (ok[u]) {
+                    // left neighbour: covered when it is the b of an occurrence of
+                    // a member (that occurrence owns the pair between the two)
+                    const uint32_t p = pv[u];
+                    lfin = p;
+                    if (p != HOLE) {
+                        const uint32_t cv = cover_of(tok, rt, sa, sb, p, ps[u]);
+                        if (cv < BK) {
+                            lfin = z0 + cv;
+                            atomicAdd(&covc, 1u);
+                        } else {
+                            vadd_b(s, E, m, V_DL, p, gcnt);
+                            vadd_b(s, E, m, V_IL, p, gcnt);
+                        }
+                    }
+                    // right neighbour: the a of a member's occurrence -> that id
+                    const int64_t kq = v_right(j, lb, n);
+                    const uint32_t q = kq < n ? tr[u] : HOLE;
+                    rfin = q;
+                    if (q != HOLE) {
+                        const uint32_t st = starts_of(tok, rt, sb, sla, q, kq, n);
+                        if (st < BK) rfin = z0 + st;
+                        vadd_b(s, E, m, V_DR, q, gcnt);
+                        vadd_b(s, E, m, V_IR, rfin, gcnt);
+                    }
+                }
+                const uint32_t slot = wave_append(ok[u], &lcount);
+                if (ok[u]) {
+                    list[slot] = (uint32_t)i;
+                    ltag[slot] = nb_tag(lfin, rfin);
+                }
+            }
+            // flush the round's list: one global atomic per block
+            __syncthreads();
+            if (tid == 0) {
+                const uint32_t c = lcount;
+                gbase = c ? atomicAdd(Rm, c) : 0u;
+                lcount = 0;
+                list_n = c;
+            }
+            __syncthreads();
+            for (uint32_t q = tid; q < list_n; q += SCAN_T) {
+                occz[gbase + q] = list[q];
+                tagz[gbase + q] = ltag[q];
+            }
+            __syncthreads();
+        }
+    } else {
+        // a == b (a batch of its own): the thread holding a run's first token
+        // walks it, pairing tokens 0-1, 2-3, ... (greedy left-to-right)
+        for (uint32_t e0 = bid * SCAN_T; e0 < len; e0 += nblk * SCAN_T) {  // uniform trip count
+            const uint32_t e = e0 + tid;
+            int64_t i = 0;
+            bool ok = false;
+            if (e >= len) {
+            } else if (mode == 2) {
+                const int64_t j = E->occ[off + e];
                 if (tag_ok(E->occnb[off + e] >> 8, want) && tok[j] == b) {
                     i = v_left<false>(tok, j);
                     ok = i >= 0 && tok[i] == a;
-                    if (ok) {
-                        tl = i > 0 ? tok[i - 1] : HOLE;
-                        tr = j + lb < n ? tok[j + lb] : HOLE;
-                    }
                 }
             } else {
                 i = (mode == 0) ? E->plist[off + e] : E->occ[off + e];
-                if (mode == 0 || tag_ok(E->occnb[off + e] & 0xFFu, want)) {
-                    j = i + la;
-                    const TokWin W = tok_window(tok, i);
-                    const int64_t kk = j + lb;
-                    const uint32_t t0 = W.at(i);
-                    const uint32_t t1 = j >= n ? HOLE : W.has(j) ? W.at(j) : tok[j];
-                    tl = i > 0 ? W.at(i - 1) : HOLE;
-                    tr = kk >= n ? HOLE : W.has(kk) ? W.at(kk) : tok[kk];
-                    ok = t0 == a && t1 == b && j < n;
-                }
+                ok = (mode == 0 || tag_ok(E->occnb[off + e] & 0xFFu, want)) && tok[i] == a && i + la < n &&
+                     tok[i + la] == b;
             }
-        }
-        if (a != b) {
-            const uint32_t slot = wave_append(ok, &lcount);
-            if (ok) {
-                list[slot] = (uint32_t)i;
-                // left neighbour: covered when it is the b of an occurrence of
-                // a member (that occurrence owns the pair between the two)
-                const int64_t ps = i == 0 ? -1 : start_of_end<false>(tl, i - 1);
-                const uint32_t p = (i > 0 && is_id(tl)) ? tl : tok_at(ps);
-                uint32_t lfin = p;
-                if (p != HOLE) {
-                    uint32_t lmk, rmk;
-                    rt.get(p, &lmk, &rmk);
-                    bool cov = false;
-                    if (rmk) {
-                        const uint32_t pp = tok_at(v_left<false>(tok, ps));
-                        for (uint32_t q = rmk; q; q &= q - 1) {
-                            const uint32_t mm = __ffs(q) - 1;
-                            if (sa[mm] == pp) {
-                                cov = true;
-                                lfin = z0 + mm;
-                            }
-                        }
-                    }
-                    if (cov) {
-                        atomicAdd(&covc, 1u);
-                    } else {
-                        vadd_b(s, E, m, V_DL, p, gcnt);
-                        vadd_b(s, E, m, V_IL, p, gcnt);
-                    }
-                }
-                // right neighbour: the a of a member's occurrence -> that id
-                const int64_t kq = v_right(j, lb, n);
-                const uint32_t q = kq < n ? tr : HOLE;
-                uint32_t rfin = q;
-                if (q != HOLE) {
-                    uint32_t lmk, rmk;
-                    rt.get(q, &lmk, &rmk);
-                    if (lmk) {
-                        const uint32_t qq = tok_at(v_right(kq, sla[__ffs(lmk) - 1], n));
-                        for (uint32_t t = lmk; t; t &= t - 1) {
-                            const uint32_t mm = __ffs(t) - 1;
-                            if (sb[mm] == qq) rfin = z0 + mm;
-                        }
-                    }
-                    vadd_b(s, E, m, V_DR, q, gcnt);
-                    vadd_b(s, E, m, V_IR, rfin, gcnt);
-                }
-                ltag[slot] = nb_tag(lfin, rfin);
-            }
-        } else if (ok) {
-            // a == b (a batch of its own): the thread holding a run's first
-            // token walks it, pairing tokens 0-1, 2-3, ... (greedy left-to-right)
-            const int64_t ps = v_left<false>(tok, i);
-            const uint32_t p = tok_at(ps);
-            bool start = true, left = p != HOLE;
+            const int64_t ps = ok ? v_left<false>(tok, i) : -1;
+            const uint32_t p = ok ? tok_at(ps) : HOLE;
+            // the run's left neighbour, unless another member's occurrence covers it
+            const uint32_t cv = (ok && p != HOLE && p != a) ? cover_of(tok, rt, sa, sb, p, ps) : BK;
+            if (cv < BK) atomicAdd(&covc, 1u);
+            const bool left = p != HOLE && cv == BK;
             int64_t pos = i;
-            if (p == a) {
-                start = false;
-                left = false;
-            }
-            for (uint32_t mi = 0; start; mi++) {
-                const int64_t jj = pos + la;
-                if (jj >= n || tok[jj] != a) break;
-                const int64_t kq = v_right(jj, la, n);
+            for (uint32_t mi = 0; ok && p != a; mi++) {  // (p == a: not the run's first token)
+                const int64_t jq = pos + la;
+                if (jq >= n || tok[jq] != a) break;
+                const int64_t kq = v_right(jq, la, n);
                 const uint32_t q = tok_at(kq);
                 const bool knext = q == a;
                 const bool nocc = knext && tok_at(v_right(kq, la, n)) == a;
-                const uint32_t pfin = mi > 0 ? z : (left ? p : (p == HOLE ? HOLE : z));
-                stage_one(list, ltag, &lcount, Rm, occz, tagz, (uint32_t)pos, nb_tag(pfin, nocc ? z : q), &bR);
+                // a right neighbour that starts another member's occurrence becomes its id
+                const uint32_t st = (!knext && q != HOLE) ? starts_of(tok, rt, sb, sla, q, kq, n) : BK;
+                const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
+                const uint32_t pfin = mi > 0 ? z : (left ? p : cv < BK ? z0 + cv : HOLE);
+                const uint32_t slot = atomicAdd(&lcount, 1u);
+                if (slot < SCAN_T * SU) {
+                    list[slot] = (uint32_t)pos;
+                    ltag[slot] = nb_tag(pfin, rq);
+                } else {  // (a long run overflows the round's list: straight out)
+                    const uint32_t g = atomicAdd(Rm, 1u);
+                    occz[g] = (uint32_t)pos;
+                    tagz[g] = nb_tag(pfin, rq);
+                }
                 if (mi == 0 && left) {
                     vadd_b(s, E, m, V_DL, p, gcnt);
                     vadd_b(s, E, m, V_IL, p, gcnt);
                 }
                 if (q != HOLE) {
                     vadd_b(s, E, m, V_DR, q, gcnt);
-                    vadd_b(s, E, m, V_IR, nocc ? z : q, gcnt);
+                    vadd_b(s, E, m, V_IR, rq, gcnt);
                 }
                 if (!knext || kq >= n) break;
                 pos = kq;
             }
+            __syncthreads();
+            if (tid == 0) {
+                const uint32_t c = min(lcount, SCAN_T * SU);
+                gbase = c ? atomicAdd(Rm, c) : 0u;
+                lcount = 0;
+                list_n = c;
+            }
+            __syncthreads();
+            for (uint32_t q = tid; q < list_n; q += SCAN_T) {
+                occz[gbase + q] = list[q];
+                tagz[gbase + q] = ltag[q];
+            }
+            __syncthreads();
         }
-        flush_list(list, ltag, &lcount, &gbase, Rm, occz, tagz, &bR);
     }
+    __syncthreads();
+    ts_mark(E, bi, BT_SCAN_CAND, false, true);
     // deltas into replica (block % BREPL) of the member's accumulators, and the
     // member's new-key bound: per block max over ids (+ covered left
     // neighbours, + every add that bypassed LDS), summed over blocks
@@ -611,6 +847,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
             atomicAdd(&B->bound[m], max(l + gcnt[V_DL] + covc, r + gcnt[V_DR]));
         }
     }
+    ts_mark(E, bi, BT_SCAN_OUT, false, true);
 }
 
 // ---------------------------------------------------------------- k_bapply
@@ -637,102 +874,100 @@ __device__ inline uint64_t hinsert_c(const Eng *E, uint32_t u, uint32_t v, uint3
 // several members or vectors takes each contribution separately, and since
 // within a batch old keys only fall and new keys only rise, D and the hot set
 // follow from each atomic's old value).
-__global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl *__restrict__ C,
-                                                 uint32_t roleA_blocks) {
+__global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (C->stop) return;
     Bat *B = E->bat;
+    const uint32_t bi = bat_idx(E);
+    ts_mark(E, bi, BT_APPLY_IN, true);
     __shared__ uint32_t sa[BK], sb[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], snl[BK * 4 + 1];
     __shared__ uint32_t sk, sj, sz0;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t k = B->k;
-    if (tid < k) {
-        const uint32_t ma = B->a[tid], mb = B->b[tid];
-        sa[tid] = ma;
-        sb[tid] = mb;
-        sla[tid] = E->tlen[ma];
-        slb[tid] = E->tlen[mb];
-        sR[tid] = B->R[tid];
-        ssb[tid] = B->sbase[tid];
-    }
-    __shared__ uint32_t scnt[BK], sbnd[BK];
-    __shared__ unsigned long long slive;
-    __shared__ uint32_t sdt;
-    if (tid < k) {
-        scnt[tid] = B->cnt[tid];
-        sbnd[tid] = B->bound[tid];
-    }
-    if (tid < k * 4) snl[tid + 1] = E->bvnl[tid];
-    if (tid == 0) {
-        sk = k;
-        sz0 = B->z0;
-        slive = C->n_live;
-        sdt = B->drop_test;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        // the verified prefix: member j is the argmax after members < j when
-        // its count beats every key they can create, and the run is still
-        // untracked when it would be selected
-        uint32_t js = k ? 1 : 0, pm = 0;
-        unsigned long long live = slive - (k ? sR[0] : 0);
-        for (uint32_t q = 1; q < k; q++) {
-            pm = max(pm, sbnd[q - 1]);
-            if (!(pm < scnt[q])) break;
-            if (sdt && (sz0 + q) % sdt == 0) break;  // (tests: forced failures)
-            if (!E->fast && live < TRACK_LIMIT) break;
-            live -= sR[q];
-            js = q + 1;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    // prologue, wave 0, lane q = member q: the verified prefix, prefix sums of
+    // the occurrences and of the listed-id counts, role A's blocks per member
+    if (tid < 64) {
+        const uint32_t k = B->k, z0 = B->z0, dt = B->drop_test;
+        const unsigned long long live0 = C->n_live;
+        const bool in = lane < k;
+        const uint32_t ma = in ? B->a[lane] : 0, mb = in ? B->b[lane] : 0;
+        const uint32_t R = in ? B->R[lane] : 0, cnt = in ? B->cnt[lane] : 0, bnd = in ? B->bound[lane] : 0;
+        const uint32_t sbase = in ? B->sbase[lane] : 0;
+        const uint32_t nl0 = 2 * lane < 4 * k ? E->bvnl[2 * lane] : 0, nl1 = 2 * lane + 1 < 4 * k ? E->bvnl[2 * lane + 1] : 0;
+        const uint32_t tla = in ? E->tlen[ma] : 0, tlb = in ? E->tlen[mb] : 0;
+        // exclusive prefix sum of R and max of bound over the members before me
+        unsigned long long rpre = R;
+        uint32_t bpre = bnd, lpre = nl0 + nl1;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long y = __shfl_up(rpre, o);
+            const uint32_t yb = __shfl_up(bpre, o), yl = __shfl_up(lpre, o);
+            if ((int)lane >= o) {
+                rpre += y;
+                bpre = max(bpre, yb);
+                lpre += yl;
+            }
         }
+        const unsigned long long rex = rpre - R;                            // occurrences of the members before me
+        const uint32_t pm = __shfl_up(bpre, 1);                              // max bound of the members before me
+        // member q is the argmax after the members before it: its count beats
+        // every key they can create, and the run is still untracked then
+        const bool fail = in && lane > 0 &&
+                          (!(pm < cnt) || (dt && (z0 + lane) % dt == 0) || (!E->fast && live0 - rex < TRACK_LIMIT));
+        const unsigned long long fm = __ballot(fail);
+        uint32_t js = fm ? (uint32_t)__ffsll(fm) - 1 : k;
         if (js < k) {  // re-form the batch with the verified prefix; apply nothing
-            B->retry = js;
+            if (lane == 0) B->retry = js;
             js = 0;
         }
-        sj = js;
-        spre[0] = 0;
-        for (uint32_t q = 0; q < k; q++) spre[q + 1] = spre[q] + sR[q];
-        snl[0] = 0;
-        for (uint32_t q = 0; q < k * 4; q++) snl[q + 1] += snl[q];
+        const uint32_t rall = (uint32_t)__shfl(rpre, (int)(k ? k - 1 : 0));
+        if (in) {
+            sa[lane] = ma;
+            sb[lane] = mb;
+            sla[lane] = tla;
+            slb[lane] = tlb;
+            sR[lane] = R;
+            ssb[lane] = sbase;
+            spre[lane] = (uint32_t)rex;
+        }
+        if (2 * lane < 4 * k) snl[2 * lane + 1] = lpre - nl1;
+        if (2 * lane + 1 < 4 * k) snl[2 * lane + 2] = lpre;
+        if (lane == 0) {
+            snl[0] = 0;
+            spre[k] = k ? rall : 0u;
+            sk = k;
+            sj = js;
+            sz0 = z0;
+        }
     }
     __syncthreads();
-    const uint32_t js = sj, z0 = sz0;
-    if (blockIdx.x < roleA_blocks) {
-        uint32_t *tok = E->tok;
-        const uint64_t n = E->n0;
+    ts_mark(E, bi, BT_APPLY_PRO, false);
+    ts_mark(E, bi, BT_APPLY_A, false);  // (role A runs in k_bsel)
+    const uint32_t k = sk, js = sj, z0 = sz0;
+    if (blockIdx.x == 0) {
+        // bookkeeping and the role-A descriptor for k_bsel's rewrite blocks
         const uint32_t top = C->occ_top;
-        const uint32_t tot = spre[js];
-        for (uint32_t e = blockIdx.x * blockDim.x + tid; e < tot; e += roleA_blocks * blockDim.x) {
-            uint32_t m = 0;
-            while (e >= spre[m + 1]) m++;
-            const uint32_t loc = ssb[m] + (e - spre[m]);
-            const uint64_t i = E->ids_out[loc];
-            const uint16_t tg = E->btag[loc];
-            const uint64_t j = i + sla[m], kq = j + slb[m];
-            tok[i] = z0 + m;
-            if (kq - 1 - i > END_MAX) C->err = 5;
-            if (kq - 1 == j) {
-                tok[j] = end_code(kq - 1 - i);
-            } else {
-                tok[j] = HOLE;
-                if (kq - 1 < n) tok[kq - 1] = end_code(kq - 1 - i);
-            }
-            E->occ[top + e] = (uint32_t)i;
-            E->occnb[top + e] = tg;
-        }
-        if (blockIdx.x == 0 && tid == 0) {
+        if (tid < js) {
             const uint32_t md = C->merges_done;
-            for (uint32_t m = 0; m < js; m++) {
-                E->merges[2 * (md + m)] = sa[m];
-                E->merges[2 * (md + m) + 1] = sb[m];
-                E->occ_off[z0 + m] = top + spre[m];
-                E->occ_len[z0 + m] = sR[m];
-            }
+            E->merges[2 * (md + tid)] = sa[tid];
+            E->merges[2 * (md + tid) + 1] = sb[tid];
+            E->occ_off[z0 + tid] = top + spre[tid];
+            E->occ_len[z0 + tid] = sR[tid];
+            B->ra_z[tid] = z0 + tid;
+            B->ra_la[tid] = sla[tid];
+            B->ra_lb[tid] = slb[tid];
+            B->ra_R[tid] = sR[tid];
+            B->ra_sbase[tid] = ssb[tid];
+            B->ra_pre[tid] = spre[tid];
+        }
+        if (tid == 0) {
+            B->ra_pre[js] = spre[js];
+            B->ra_top = top;
+            B->ra_done = 0;
+            B->ra_k = js;
             B->jstar = js;
             B->applied = 1;
         }
-        return;
     }
     // role B
-    const uint32_t nB = gridDim.x - roleA_blocks, bidB = blockIdx.x - roleA_blocks;
+    const uint32_t nB = gridDim.x, bidB = blockIdx.x;
     const uint32_t Wd = min(DENSE, z0 + k);
     const uint32_t per = 1 + 4 * Wd;
     const uint32_t dense_total = k * per;
@@ -821,6 +1056,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         if (t != 0) atomicAdd(&B->dD, (unsigned long long)t);
         if (ni != 0) atomicAdd(&C->nkeys, ni);
     }
+    ts_mark(E, bi, BT_APPLY_B, false, true);
 }
 
 }  // namespace bpeamd

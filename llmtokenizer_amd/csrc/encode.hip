@@ -199,6 +199,10 @@ constexpr uint32_t ESCAN_T = 1024;
 template <bool SH>
 __global__ __launch_bounds__(ESCAN_T) void k_scan_batch(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (C->stop) return;
+    if (C->err) {  // the last apply wrote a token an end code cannot hold
+        if (blockIdx.x == 0 && threadIdx.x == 0) C->stop = STOP_ERROR;
+        return;
+    }
     EncBatch *B = E->eb + C->ebp;
     const uint32_t nb = batch_size<SH>(E, B);
     if (nb == 0) {  // merge list exhausted
@@ -387,6 +391,9 @@ __global__ __launch_bounds__(256) void k_apply_batch(const Eng *__restrict__ E, 
         const uint64_t j = i + sla[m], k = j + slb[m];
         tok[i] = sz[m];
         if (!SH || j < n) {  // else: b starts in a later shard, which retires it
+            // an end code holds at most end_max: longer tokens (runs of one
+            // byte merged past 2 GiB) stop the replay with an error
+            if (k - 1 - i > E->end_max) C->err = 5;
             if (k - 1 == j) {
                 tok[j] = end_code(k - 1 - i);
             } else {

@@ -88,11 +88,10 @@ bool PIPE_ON = !getenv("BPE_PIPE") || atoi(getenv("BPE_PIPE")) != 0;  // pipelin
 bool GRAPH_ON = !getenv("BPE_GRAPH") || atoi(getenv("BPE_GRAPH")) != 0;
 // BPE_HOT=0: the level summaries instead of the hot-set argmax (A/B runs)
 bool HOT_ON = !getenv("BPE_HOT") || atoi(getenv("BPE_HOT")) != 0;
-// BPE_BATCH=0: one merge per kernel pair (the speculative graph) instead of batches
-bool BATCH_ON = !getenv("BPE_BATCH") || atoi(getenv("BPE_BATCH")) != 0;
-// k_bapply blocks of 1024 threads: role A (spans, lists), role B (table);
-// BPE_BGRID="a,b" overrides them for tuning runs
-uint32_t BAPPLY_A = 64, BAPPLY_B = 192;
+// k_bapply blocks (the table updates) and k_bsel's extra blocks (the applied
+// batch's token rewrite, beside the selection), 1024 threads each;
+// BPE_BGRID="a,b" overrides them (a: rewrite blocks, b: table blocks) for tuning runs
+uint32_t BAPPLY_A = 224, BAPPLY_B = 256;
 constexpr uint32_t BATCHES_PER_GRAPH = 8;
 // ids >= DENSE of the batch delta vectors: per (member, vector) one slot per
 // id, so runs with a larger vocabulary cap than this stay on one merge per pair
@@ -101,7 +100,7 @@ struct BatchInit {
     BatchInit() {
         if (const char *g = getenv("BPE_BGRID")) {
             unsigned a = 0, b = 0;
-            if (sscanf(g, "%u,%u", &a, &b) == 2 && a >= 1 && b >= 1 && a + b <= 2048) {
+            if (sscanf(g, "%u,%u", &a, &b) == 2 && a >= BK && b >= 1 && a + b <= 2048) {  // (>= 1 role-A block per member)
                 BAPPLY_A = a; BAPPLY_B = b;
             }
         }
@@ -394,6 +393,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.ids_out = h.occ + occ_n;
     if ((r = dalloc(c, &h.occnb, occ_n, false))) return r;
     h.xfused = c->sharded && c->xfused && !encode;
+    h.end_max = END_MAX;
+    if (const char *t = getenv("BPE_END_MAX")) h.end_max = std::min<uint64_t>(END_MAX, std::max(1ll, atoll(t)));
     h.xtimeout = c->xtimeout;
     h.xstride = (uint32_t)(((4ull * h.vcap + 2) + 63) & ~63ull);
     if (c->sharded) {
@@ -444,7 +445,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         if ((r = dalloc(c, &h.hotp_tie, SPEC_RB))) return r;
     }
     // batched training (batch.hip): the hot set's one-shard runs
-    h.batch = BATCH_ON && h.hot && h.vcap <= BATCH_VCAP_MAX ? 1 : 0;
+    // (BPE_BATCH=0: one merge per kernel pair, the speculative graph; read per run)
+    h.batch = getenv_int("BPE_BATCH", 1) && h.hot && h.vcap <= BATCH_VCAP_MAX ? 1 : 0;
     h.bat = nullptr;
     h.btag = nullptr;
     h.bvecd = h.bvec = h.bvlist = h.bvnl = nullptr;
@@ -646,8 +648,8 @@ void launch_argmax_inputs(bpe_gpu_ctx *c) {
 // one batch: scan, verify + apply, select the next (batch.hip)
 void launch_batch(bpe_gpu_ctx *c) {
     k_bscan<<<BSB, SCAN_T, 0, c->st>>>(c->dE, c->dC);
-    k_bapply<<<BAPPLY_A + BAPPLY_B, 1024, 0, c->st>>>(c->dE, c->dC, BAPPLY_A);
-    k_bsel<<<BRB, 1024, 0, c->st>>>(c->dE, c->dC);
+    k_bapply<<<BAPPLY_B, 1024, 0, c->st>>>(c->dE, c->dC);
+    k_bsel<<<BRB + BAPPLY_A, 1024, 0, c->st>>>(c->dE, c->dC);
 }
 
 void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
@@ -1076,7 +1078,7 @@ int relist(bpe_gpu_ctx *c) {
 // (k_bsel forms one) or one merge (k_select commits it; the caller scans it)
 int select_next(bpe_gpu_ctx *c, bool tracked) {
     if (c->h.batch) {
-        k_bsel<<<BRB, 1024, 0, c->st>>>(c->dE, c->dC);
+        k_bsel<<<BRB + BAPPLY_A, 1024, 0, c->st>>>(c->dE, c->dC);
     } else {
         launch_argmax_inputs(c);
         k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
@@ -1167,7 +1169,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             return 0;
         case STOP_ERROR:
             return fail(C.err == 5 ? BPE_GPU_ERANGE : BPE_GPU_EINTERNAL,
-                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than 2^31 - 3 bytes" : "thread-stat table full");
+                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than an end code holds (2^31 - 3 bytes)" : "thread-stat table full");
         case STOP_REDO:  // missed prediction: k_select committed the real merge
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;
@@ -1203,10 +1205,8 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             C.relist_o0 = (uint32_t)C.counters[5];
             if ((r = push_ctl(c))) return r;
             if ((r = relist(c))) return r;
-            launch_argmax_inputs(c);
-            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, SEL_PLAIN);
-            HIPCHK(hipGetLastError());
-            need_scan = true;
+            if ((r = select_next(c, false))) return r;
+            need_scan = !c->h.batch;
             break;
         case STOP_HOT:
             C.stop = STOP_NONE;
@@ -1266,6 +1266,41 @@ void print_timeline(bpe_gpu_ctx *c, uint32_t zlast) {
     fprintf(stderr, "block timeline over %u merges (us from K1's first block entry):", n);
     for (int k = 1; k < TS_N; k++) fprintf(stderr, " %s %.2f;", nm[k], sum[k] / n);
     fprintf(stderr, " K2 end -> next K1 in %.2f\n", ng ? gap / ng : 0.0);
+}
+
+// BPE_DEBUG_TS, batch engine: average per-batch timeline (us from k_bscan's
+// first block entry), over batches with every stamp present
+void print_batch_timeline(bpe_gpu_ctx *c, uint64_t nb) {
+    std::vector<unsigned long long> t((size_t)TS_SLOTS * TS_N);
+    if (hipMemcpy(t.data(), c->h.dbgts, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    int ikhz = 0;
+    (void)hipDeviceGetAttribute(&ikhz, hipDeviceAttributeWallClockRate, c->dev);
+    const double khz = ikhz > 0 ? ikhz : 100000.0;
+    static const char *nm[BT_N] = {"scan in", "scan cands done", "scan out", "apply in", "apply prologue",
+                                   "role A out", "role B out", "sel in", "reduce published", "list merged", "sel out"};
+    double sum[BT_N] = {}, gap = 0;
+    uint32_t n = 0, ng = 0;
+    for (uint64_t b = 1; b + 1 < nb && b < TS_SLOTS; b++) {
+        const unsigned long long *r = &t[(size_t)b * TS_N];
+        bool ok = true;
+        for (int k = 0; k < BT_N; k++) ok = ok && r[k] != 0;
+        if (!ok) continue;
+        const double t0 = (double)~r[BT_SCAN_IN];
+        for (int k = 0; k < BT_N; k++) {
+            const bool in = k == BT_SCAN_IN || k == BT_APPLY_IN || k == BT_SEL_IN;
+            sum[k] += ((in ? (double)~r[k] : (double)r[k]) - t0) * 1000.0 / khz;
+        }
+        n++;
+        const unsigned long long *q = &t[(size_t)(b + 1) * TS_N];
+        if (q[BT_SCAN_IN]) {
+            gap += ((double)~q[BT_SCAN_IN] - (double)r[BT_SEL_OUT]) * 1000.0 / khz;
+            ng++;
+        }
+    }
+    if (!n) return;
+    fprintf(stderr, "batch timeline over %u batches (us from k_bscan's first block entry):", n);
+    for (int k = 1; k < BT_N; k++) fprintf(stderr, " %s %.2f;", nm[k], sum[k] / n);
+    fprintf(stderr, " sel out -> next scan in %.2f\n", ng ? gap / ng : 0.0);
 }
 
 int compact_ids(bpe_gpu_ctx *c) {
@@ -1651,7 +1686,7 @@ const char *bpe_gpu_strerror(int code) {
     case BPE_GPU_ENOMEM: return "device out of memory";
     case BPE_GPU_ENODEV: return "no such GPU";
     case BPE_GPU_ESTATE: return "call out of order";
-    case BPE_GPU_ERANGE: return "corpus too large for one device (max 2^32-2 bytes)";
+    case BPE_GPU_ERANGE: return "out of range (corpus > 2^32-2 bytes per device, or a token > 2^31-3 bytes)";
     case BPE_GPU_EDATA: return "unknown token id or corrupt merge list";
     case BPE_GPU_EINTERNAL: return "engine invariant violated";
     case BPE_GPU_EIO: return "file read error (errno is set)";
@@ -1812,6 +1847,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
         c->stats.batches = hb.nbatch;
         c->stats.batch_dropped = hb.ndrop;
         c->stats.batch_retries = hb.nretry;
+        if (c->h.dbgts) print_batch_timeline(c, hb.nbatch + hb.nretry);
         if (getenv("BPE_DEBUG"))
             fprintf(stderr, "batches %llu, dropped %llu, re-formed %llu; formation ended by: list %llu, cap/count/hot_T %llu, a==b %llu, "
                     "duplicate %llu, tie %llu, conflict %llu, table margin %llu, staging %llu\n", hb.nbatch, hb.ndrop, hb.nretry,
@@ -2000,7 +2036,12 @@ int bpe_gpu_load_fd(bpe_gpu_ctx *c, int fd, size_t size, size_t *n_loaded) {
     if (!c || fd < 0 || !n_loaded) return BPE_GPU_EINVAL;
     HIPCHK(hipSetDevice(c->dev));
     int r;
-    if ((r = alloc_bytes(c, size))) return r;
+    // the corpus is at most 2^32 - 2 bytes (u32 positions); a longer file is
+    // fine when a NUL ends the text before that, so the limit is only checked
+    // once it is reached
+    constexpr size_t LIMIT = 0xFFFFFFFEull;
+    const size_t want_total = std::min(size, LIMIT);
+    if ((r = alloc_bytes(c, want_total))) return r;
     constexpr size_t CH = 64u << 20;
     for (int k = 0; k < 2; k++) {
         if (!c->stage[k]) HIPCHK(hipHostMalloc((void **)&c->stage[k], CH, hipHostMallocDefault));
@@ -2008,10 +2049,10 @@ int bpe_gpu_load_fd(bpe_gpu_ctx *c, int fd, size_t size, size_t *n_loaded) {
     }
     size_t off = 0;
     bool done = false;
-    for (uint64_t k = 0; off < size && !done; k++) {
+    for (uint64_t k = 0; off < want_total && !done; k++) {
         uint8_t *buf = c->stage[k & 1];
         if (k >= 2) HIPCHK(hipEventSynchronize(c->stage_ev[k & 1]));  // its previous copy is done
-        const size_t want = std::min(CH, size - off);
+        const size_t want = std::min(CH, want_total - off);
         size_t got = 0;
         while (got < want) {
             const ssize_t q = pread(fd, buf + got, want - got, (off_t)(off + got));
@@ -2039,6 +2080,18 @@ int bpe_gpu_load_fd(bpe_gpu_ctx *c, int fd, size_t size, size_t *n_loaded) {
         off += got;
     }
     HIPCHK(hipStreamSynchronize(c->st));
+    if (!done && off == LIMIT && size > LIMIT) {
+        // the text goes on past the limit unless the next byte ends it
+        uint8_t nx = 0;
+        ssize_t q;
+        do {
+            q = pread(fd, &nx, 1, (off_t)LIMIT);
+        } while (q < 0 && errno == EINTR);
+        if (q == 1 && nx != 0) {
+            c->n0 = 0;
+            return fail(BPE_GPU_ERANGE, "corpus > 2^32-2 bytes before its first NUL");
+        }
+    }
     c->n0 = off;
     *n_loaded = off;
     return 0;

@@ -131,6 +131,10 @@ struct Bat {
     uint32_t R[BK];                   // occurrences found (k_bscan, atomic)
     uint32_t bound[BK];               // bound on the count any key made by the member can reach (atomic)
     unsigned long long pv[BRB * TOPK], pk[BRB * TOPK];  // k_bsel partial lists: packed value, key
+    // the applied batch's token rewrite (role A), done by k_bsel's extra blocks
+    // beside the selection; written by k_bapply (the select never touches it)
+    uint32_t ra_k, ra_top, ra_done, ra_err;  // members (0: nothing pending), pool offset, blocks finished, error
+    uint32_t ra_z[BK], ra_la[BK], ra_lb[BK], ra_R[BK], ra_sbase[BK], ra_pre[BK + 1];
 };
 
 // Device-resident descriptor: every kernel takes a pointer to it, so tables can
@@ -218,6 +222,9 @@ struct Eng {
     uint32_t *bvec;       // [BK][4][bvs] ids >= DENSE (x - DENSE), listed on first touch in bvlist
     uint32_t *bvlist;     // [BK][4][bvs]
     uint32_t *bvnl;       // [BK][4] list lengths
+    // longest token span (end distance) an end code may hold: END_MAX, or less
+    // for tests (BPE_END_MAX) that drive the over-long-token error paths
+    uint64_t end_max;
 };
 
 // Control block.  Everything up to Dp is owned by k_select, which stages it in

@@ -677,7 +677,7 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
             }
             tok[i] = z;
             if (j < n) {  // else: b starts in a later shard, which retires it
-                if (k - 1 - i > END_MAX) C->err = 5;  // (a token longer than an end code holds)
+                if (k - 1 - i > E->end_max) C->err = 5;  // (a token longer than an end code holds)
                 if (k - 1 == j) {
                     tok[j] = end_code(k - 1 - i);
                 } else {

@@ -363,6 +363,7 @@ int drive_group(bpe_gpu_group *g) {
         case STOP_ENC_END:
             return 0;
         case STOP_ERROR:
+            if (C0.err == 5) return fail(BPE_GPU_ERANGE, "a token longer than an end code holds (2^31 - 3 bytes)");
             return fail(BPE_GPU_EINTERNAL, (C0.err & P2P_ERR_BIT) ? "p2p exchange timed out (a peer rank stopped or diverged)"
                                            : C0.err == 1 ? "engine invariant violated (count decrement of an absent pair)"
                                                          : "pair table full");

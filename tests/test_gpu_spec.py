@@ -30,7 +30,8 @@ def _cases():
     return out
 
 
-def test_speculation_hits_and_misses_match_oracle():
+def test_speculation_hits_and_misses_match_oracle(monkeypatch):
+    monkeypatch.setenv("BPE_BATCH", "0")  # the one-merge engine (batches replace it by default)
     hits = misses = 0
     for data, mm in _cases():
         e = api.Engine(0)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel averages of rocprofv3 --pmc counter collections (any counters),
 optionally over the dispatches from index --from on (per kernel).
-usage: pmc_latency.py [--from K] <counter_collection.csv>..."""
+usage: pmc_latency.py [--from K] [--kernels k_a,k_b] <counter_collection.csv>..."""
 import csv
 import re
 import sys
@@ -11,8 +11,12 @@ from collections import defaultdict
 def main():
     args = sys.argv[1:]
     k0 = 0
-    if args and args[0] == "--from":
-        k0 = int(args[1])
+    kern = ("k_rescan_spec", "k_fused")
+    while args and args[0] in ("--from", "--kernels"):
+        if args[0] == "--from":
+            k0 = int(args[1])
+        else:
+            kern = tuple(args[1].split(","))
         args = args[2:]
     vals = defaultdict(lambda: defaultdict(list))
     for path in args:
@@ -21,7 +25,7 @@ def main():
                 name = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0].replace("bpeamd::", "").replace("void ", "")).strip()
                 vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for name, cs in sorted(vals.items()):
-        if not name.startswith("k_rescan_spec") and not name.startswith("k_fused"):
+        if not name.startswith(kern):
             continue
         parts = []
         for c, v in sorted(cs.items()):
