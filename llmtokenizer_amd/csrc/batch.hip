@@ -41,7 +41,14 @@ namespace bpeamd {
 static_assert(TOPK == 32, "wave merges hold two 32-entry lists");
 static_assert(BRB == 2 * (1024 / 64), "the select's 16 waves merge two partial lists each");
 static_assert(BK < 32, "member masks are 32-bit");
-constexpr uint32_t SU = 4;  // candidates (k_bscan) / occurrences (rewrite) per thread per round
+#ifndef BPE_SU
+#define BPE_SU 1
+#endif
+#ifndef BPE_RU
+#define BPE_RU 4
+#endif
+constexpr uint32_t SU = BPE_SU;  // k_bscan candidates per thread per round (1: measured fastest, 85 vs 91 ms at 4)
+constexpr uint32_t RU = BPE_RU;  // rewrite occurrences per thread per round
 
 // debug timeline of a batch (BPE_DEBUG_TS; E->dbgts rows indexed by batch)
 enum { BT_SCAN_IN = 0, BT_SCAN_CAND, BT_SCAN_OUT, BT_APPLY_IN, BT_APPLY_PRO, BT_APPLY_A, BT_APPLY_B, BT_SEL_IN,
@@ -407,17 +414,17 @@ __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat 
         const uint64_t n = E->n0;
         const uint32_t z = sz[m], la = sla[m], lb = slb[m], Rm = sR[m], base = ssb[m], obase = stop_ + spre[m];
         const uint32_t bidm = bid - ablk[m], nbm = ablk[m + 1] - ablk[m];
-        for (uint32_t e0 = bidm * blockDim.x * SU; e0 < Rm; e0 += nbm * blockDim.x * SU) {
-            uint32_t pos[SU];
-            uint16_t tg[SU];
+        for (uint32_t e0 = bidm * blockDim.x * RU; e0 < Rm; e0 += nbm * blockDim.x * RU) {
+            uint32_t pos[RU];
+            uint16_t tg[RU];
 #pragma unroll
-            for (uint32_t u = 0; u < SU; u++) {
+            for (uint32_t u = 0; u < RU; u++) {
                 const uint32_t e = e0 + u * blockDim.x + tid;
                 pos[u] = e < Rm ? E->ids_out[base + e] : 0u;
                 tg[u] = e < Rm ? E->btag[base + e] : (uint16_t)0;
             }
 #pragma unroll
-            for (uint32_t u = 0; u < SU; u++) {
+            for (uint32_t u = 0; u < RU; u++) {
                 const uint32_t e = e0 + u * blockDim.x + tid;
                 if (e >= Rm) continue;
                 const uint64_t i = pos[u], j = i + la, kq = j + lb;
