@@ -22,12 +22,13 @@ final ids compacted in HBM.  `--steps K` jobs are timed back to back after
 value = corpus_MB * merges * K / wall  (MB = 1e6 bytes; whole job, max over ranks)
 
 The line also carries
-  roofline        the dominant per-merge kernel (k_rescan_spec): algorithmic
-                  bytes per launch (8 B/candidate + 20 B/occurrence + 12 B per
-                  dirty summary slot) and its average span from the
-                  device wall clock, both over the LAST timed job; the committed
-                  rocprofv3 summary and PMC traffic of this same command
-                  (profiles/r2_*) beside them;
+  roofline        the dominant kernel of the merge loop, the batch scan
+                  k_bscan (several merges per scan / apply pair):
+                  algorithmic bytes per launch (8 B/candidate + 20 B/occurrence)
+                  and its average span from the device wall clock, both over
+                  the LAST timed job; the committed rocprofv3 summary and PMC
+                  traffic of this same command (profiles/r3_*) beside them;
+  roofline_apply  the batch apply k_bapply (table updates, 16 B each), same way;
   roofline_count_pass  the corpus-wide pair-count pass, priced at SURVEY 8(d)
                   widths (1 B/token read + 2 B/token id write while V <= 65536);
   correctness     merges md5 + position-keyed ids checksum (bpe_gpu_ids_checksum)
@@ -54,7 +55,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 GIB = 1 << 30
-PROFILE_TAG = "r2"     # profiles/<tag>_train_kernel_stats.csv, <tag>_pmc_traffic.json (tools/gpu_profile.sh)
+PROFILE_TAG = "r3"     # profiles/<tag>_train_kernel_stats.csv, <tag>_pmc_traffic.json (tools/gpu_profile.sh)
 
 
 def cpu_baseline(seed, size, merges):
@@ -84,9 +85,9 @@ def cpu_baseline(seed, size, merges):
             dt = time.time() - t0
             kind, cores = "port", 1
     return {"value": round(size / 1e6 * merges / dt, 3), "unit": "corpus MB/s per merge iter",
-            "cores": cores, "kind": kind,
+            "cores": cores, "kind": kind, "s_per_merge": round(dt / merges, 4),
             "sample": f"{size / 2**20:.0f} MiB prefix of the seed-{seed} corpus, {merges} merges, "
-                      f"{dt:.1f} s wall (reference hard-codes 16 pthreads; host nproc={os.cpu_count()})"}
+                      f"{dt:.1f} s wall incl. load (reference hard-codes 16 pthreads; host nproc={os.cpu_count()})"}
 
 
 def cpu_encode_baseline(merges, seed, size):
@@ -242,6 +243,11 @@ def train_single(args, cx, out):
             extra["config1"]["equals_reference_golden"] = bool(hashlib.md5(gm.tobytes()).hexdigest() ==
                                                                extra["config1"]["merges_md5"])
         c1.close()
+        if not args.no_cpu_baseline:
+            # the reference on configs[1] itself (64 of the 1024 merges) and
+            # on the 1 GiB corpus (4 merges: its per-iteration cost), same host
+            extra["config1"]["cpu_baseline"] = cpu_baseline(1, 1 << 20, 64)
+            extra["cpu_baseline_1g"] = cpu_baseline(args.seed, GIB, 4)
     e.close()
     return el, merges, st, prof, got, extra
 
@@ -452,10 +458,12 @@ def main():
         "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "bytes_per_launch": round(kbytes), "avg_ms": round(kms, 5), "launches": launches,
-                     "window": "the last timed job (bytes and span from the same merges)",
+                     "window": "the last timed job (bytes and span from the same launches)",
                      "avg_ms_source": "device wall clock (first block entry to the last block's retired "
                                       "memory operations) inside the timed run",
-                     "note": "per-merge kernel: dependent random gathers, latency-bound"},
+                     "note": ("batch scan: one random token-window gather per candidate (8 B algorithmic, a "
+                              "128-B line moved), bound by the random-line rate" if name == "k_bscan" else
+                              "per-merge kernel: dependent random gathers, latency-bound")},
         "roofline_count_pass": {"kernel": "k_pair_hist_span" if st["count_pass_span"] else "k_pair_hist",
                                 "bound": "hbm", "achieved": round(cp_achieved, 1), "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": round(cp_achieved / HBM_PEAK_GBS, 4),
@@ -465,8 +473,10 @@ def main():
         "breakdown_ms": {"init": round(st["ms_init"], 3), "loop": round(st["ms_train"], 3),
                          "total_engine": round(st["ms_total"], 3), "per_merge_us": round(st["ms_train"] * 1e3 / merges, 2)},
         "engine": {k2: st[k2] for k2 in ("n_out", "iterations", "distinct_pairs", "merged_buckets",
-                                          "rule_ties", "table_grows", "keys", "l1_rescanned", "spec_hits",
-                                          "spec_misses", "candidates", "occurrences", "hot_rebuilds", "hot_mode", "hot_scanned")},
+                                          "rule_ties", "table_grows", "keys", "candidates", "occurrences",
+                                          "hot_rebuilds", "hot_mode", "hot_scanned", "relists", "batches",
+                                          "batch_dropped", "batch_retries", "table_updates", "spec_hits",
+                                          "spec_misses")},
     })
     out.update(extra)
     cp = committed_profile(name)
@@ -475,19 +485,18 @@ def main():
         out["roofline"]["traffic"] = cp["traffic"]
     if "avg_ms_rocprof" in cp:
         out["roofline"]["frac_at_rocprof_avg"] = round(kbytes / (cp["avg_ms_rocprof"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-    # the other per-merge kernel (apply + select; the larger share of the loop's
-    # kernel time once the scan's deltas stay in LDS): rocprof average and PMC
-    # traffic from the same committed profile, priced at 12 B per occurrence
-    fz = committed_profile("k_fused")
-    if "avg_ms_rocprof" in fz and merges:
-        fb = 12.0 * st["occurrences"] / merges
-        fa = fb / (fz["avg_ms_rocprof"] * 1e-3) / 1e9
-        out["roofline_k_fused"] = {"kernel": "k_fused", "bound": "hbm", "achieved": round(fa, 1), "peak": HBM_PEAK_GBS,
-                                   "unit": "GB/s", "frac": round(fa / HBM_PEAK_GBS, 4), "traffic": fz.get("traffic"),
-                                   "bytes_per_launch": round(fb), "avg_ms_rocprof": fz["avg_ms_rocprof"],
-                                   "rocprof_summary": fz.get("rocprof_summary"),
-                                   "note": "12 B x occurrences per merge (the span rewrite); dependent table "
-                                           "updates, latency-bound"}
+    # the batch apply (the pair-table updates): 16 B per update (the key probed,
+    # the count read and written), span from the device wall clock like the scan
+    nl = st["batches"] + st["batch_retries"]
+    if nl and st["ms_apply_span"] > 0:
+        ab = 16.0 * st["table_updates"] / nl
+        aa = ab / (st["ms_apply_span"] * 1e-3) / 1e9
+        ap = committed_profile("k_bapply")
+        out["roofline_apply"] = {"kernel": "k_bapply", "bound": "hbm", "achieved": round(aa, 1), "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": round(aa / HBM_PEAK_GBS, 4), "traffic": ap.get("traffic"),
+                                 "bytes_per_launch": round(ab), "avg_ms": round(st["ms_apply_span"], 5), "launches": nl,
+                                 "avg_ms_rocprof": ap.get("avg_ms_rocprof"), "rocprof_summary": ap.get("rocprof_summary"),
+                                 "note": "16 B per pair-table update (random key probe + count); random-line bound"}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.cpu_size, args.cpu_merges)
     if enc is not None:

@@ -80,6 +80,9 @@ typedef struct {
     uint64_t batches;         /* training: merge batches (several merges per scan/apply pair) */
     uint64_t batch_dropped;   /* training: batch members that failed the verification */
     uint64_t batch_retries;   /* training: batches formed again (shorter) after a failed member */
+    uint64_t table_updates;   /* training, batches: pair-table updates of the applies */
+    double ms_scan_span;      /* training, batches: average k_bscan span (device wall clock) */
+    double ms_apply_span;     /* training, batches: average k_bapply span (device wall clock) */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */

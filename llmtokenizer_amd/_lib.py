@@ -44,7 +44,8 @@ class GpuStats(ctypes.Structure):
         [(n, ctypes.c_uint64) for n in ("candidates", "occurrences", "l1_rescanned", "spec_hits", "spec_misses",
                                                      "count_pass_span", "hot_rebuilds", "hot_mode", "hot_scanned",
                                                      "enc_path", "enc_windows", "relists", "batches",
-                                                     "batch_dropped", "batch_retries")]
+                                                     "batch_dropped", "batch_retries", "table_updates")] + \
+        [(n, ctypes.c_double) for n in ("ms_scan_span", "ms_apply_span")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -314,6 +314,12 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             }
         }
         if (lane == 0) {
+            if (B->sc_out && B->ap_out) {  // spans of the batch just scanned and applied
+                B->sc_ticks += B->sc_out - ~B->sc_in;
+                B->ap_ticks += B->ap_out - ~B->ap_in;
+                B->nspan++;
+            }
+            B->sc_in = B->sc_out = B->ap_in = B->ap_out = 0;
             if (applied) {
                 C->merges_done = md;
                 C->occ_top += (uint32_t)rs;
@@ -574,6 +580,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     Bat *B = E->bat;
     const uint32_t bi = bat_idx(E);
     ts_mark(E, bi, BT_SCAN_IN, true);
+    if (threadIdx.x == 0) atomicMax(&B->sc_in, ~wall_clock64());
     __shared__ uint32_t s[4][DENSE];
     __shared__ uint32_t list[SCAN_T * SU];  // this round's occurrences (position, tag), flushed per round
     __shared__ uint16_t ltag[SCAN_T * SU];
@@ -604,7 +611,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     }
     __syncthreads();
     const uint32_t k = sk, m = sm, z0 = sz0;
-    if (m >= k) return;  // block-uniform: no member for this block
+    if (m >= k) {  // block-uniform: no member for this block
+        if (tid == 0) atomicMax(&B->sc_out, wall_clock64());
+        return;
+    }
     if (tid < k) {
         rt.put(sa[tid], false, tid);
         rt.put(sb[tid], true, tid);
@@ -855,6 +865,9 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         }
     }
     ts_mark(E, bi, BT_SCAN_OUT, false, true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) atomicMax(&B->sc_out, wall_clock64());
 }
 
 // ---------------------------------------------------------------- k_bapply
@@ -886,6 +899,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     Bat *B = E->bat;
     const uint32_t bi = bat_idx(E);
     ts_mark(E, bi, BT_APPLY_IN, true);
+    if (threadIdx.x == 0) atomicMax(&B->ap_in, ~wall_clock64());
     __shared__ uint32_t sa[BK], sb[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], snl[BK * 4 + 1];
     __shared__ uint32_t sk, sj, sz0;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -982,7 +996,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     const uint32_t hotT = C->hot_T;
     const bool hot = E->hot != 0;
     long long dD = 0;
-    uint32_t nins = 0;
+    uint32_t nins = 0, nupd = 0;
     for (uint32_t t0 = bidB * blockDim.x; t0 < total; t0 += nB * blockDim.x) {  // uniform per block
         const uint32_t t = t0 + tid;
         uint32_t m = BK, cat = 0, x = 0, val = 0;
@@ -1035,6 +1049,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                 dD += (long long)(nw != 0) - (long long)(old != 0);
                 hot_in = hot && d > 0 && nw >= hotT && old < hotT;
                 hslot = (uint32_t)slot;
+                nupd++;
             }
         }
         if (hot) {
@@ -1045,23 +1060,29 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     for (int o = 32; o > 0; o >>= 1) {
         dD += __shfl_xor(dD, o);
         nins += __shfl_xor(nins, o);
+        nupd += __shfl_xor(nupd, o);
     }
     __shared__ long long sd[16];
-    __shared__ uint32_t si[16];
+    __shared__ uint32_t si[16], su[16];
     if ((tid & 63) == 0) {
         sd[tid >> 6] = dD;
         si[tid >> 6] = nins;
+        su[tid >> 6] = nupd;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         long long t = 0;
-        unsigned long long ni = 0;
+        unsigned long long ni = 0, nu = 0;
         for (uint32_t w = 0; w < blockDim.x / 64; w++) {
             t += sd[w];
             ni += si[w];
+            nu += su[w];
         }
         if (t != 0) atomicAdd(&B->dD, (unsigned long long)t);
         if (ni != 0) atomicAdd(&C->nkeys, ni);
+        if (nu != 0) atomicAdd(&B->nupd, nu);
+        atomicMax(&B->ap_out, wall_clock64());
     }
     ts_mark(E, bi, BT_APPLY_B, false, true);
 }

@@ -1854,6 +1854,15 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
         c->stats.batches = hb.nbatch;
         c->stats.batch_dropped = hb.ndrop;
         c->stats.batch_retries = hb.nretry;
+        c->stats.table_updates = hb.nupd;
+        if (hb.nspan) {
+            int khz = 0;
+            (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
+            if (khz > 0) {
+                c->stats.ms_scan_span = (double)hb.sc_ticks / hb.nspan / khz;
+                c->stats.ms_apply_span = (double)hb.ap_ticks / hb.nspan / khz;
+            }
+        }
         if (c->h.dbgts) print_batch_timeline(c, hb.nbatch + hb.nretry);
         if (getenv("BPE_DEBUG"))
             fprintf(stderr, "batches %llu, dropped %llu, re-formed %llu; formation ended by: list %llu, cap/count/hot_T %llu, a==b %llu, "
@@ -1869,6 +1878,16 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.ms_train = t2 - t1;
     c->stats.ms_total = t2 - t0;
     fill_profile(c);
+    if (c->stats.batches) {
+        // the batch engine's dominant kernel: k_bscan, 8 B per candidate (its
+        // list entry and the token word it validates) + 20 B per occurrence
+        // (partner, both neighbours, the staged list entry), per launch
+        const double nl = (double)(c->stats.batches + c->stats.batch_retries);
+        c->prof_name = "k_bscan";
+        c->prof_ms = c->stats.ms_scan_span;
+        c->prof_bytes = (8.0 * c->stats.candidates + 20.0 * c->stats.occurrences) / nl;
+        c->prof_launches = (uint64_t)nl;
+    }
     return 0;
 }
 

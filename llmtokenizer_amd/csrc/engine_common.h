@@ -125,6 +125,10 @@ struct Bat {
     unsigned long long nbatch, ndrop, nretry;  // batches applied; members dropped by the verification; batches re-formed
     unsigned long long why[8];        // what ended each batch's formation (BPE_DEBUG report)
     uint32_t drop_test, pad1, pad2, pad3;  // > 0: members j >= 1 with (z0 + j) % drop_test == 0 fail (tests)
+    // device wall-clock spans (first block entry, complemented, and last block
+    // exit of this batch's k_bscan / k_bapply; folded by the select) and
+    // their sums; table updates role B made
+    unsigned long long sc_in, sc_out, ap_in, ap_out, sc_ticks, ap_ticks, nspan, nupd;
     uint32_t a[BK], b[BK], cnt[BK], mode[BK], off[BK], len[BK];
     uint32_t blk0[BK + 1];            // k_bscan block range of each member
     uint32_t sbase[BK + 1];           // member's slice of the occurrence staging area (prefix of len)
