@@ -173,8 +173,10 @@ def committed_profile(name):
     """rocprof average (ms) of kernel `name` and PMC traffic per launch from
     the committed summaries of this same command (profiles/<tag>_*)"""
     out = {}
-    p = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_train_kernel_stats.csv")
-    if os.path.exists(p):
+    for kind in ("train", "sharded"):  # single-GPU bench command, then the sharded one
+        p = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_{kind}_kernel_stats.csv")
+        if "avg_ms_rocprof" in out or not os.path.exists(p):
+            continue
         with open(p) as f:
             for r in csv.DictReader(f):
                 nm = r["Name"].split("(")[0].replace("bpeamd::", "").replace("void ", "").strip()

@@ -124,6 +124,8 @@ int bpe_gpu_fetch_merges(bpe_gpu_ctx *ctx, uint32_t *pairs, size_t cap, size_t *
 
 /* final token ids of the loaded corpus (after train or encode) */
 int bpe_gpu_fetch_ids(bpe_gpu_ctx *ctx, uint32_t *ids, size_t cap, size_t *len);
+/* ids [first, first + count) of them */
+int bpe_gpu_fetch_ids_range(bpe_gpu_ctx *ctx, size_t first, uint32_t *ids, size_t count);
 
 /* Encode the loaded corpus with a given merge list (pairs, id 256 + r). */
 int bpe_gpu_encode(bpe_gpu_ctx *ctx, const uint32_t *pairs, size_t n_merges);
@@ -215,6 +217,8 @@ int bpe_gpu_group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges);
 int bpe_gpu_group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges);
 int bpe_gpu_group_fetch_merges(bpe_gpu_group *g, uint32_t *pairs, size_t cap, size_t *count);
 int bpe_gpu_group_fetch_ids(bpe_gpu_group *g, int k, uint32_t *ids, size_t cap, size_t *len);
+/* ids [first, first + count) of local shard k (ranged reads of huge outputs) */
+int bpe_gpu_group_fetch_ids_range(bpe_gpu_group *g, int k, size_t first, uint32_t *ids, size_t count);
 int bpe_gpu_group_get_stats(bpe_gpu_group *g, bpe_gpu_stats *st);
 /* bpe_gpu_ids_checksum over the group's local shards in order (the first
  * starting at global index `base`); *n_ids = the local ids counted */

@@ -33,6 +33,7 @@ EXPORTS = [
     "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo", "bpe_gpu_group_kernel_profile",
     "bpe_gpu_group_create_p2p", "bpe_gpu_group_p2p_connect", "bpe_gpu_group_transport",
     "bpe_gpu_group_create_local_p2p", "bpe_gpu_ids_checksum", "bpe_gpu_group_ids_checksum", "bpe_gpu_load_fd",
+    "bpe_gpu_fetch_ids_range", "bpe_gpu_group_fetch_ids_range",
 ]
 
 
@@ -98,6 +99,8 @@ def load():
     L.bpe_gpu_group_encode.argtypes = [vp, vp, sz]
     L.bpe_gpu_group_fetch_merges.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_group_fetch_ids.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.POINTER(sz)]
+    L.bpe_gpu_group_fetch_ids_range.argtypes = [vp, ctypes.c_int, sz, vp, sz]
+    L.bpe_gpu_fetch_ids_range.argtypes = [vp, sz, vp, sz]
     L.bpe_gpu_group_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats)]
     L.bpe_gpu_group_exchange_mode.argtypes = [vp, ip]
     L.bpe_gpu_group_kernel_profile.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),

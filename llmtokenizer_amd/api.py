@@ -368,6 +368,18 @@ class ShardGroup:
                                                   ctypes.byref(n)), "fetch_ids")
         return out[: n.value]
 
+    def ids_count(self, k):
+        n = ctypes.c_size_t(0)
+        _lib.check(self.L.bpe_gpu_group_fetch_ids(self.g, int(k), None, 0, ctypes.byref(n)), "fetch_ids")
+        return n.value
+
+    def ids_range(self, k, first, count):
+        """ids [first, first + count) of local shard k"""
+        out = np.zeros(max(int(count), 1), dtype=np.uint32)
+        _lib.check(self.L.bpe_gpu_group_fetch_ids_range(self.g, int(k), int(first), out.ctypes.data_as(ctypes.c_void_p),
+                                                        int(count)), "fetch_ids_range")
+        return out[: int(count)]
+
     def all_ids(self):
         return np.concatenate([self.ids(k) for k in range(self.local_shards)])
 

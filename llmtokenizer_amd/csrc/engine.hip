@@ -1916,6 +1916,18 @@ int bpe_gpu_fetch_ids(bpe_gpu_ctx *c, uint32_t *ids, size_t cap, size_t *len) {
     return 0;
 }
 
+int bpe_gpu_fetch_ids_range(bpe_gpu_ctx *c, size_t first, uint32_t *ids, size_t count) {
+    if (!c || (!ids && count)) return BPE_GPU_EINVAL;
+    if (!c->ids_ready) return fail(BPE_GPU_ESTATE, "no ids: train or encode first");
+    if (first > c->ids_len || count > c->ids_len - first) return fail(BPE_GPU_EINVAL, "id range out of bounds");
+    HIPCHK(hipSetDevice(c->dev));
+    if (count) {
+        HIPCHK(hipMemcpyAsync(ids, c->h.ids_out + first, count * 4, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+    }
+    return 0;
+}
+
 int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
     if (!c || (!pairs && n_merges)) return BPE_GPU_EINVAL;
     if (!c->loaded) return fail(BPE_GPU_ESTATE, "encode before load");

@@ -517,14 +517,18 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     HIPCHK(hipStreamSynchronize(g->st));
     const double t2 = now_ms();
     if ((r = p2p_check(g))) return r;
-    uint64_t nout = 0;
+    uint64_t nout = 0, ncand = 0, nocc = 0;
     for (bpe_gpu_ctx *c : g->cs) {
         if ((r = pull_ctl(c))) return r;
         if ((r = compact_ids(c))) return r;
         c->merges_done = c->hC->merges_done;
         nout += c->ids_len;
+        ncand += c->hC->counters[4];  // this shard's candidates and occurrences
+        nocc += c->hC->counters[5];
         fill_profile(c);
     }
+    g->stats.candidates = ncand;
+    g->stats.occurrences = nocc;
     const Ctl &C = *g->cs[0]->hC;
     g->merges_done = C.merges_done;
     *n_merges = C.merges_done;
@@ -1092,6 +1096,12 @@ int bpe_gpu_group_fetch_ids(bpe_gpu_group *g, int k, uint32_t *ids, size_t cap, 
     bpe_gpu_ctx *c = group_shard(g, k);
     if (!c) return BPE_GPU_EINVAL;
     return bpe_gpu_fetch_ids(c, ids, cap, len);
+}
+
+int bpe_gpu_group_fetch_ids_range(bpe_gpu_group *g, int k, size_t first, uint32_t *ids, size_t count) {
+    bpe_gpu_ctx *c = group_shard(g, k);
+    if (!c) return BPE_GPU_EINVAL;
+    return bpe_gpu_fetch_ids_range(c, first, ids, count);
 }
 
 int bpe_gpu_group_ids_checksum(bpe_gpu_group *g, uint64_t base, uint64_t *sum, uint64_t *n_ids) {

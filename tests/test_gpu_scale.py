@@ -13,7 +13,9 @@ at scale").  The oracle cannot train 1 GiB x 8192 merges end to end, so:
   configs[4]  a 3 GiB stream through a 32k-merge list: one context, 2 shards
               and 4 uneven shards give the same ids checksum and length; decode
               of id windows gives the stream's bytes back; a 256 KiB chunk
-              encoded alone matches the oracle.
+              encoded alone matches the oracle.  And at the stated 10 GiB: 4 and
+              5 shard cuts agree, tokens around the stream start and two shard
+              seams equal the oracle's on 256 KiB windows.
 Plus the reference CLI (main.c) run through tools/bpe_main: its stdout equals
 what the reference's main.c printed (fixture print_text_md5)."""
 import hashlib
@@ -159,6 +161,91 @@ def test_config4_encode_3g_through_32k_merges_cut_independent():
     chunk = synth_bytes(3, 256 << 10, lo=5 * (1 << 28))
     assert (api.encode(chunk, M) == O.encode(chunk, M)).all()
     d.close()
+
+
+def _shard_head(g, k, S, el, M, T):
+    """(start positions, ids) of the first T tokens of local shard k whose
+    bytes begin at S.  The left shard owns a pair across the cut, so the first
+    token of shard k starts at the end E >= S of the left shard's last token:
+    found by locating the decoded head in the stream near S."""
+    head = g.ids_range(k, 0, T)
+    hb = O.decode(head[:64], M)
+    near = synth_bytes(3, (1 << 16) + len(hb), lo=S)
+    off = near.find(hb)
+    assert off >= 0, (k, S)
+    E = S + off
+    pos = E + np.concatenate([[0], np.cumsum(el[head], dtype=np.int64)[:-1]])
+    return pos, head, E
+
+
+def _shard_tail(g, k, E, el, T):
+    """(start positions, ids) of the last T tokens of local shard k, ending at E"""
+    n = g.ids_count(k)
+    tail = g.ids_range(k, n - T, T)
+    ends = E - np.concatenate([np.cumsum(el[tail][::-1], dtype=np.int64)[::-1][1:], [0]])
+    return ends - el[tail], tail
+
+
+def _oracle_window(M, el, lo, hi, margin=32 << 10):
+    """(positions, ids) of the tokens inside [lo, hi) when the oracle encodes
+    [lo - margin, hi + margin) alone (the margin absorbs its chunk edges)"""
+    c0 = max(0, lo - margin)
+    oids = O.encode(synth_bytes(3, hi + margin - c0, lo=c0), M)
+    pos = c0 + np.concatenate([[0], np.cumsum(el[oids], dtype=np.int64)[:-1]])
+    keep = (pos >= lo) & (pos + el[oids] <= hi)
+    return pos[keep], oids[keep]
+
+
+def test_config4_encode_10g_through_32k_merges():
+    """BASELINE configs[4] at its stated size: a 10 GiB stream through the first
+    32,768 merges the trainer learns on the 1 GiB corpus.  Four even and five
+    uneven shard cuts give the same ids (checksum, count); n_out + occurrences
+    == bytes; around the stream start and two shard seams the tokens (positions
+    and ids) equal the oracle's sequential replace passes (bpe.c:760-779) on a
+    256 KiB window; 1 Mi-id windows decode to the stream's bytes."""
+    tr = api.Engine(0)
+    tr.synth(2, GIB)
+    assert tr.train(32768) == 32768
+    M = tr.merges()
+    tr.close()
+    el = _elen(M)
+    n = 10 * GIB
+    res = {}
+    for name, cuts in (("even4", [0, n // 4, n // 2, 3 * n // 4, n]),
+                       ("uneven5", [0, GIB + 1, 3 * GIB - 12345, 5 * GIB + 777, 7 * GIB + GIB // 2 + 3, n])):
+        g = api.ShardGroup(0, local_shards=len(cuts) - 1)
+        for q in range(len(cuts) - 1):
+            g.synth(q, 3, cuts[q + 1] - cuts[q], cuts[q])
+        g.encode(M)
+        st = g.stats()
+        csum, cnt = g.ids_checksum()
+        assert cnt == st["n_out"] and st["n_out"] + st["occurrences"] == n, (name, st["n_out"], st["occurrences"])
+        res[name] = (csum, cnt)
+        if name == "even4":
+            T, W = 200000, 128 << 10
+            d = api.Engine(0)
+            # the stream start
+            pos, ids, _ = _shard_head(g, 0, 0, el, M, T)
+            keep = pos + el[ids] <= 2 * W
+            opos, oids = _oracle_window(M, el, 0, 2 * W)
+            assert (pos[keep] == opos).all() and (ids[keep] == oids).all()
+            out = d.decode(ids[: 1 << 20], M) if ids.size >= (1 << 20) else d.decode(g.ids_range(0, 0, 1 << 20), M)
+            assert out == synth_bytes(3, len(out), lo=0)
+            # two shard seams: the tail of shard k and the head of shard k+1
+            for k in (0, 2):
+                S = cuts[k + 1]
+                hpos, hid, E = _shard_head(g, k + 1, S, el, M, T)
+                tpos, tid = _shard_tail(g, k, E, el, T)
+                gp, gi = np.concatenate([tpos, hpos]), np.concatenate([tid, hid])
+                keep = (gp >= S - W) & (gp + el[gi] <= S + W)
+                opos, oids = _oracle_window(M, el, S - W, S + W)
+                assert (gp[keep] == opos).all() and (gi[keep] == oids).all(), (k, S)
+                w = g.ids_range(k + 1, 0, 1 << 20)
+                out = d.decode(w, M)
+                assert out == synth_bytes(3, len(out), lo=E)
+            d.close()
+        g.close()
+    assert res["even4"] == res["uneven5"], res
 
 
 @pytest.mark.parametrize("name", ["prose", "synth_s1_4k", "binary_5k", "nul_truncates"])
