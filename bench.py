@@ -29,8 +29,9 @@ The line also carries
                   the LAST timed job; the committed rocprofv3 summary and PMC
                   traffic of this same command (profiles/r3_*) beside them;
   roofline_apply  the batch apply k_bapply (table updates, 16 B each), same way;
-  roofline_count_pass  the corpus-wide pair-count pass, priced at SURVEY 8(d)
-                  widths (1 B/token read + 2 B/token id write while V <= 65536);
+  roofline_count_pass  the corpus-wide pair-count pass (1 B/token read; the
+                  initial u32 ids are written by the counting sort's first
+                  pass, k_sort_a, which streams the bytes anyway);
   correctness     merges md5 + position-keyed ids checksum (bpe_gpu_ids_checksum)
                   of the warm-up and the timed jobs: they must agree, else the
                   line carries "error" and the process exits non-zero;
@@ -425,12 +426,10 @@ def main():
     value = corpus_mb * merges * k / el
     name, kms, kbytes, launches = prof
     achieved = kbytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
-    # count pass at SURVEY 8(d) widths: 1 B/token read (V = 256) + the fused
-    # initial id write at 2 B/token (V <= 65536); the engine stores u32 ids
-    V = 256 + merges
-    w_ids = 2 if V <= 65536 else 4
+    # count pass: reads the corpus once, 1 B/token (V = 256); the initial ids
+    # are written by k_sort_a
     cp_ms = st["ms_count_pass"]
-    cp_bytes = args.size * (1 + w_ids) if st["count_pass_span"] else args.size
+    cp_bytes = args.size
     cp_achieved = cp_bytes / (cp_ms * 1e-3) / 1e9 if cp_ms > 0 else 0.0
     world = cx.world
     if sharded:
@@ -470,8 +469,8 @@ def main():
                                 "bound": "hbm", "achieved": round(cp_achieved, 1), "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": round(cp_achieved / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": cp_bytes, "avg_ms": round(cp_ms, 4),
-                                "note": f"SURVEY 8(d) widths: 1 B/token read + {w_ids} B/token fused id write "
-                                        "(the engine stores u32 ids: 5 B/token moved)"},
+                                "note": "histogram of byte-pair rank keys: 1 B/token read, bins in LDS "
+                                        "(SURVEY 8(d)); the initial ids are written by k_sort_a"},
         "breakdown_ms": {"init": round(st["ms_init"], 3), "loop": round(st["ms_train"], 3),
                          "total_engine": round(st["ms_total"], 3), "per_merge_us": round(st["ms_train"] * 1e3 / merges, 2)},
         "engine": {k2: st[k2] for k2 in ("n_out", "iterations", "distinct_pairs", "merged_buckets",

@@ -63,13 +63,13 @@ typedef struct {
     double ms_init;           /* device-side setup (counting sort, table)      */
     double ms_train;          /* merge loop                                    */
     double ms_total;          /* init + loop (what bench.py times end to end)  */
-    double ms_count_pass;     /* the one corpus-wide pair-count pass (k_pair_hist) */
+    double ms_count_pass;     /* the one corpus-wide pair-count pass (k_pair_hist*, reads the bytes) */
     uint64_t candidates;      /* candidate positions examined by the scans      */
     uint64_t occurrences;     /* pair occurrences replaced                       */
     uint64_t l1_rescanned;    /* level-1 summary blocks rescanned                 */
     uint64_t spec_hits;       /* next merges found by the speculative scan        */
     uint64_t spec_misses;     /* mispredicted next merges (host re-scan)          */
-    uint64_t count_pass_span; /* 1: the count pass ran in span form (k_pair_hist_span) */
+    uint64_t count_pass_span; /* >0: the count pass ran in span form (k_pair_hist_span), value = LDS histogram copies */
     uint64_t hot_rebuilds;    /* hot-set argmax: full-table rebuilds of the listed keys */
     uint64_t hot_mode;        /* 0 level summaries, 1 hot set, 2 hot set given up mid-run */
     uint64_t hot_scanned;     /* hot-set entries reduced, summed over the merges */

@@ -1328,13 +1328,24 @@ int compact_ids(bpe_gpu_ctx *c) {
     return 0;
 }
 
-// init phase 1: the set of byte values present (tok[] is written in phase 2)
+// init phase 1: the set of byte values present (tok[] is written by k_sort_a)
 int init_presence(bpe_gpu_ctx *c, uint32_t **d_bh) {
     int r;
     if ((r = dalloc(c, d_bh, 256))) return r;
-    k_init_tok<false, true><<<1024, 256, 0, c->st>>>(c->dE, *d_bh);
+    k_init_tok<false><<<1024, 256, 0, c->st>>>(c->dE, *d_bh);
     HIPCHK(hipGetLastError());
     return 0;
+}
+
+// the LDS a count-pass block may take (two 1024-thread blocks per CU)
+constexpr size_t HIST_LDS_MAX = 80 * 1024;
+
+template <uint32_t R>
+void launch_hist_span(bpe_gpu_ctx *c, size_t lds, uint32_t ntl, uint32_t *d_hist, uint64_t tile, uint32_t lo,
+                      uint32_t S) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_hist_span<R>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    k_pair_hist_span<R><<<ntl, 1024, lds, c->st>>>(c->dE, d_hist, tile, lo, S);
 }
 
 // init phase 2: byte ranks (from the presence vector `bh`, nonzero = present),
@@ -1365,19 +1376,28 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
     if ((r = dalloc(c, &d_hist, (size_t)ntl * AA, false))) return r;
     if ((r = dalloc(c, &d_tot, AA + 1))) return r;
     // byte values present span [lo, lo + S): the span form of the count pass
-    // (which also writes tok[]) when S is small
+    // when S is small
     const uint32_t lo = unrank.empty() ? 0 : unrank.front();
     const uint32_t S = unrank.empty() ? 0 : unrank.back() - lo + 1;
     const bool span = npairs > 0 && S >= 1 && S <= SPAN_MAX &&
                       !(getenv("BPE_HIST_SPAN") && !atoi(getenv("BPE_HIST_SPAN")));
-    if (!span) k_tok_words<<<1024, 256, 0, c->st>>>(c->dE);
     if (npairs > 0) {
         // the one full pass over the corpus: time it with events on our stream
         hipEvent_t e0, e1;
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
         HIPCHK(hipEventRecord(e0, c->st));
-        if (span) k_pair_hist_span<<<ntl, 1024, 0, c->st>>>(c->dE, d_hist, tile, lo, S);
+        if (span) {
+            // copies of the LDS histogram: 2 while two blocks still fit a CU (measured,
+            // 1 GiB: 1 copy 0.380 ms, 2 copies 0.368, 4 copies (one block per CU) 0.418)
+            uint32_t R = 2;
+            while (R > 1 && ((size_t)R * S * S + 256) * 4 > HIST_LDS_MAX) R >>= 1;
+            if (const char *t = getenv("BPE_HIST_R")) R = std::min<uint32_t>(R, (uint32_t)atoi(t));  // tuning
+            const size_t lds = ((size_t)R * S * S + 256) * 4;
+            if (R >= 2) launch_hist_span<2>(c, lds, ntl, d_hist, tile, lo, S);
+            else launch_hist_span<1>(c, lds, ntl, d_hist, tile, lo, S);
+            c->stats.count_pass_span = R;
+        }
         else k_pair_hist<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
         HIPCHK(hipEventRecord(e1, c->st));
         HIPCHK(hipEventSynchronize(e1));
@@ -1387,10 +1407,11 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
         hipEventDestroy(e1);
         c->prof_name = span ? "k_pair_hist_span" : "k_pair_hist";
         c->stats.ms_count_pass = ms;
-        c->stats.count_pass_span = span;
+        if (!span) c->stats.count_pass_span = 0;
         c->prof_ms = ms;
-        // 1 B/token read (V = 256; re-read once per bin part), + 4 B/token tok[] write when fused
-        c->prof_bytes = (double)c->n0 * (span ? 5 : parts);
+        // 1 B/token read (V = 256: re-read once per bin part); tok[] was
+        // written by init_presence's streaming pass
+        c->prof_bytes = (double)c->n0 * (span ? 1 : parts);
         c->prof_launches = 1;
         const uint32_t per = (ntl + COLSCAN_GROUPS - 1) / COLSCAN_GROUPS;
         const uint32_t ngr = (ntl + per - 1) / per;
@@ -1409,6 +1430,7 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
         HIPCHK(hipGetLastError());
     } else {
         HIPCHK(hipMemsetAsync(h.poff, 0, 4ull * (AA + 1), c->st));
+        k_init_tok<true><<<1, 256, 0, c->st>>>(c->dE, nullptr);  // (no k_sort_a to write tok[])
     }
     *unrank_out = unrank;
     *d_tot_out = d_tot;
@@ -1987,7 +2009,7 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
     } else {
         uint32_t *d_bh;
         if ((r = dalloc(c, &d_bh, 256))) return r;
-        k_init_tok<true, true><<<1, 256, 0, c->st>>>(c->dE, d_bh);
+        k_init_tok<true><<<1, 256, 0, c->st>>>(c->dE, d_bh);
     }
     // merges in commuting batches: first batch, then graphs of (scan, apply + next batch)
     EncBatch *d_eb;

@@ -1889,44 +1889,6 @@ __global__ void k_init_cross(const Eng *__restrict__ E, uint32_t *__restrict__ t
 
 
 // ------------------------------------------------------------- init kernels
-// tok[i] = byte i (16 bytes per thread, uint4 in / 4 x uint4 out) and / or
-// the set of byte values present (only presence is needed to rank them).
-// Training runs presence alone first; tok is then written by the count pass
-// (k_pair_hist_span) or by the TOK-only instance.
-template <bool TOK, bool PRES>
-__global__ __launch_bounds__(256) void k_init_tok(const Eng *__restrict__ E, uint32_t *__restrict__ present) {
-    __shared__ uint32_t seen[256];
-    if (PRES) {
-        for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x) seen[x] = 0;
-        __syncthreads();
-    }
-    const uint64_t n0 = E->n0, nv = n0 / 16;
-    const uint4 *src = reinterpret_cast<const uint4 *>(E->bytes);
-    uint4 *dst = reinterpret_cast<uint4 *>(E->tok);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nv; c += stride) {
-        const uint4 v = src[c];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t b0 = w[q] & 0xFF, b1 = (w[q] >> 8) & 0xFF, b2 = (w[q] >> 16) & 0xFF, b3 = w[q] >> 24;
-            if (TOK) dst[4 * c + q] = make_uint4(b0, b1, b2, b3);
-            if (PRES) { seen[b0] = 1; seen[b1] = 1; seen[b2] = 1; seen[b3] = 1; }  // benign same-value races
-        }
-    }
-    if (blockIdx.x == 0)
-        for (uint64_t k = nv * 16 + threadIdx.x; k < n0; k += blockDim.x) {
-            if (TOK) E->tok[k] = E->bytes[k];
-            if (PRES) seen[E->bytes[k]] = 1;
-        }
-    if (PRES) {
-        __syncthreads();
-        for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x)
-            if (seen[x] && !present[x]) atomicOr(&present[x], 1u);
-    }
-}
-template __global__ void k_init_tok<true, true>(const Eng *, uint32_t *);
-template __global__ void k_init_tok<false, true>(const Eng *, uint32_t *);
 
 // per-(tile, part) histogram of byte-pair rank keys; LDS u32 bins.
 // 16 pair positions per thread from one uint4 load (+1 byte of the next).
@@ -1968,18 +1930,10 @@ __global__ __launch_bounds__(1024) void k_pair_hist(const Eng *__restrict__ E, u
     for (uint32_t k = lo + threadIdx.x; k < hi; k += blockDim.x) hist[(uint64_t)tl * AA + k] = h[k - lo];
 }
 
-// Span form of k_pair_hist (it also writes the initial tok[]), for corpora
-// whose byte values lie in [lo, lo + S)
-// with S <= SPAN_MAX (text): the bin of pair (x, y) is (x - lo) * S + (y - lo),
-// computed from the bytes alone, so each pair costs ONE LDS operation (the
-// bin add) instead of two (rank lookup + add): the count pass is bound by
-// LDS bank cycles, not by HBM.  Bins are written out in rank-key order, so
-// hist[] is identical to k_pair_hist's.  Per thread and round: two 16-byte
-// loads in flight (chunks c and c + blockDim); the byte after a chunk comes
-// from the next lane's load (one 1-byte load per wave for lane 63).
+// largest byte-value span the count pass bins directly (k_pair_hist_span)
 constexpr uint32_t SPAN_MAX = 128;
 
-// Word-granular layout shared by the passes that write the initial tok[]:
+// Word-granular layout shared by k_init_tok, k_pair_hist_span and k_sort_a:
 // a wave owns 1 KB blocks of the corpus; lane L of round q (0..3) holds byte
 // word 64q + L, so each dword load is one coalesced 256-B access and each
 // uint4 store of the 4 widened tokens one contiguous 1-KB run (16-B lanes at
@@ -1988,25 +1942,29 @@ __device__ __forceinline__ uint4 widen4(uint32_t w) {
     return make_uint4(w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFF, w >> 24);
 }
 
-// the 4 pairs starting in word w (next = the following byte); lim < 4 near the tile end
+// the 4 pairs starting in word w (next = the following byte); lim < 4 near
+// the tile end.  R interleaved copies of the histogram: lane class rl = lane
+// mod R adds to word bin * R + rl, so lanes of different classes never share a
+// bank and a random 32-lane group spreads over R smaller balls-into-bins draws
+template <uint32_t R>
 __device__ __forceinline__ void span_count4(uint32_t *h, uint32_t w, uint32_t next, uint32_t S, uint32_t off,
-                                            uint32_t lim) {
+                                            uint32_t lim, uint32_t rl) {
     const uint32_t b0 = w & 0xFF, b1 = (w >> 8) & 0xFF, b2 = (w >> 16) & 0xFF, b3 = w >> 24, b4 = next & 0xFF;
     if (lim >= 4) {
-        atomicAdd(&h[b0 * S + b1 - off], 1u);
-        atomicAdd(&h[b1 * S + b2 - off], 1u);
-        atomicAdd(&h[b2 * S + b3 - off], 1u);
-        atomicAdd(&h[b3 * S + b4 - off], 1u);
+        atomicAdd(&h[(b0 * S + b1 - off) * R + rl], 1u);
+        atomicAdd(&h[(b1 * S + b2 - off) * R + rl], 1u);
+        atomicAdd(&h[(b2 * S + b3 - off) * R + rl], 1u);
+        atomicAdd(&h[(b3 * S + b4 - off) * R + rl], 1u);
     } else {
-        if (lim > 0) atomicAdd(&h[b0 * S + b1 - off], 1u);
-        if (lim > 1) atomicAdd(&h[b1 * S + b2 - off], 1u);
-        if (lim > 2) atomicAdd(&h[b2 * S + b3 - off], 1u);
+        if (lim > 0) atomicAdd(&h[(b0 * S + b1 - off) * R + rl], 1u);
+        if (lim > 1) atomicAdd(&h[(b1 * S + b2 - off) * R + rl], 1u);
+        if (lim > 2) atomicAdd(&h[(b2 * S + b3 - off) * R + rl], 1u);
     }
 }
 
 // one 1-KB block kb of a wave: count its pairs below e (HIST), write its full
 // token words (TOK); w[q] = word 64q + lane of the block
-template <bool HIST, bool TOK>
+template <bool HIST, bool TOK, uint32_t R = 1>
 __device__ __forceinline__ void kb_body(uint32_t *h, uint4 *tok, const uint8_t *bytes, uint64_t kb, const uint32_t w[4],
                                         uint64_t e, uint64_t n0, uint32_t S, uint32_t off) {
     const uint32_t lane = threadIdx.x & 63;
@@ -2021,26 +1979,31 @@ __device__ __forceinline__ void kb_body(uint32_t *h, uint4 *tok, const uint8_t *
             } else if (lane == 63) {
                 nxt = (kb + 1) * 1024 < n0 ? bytes[(kb + 1) * 1024] : 0;
             }
-            if (p < e) span_count4(h, w[q], nxt, S, off, (uint32_t)min<uint64_t>(4, e - p));
+            if (p < e) span_count4<R>(h, w[q], nxt, S, off, (uint32_t)min<uint64_t>(4, e - p), lane & (R - 1));
         }
         if (TOK && p + 4 <= n0) tok[wi] = widen4(w[q]);
     }
 }
 
-// Span form of k_pair_hist (it also writes the initial tok[]), for corpora
+// Span form of k_pair_hist (a read-only pass: k_sort_a writes the initial
+// tok[]), for corpora
 // whose byte values lie in [lo, lo + S) with S <= SPAN_MAX (text): the bin of
 // pair (x, y) is (x - lo) * S + (y - lo), computed from the bytes alone, so
 // each pair costs ONE LDS operation (the bin add) instead of two (rank lookup
 // + add).  Bins are written out in rank-key order, so hist[] is identical to
 // k_pair_hist's.  Tiles are 1-KB aligned; each wave walks its own 1-KB blocks,
-// two in flight (8 dword loads per lane).
+// two in flight (8 dword loads per lane).  The bin adds are bound by LDS bank
+// conflicts (random bins: the busiest bank of a 32-lane group sets its
+// cycles), so the histogram is kept in R interleaved copies as the LDS allows
+// (dynamic LDS: R * S * S words + the 256-word unrank table).
+template <uint32_t R>
 __global__ __launch_bounds__(1024) void k_pair_hist_span(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
                                                          uint64_t tile, uint32_t lo, uint32_t S) {
-    __shared__ uint32_t h[SPAN_MAX * SPAN_MAX];
-    __shared__ uint32_t ur[256];
+    extern __shared__ uint32_t hdyn[];
     const uint32_t A = E->A, AA = A * A, SS = S * S;
+    uint32_t *h = hdyn, *ur = hdyn + R * SS;
     const uint32_t tl = blockIdx.x, T = blockDim.x, lane = threadIdx.x & 63;
-    for (uint32_t i = threadIdx.x; i < SS; i += T) h[i] = 0;
+    for (uint32_t i = threadIdx.x; i < R * SS; i += T) h[i] = 0;
     for (uint32_t x = threadIdx.x; x < 256; x += T) {
         const uint32_t r = E->rank[x];
         if (r != HOLE) ur[r] = x;
@@ -2050,7 +2013,6 @@ __global__ __launch_bounds__(1024) void k_pair_hist_span(const Eng *__restrict__
     const uint64_t s = (uint64_t)tl * tile, e = min(n0 - 1, s + tile);  // pair positions [s, e), tile % 1024 == 0
     const uint32_t *src = reinterpret_cast<const uint32_t *>(E->bytes);
     const uint8_t *bytes = E->bytes;
-    uint4 *tok = reinterpret_cast<uint4 *>(E->tok);
     const uint32_t off = lo * S + lo;
     const uint64_t nw = T / 64, kb0 = s / 1024, kb1 = (e + 1023) / 1024;
     const uint64_t nwords = (n0 + 3) / 4;  // (bytes is zero-padded past n0)
@@ -2063,39 +2025,71 @@ __global__ __launch_bounds__(1024) void k_pair_hist_span(const Eng *__restrict__
             wa[q] = ia < nwords ? src[ia] : 0u;
             wb[q] = kc < kb1 && ib < nwords ? src[ib] : 0u;
         }
-        kb_body<true, true>(h, tok, bytes, kb, wa, e, n0, S, off);
-        if (kc < kb1) kb_body<true, true>(h, tok, bytes, kc, wb, e, n0, S, off);
+        kb_body<true, false, R>(h, nullptr, bytes, kb, wa, e, n0, S, off);
+        if (kc < kb1) kb_body<true, false, R>(h, nullptr, bytes, kc, wb, e, n0, S, off);
     }
-    // the tail of the last partial word (every full word lies in some tile's blocks)
-    if (tl == gridDim.x - 1)
-        for (uint64_t k = n0 / 4 * 4 + threadIdx.x; k < n0; k += T) E->tok[k] = bytes[k];
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < AA; k += T) {
         const uint32_t x = ur[k / A] - lo, y = ur[k % A] - lo;
-        hist[(uint64_t)tl * AA + k] = h[x * S + y];
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) v += h[(x * S + y) * R + r];
+        hist[(uint64_t)tl * AA + k] = v;
     }
 }
+template __global__ void k_pair_hist_span<1>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
+template __global__ void k_pair_hist_span<2>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
 
-// tok[] = bytes alone, in the same coalesced layout (count passes other than
-// the span form): grid-stride over 1-KB blocks, one per wave
-__global__ __launch_bounds__(256) void k_tok_words(const Eng *__restrict__ E) {
+// Init phase 1: the set of byte values present (only presence is needed to
+// rank them), plus tok[] = bytes when TOK (inputs too short for the counting
+// sort, whose first pass k_sort_a writes tok[] otherwise).  Grid-stride over
+// 1-KB blocks, one per wave, two blocks in flight.
+template <bool TOK>
+__global__ __launch_bounds__(256) void k_init_tok(const Eng *__restrict__ E, uint32_t *__restrict__ present) {
+    __shared__ uint32_t seen[256];
+    seen[threadIdx.x] = 0;
+    __syncthreads();
     const uint64_t n0 = E->n0, nwords = (n0 + 3) / 4, nkb = (n0 + 1023) / 1024;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(E->bytes);
     uint4 *tok = reinterpret_cast<uint4 *>(E->tok);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nwv = (uint64_t)gridDim.x * (blockDim.x / 64);
-    for (uint64_t kb = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); kb < nkb; kb += nwv) {
-        uint32_t w[4];
+    auto mark = [&](const uint32_t w[4]) {  // benign same-value races
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {
-            const uint64_t i = kb * 256 + 64 * q + lane;
-            w[q] = i < nwords ? src[i] : 0u;
+            seen[w[q] & 0xFF] = 1;
+            seen[(w[q] >> 8) & 0xFF] = 1;
+            seen[(w[q] >> 16) & 0xFF] = 1;
+            seen[w[q] >> 24] = 1;
         }
-        kb_body<false, true>(nullptr, tok, E->bytes, kb, w, 0, n0, 0, 0);
+    };
+    for (uint64_t kb = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); kb < nkb; kb += 2 * nwv) {
+        const uint64_t kc = kb + nwv;
+        uint32_t wa[4], wb[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            const uint64_t ia = kb * 256 + 64 * q + lane, ib = kc * 256 + 64 * q + lane;
+            wa[q] = ia < nwords ? src[ia] : 0u;
+            wb[q] = ib < nwords ? src[ib] : 0u;
+        }
+        // (bytes is zero-padded past n0: byte 0 of a padding word is not a token)
+        if (TOK) kb_body<false, true>(nullptr, tok, E->bytes, kb, wa, 0, n0, 0, 0);
+        if (kb * 1024 + 1024 <= n0) mark(wa);
+        if (kc < nkb) {
+            if (TOK) kb_body<false, true>(nullptr, tok, E->bytes, kc, wb, 0, n0, 0, 0);
+            if (kc * 1024 + 1024 <= n0) mark(wb);
+        }
     }
-    if (blockIdx.x == 0)
-        for (uint64_t k = n0 / 4 * 4 + threadIdx.x; k < n0; k += blockDim.x) E->tok[k] = E->bytes[k];
+    if (blockIdx.x == gridDim.x - 1) {  // the last partial 1-KB block: byte-wise
+        for (uint64_t k = n0 / 1024 * 1024 + threadIdx.x; k < n0; k += blockDim.x) seen[E->bytes[k]] = 1;
+        if (TOK)
+            for (uint64_t k = n0 / 4 * 4 + threadIdx.x; k < n0; k += blockDim.x) E->tok[k] = E->bytes[k];
+    }
+    __syncthreads();
+    if (present && seen[threadIdx.x] && !present[threadIdx.x]) atomicOr(&present[threadIdx.x], 1u);
 }
+template __global__ void k_init_tok<true>(const Eng *, uint32_t *);
+template __global__ void k_init_tok<false>(const Eng *, uint32_t *);
 
 // column scan over tiles: hist[t][k] := sum_{t' < t} hist[t'][k]; tot[k] =
 // total.  Two launches over a (key, tile group) grid so that every CU has
@@ -2314,9 +2308,16 @@ __device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const uin
 }
 
 // pass A: tile t -> packed entries (k2 << 24 | position - tile start) grouped
-// by k1, in the same slot range plist will use for that tile's k1 group
+// by k1, in the same slot range plist will use for that tile's k1 group.  It
+// also writes the tile's initial tok[] = bytes (u32 ids), so the count pass
+// only reads the corpus.  A wave takes 512 consecutive bytes per round in the
+// word layout of k_pair_hist_span (lane L holds words L and 64 + L; the byte
+// after a word comes from the next lane), so each widened uint4 store is one
+// contiguous 1-KB run of tok[]; the next round's words are loaded before this
+// round's LDS sort.
 __global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
                                                    uint64_t tile, uint32_t *__restrict__ tmp) {
+    static_assert(SORT_PER == 8, "two 4-byte words per lane and round");
     __shared__ SortLds L;
     __shared__ uint32_t rk[256];
     const uint32_t A = E->A, AA = A * A;
@@ -2330,34 +2331,51 @@ __global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, co
         L.gcur[threadIdx.x] = s0;
     }
     __syncthreads();
-    const uint64_t n0 = E->n0;
-    const uint64_t s = (uint64_t)t * tile, e = min(n0 - 1, s + tile);
-    // each thread takes SORT_PER = 8 consecutive positions per round (uint2 load
-    // + 1 byte); the next round's bytes are loaded before this round's LDS sort
-    auto fetch = [&](uint64_t p, uint2 *w, uint32_t *b8) {
-        *w = make_uint2(0, 0);
-        *b8 = 0;
-        if (p < e) {
-            *w = *reinterpret_cast<const uint2 *>(E->bytes + p);
-            *b8 = p + SORT_PER < n0 ? E->bytes[p + SORT_PER] : 0;
+    const uint64_t n0 = E->n0, nwords = (n0 + 3) / 4;
+    // pair positions [s, e); token positions [s, te) (the last tile owns n0 - 1)
+    const uint64_t s = (uint64_t)t * tile, e = min(n0 - 1, s + tile), te = min(n0, s + tile);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(E->bytes);
+    uint4 *tok4 = reinterpret_cast<uint4 *>(E->tok);
+    auto fetch = [&](uint64_t wb, uint32_t *x0, uint32_t *x1, uint32_t *b8) {
+        const uint64_t i0 = wb / 4 + lane, i1 = i0 + 64;
+        const bool in = wb < te;
+        *x0 = in && i0 < nwords ? src[i0] : 0u;
+        *x1 = in && i1 < nwords ? src[i1] : 0u;
+        *b8 = in && lane == 63 && wb + 512 < n0 ? E->bytes[wb + 512] : 0u;
+    };
+    auto store = [&](uint64_t wi, uint32_t x) {  // tok[4wi .. 4wi + 3] below te
+        if (4 * wi + 4 <= te) {
+            tok4[wi] = widen4(x);
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++)
+                if (4 * wi + k < te) E->tok[4 * wi + k] = (x >> (8 * k)) & 0xFF;
         }
     };
-    uint2 wn;
-    uint32_t bn;
-    fetch(s + threadIdx.x * SORT_PER, &wn, &bn);
-    for (uint64_t p0 = s + threadIdx.x * SORT_PER; p0 - threadIdx.x * SORT_PER < e; p0 += SORT_CH) {
+    uint32_t n0w, n1w, nb8;
+    fetch(s + wv * 512, &n0w, &n1w, &nb8);
+    for (uint64_t r0 = s; r0 < te; r0 += SORT_CH) {  // block-uniform rounds
+        const uint64_t wb = r0 + wv * 512;
+        const uint32_t x0 = n0w, x1 = n1w, b8 = nb8;
+        fetch(wb + SORT_CH, &n0w, &n1w, &nb8);
+        // the byte after each word (all lanes take part in the shuffles)
+        uint32_t nx0 = __shfl_down(x0, 1), nx1 = __shfl_down(x1, 1);
+        const uint32_t f = __shfl(x1, 0);
+        if (lane == 63) { nx0 = f; nx1 = b8; }
         uint32_t bins[SORT_PER], vals[SORT_PER];
-        uint32_t by[SORT_PER + 1];
-        const uint2 w = wn;
-        by[SORT_PER] = bn;
-        fetch(p0 + SORT_CH, &wn, &bn);
 #pragma unroll
-        for (uint32_t k = 0; k < 4; k++) { by[k] = (w.x >> (8 * k)) & 0xFF; by[4 + k] = (w.y >> (8 * k)) & 0xFF; }
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t x = h ? x1 : x0, nx = h ? nx1 : nx0;
+            const uint64_t p = wb + 256 * h + 4 * lane;
 #pragma unroll
-        for (uint32_t k = 0; k < SORT_PER; k++) {
-            const bool in = p0 + k < e;
-            bins[k] = in ? rk[by[k]] : 256u;
-            vals[k] = in ? (rk[by[k + 1]] << SORT_LOCAL_BITS) | (uint32_t)(p0 + k - s) : 0u;
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t b0 = (x >> (8 * k)) & 0xFF, b1 = k < 3 ? (x >> (8 * k + 8)) & 0xFF : nx & 0xFF;
+                const bool in = p + k < e;
+                bins[4 * h + k] = in ? rk[b0] : 256u;
+                vals[4 * h + k] = in ? (rk[b1] << SORT_LOCAL_BITS) | (uint32_t)(p + k - s) : 0u;
+            }
+            if (p < te) store(p / 4, x);
         }
         lds_sort_emit(L, bins, vals, A, tmp);
     }
