@@ -152,7 +152,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
     __shared__ BatHead sbh;
     __shared__ KV part[16][TOPK];
     __shared__ uint32_t srank[256];
-    __shared__ uint32_t clear_k, nmem;
+    __shared__ uint32_t clear_k, nmem, xclr_k, xclr_w;
     __shared__ uint32_t ctl[BK];
     constexpr uint32_t CW = sizeof(Ctl) / 4;
     static_assert(CW <= 1024 && BAT_HEAD_WORDS <= 1024, "staged one word per thread");
@@ -176,7 +176,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
     if (tid < CW) scw[tid] = cv;
     if (tid < BAT_HEAD_WORDS) sbw[tid] = bv;
     if (tid < 256) srank[tid] = rk;
-    if (tid == 0) clear_k = nmem = 0;
+    if (tid == 0) clear_k = nmem = xclr_k = 0;
     __syncthreads();
     block_list_tree(part, blockDim.x >> 6);
     ts_mark(E, bi, BT_SEL_LIST, false);
@@ -194,11 +194,16 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         const uint32_t olda = jst ? B->a[jst - 1] : 0, oldb = jst ? B->b[jst - 1] : 0, oldz0 = B->z0;
         const uint32_t oldsum = B->sumlen;
         const uint32_t raerr = aload(&Bg->ra_err);  // a token too long for an end code (rewrite blocks)
-        unsigned long long rs = lane < jst ? B->R[lane] : 0ull;
-        for (int o = 32; o > 0; o >>= 1) rs += __shfl_xor(rs, o);
+        const bool sh = E->sharded != 0;
+        unsigned long long rs = lane < jst ? B->R[lane] : 0ull;   // this shard's occurrences
+        unsigned long long rg = lane < jst ? (sh ? B->Rg[lane] : B->R[lane]) : 0ull;  // all shards'
+        for (int o = 32; o > 0; o >>= 1) {
+            rs += __shfl_xor(rs, o);
+            rg += __shfl_xor(rg, o);
+        }
         const unsigned long long D = C->D + (applied ? B->dD : 0ull);
         const uint32_t md = C->merges_done + jst;
-        const unsigned long long n_live = C->n_live - rs;
+        const unsigned long long n_live = C->n_live - rg;
         // ---- the list, one entry per lane
         const KV e = lane < TOPK ? part[0][lane] : kv_empty();
         const unsigned long long kprev = __shfl(e.k, (int)(lane ? lane - 1 : 0));
@@ -266,19 +271,34 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 cand_of(E, u, v, true, srank, E->poff, &mode, &off, &len);
                 tl = E->tlen[u] + E->tlen[v];
             }
-            // the members' candidates fit the occurrence staging (ids_out, n0 positions)
-            unsigned long long pre = len;  // inclusive prefix
+            // the members' candidates fit the occurrence staging (ids_out, n0
+            // positions; sharded: + one slot per member for the occurrence
+            // across my right edge, which no candidate list holds)
+            const uint32_t slot = len + (sh && lane < k ? 1u : 0u);
+            unsigned long long pre = slot;  // inclusive prefix
             for (int o = 1; o < 64; o <<= 1) {
                 const unsigned long long y = __shfl_up(pre, o);
                 if ((int)lane >= o) pre += y;
             }
             const unsigned long long over = __ballot(lane > 0 && lane < k && pre > E->n0);
             uint32_t why_end = endwhy == 8 ? 0 : endwhy;
-            if (over) {
-                k = (uint32_t)__ffsll(over) - 1;
+            // sharded: every shard must form the same batch, so a shard whose
+            // staging overflows scans nothing from that member on and flags it
+            // in the exchange; the verification then drops the batch there
+            const uint32_t ovm = over ? (uint32_t)__ffsll(over) - 1 : BK;
+            if (over && !sh) {
+                k = ovm;
                 why_end = 7;
             }
-            const unsigned long long sumlen = __shfl(pre, (int)(k - 1));
+            uint32_t slot_k = slot;
+            if (sh && lane >= ovm) len = slot_k = 0;
+            if (sh && ovm < k) {  // (members from ovm on scan nothing here)
+                const unsigned long long pcut = __shfl(pre, (int)ovm - 1);
+                if (lane >= ovm) pre = pcut;
+            }
+            const unsigned long long stage_end = __shfl(pre, (int)(k - 1));
+            unsigned long long sumlen = lane < k ? len : 0u;  // candidates
+            for (int o = 32; o > 0; o >>= 1) sumlen += __shfl_xor(sumlen, o);
             // scan blocks in proportion to the candidate lists (>= 1 each), the
             // rest to the largest member
             const uint32_t nb = lane < k ? 1 + (uint32_t)(sumlen ? (uint64_t)(BSB - k) * len / sumlen : 0) : 0;
@@ -299,16 +319,17 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->mode[lane] = mode;
                 B->off[lane] = off;
                 B->len[lane] = len;
-                B->sbase[lane] = (uint32_t)(pre - len);
+                B->sbase[lane] = (uint32_t)(pre - slot_k);
                 B->R[lane] = 0;
                 B->bound[lane] = 0;
                 B->blk0[lane] = bpre - nb + (lane > bigm ? extra : 0);
                 ctl[lane] = tl;
             }
             if (lane == 0) {
-                B->sbase[k] = (uint32_t)sumlen;
+                B->sbase[k] = (uint32_t)stage_end;
                 B->blk0[k] = BSB;
                 B->sumlen = (uint32_t)sumlen;
+                B->over = ovm < k ? ovm : BK;
                 B->why[why_end]++;
                 if (ties > 1) C->counters[2]++;
             }
@@ -344,6 +365,8 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->dD = 0;
             }
             clear_k = kpr;
+            xclr_k = sh && applied ? kpr : 0u;
+            xclr_w = oldz0 + kpr;
             C->hot_scanned += nhot;
             C->stop_z = C->z;
             C->B = Bsz;
@@ -361,9 +384,20 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
     }
     __syncthreads();
     if (tid < nmem) E->tlen[256 + sc.merges_done + tid] = ctl[tid];
-    for (uint32_t q = tid; q < CW; q += blockDim.x) reinterpret_cast<uint32_t *>(Cg)[q] = scw[q];
+    // the select's words of the control block; of the tail (which sharded
+    // runs' rewrite blocks write beside this launch: F1, L1new) only the two
+    // words the select changes
+    for (uint32_t q = tid; q < CTL_SELECT_WORDS; q += blockDim.x) reinterpret_cast<uint32_t *>(Cg)[q] = scw[q];
+    if (tid == 0) {
+        Cg->hot_scanned = sc.hot_scanned;
+        if (sc.err) Cg->err = sc.err;
+    }
     for (uint32_t q = tid; q < BAT_HEAD_WORDS; q += blockDim.x) reinterpret_cast<uint32_t *>(Bg)[q] = sbw[q];
     for (uint32_t q = tid; q < clear_k * 4; q += blockDim.x) E->bvnl[q] = 0;
+    if (xclr_k) {  // sharded: the words every k_bapply block's prologue read
+        if (tid < BK) E->xbat[tid] = 0;
+        if (tid < 2 * xclr_k) E->xbat[BK + (uint64_t)(tid >> 1) * xbat_member_words(xclr_w) + (tid & 1)] = 0;
+    }
     if (tid == 0 && sc.stop != STOP_NONE && E->hprobe) {
         __hip_atomic_store(E->hprobe, sc.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -415,9 +449,25 @@ __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat 
     if (tid < k && bid >= ablk[tid] && bid < ablk[tid + 1]) am = tid;
     __syncthreads();
     const uint32_t m = am;
+    const bool sh = E->sharded != 0;
+    uint32_t *tok = E->tok;
+    const uint64_t n = E->n0;
+    if (sh && bid == 0 && tid == 0) {
+        // my first token is the b of an occurrence the left shard owns: retired
+        const uint32_t xl = B->ra_xl;
+        if (xl != HOLE) {
+            const uint64_t end = (uint64_t)xl + B->ra_xlb;
+            if (end - 1 == xl) {
+                tok[xl] = MARKV;
+            } else {
+                tok[xl] = HOLE;
+                if (end - 1 < n) tok[end - 1] = MARKV;
+            }
+            C->F1 = (uint32_t)(end < n ? end : n);
+        }
+    }
     if (m < k) {
-        uint32_t *tok = E->tok;
-        const uint64_t n = E->n0;
+        const uint64_t L1 = sh ? C->L1 : ~0ull;
         const uint32_t z = sz[m], la = sla[m], lb = slb[m], Rm = sR[m], base = ssb[m], obase = stop_ + spre[m];
         const uint32_t bidm = bid - ablk[m], nbm = ablk[m + 1] - ablk[m];
         for (uint32_t e0 = bidm * blockDim.x * RU; e0 < Rm; e0 += nbm * blockDim.x * RU) {
@@ -435,12 +485,15 @@ __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat 
                 if (e >= Rm) continue;
                 const uint64_t i = pos[u], j = i + la, kq = j + lb;
                 tok[i] = z;
-                if (kq - 1 - i > E->end_max) B->ra_err = 5;  // (the select's staged control block would drop C->err)
-                if (kq - 1 == j) {
-                    tok[j] = end_code(kq - 1 - i);
-                } else {
-                    tok[j] = HOLE;
-                    if (kq - 1 < n) tok[kq - 1] = end_code(kq - 1 - i);
+                if (j < n) {  // (sharded: else b starts in a later shard, which retires it)
+                    if (kq - 1 - i > E->end_max) B->ra_err = 5;  // (the select's staged control block would drop C->err)
+                    if (kq - 1 == j) {
+                        tok[j] = end_code(kq - 1 - i);
+                    } else {
+                        tok[j] = HOLE;
+                        if (kq - 1 < n) tok[kq - 1] = end_code(kq - 1 - i);
+                    }
+                    if (j == L1) C->L1new = (uint32_t)i;  // my last token moved
                 }
                 E->occ[obase + e] = (uint32_t)i;
                 E->occnb[obase + e] = tg[u];
@@ -536,23 +589,48 @@ __device__ inline void vadd_b(uint32_t (*s)[DENSE], const Eng *E, uint32_t m, in
     if (v == V_DL || v == V_DR) atomicAdd(&gcnt[v], 1u);
 }
 
+// Sharded batches: the tokens just outside my shard (HL[m]: m-th token left
+// of my first token, HR[m]: right of my last one) and, per member, the a==b
+// run state at my edges (hlr: how many of its a precede my first token, myi:
+// the run index of my last token), from the edge records (shard_halo)
+struct BHalo {
+    uint32_t HL[3], HR[3], hlr[BK], myi[BK];
+};
+
+// token id at position p; SH: -1-m is HL[m], n+m is HR[m]
+template <bool SH>
+__device__ inline uint32_t tok_at_b(const uint32_t *__restrict__ tok, const BHalo &H, int64_t p, int64_t n) {
+    if (p < 0) return SH && p >= -3 ? get3(H.HL, (uint32_t)(-1 - p)) : HOLE;
+    if (p >= n) return SH && p - n < 3 ? get3(H.HR, (uint32_t)(p - n)) : HOLE;
+    return tok[p];
+}
+
 // The member whose occurrence covers the token p starting at ps (p is that
 // member's b and the token before it its a), or BK.  For an a == b member the
 // run of p ending at ps decides: greedy pairing from the run's first token
-// (bpe.c:760-772) makes p the second token of a pair iff the run is even.
+// (bpe.c:760-772) makes p the second token of a pair iff the run is even
+// (sharded: the run may continue into the shards on my left, H.hlr).
+template <bool SH>
 __device__ inline uint32_t cover_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const uint32_t *sa,
-                                    const uint32_t *sb, uint32_t p, int64_t ps) {
+                                    const uint32_t *sb, const BHalo &H, uint32_t p, int64_t ps, int64_t n) {
     uint32_t lmk, rmk;
     rt.get(p, &lmk, &rmk);
     if (!rmk) return BK;
-    const int64_t pps = v_left<false>(tok, ps);
-    const uint32_t pp = pps < 0 ? HOLE : tok[pps];
+    const int64_t pps = v_left<SH>(tok, ps);
+    const uint32_t pp = tok_at_b<SH>(tok, H, pps, n);
     for (uint32_t q = rmk; q; q &= q - 1) {
         const uint32_t mm = __ffs(q) - 1;
         if (sa[mm] != pp) continue;
         if (sa[mm] != sb[mm]) return mm;
-        uint32_t L = 2;  // p and pp; then the rest of the run leftwards
-        for (int64_t x = v_left<false>(tok, pps); x >= 0 && tok[x] == p; x = v_left<false>(tok, x)) L++;
+        uint32_t L;  // run of p ending at ps
+        if (SH && ps < 0) {
+            L = H.hlr[mm];
+        } else {
+            L = 1;
+            int64_t x = v_left<SH>(tok, ps);
+            for (; x >= 0 && tok[x] == p; x = v_left<SH>(tok, x)) L++;
+            if (SH && x < 0) L += H.hlr[mm];  // the run reaches my first token and goes on leftwards
+        }
         return (L & 1) ? BK : mm;
     }
     return BK;
@@ -561,13 +639,14 @@ __device__ inline uint32_t cover_of(const uint32_t *__restrict__ tok, const Role
 // The member whose occurrence starts at the token q at kq (q is its a and the
 // token after it its b: for a != b always an occurrence; for a == b q starts
 // a run -- the token before it is an occurrence's b -- so it pairs), or BK.
+template <bool SH>
 __device__ inline uint32_t starts_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const uint32_t *sb,
-                                     const uint32_t *sla, uint32_t q, int64_t kq, int64_t n) {
+                                     const uint32_t *sla, const BHalo &H, uint32_t q, int64_t kq, int64_t n) {
     uint32_t lmk, rmk;
     rt.get(q, &lmk, &rmk);
     if (!lmk) return BK;
     const int64_t kn = v_right(kq, sla[__ffs(lmk) - 1], n);
-    const uint32_t qq = kn < n ? tok[kn] : HOLE;
+    const uint32_t qq = tok_at_b<SH>(tok, H, kn, n);
     for (uint32_t t = lmk; t; t &= t - 1) {
         const uint32_t mm = __ffs(t) - 1;
         if (sb[mm] == qq) return mm;
@@ -575,6 +654,14 @@ __device__ inline uint32_t starts_of(const uint32_t *__restrict__ tok, const Rol
     return BK;
 }
 
+// Every member's occurrences in the pre-batch tokens and the batch's count
+// deltas.  SH (sharded corpus): neighbours beyond my edges come from the
+// halo; an occurrence whose a is my last token and whose b starts the next
+// shard is mine (the edge step below), one whose a ends the previous shard is
+// that shard's (I retire my first token, Bat::xl_m); deltas, occurrence
+// counts and bounds leave through the exchange buffer (xbat), summed over the
+// shards before k_bapply reads them.
+template <bool SH>
 __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, const Ctl *__restrict__ C) {
     if (C->stop) return;
     Bat *B = E->bat;
@@ -584,15 +671,16 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     __shared__ uint32_t s[4][DENSE];
     __shared__ uint32_t list[SCAN_T * SU];  // this round's occurrences (position, tag), flushed per round
     __shared__ uint16_t ltag[SCAN_T * SU];
-    __shared__ uint32_t lcount, gbase, list_n, covc, sm, sk, sz0;
+    __shared__ uint32_t lcount, gbase, list_n, covc, sm, sk, sz0, bRs;
     __shared__ uint32_t gcnt[2];
     __shared__ uint32_t sa[BK], sb[BK], sla[BK];
     __shared__ RoleTab rt;
+    __shared__ BHalo H;
     __shared__ uint32_t wmx[2][16];
     const uint32_t tid = threadIdx.x;
     if (tid == 0) {
         sm = BK;
-        covc = lcount = 0;
+        covc = lcount = bRs = 0;
         gcnt[0] = gcnt[1] = 0;
         sk = B->k;
         sz0 = B->z0;
@@ -618,6 +706,17 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     if (tid < k) {
         rt.put(sa[tid], false, tid);
         rt.put(sb[tid], true, tid);
+        if (SH) {
+            Halo h;
+            shard_halo(E->erec, E->nshards, E->shard, sa[tid], &h);
+            H.hlr[tid] = h.hlrun;
+            H.myi[tid] = h.myidx;
+            if (tid == 0)
+                for (int q = 0; q < 3; q++) {
+                    H.HL[q] = h.HL[q];
+                    H.HR[q] = h.HR[q];
+                }
+        }
     }
     const uint32_t a = sa[m], b = sb[m], z = z0 + m, la = sla[m];
     const uint32_t lb = E->tlen[b];
@@ -635,7 +734,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     for (uint32_t v = 0; v < 4; v++)
         for (uint32_t x = tid; x < lim; x += SCAN_T) s[v][x] = 0;
     __syncthreads();
-    auto tok_at = [&](int64_t p) -> uint32_t { return (p < 0 || p >= n) ? HOLE : tok[p]; };
+    auto tok_at = [&](int64_t p) -> uint32_t { return tok_at_b<SH>(tok, H, p, n); };
 
     if (a != b) {
         // SU candidates per thread per round, in stages, so that their chains of
@@ -682,8 +781,9 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 const int64_t j = jj[u];
                 if (mode == 2) {
                     // the b at j (its list), the a left of it from the end slot j-1
+                    // (i < 0: the a ends the left shard, whose occurrence it is)
                     const uint32_t wl = j > 0 ? W[u].at(j - 1) : HOLE;
-                    const int64_t i = j > 0 ? start_of_end<false>(wl, j - 1) : -1;
+                    const int64_t i = j > 0 ? start_of_end<SH>(wl, j - 1) : -1;
                     ii[u] = i;
                     if (W[u].at(j) != b || i < 0) continue;
                     const uint32_t ti = W[u].has(i) ? W[u].at(i) : tok[i];
@@ -692,6 +792,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     tr[u] = kk < n ? (W[u].has(kk) ? W[u].at(kk) : tok[kk]) : HOLE;
                     ok[u] = ti == a;
                 } else {
+                    // (j >= n: the b starts the next shard -- the edge step's)
                     const int64_t i = ii[u], kk = j + lb;
                     const uint32_t t1 = j >= n ? HOLE : W[u].has(j) ? W[u].at(j) : tok[j];
                     tl[u] = i > 0 ? W[u].at(i - 1) : HOLE;
@@ -705,8 +806,8 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
 #pragma unroll
             for (uint32_t u = 0; u < SU; u++) {
                 const int64_t i = ii[u];
-                ps[u] = i <= 0 ? -1 : start_of_end<false>(tl[u], i - 1);
-                pv[u] = (ok[u] && i > 0) ? (is_id(tl[u]) ? tl[u] : tok[ps[u]]) : HOLE;
+                ps[u] = i <= 0 ? -1 : start_of_end<SH>(tl[u], i - 1);
+                pv[u] = ok[u] ? ((i > 0 && is_id(tl[u])) ? tl[u] : tok_at(ps[u])) : HOLE;
             }
 #pragma unroll
             for (uint32_t u = 0; u < SU; u++) {
@@ -718,7 +819,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     const uint32_t p = pv[u];
                     lfin = p;
                     if (p != HOLE) {
-                        const uint32_t cv = cover_of(tok, rt, sa, sb, p, ps[u]);
+                        const uint32_t cv = cover_of<SH>(tok, rt, sa, sb, H, p, ps[u], n);
                         if (cv < BK) {
                             lfin = z0 + cv;
                             atomicAdd(&covc, 1u);
@@ -729,10 +830,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     }
                     // right neighbour: the a of a member's occurrence -> that id
                     const int64_t kq = v_right(j, lb, n);
-                    const uint32_t q = kq < n ? tr[u] : HOLE;
+                    const uint32_t q = kq < n ? tr[u] : tok_at(kq);
                     rfin = q;
                     if (q != HOLE) {
-                        const uint32_t st = starts_of(tok, rt, sb, sla, q, kq, n);
+                        const uint32_t st = starts_of<SH>(tok, rt, sb, sla, H, q, kq, n);
                         if (st < BK) rfin = z0 + st;
                         vadd_b(s, E, m, V_DR, q, gcnt);
                         vadd_b(s, E, m, V_IR, rfin, gcnt);
@@ -749,6 +850,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
             if (tid == 0) {
                 const uint32_t c = lcount;
                 gbase = c ? atomicAdd(Rm, c) : 0u;
+                bRs += c;
                 lcount = 0;
                 list_n = c;
             }
@@ -761,7 +863,8 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         }
     } else {
         // a == b (a batch of its own): the thread holding a run's first token
-        // walks it, pairing tokens 0-1, 2-3, ... (greedy left-to-right)
+        // walks it, pairing tokens 0-1, 2-3, ... (greedy left-to-right); a run
+        // that enters from the left shard continues its parity (H.hlr)
         for (uint32_t e0 = bid * SCAN_T; e0 < len; e0 += nblk * SCAN_T) {  // uniform trip count
             const uint32_t e = e0 + tid;
             int64_t i = 0;
@@ -770,7 +873,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
             } else if (mode == 2) {
                 const int64_t j = E->occ[off + e];
                 if (tag_ok(E->occnb[off + e] >> 8, want) && tok[j] == b) {
-                    i = v_left<false>(tok, j);
+                    i = v_left<SH>(tok, j);
                     ok = i >= 0 && tok[i] == a;
                 }
             } else {
@@ -778,30 +881,34 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 ok = (mode == 0 || tag_ok(E->occnb[off + e] & 0xFFu, want)) && tok[i] == a && i + la < n &&
                      tok[i + la] == b;
             }
-            const int64_t ps = ok ? v_left<false>(tok, i) : -1;
+            const int64_t ps = ok ? v_left<SH>(tok, i) : -1;
             const uint32_t p = ok ? tok_at(ps) : HOLE;
             // the run's left neighbour, unless another member's occurrence covers it
-            const uint32_t cv = (ok && p != HOLE && p != a) ? cover_of(tok, rt, sa, sb, p, ps) : BK;
+            const uint32_t cv = (ok && p != HOLE && p != a) ? cover_of<SH>(tok, rt, sa, sb, H, p, ps, n) : BK;
             if (cv < BK) atomicAdd(&covc, 1u);
-            const bool left = p != HOLE && cv == BK;
-            int64_t pos = i;
-            for (uint32_t mi = 0; ok && p != a; mi++) {  // (p == a: not the run's first token)
+            const bool left = p != HOLE && p != a && cv == BK;
+            // my first token continues a run of the left shard: pairs with its
+            // last token (the left shard's occurrence) when an odd number precede
+            const bool cont = SH && ok && p == a && ps < 0;
+            int64_t pos = (cont && (H.hlr[m] & 1)) ? i + la : i;
+            for (uint32_t mi = 0; ok && (p != a || cont); mi++) {  // (else: not the run's first token)
                 const int64_t jq = pos + la;
-                if (jq >= n || tok[jq] != a) break;
+                if (jq >= n || tok[jq] != a) break;  // (jq >= n: the pair across my right edge, the edge step's)
                 const int64_t kq = v_right(jq, la, n);
                 const uint32_t q = tok_at(kq);
                 const bool knext = q == a;
                 const bool nocc = knext && tok_at(v_right(kq, la, n)) == a;
                 // a right neighbour that starts another member's occurrence becomes its id
-                const uint32_t st = (!knext && q != HOLE) ? starts_of(tok, rt, sb, sla, q, kq, n) : BK;
+                const uint32_t st = (!knext && q != HOLE) ? starts_of<SH>(tok, rt, sb, sla, H, q, kq, n) : BK;
                 const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
-                const uint32_t pfin = mi > 0 ? z : (left ? p : cv < BK ? z0 + cv : HOLE);
+                const uint32_t pfin = (mi > 0 || cont) ? z : (left ? p : cv < BK ? z0 + cv : HOLE);
                 const uint32_t slot = atomicAdd(&lcount, 1u);
                 if (slot < SCAN_T * SU) {
                     list[slot] = (uint32_t)pos;
                     ltag[slot] = nb_tag(pfin, rq);
                 } else {  // (a long run overflows the round's list: straight out)
                     const uint32_t g = atomicAdd(Rm, 1u);
+                    atomicAdd(&bRs, 1u);
                     occz[g] = (uint32_t)pos;
                     tagz[g] = nb_tag(pfin, rq);
                 }
@@ -820,6 +927,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
             if (tid == 0) {
                 const uint32_t c = min(lcount, SCAN_T * SU);
                 gbase = c ? atomicAdd(Rm, c) : 0u;
+                bRs += c;
                 lcount = 0;
                 list_n = c;
             }
@@ -833,18 +941,75 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     }
     __syncthreads();
     ts_mark(E, bi, BT_SCAN_CAND, false, true);
-    // deltas into replica (block % BREPL) of the member's accumulators, and the
-    // member's new-key bound: per block max over ids (+ covered left
-    // neighbours, + every add that bypassed LDS), summed over blocks
-    uint32_t *rep = E->bvecd + (uint64_t)(m * BREPL + bid % BREPL) * 4 * DENSE;
+    const uint32_t Wx = z0 + k;  // SH: ids per delta vector in the exchange
+    uint32_t *xm = SH ? E->xbat + BK + (uint64_t)m * xbat_member_words(Wx) : nullptr;
+    if (SH && blockIdx.x == 0 && tid == 0) {
+        // Shard edges (thread 0 of block 0, beside the other blocks' flushes).
+        // Left: my first token is the b of an occurrence the left shard owns
+        // (k_bapply hands it to the rewrite, which retires the token).  Right:
+        // my last token and the first token after it form an occurrence I own.
+        uint32_t xlm = BK;
+        const int64_t F1 = C->F1, L1 = C->L1;
+        const uint32_t over = B->over;
+        if (F1 < n) {
+            const uint32_t tf = tok[F1], tl1 = tok[L1];
+            for (uint32_t mm = 0; mm < k; mm++)
+                if (H.HL[0] == sa[mm] && tf == sb[mm] && (sa[mm] != sb[mm] || (H.hlr[mm] & 1))) {
+                    xlm = mm;
+                    break;
+                }
+            for (uint32_t mm = 0; mm < k && mm < over; mm++) {
+                if (!(tl1 == sa[mm] && H.HR[0] == sb[mm] && (sa[mm] != sb[mm] || !(H.myi[mm] & 1)))) continue;
+                uint32_t *xo = E->xbat + BK + (uint64_t)mm * xbat_member_words(Wx);
+                const uint32_t zz = z0 + mm;
+                const int64_t ps = v_left<SH>(tok, L1);
+                const uint32_t p = tok_at(ps);
+                uint32_t lfin = p, bnd = 1;
+                if (p != HOLE) {
+                    const uint32_t cv = cover_of<SH>(tok, rt, sa, sb, H, p, ps, n);
+                    if (cv < BK) {
+                        lfin = z0 + cv;
+                        bnd = 2;
+                    } else {
+                        atomicAdd(&xo[2 + V_DL * Wx + p], 1u);
+                        atomicAdd(&xo[2 + V_IL * Wx + p], 1u);
+                    }
+                }
+                const uint32_t q = H.HR[1];
+                uint32_t rfin = q;
+                if (q != HOLE) {
+                    const uint32_t st = starts_of<SH>(tok, rt, sb, sla, H, q, n + 1, n);
+                    if (st < BK) rfin = z0 + st;
+                    atomicAdd(&xo[2 + V_DR * Wx + q], 1u);
+                    atomicAdd(&xo[2 + V_IR * Wx + rfin], 1u);
+                }
+                (void)zz;
+                const uint32_t g = atomicAdd(&B->R[mm], 1u);  // (its staging slice has one slot to spare)
+                E->ids_out[B->sbase[mm] + g] = (uint32_t)L1;
+                E->btag[B->sbase[mm] + g] = nb_tag(lfin, rfin);
+                atomicAdd(&xo[0], 1u);
+                atomicAdd(&xo[1], bnd);
+                break;
+            }
+        }
+        B->xl_m = xlm;
+        if (over < k) atomicAdd(&E->xbat[over], 1u);  // my staging overflowed there
+    }
+    // deltas into replica (block % BREPL) of the member's accumulators (SH:
+    // the exchange buffer), and the member's new-key bound: per block max over
+    // ids (+ covered left neighbours, + every add that bypassed LDS), summed
+    // over blocks
+    uint32_t *rep = SH ? xm + 2 : E->bvecd + (uint64_t)(m * BREPL + bid % BREPL) * 4 * DENSE;
+    const uint32_t vstride = SH ? Wx : DENSE;
     uint32_t mxl = 0, mxr = 0;
     for (uint32_t v = 0; v < 4; v++)
         for (uint32_t x = tid; x < lim; x += SCAN_T) {
             const uint32_t c = s[v][x];
-            if (c) atomicAdd(&rep[v * DENSE + x], c);
+            if (c) atomicAdd(&rep[v * vstride + x], c);
             if (v == V_DL) mxl = max(mxl, c);
             if (v == V_DR) mxr = max(mxr, c);
         }
+    if (SH && tid == 0 && bRs) atomicAdd(&xm[0], bRs);  // this block's occurrences, summed over shards
     if (k > 1) {
         for (int o = 32; o > 0; o >>= 1) {
             mxl = max(mxl, (uint32_t)__shfl_xor(mxl, o));
@@ -861,7 +1026,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 l = max(l, wmx[0][q]);
                 r = max(r, wmx[1][q]);
             }
-            atomicAdd(&B->bound[m], max(l + gcnt[V_DL] + covc, r + gcnt[V_DR]));
+            atomicAdd(SH ? &xm[1] : &B->bound[m], max(l + gcnt[V_DL] + covc, r + gcnt[V_DR]));
         }
     }
     ts_mark(E, bi, BT_SCAN_OUT, false, true);
@@ -869,6 +1034,8 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     __syncthreads();
     if (tid == 0) atomicMax(&B->sc_out, wall_clock64());
 }
+template __global__ void k_bscan<false>(const Eng *, const Ctl *);
+template __global__ void k_bscan<true>(const Eng *, const Ctl *);
 
 // ---------------------------------------------------------------- k_bapply
 __device__ inline uint64_t hinsert_c(const Eng *E, uint32_t u, uint32_t v, uint32_t *nins) {
@@ -894,13 +1061,16 @@ __device__ inline uint64_t hinsert_c(const Eng *E, uint32_t u, uint32_t v, uint3
 // several members or vectors takes each contribution separately, and since
 // within a batch old keys only fall and new keys only rise, D and the hot set
 // follow from each atomic's old value).
+// SH: the occurrence counts, bounds, deltas and staging-overflow flags come
+// summed over the shards from the exchange buffer (xbat), cleared as read.
+template <bool SH>
 __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     if (C->stop) return;
     Bat *B = E->bat;
     const uint32_t bi = bat_idx(E);
     ts_mark(E, bi, BT_APPLY_IN, true);
     if (threadIdx.x == 0) atomicMax(&B->ap_in, ~wall_clock64());
-    __shared__ uint32_t sa[BK], sb[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], snl[BK * 4 + 1];
+    __shared__ uint32_t sa[BK], sb[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], snl[BK * 4 + 1], sRg[BK];
     __shared__ uint32_t sk, sj, sz0;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     // prologue, wave 0, lane q = member q: the verified prefix, prefix sums of
@@ -910,7 +1080,21 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         const unsigned long long live0 = C->n_live;
         const bool in = lane < k;
         const uint32_t ma = in ? B->a[lane] : 0, mb = in ? B->b[lane] : 0;
-        const uint32_t R = in ? B->R[lane] : 0, cnt = in ? B->cnt[lane] : 0, bnd = in ? B->bound[lane] : 0;
+        const uint32_t R = in ? B->R[lane] : 0, cnt = in ? B->cnt[lane] : 0;
+        uint32_t bnd = in && !SH ? B->bound[lane] : 0;
+        unsigned long long ovm = 0;  // SH: members some shard could not stage
+        if (SH) {
+            uint32_t *xm = E->xbat + BK + (uint64_t)lane * xbat_member_words(z0 + k);
+            // (every block's prologue reads these words: the next select clears them)
+            if (in) {
+                const uint32_t rg = xm[0];
+                bnd = xm[1];
+                if (blockIdx.x == 0) B->Rg[lane] = rg;
+                sRg[lane] = rg;
+            }
+            const uint32_t ov = lane < BK ? E->xbat[lane] : 0;
+            ovm = __ballot(lane < k && ov != 0);
+        }
         const uint32_t sbase = in ? B->sbase[lane] : 0;
         const uint32_t nl0 = 2 * lane < 4 * k ? E->bvnl[2 * lane] : 0, nl1 = 2 * lane + 1 < 4 * k ? E->bvnl[2 * lane + 1] : 0;
         const uint32_t tla = in ? E->tlen[ma] : 0, tlb = in ? E->tlen[mb] : 0;
@@ -931,7 +1115,8 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         // member q is the argmax after the members before it: its count beats
         // every key they can create, and the run is still untracked then
         const bool fail = in && lane > 0 &&
-                          (!(pm < cnt) || (dt && (z0 + lane) % dt == 0) || (!E->fast && live0 - rex < TRACK_LIMIT));
+                          (!(pm < cnt) || (dt && (z0 + lane) % dt == 0) || (!E->fast && live0 - rex < TRACK_LIMIT) ||
+                           (ovm & ((2ull << lane) - 1ull)) != 0);
         const unsigned long long fm = __ballot(fail);
         uint32_t js = fm ? (uint32_t)__ffsll(fm) - 1 : k;
         if (js < k) {  // re-form the batch with the verified prefix; apply nothing
@@ -981,6 +1166,16 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         if (tid == 0) {
             B->ra_pre[js] = spre[js];
             B->ra_top = top;
+            uint32_t xl = HOLE, xlb = 0;
+            if (SH) {
+                const uint32_t xm = B->xl_m;
+                if (xm < js) {
+                    xl = C->F1;
+                    xlb = slb[xm];
+                }
+            }
+            B->ra_xl = xl;
+            B->ra_xlb = xlb;
             B->ra_done = 0;
             B->ra_k = js;
             B->jstar = js;
@@ -989,10 +1184,10 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     }
     // role B
     const uint32_t nB = gridDim.x, bidB = blockIdx.x;
-    const uint32_t Wd = min(DENSE, z0 + k);
-    const uint32_t per = 1 + 4 * Wd;
+    const uint32_t Wd = SH ? z0 + k : min(DENSE, z0 + k);
+    const uint32_t per = SH ? xbat_member_words(Wd) : 1 + 4 * Wd;
     const uint32_t dense_total = k * per;
-    const uint32_t total = dense_total + snl[k * 4];
+    const uint32_t total = dense_total + (SH ? 0u : snl[k * 4]);
     const uint32_t hotT = C->hot_T;
     const bool hot = E->hot != 0;
     long long dD = 0;
@@ -1000,7 +1195,21 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     for (uint32_t t0 = bidB * blockDim.x; t0 < total; t0 += nB * blockDim.x) {  // uniform per block
         const uint32_t t = t0 + tid;
         uint32_t m = BK, cat = 0, x = 0, val = 0;
-        if (t < dense_total) {
+        if (SH && t < dense_total) {
+            // [R, bound, DL, DR, IL, IR] per member (R and bound were read by the prologue)
+            m = t / per;
+            const uint32_t r = t % per;
+            if (r == 0) {
+                cat = 4;
+                val = sRg[m];
+            } else if (r >= 2) {
+                cat = (r - 2) / Wd;
+                x = (r - 2) % Wd;
+                uint32_t *pw = E->xbat + BK + (uint64_t)m * per + r;
+                val = *pw;
+                if (val) *pw = 0;
+            }
+        } else if (t < dense_total) {
             m = t / per;
             const uint32_t r = t % per;
             if (r == 0) {
@@ -1086,5 +1295,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     }
     ts_mark(E, bi, BT_APPLY_B, false, true);
 }
+template __global__ void k_bapply<false>(const Eng *, Ctl *);
+template __global__ void k_bapply<true>(const Eng *, Ctl *);
 
 }  // namespace bpeamd

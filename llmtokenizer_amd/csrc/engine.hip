@@ -245,6 +245,7 @@ struct bpe_gpu_ctx {
     uint32_t fast = 0;                     // schedule-free tie rule everywhere
     uint32_t sharded = 0, shard = 0, nshards = 1;
     uint32_t xfused = 0;                   // fused sharded step (P2P group, shard.hip)
+    uint32_t sbatch = 0;                   // sharded training in batches (shard.hip, batch.hip)
     const P2P *xp2p = nullptr;             // its exchange descriptor (device)
     unsigned long long xtimeout = 0;       // its wait bound (wall-clock ticks)
     Eng h{};
@@ -421,7 +422,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.spec_on = SPEC_ON && !encode && (!c->sharded || h.xfused);
     h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? 1 + SPEC_RB + SPEC_SB : 0);
     // hot-set argmax: untracked one-shard training with the speculative graph
-    h.hot = HOT_ON && h.spec_on && !c->sharded && (c->fast || n0 >= TRACK_LIMIT) ? 1 : 0;
+    // (sharded: the batch engine's runs)
+    h.hot = HOT_ON && !encode && (c->sharded ? c->sbatch != 0 : h.spec_on && (c->fast || n0 >= TRACK_LIMIT)) ? 1 : 0;
     // byte-pair list rebuilds (STOP_RELIST, opt-in with BPE_RELIST=1): they
     // cut configs[2]'s scanned candidates from 974 M to 0.48-0.53 G with
     // identical merges, but the late merges did not get faster
@@ -453,7 +455,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     }
     // batched training (batch.hip): the hot set's one-shard runs
     // (BPE_BATCH=0: one merge per kernel pair, the speculative graph; read per run)
-    h.batch = getenv_int("BPE_BATCH", 1) && h.hot && h.vcap <= BATCH_VCAP_MAX ? 1 : 0;
+    h.batch = getenv_int("BPE_BATCH", 1) && h.hot && h.vcap <= BATCH_VCAP_MAX && (!c->sharded || h.vcap <= DENSE) ? 1 : 0;
+    h.xbat = nullptr;
     h.bat = nullptr;
     h.btag = nullptr;
     h.bvecd = h.bvec = h.bvlist = h.bvnl = nullptr;
@@ -465,6 +468,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         if ((r = dalloc(c, &h.bvec, (size_t)BK * 4 * h.bvs))) return r;
         if ((r = dalloc(c, &h.bvlist, (size_t)BK * 4 * h.bvs, false))) return r;
         if ((r = dalloc(c, &h.bvnl, (size_t)BK * 4))) return r;
+        // sharded: the batch exchange (zero between batches; a multiple of 4 words)
+        if (c->sharded && (r = dalloc(c, &h.xbat, (xbat_words(BK, h.vcap) + 3) / 4 * 4))) return r;
         // BPE_BATCH_DROP_TEST=d: the verification drops members j >= 1 of id
         // z = 0 mod d (tests drive the drop path with it)
         const uint32_t dt = (uint32_t)getenv_int("BPE_BATCH_DROP_TEST", 0);
@@ -654,8 +659,8 @@ void launch_argmax_inputs(bpe_gpu_ctx *c) {
 
 // one batch: scan, verify + apply, select the next (batch.hip)
 void launch_batch(bpe_gpu_ctx *c) {
-    k_bscan<<<BSB, SCAN_T, 0, c->st>>>(c->dE, c->dC);
-    k_bapply<<<BAPPLY_B, 1024, 0, c->st>>>(c->dE, c->dC);
+    k_bscan<false><<<BSB, SCAN_T, 0, c->st>>>(c->dE, c->dC);
+    k_bapply<false><<<BAPPLY_B, 1024, 0, c->st>>>(c->dE, c->dC);
     k_bsel<<<BRB + BAPPLY_A, 1024, 0, c->st>>>(c->dE, c->dC);
 }
 
@@ -1310,6 +1315,43 @@ void print_batch_timeline(bpe_gpu_ctx *c, uint64_t nb) {
     fprintf(stderr, " sel out -> next scan in %.2f\n", ng ? gap / ng : 0.0);
 }
 
+// the batch engine's counters (Bat head) into c->stats (+ BPE_DEBUG reports)
+int batch_stats(bpe_gpu_ctx *c) {
+    if (!c->h.bat) return 0;
+    Bat hb;
+    HIPCHK(hipMemcpy(&hb, c->h.bat, offsetof(Bat, pv), hipMemcpyDeviceToHost));
+    c->stats.batches = hb.nbatch;
+    c->stats.batch_dropped = hb.ndrop;
+    c->stats.batch_retries = hb.nretry;
+    c->stats.table_updates = hb.nupd;
+    if (hb.nspan) {
+        int khz = 0;
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
+        if (khz > 0) {
+            c->stats.ms_scan_span = (double)hb.sc_ticks / hb.nspan / khz;
+            c->stats.ms_apply_span = (double)hb.ap_ticks / hb.nspan / khz;
+        }
+    }
+    if (c->h.dbgts) print_batch_timeline(c, hb.nbatch + hb.nretry);
+    if (getenv("BPE_DEBUG"))
+        fprintf(stderr, "batches %llu, dropped %llu, re-formed %llu; formation ended by: list %llu, cap/count/hot_T %llu, a==b %llu, "
+                "duplicate %llu, tie %llu, conflict %llu, table margin %llu, staging %llu\n", hb.nbatch, hb.ndrop, hb.nretry,
+                hb.why[0], hb.why[1], hb.why[2], hb.why[3], hb.why[4], hb.why[5], hb.why[6], hb.why[7]);
+    return 0;
+}
+
+// the batch engine's dominant kernel for bench.py's roofline: k_bscan, 8 B per
+// candidate (its list entry and the token word it validates) + 20 B per
+// occurrence (partner, both neighbours, the staged list entry), per launch
+void batch_profile(bpe_gpu_ctx *c) {
+    if (!c->stats.batches) return;
+    const double nl = (double)(c->stats.batches + c->stats.batch_retries);
+    c->prof_name = "k_bscan";
+    c->prof_ms = c->stats.ms_scan_span;
+    c->prof_bytes = (8.0 * c->stats.candidates + 20.0 * c->stats.occurrences) / nl;
+    c->prof_launches = (uint64_t)nl;
+}
+
 int compact_ids(bpe_gpu_ctx *c) {
     // single pass (k_live_compact): tile status words + ticket + total, zeroed
     int r;
@@ -1870,27 +1912,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.hot_scanned = C.hot_scanned;
     c->stats.hot_mode = c->h.hot ? 1 : c->hot_fallback ? 2 : 0;
     c->stats.relists = c->relists;
-    if (c->h.bat) {
-        Bat hb;
-        HIPCHK(hipMemcpy(&hb, c->h.bat, offsetof(Bat, pv), hipMemcpyDeviceToHost));
-        c->stats.batches = hb.nbatch;
-        c->stats.batch_dropped = hb.ndrop;
-        c->stats.batch_retries = hb.nretry;
-        c->stats.table_updates = hb.nupd;
-        if (hb.nspan) {
-            int khz = 0;
-            (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
-            if (khz > 0) {
-                c->stats.ms_scan_span = (double)hb.sc_ticks / hb.nspan / khz;
-                c->stats.ms_apply_span = (double)hb.ap_ticks / hb.nspan / khz;
-            }
-        }
-        if (c->h.dbgts) print_batch_timeline(c, hb.nbatch + hb.nretry);
-        if (getenv("BPE_DEBUG"))
-            fprintf(stderr, "batches %llu, dropped %llu, re-formed %llu; formation ended by: list %llu, cap/count/hot_T %llu, a==b %llu, "
-                    "duplicate %llu, tie %llu, conflict %llu, table margin %llu, staging %llu\n", hb.nbatch, hb.ndrop, hb.nretry,
-                    hb.why[0], hb.why[1], hb.why[2], hb.why[3], hb.why[4], hb.why[5], hb.why[6], hb.why[7]);
-    }
+    if ((r = batch_stats(c))) return r;
     if (c->h.dbgts) print_timeline(c, C.z);
     if (getenv("BPE_DEBUG"))
         fprintf(stderr, "select phases (ticks/iter): reduce %.1f merge %.1f tail %.1f\n",
@@ -1900,16 +1922,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.ms_train = t2 - t1;
     c->stats.ms_total = t2 - t0;
     fill_profile(c);
-    if (c->stats.batches) {
-        // the batch engine's dominant kernel: k_bscan, 8 B per candidate (its
-        // list entry and the token word it validates) + 20 B per occurrence
-        // (partner, both neighbours, the staged list entry), per launch
-        const double nl = (double)(c->stats.batches + c->stats.batch_retries);
-        c->prof_name = "k_bscan";
-        c->prof_ms = c->stats.ms_scan_span;
-        c->prof_bytes = (8.0 * c->stats.candidates + 20.0 * c->stats.occurrences) / nl;
-        c->prof_launches = (uint64_t)nl;
-    }
+    batch_profile(c);
     return 0;
 }
 

@@ -132,14 +132,26 @@ struct Bat {
     uint32_t a[BK], b[BK], cnt[BK], mode[BK], off[BK], len[BK];
     uint32_t blk0[BK + 1];            // k_bscan block range of each member
     uint32_t sbase[BK + 1];           // member's slice of the occurrence staging area (prefix of len)
-    uint32_t R[BK];                   // occurrences found (k_bscan, atomic)
+    uint32_t R[BK];                   // occurrences found (k_bscan, atomic; sharded: this shard's)
     uint32_t bound[BK];               // bound on the count any key made by the member can reach (atomic)
+    uint32_t Rg[BK];                  // sharded: occurrences over all shards (k_bapply, from the exchange)
+    uint32_t over;                    // sharded: first member whose candidates overflow this shard's staging
+    uint32_t xl_m;                    // sharded: member whose occurrence (owned by the left shard) ends at
+                                      // my first token (k_bscan's edge step), else BK
+    uint32_t pad4, pad5;
     unsigned long long pv[BRB * TOPK], pk[BRB * TOPK];  // k_bsel partial lists: packed value, key
     // the applied batch's token rewrite (role A), done by k_bsel's extra blocks
     // beside the selection; written by k_bapply (the select never touches it)
     uint32_t ra_k, ra_top, ra_done, ra_err;  // members (0: nothing pending), pool offset, blocks finished, error
     uint32_t ra_z[BK], ra_la[BK], ra_lb[BK], ra_R[BK], ra_sbase[BK], ra_pre[BK + 1];
+    uint32_t ra_xl, ra_xlb;           // sharded: my first token, retired (its b's length), or HOLE
 };
+
+// Sharded batches: the words one batch exchanges (summed over the shards):
+// [BK] staging-overflow flags, then per member [R, bound, DL, DR, IL, IR] with
+// the four delta vectors dense over the ids < z0 + k (the batch's W)
+__host__ __device__ inline uint32_t xbat_member_words(uint32_t W) { return 2 + 4 * W; }
+__host__ __device__ inline uint32_t xbat_words(uint32_t k, uint32_t W) { return BK + k * xbat_member_words(W); }
 
 // Device-resident descriptor: every kernel takes a pointer to it, so tables can
 // be regrown without re-capturing the iteration graph.
@@ -226,6 +238,7 @@ struct Eng {
     uint32_t *bvec;       // [BK][4][bvs] ids >= DENSE (x - DENSE), listed on first touch in bvlist
     uint32_t *bvlist;     // [BK][4][bvs]
     uint32_t *bvnl;       // [BK][4] list lengths
+    uint32_t *xbat;       // sharded batches: the exchange buffer (xbat_words), zero between batches
     // longest token span (end distance) an end code may hold: END_MAX, or less
     // for tests (BPE_END_MAX) that drive the over-long-token error paths
     uint64_t end_max;

@@ -1867,6 +1867,17 @@ __global__ __launch_bounds__(256) void k_xsum(uint32_t *const *__restrict__ bufs
     }
 }
 
+// the batch form: the batch's words only (its size from shard 0's descriptor)
+__global__ __launch_bounds__(256) void k_xbsum(uint32_t *const *__restrict__ bufs, uint32_t nb,
+                                               const Bat *__restrict__ B) {
+    const uint32_t count = xbat_words(B->k, B->z0 + B->k);
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += gridDim.x * blockDim.x) {
+        uint32_t sum = 0;
+        for (uint32_t q = 0; q < nb; q++) sum += bufs[q][t];
+        for (uint32_t q = 0; q < nb; q++) bufs[q][t] = sum;
+    }
+}
+
 __global__ void k_xgather(uint32_t *const *__restrict__ src, uint32_t *const *__restrict__ dst, uint32_t nb,
                           uint32_t words) {
     for (uint32_t t = threadIdx.x; t < nb * words; t += blockDim.x)

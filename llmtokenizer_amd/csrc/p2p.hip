@@ -29,7 +29,9 @@ constexpr uint32_t MB_FLAG0 = 0;             // [rank * 16]: sum channel flags (
 constexpr uint32_t MB_FLAG1 = 16 * P2P_MAXR; // [rank * 16]: gather channel flags
 constexpr uint32_t MB_DATA1 = 32 * P2P_MAXR; // [2][P2P_MAXR][EDGE_WORDS]
 constexpr uint32_t MB_DATA0 = MB_DATA1 + 2 * P2P_MAXR * EDGE_WORDS;  // [2][W][c0]
-enum { XS_SEQ0 = 0, XS_PUSH0 = 1, XS_SEQ1 = 2, XS_ERR = 3 };
+// (words 4..7: group_total's scratch)
+enum { XS_SEQ0 = 0, XS_PUSH0 = 1, XS_SEQ1 = 2, XS_ERR = 3, XS_TMP = 4, XS_SEQB = 8, XS_PUSHB = 9, XS_PEER = 16 };
+constexpr uint32_t XS_WORDS = XS_PEER + P2P_MAXR;  // g->xs
 constexpr uint32_t P2P_ERR_BIT = 16;  // Ctl::err bit of a timed-out exchange
 
 struct P2P {
@@ -125,6 +127,58 @@ __global__ __launch_bounds__(256) void k_p2p_sum(const P2P *__restrict__ X, uint
     }
     // every block read seq before it pushed; block 0 passed the push count
     if (blockIdx.x == 0 && tid == 0) X->xs[XS_SEQ0] = seq;
+}
+
+// Sum channel, batch form (sharded batches): buf[0 .. xbat_words(k, z0 + k))
+// := sum over ranks, with the size read from the batch descriptor (identical
+// on every rank), so the graph-captured launch moves only the batch's words.
+// Grid W x PSLICE: block b pushes slice b / W of the buffer to rank
+// (me + b) % W (the last of a rank's slices to land stores my flag there),
+// then, once every rank's flag is in, reduces a 1/grid share of the words.
+constexpr uint32_t PSLICE = 16;
+
+__global__ __launch_bounds__(256) void k_p2p_bsum(const P2P *__restrict__ X, uint32_t *__restrict__ buf,
+                                                  const Bat *__restrict__ B) {
+    const uint32_t W = X->W, me = X->rank, c0 = X->c0, tid = threadIdx.x, G = gridDim.x;
+    const uint32_t count = xbat_words(B->k, B->z0 + B->k);
+    const uint32_t seq = X->xs[XS_SEQ0] + 1u, par = seq & 1u;
+    const uint32_t sb = X->xs[XS_SEQB] + 1u;  // batch sums so far, this one included
+    const uint32_t p = (me + blockIdx.x) % W, sl = blockIdx.x / W, ns = G / W;
+    const uint32_t nv = (count + 3) / 4;  // (the buffer is zero past count, up to a multiple of 4)
+    const uint32_t per = (nv + ns - 1) / ns;
+    uint32_t *dst = X->mb[p] + MB_DATA0 + ((uint64_t)par * W + me) * c0;
+    for (uint32_t i = sl * per + tid; i < min(nv, (sl + 1) * per); i += blockDim.x)
+        sys_store4(dst + 4 * i, reinterpret_cast<const uint4 *>(buf)[i]);
+    p2p_release_point();
+    if (tid == 0) {
+        if (X->fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        const uint32_t landed = __hip_atomic_fetch_add(X->xs + XS_PEER + p, 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        if (landed == ns * sb)  // my last slice for rank p: my flag there
+            __hip_atomic_store(X->mb[p] + MB_FLAG0 + 16 * me, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_add(X->xs + XS_PUSHB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned long long t0 = wall_clock64();
+    if (tid < W) p2p_wait(X, X->mb[me] + MB_FLAG0 + 16 * tid, seq, t0);
+    else if (tid == 64) p2p_wait(X, X->xs + XS_PUSHB, G * sb, t0);  // every block pushed: buf may change
+    if (X->fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __syncthreads();
+    const uint32_t *src = X->mb[me] + MB_DATA0 + (uint64_t)par * W * c0;
+    const uint32_t share = (nv + G - 1) / G;
+    for (uint32_t i = blockIdx.x * share + tid; i < min(nv, (blockIdx.x + 1) * share); i += blockDim.x) {
+        uint4 s = make_uint4(0, 0, 0, 0);
+        for (uint32_t r = 0; r < W; r++) {
+            const uint32_t *q = src + (uint64_t)r * c0 + 4 * i;
+            s.x += sys_load(q); s.y += sys_load(q + 1); s.z += sys_load(q + 2); s.w += sys_load(q + 3);
+        }
+        reinterpret_cast<uint4 *>(buf)[i] = s;
+    }
+    // every block read seq before it pushed; block 0 passed the push count
+    if (blockIdx.x == 0 && tid == 0) {
+        X->xs[XS_SEQ0] = seq;
+        X->xs[XS_SEQB] = sb;
+        __hip_atomic_fetch_add(X->xs + XS_PUSH0, W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (k_p2p_sum's count)
+    }
 }
 
 // Gather channel: dst[r * EDGE_WORDS + w] := rank r's src[w].  One wave.

@@ -230,6 +230,55 @@ int launch_group_iteration(bpe_gpu_group *g) {
     return 0;
 }
 
+// the batch exchange: xbat summed over the shards (its size from the batch
+// descriptor where the transport allows: P2P and the one-device sum; RCCL
+// moves the largest batch's words)
+int ex_bsum(bpe_gpu_group *g) {
+    bpe_gpu_ctx *c0 = g->cs[0];
+    if (g->p2p) {
+        k_p2p_bsum<<<g->hp.W * PSLICE, 256, 0, g->st>>>(g->d_p2p, c0->h.xbat, c0->h.bat);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
+    if (g->rccl) {
+        const size_t count = xbat_words(BK, c0->h.vcap);
+        ncclResult_t e = g->rccl->allReduce(c0->h.xbat, c0->h.xbat, count, ncclUint32, ncclSum, g->comm, g->st);
+        if (e != ncclSuccess) return rccl_fail(g->rccl, "ncclAllReduce", e);
+        return 0;
+    }
+    const uint32_t K = (uint32_t)g->cs.size();
+    if (K == 1) return 0;
+    k_xbsum<<<256, 256, 0, g->st>>>(g->d_ptrs + 3 * K, K, c0->h.bat);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// Sharded batches (batch.hip): every shard scans the batch's members in its
+// tokens, the deltas are summed over the shards, every shard verifies and
+// applies the same prefix to its replica of the table and selects the same
+// next batch (beside its own token rewrite), and the shards' new edge
+// records are gathered for the next scan's halo.  Two exchanges per batch of
+// up to BK merges instead of two per merge.
+int launch_group_bstep(bpe_gpu_group *g) {
+    int r;
+    for (bpe_gpu_ctx *c : g->cs) k_bscan<true><<<BSB, SCAN_T, 0, g->st>>>(c->dE, c->dC);
+    if ((r = ex_bsum(g))) return r;
+    for (bpe_gpu_ctx *c : g->cs) k_bapply<true><<<BAPPLY_B, 1024, 0, g->st>>>(c->dE, c->dC);
+    for (bpe_gpu_ctx *c : g->cs) k_bsel<<<BRB + BAPPLY_A, 1024, 0, g->st>>>(c->dE, c->dC);
+    for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 1);  // (after the rewrite)
+    HIPCHK(hipGetLastError());
+    return ex_records(g, g->d_ptrs);
+}
+
+// after a host-side stop: the next selection on every shard (its rewrite
+// blocks finish any pending one), then the records of the current tokens
+int group_bselect(bpe_gpu_group *g) {
+    for (bpe_gpu_ctx *c : g->cs) k_bsel<<<BRB + BAPPLY_A, 1024, 0, g->st>>>(c->dE, c->dC);
+    for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 1);
+    HIPCHK(hipGetLastError());
+    return ex_records(g, g->d_ptrs);
+}
+
 // one encode batch on every shard: scan, apply (+ next batch), edge records
 int launch_group_batch(bpe_gpu_group *g) {
     for (bpe_gpu_ctx *c : g->cs) k_scan_batch<true><<<SCAN_BLOCKS, ESCAN_T, 0, g->st>>>(c->dE, c->dC);
@@ -280,6 +329,7 @@ int launch_group_redo(bpe_gpu_group *g) {
 
 int group_step(bpe_gpu_group *g) {
     if (g->encoding) return launch_group_batch(g);
+    if (g->cs[0]->h.batch) return launch_group_bstep(g);
     if (group_fused(g)) {
         launch_group_fused(g);
         HIPCHK(hipGetLastError());
@@ -292,7 +342,8 @@ int capture_group(bpe_gpu_group *g) {
     hipGraph_t gr;
     HIPCHK(hipStreamBeginCapture(g->st, hipStreamCaptureModeThreadLocal));
     int r = 0;
-    for (uint32_t k = 0; k < ITERS_PER_GRAPH && !r; k++) r = group_step(g);
+    const uint32_t steps = (!g->encoding && g->cs[0]->h.batch) ? BATCHES_PER_GRAPH : ITERS_PER_GRAPH;
+    for (uint32_t k = 0; k < steps && !r; k++) r = group_step(g);
     hipError_t e = hipStreamEndCapture(g->st, &gr);
     if (r || e != hipSuccess) {
         (void)hipGetLastError();
@@ -305,6 +356,24 @@ int capture_group(bpe_gpu_group *g) {
         g->graph = nullptr;
         return fail(BPE_GPU_EHIP, "hipGraphInstantiate", e);
     }
+    return 0;
+}
+
+// batch runs after a hot-set rebuild: the next batch, or (every shard gave
+// the hot set up alike: the same table) the one-merge sharded step from the
+// level summaries
+int group_after_rebuild(bpe_gpu_group *g) {
+    int r;
+    if (g->cs[0]->h.batch) return group_bselect(g);
+    group_free_graph(g);  // (the batch graph)
+    for (bpe_gpu_ctx *c : g->cs) {
+        if (c->h.batch) return fail(BPE_GPU_EINTERNAL, "shards diverged (hot set)");
+        launch_summaries(c);
+        k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
+    }
+    for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 1);
+    HIPCHK(hipGetLastError());
+    if ((r = ex_records(g, g->d_ptrs))) return r;
     return 0;
 }
 
@@ -354,7 +423,8 @@ int drive_group(bpe_gpu_group *g) {
             } else if (g->graph) {
                 HIPCHK(hipGraphLaunch(g->graph, g->st));
             } else {
-                for (uint32_t k = 0; k < ITERS_PER_GRAPH; k++)
+                const uint32_t steps = (!g->encoding && g->cs[0]->h.batch) ? BATCHES_PER_GRAPH : ITERS_PER_GRAPH;
+                for (uint32_t k = 0; k < steps; k++)
                     if ((r = group_step(g))) return r;
             }
             break;
@@ -367,7 +437,28 @@ int drive_group(bpe_gpu_group *g) {
             return fail(BPE_GPU_EINTERNAL, (C0.err & P2P_ERR_BIT) ? "p2p exchange timed out (a peer rank stopped or diverged)"
                                            : C0.err == 1 ? "engine invariant violated (count decrement of an absent pair)"
                                                          : "pair table full");
+        case STOP_HOT: {  // batch runs: the hot set's rebuild, the same on every shard
+            if (!g->cs[0]->h.batch) return fail(BPE_GPU_EINTERNAL, "unexpected stop state in sharded training");
+            for (bpe_gpu_ctx *c : g->cs) {
+                c->hC->stop = STOP_NONE;
+                if ((r = push_ctl(c))) return r;
+                if ((r = hot_rebuild(c))) return r;
+            }
+            if ((r = group_after_rebuild(g))) return r;
+            break;
+        }
         case STOP_GROW:
+            if (g->cs[0]->h.batch) {
+                for (bpe_gpu_ctx *c : g->cs) {
+                    c->hC->stop = STOP_NONE;
+                    c->hC->full = 1;
+                    if ((r = push_ctl(c))) return r;
+                    if ((r = grow_table(c, c->h.hcap * 4))) return r;
+                    if ((r = hot_rebuild(c))) return r;  // (slots moved)
+                }
+                if ((r = group_after_rebuild(g))) return r;
+                break;
+            }
             // the captured steps read the tables through the device descriptors;
             // recapture only when the level-2 summary launch appears
             if (g->cs[0]->h.hcap / L1W <= SELECT_L1_MAX && 4 * g->cs[0]->h.hcap / L1W > SELECT_L1_MAX) {
@@ -402,7 +493,7 @@ int group_total(bpe_gpu_group *g, uint64_t *tot) {
         return 0;
     }
     if (g->p2p) {  // n0 < 2^32 per rank, <= 16 ranks: 24-bit halves sum without carry
-        uint32_t *d = g->xs + 4;
+        uint32_t *d = g->xs + XS_TMP;
         const uint32_t w[4] = {(uint32_t)(local & 0xFFFFFF), (uint32_t)(local >> 24), 0, 0};
         HIPCHK(hipMemcpyAsync(d, w, 16, hipMemcpyHostToDevice, g->st));
         int r;
@@ -451,7 +542,11 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         c->sharded = 1;
         c->shard = g->shard0 + k;
         c->nshards = g->nshards;
-        c->xfused = g->p2p && K == 1 && FUSED_SH;
+        // batches: schedule-free ties (sharded runs always), dense exchange
+        // vectors over the whole vocabulary, a mailbox slot that holds them
+        const uint64_t vc = 256 + cap;
+        c->sbatch = getenv_int("BPE_BATCH", 1) && vc <= DENSE && (!g->p2p || xbat_words(BK, (uint32_t)vc) <= g->hp.c0);
+        c->xfused = g->p2p && K == 1 && FUSED_SH && !c->sbatch;
         c->xtimeout = g->hp.timeout;
         c->xp2p = c->xfused ? g->d_p2p : nullptr;
         if ((r = setup_run(c, (uint32_t)cap, false))) return r;
@@ -461,13 +556,14 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     // pointer tables for the one-device exchange
     if (local_mode(g)) {
         if (!g->d_ptrs) {
-            HIPCHK(hipMalloc(&g->d_ptrs, 3ull * K * sizeof(uint32_t *)));
+            HIPCHK(hipMalloc(&g->d_ptrs, 4ull * K * sizeof(uint32_t *)));
             HIPCHK(hipMalloc(&g->d_ptrs_tmp, (size_t)K * sizeof(uint32_t *)));
         }
         std::vector<uint32_t *> t;
         for (auto *c : g->cs) t.push_back(c->h.xbuf);
         for (auto *c : g->cs) t.push_back(c->h.myrec);
         for (auto *c : g->cs) t.push_back(c->h.erec);
+        for (auto *c : g->cs) t.push_back(c->h.xbat);  // (batch runs)
         if ((r = upload_table(g, g->d_ptrs, t))) return r;
     }
     // 1. global byte alphabet
@@ -505,9 +601,17 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
         for (auto *c : g->cs) HIPCHK(hipMemsetAsync(c->h.xbuf, 0, 2ull * c->h.xstride * 4, g->st));
     }
-    for (bpe_gpu_ctx *c : g->cs) {
-        launch_summaries(c);
-        k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
+    if (g->cs[0]->h.batch) {
+        // the hot set and the first batch (the records of the initial tokens
+        // are current: gathered above)
+        for (bpe_gpu_ctx *c : g->cs)
+            if ((r = hot_rebuild(c))) return r;
+        if ((r = group_after_rebuild(g))) return r;
+    } else {
+        for (bpe_gpu_ctx *c : g->cs) {
+            launch_summaries(c);
+            k_select<<<1, 1024, 0, g->st>>>(c->dE, c->dC, 0u);
+        }
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(g->st));
@@ -525,8 +629,22 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         nout += c->ids_len;
         ncand += c->hC->counters[4];  // this shard's candidates and occurrences
         nocc += c->hC->counters[5];
+        c->stats.candidates = c->hC->counters[4];
+        c->stats.occurrences = c->hC->counters[5];
         fill_profile(c);
+        if ((r = batch_stats(c))) return r;
+        batch_profile(c);
     }
+    const bpe_gpu_stats &s0 = g->cs[0]->stats;
+    g->stats.batches = s0.batches;
+    g->stats.batch_dropped = s0.batch_dropped;
+    g->stats.batch_retries = s0.batch_retries;
+    g->stats.table_updates = s0.table_updates;
+    g->stats.ms_scan_span = s0.ms_scan_span;
+    g->stats.ms_apply_span = s0.ms_apply_span;
+    g->stats.hot_rebuilds = g->cs[0]->hC->hot_rebuilds;
+    g->stats.hot_scanned = g->cs[0]->hC->hot_scanned;
+    g->stats.hot_mode = g->cs[0]->h.hot ? 1 : 0;
     g->stats.candidates = ncand;
     g->stats.occurrences = nocc;
     const Ctl &C = *g->cs[0]->hC;
@@ -772,13 +890,14 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
     }
     if (local_mode(g)) {
         if (!g->d_ptrs) {
-            HIPCHK(hipMalloc(&g->d_ptrs, 3ull * K * sizeof(uint32_t *)));
+            HIPCHK(hipMalloc(&g->d_ptrs, 4ull * K * sizeof(uint32_t *)));
             HIPCHK(hipMalloc(&g->d_ptrs_tmp, (size_t)K * sizeof(uint32_t *)));
         }
         std::vector<uint32_t *> t;
         for (auto *c : g->cs) t.push_back(c->h.xbuf);
         for (auto *c : g->cs) t.push_back(c->h.myrec);
         for (auto *c : g->cs) t.push_back(c->h.erec);
+        for (auto *c : g->cs) t.push_back(c->h.xbat);  // (batch runs)
         if ((r = upload_table(g, g->d_ptrs, t))) return r;
     }
     for (bpe_gpu_ctx *c : g->cs) {
@@ -921,8 +1040,13 @@ static int group_create_p2p(int device, int nranks, int rank, long max_merges, u
     hipError_t e = hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking);
     if (e != hipSuccess) { delete g; return fail(BPE_GPU_EHIP, "hipStreamCreate", e); }
     // sum slots hold the per-merge delta vectors (4 * (256 + merges) + 2
-    // words) and the set-up exchanges (byte-pair counts: up to 256^2 words)
-    const uint64_t c0 = ((std::max<uint64_t>(65536, 4ull * (256 + (uint64_t)max_merges) + 2) + 3) / 4) * 4;
+    // words), the set-up exchanges (byte-pair counts: up to 256^2 words) and,
+    // while the vocabulary fits the batch engine's dense vectors, a batch's
+    // exchange (xbat_words: BK members' vectors)
+    const uint64_t vc = 256 + (uint64_t)max_merges;
+    uint64_t c0 = std::max<uint64_t>(65536, 4 * vc + 2);
+    if (vc <= DENSE) c0 = std::max<uint64_t>(c0, xbat_words(BK, (uint32_t)vc));
+    c0 = (c0 + 3) / 4 * 4;
     const size_t bytes = ((size_t)MB_DATA0 + 2ull * nranks * c0) * 4;
     // uncached (peers on other devices write it while my kernels poll it);
     // kept out of the allocator after use (uc_take / uc_give).
@@ -933,7 +1057,7 @@ static int group_create_p2p(int device, int nranks, int rank, long max_merges, u
                       : hipMalloc((void **)&g->mailbox, bytes);
     if (e != hipSuccess) { g->mailbox = nullptr; bpe_gpu_group_destroy(g); return fail(BPE_GPU_ENOMEM, "uncached mailbox", e); }
     if ((e = hipMemset(g->mailbox, 0, bytes)) != hipSuccess ||
-        (e = hipMalloc(&g->xs, 64)) != hipSuccess || (e = hipMemset(g->xs, 0, 64)) != hipSuccess ||
+        (e = hipMalloc(&g->xs, XS_WORDS * 4)) != hipSuccess || (e = hipMemset(g->xs, 0, XS_WORDS * 4)) != hipSuccess ||
         (e = hipMalloc(&g->d_p2p, sizeof(P2P))) != hipSuccess) {
         bpe_gpu_group_destroy(g);
         return fail(BPE_GPU_EHIP, "p2p set-up", e);

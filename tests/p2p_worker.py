@@ -31,7 +31,7 @@ def main():
         g.train(mm)
         st = g.stats()
         np.savez(out, merges=g.merges(), ids=g.ids(0),
-                 stats=np.array([st["ms_train"], st["spec_hits"], st["spec_misses"]], dtype=np.float64))
+                 stats=np.array([st["ms_train"], st["spec_hits"], st["spec_misses"], st["batches"]], dtype=np.float64))
     else:
         merges = np.load(sys.argv[9])["merges"]
         g.encode(merges)

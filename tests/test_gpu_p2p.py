@@ -1,6 +1,8 @@
-"""GPU parity of the P2P transport (p2p.hip) and the fused sharded step
-(kernels.hip k_rescan_spec_sh / k_fused): shard groups whose ranks are
-separate processes exchanging through IPC-mapped uncached mailboxes.  On the
+"""GPU parity of the P2P transport (p2p.hip), the sharded batch engine
+(batch.hip, k_p2p_bsum: one delta sum and one record gather per batch) and
+the fused one-merge sharded step (kernels.hip k_rescan_spec_sh / k_fused,
+BPE_BATCH=0): shard groups whose ranks are separate processes exchanging
+through IPC-mapped uncached mailboxes.  On the
 one-GPU test box every rank maps the same device, which exercises the whole
 protocol (handles, pushes, flags, parity slots, graph replay, speculative
 hits and reverted misses) except the xGMI hop itself.  Bit-exact bar: merges
@@ -81,8 +83,15 @@ def _single_rank(data, mm):
     return g
 
 
-def test_p2p_single_rank_equals_engine():
-    """W = 1: the fused step (records / delta pushes to itself) against the plain engine"""
+@pytest.fixture(params=["batch", "merge"])
+def mode(request, monkeypatch):
+    """the sharded engine: batches (default) or the fused one-merge step"""
+    monkeypatch.setenv("BPE_BATCH", "1" if request.param == "batch" else "0")
+    return request.param
+
+
+def test_p2p_single_rank_equals_engine(mode):
+    """W = 1: the sharded step (records / delta pushes to itself) against the plain engine"""
     n = 3 << 20
     data = synth_bytes(981, n)
     g = _single_rank(data, 300)
@@ -91,14 +100,34 @@ def test_p2p_single_rank_equals_engine():
     e.train(300)
     assert (g.merges() == e.merges()).all()
     assert (g.all_ids() == e.ids()).all()
-    assert g.stats()["spec_hits"] > 0
+    if mode == "merge":
+        assert g.stats()["spec_hits"] > 0
+    else:
+        assert 0 < g.stats()["batches"] < 300
     g.train(300)  # second run on the same group: the sequence counters carry over
     assert (g.merges() == e.merges()).all()
 
 
-def test_p2p_single_rank_spec_hits_and_misses():
+def test_p2p_single_rank_batches_vs_oracle(monkeypatch):
+    """sharded batches on small alphabets (ties, a==b runs, retried batches)
+    and text: bit-exact vs the oracle (RULE)"""
+    monkeypatch.setenv("BPE_BATCH", "1")
+    rng = random.Random(778)
+    for k in range(10):
+        alpha = rng.choice(["ab", "abc", "aab", "abcd", "a b", "abcdefgh"])
+        n = rng.randint(200, 30000)
+        mm = rng.choice([-1, 50, 300])
+        data = corpus(f"alpha:{k}:{n}:{alpha}")
+        g = _single_rank(data, mm)
+        om, oi, _ = O.train(data, mm, O.RULE)
+        assert (g.merges() == om).all() and (g.all_ids() == oi).all(), (alpha, n, mm)
+        g.close()
+
+
+def test_p2p_single_rank_spec_hits_and_misses(monkeypatch):
     """fused sharded step on small alphabets (many missed predictions, each
     reverted by the host) and text (hits): bit-exact vs the oracle (RULE)"""
+    monkeypatch.setenv("BPE_BATCH", "0")
     rng = random.Random(777)
     hits = misses = 0
     for k in range(10):
@@ -117,7 +146,7 @@ def test_p2p_single_rank_spec_hits_and_misses():
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_p2p_ranks_equal_local_group(tmp_path, world):
+def test_p2p_ranks_equal_local_group(tmp_path, world, mode):
     n = 4 << 20
     rng = random.Random(world)
     cuts = [0] + sorted(rng.sample(range(1, n), world - 1)) + [n]
@@ -126,12 +155,14 @@ def test_p2p_ranks_equal_local_group(tmp_path, world):
     for r in res:
         assert (r["merges"] == m0).all()
     assert (np.concatenate([r["ids"] for r in res]) == ids0).all()
-    print("ms_train per rank:", [float(r["stats"][0]) for r in res], "hits/misses:", res[0]["stats"][1:])
+    print("ms_train per rank:", [float(r["stats"][0]) for r in res], "hits/misses/batches:", res[0]["stats"][1:])
+    if mode == "batch":
+        assert res[0]["stats"][3] > 0
 
 
-def test_p2p_ranks_misses_across_edges(tmp_path):
+def test_p2p_ranks_misses_across_edges(tmp_path, mode):
     """3 ranks on a small alphabet (long a==b runs across shard edges, many
-    reverted predictions): vs the oracle (RULE)"""
+    reverted predictions in the one-merge step): vs the oracle (RULE)"""
     n = 20000
     spec = f"alpha:5:{n}:aab"
     data = corpus(spec)
@@ -141,10 +172,11 @@ def test_p2p_ranks_misses_across_edges(tmp_path):
     for r in res:
         assert (r["merges"] == om).all()
     assert (np.concatenate([r["ids"] for r in res]) == oids).all()
-    assert res[0]["stats"][2] > 0, "no missed prediction exercised"
+    if mode == "merge":
+        assert res[0]["stats"][2] > 0, "no missed prediction exercised"
 
 
-def test_p2p_ranks_small_vs_oracle_and_encode(tmp_path):
+def test_p2p_ranks_small_vs_oracle_and_encode(tmp_path, mode):
     """tiny shards (one of 1 byte) vs the oracle's RULE mode, then an encode
     through the records channel vs the oracle encoder"""
     n = 3000

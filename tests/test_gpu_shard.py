@@ -1,8 +1,8 @@
 """GPU parity of sharded training (bpe_gpu.h group API).
 
-Shard groups on one device run the exact per-merge exchange the multi-GPU
-path runs (dense delta allreduce + edge-record allgather), through a sum /
-gather kernel instead of RCCL.  Bit-exact bar: the merges and the
+Shard groups on one device run the exact exchanges the multi-GPU path runs
+(dense delta sums + edge-record gathers, per batch of merges or per merge),
+through a sum / gather kernel instead of RCCL.  Bit-exact bar: the merges and the
 concatenated ids equal the oracle's RULE mode (small corpora), the
 single-GPU engine (BPE_GPU_FAST, and its default where both coincide), and
 the reference goldens at 64 MiB / 1 GiB.  An RCCL group of one rank checks
@@ -18,6 +18,14 @@ from llmtokenizer_amd import api
 from llmtokenizer_amd.synth import synth_bytes
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["batch", "merge"])
+def engine_mode(request, monkeypatch):
+    """every test on both sharded engines: batches of merges per exchange
+    (the default) and one merge per exchange (BPE_BATCH=0)"""
+    monkeypatch.setenv("BPE_BATCH", "1" if request.param == "batch" else "0")
+    return request.param
 
 
 def _split(n, k, rng):
