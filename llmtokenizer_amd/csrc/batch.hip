@@ -245,14 +245,34 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 const unsigned long long y = __shfl_up(span, o);
                 if ((int)lane >= o) span += y;
             }
-            const bool stable = summary_B(D > span ? D - span : 0) == Bsz && summary_B(D + span) == Bsz;
+            const uint64_t Blo = summary_B(D > span ? D - span : 0), Bhi = summary_B(D + span);
+            const bool stable = Blo == Bsz && Bhi == Bsz;
             const uint32_t cnext = __shfl(c, (int)(lane < 63 ? lane + 1 : 63));
+            // otherwise keys of one count keep my order against them under every
+            // B the members before me can reach (bucket = murmur & (B - 1), then
+            // the key): checked against the listed keys of my count after me
+            const uint32_t hsh = murmur_pair(u, v);
+            const uint32_t clast = __shfl(c, (int)(nl ? nl - 1 : 0));
+            bool order_ok = true;
+            for (uint32_t p = 1; p < TOPK; p++) {  // (uniform loop; readlane needs every lane)
+                const uint32_t cp = __builtin_amdgcn_readlane((int)c, (int)p);
+                const uint32_t hp = __builtin_amdgcn_readlane((int)hsh, (int)p);
+                const unsigned long long kp =
+                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)u, (int)p) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p);
+                if (p > lane && p < nl && cp == c)
+                    for (uint64_t Bx = Blo; Bx <= Bhi; Bx <<= 1) {
+                        const uint64_t bj = hsh & (Bx - 1), bp = hp & (Bx - 1);
+                        if (!(bj < bp || (bj == bp && e.k < kp))) order_ok = false;
+                    }
+            }
             uint32_t why = 0;  // 0: qualifies
             if (lane >= nl || lane >= BK) why = 8;  // past the list (reported as "list")
             else if (lane > 0) {
                 if (e.k == kprev) why = 3;  // the same key listed twice (the one-merge engine's undo): end here
                 else if (md + lane >= E->mcap || c <= 1 || (hotT > 2 && c < hotT)) why = 1;
-                else if (!stable && ((lane + 1 >= nl && truncated) || !(c > (lane + 1 < nl ? cnext : 0u)))) why = 4;
+                else if (!stable && ((truncated && c == clast) || (!(c > (lane + 1 < nl ? cnext : 0u)) && !order_ok)))
+                    why = 4;  // (a tie whose order the batch could change, or one running past the list)
                 else if (C->nkeys + 4ull * (256ull + md + lane + 2) * (lane + 1) >= E->hcap / 2) why = 6;
             }
             // commuting: no earlier entry uses my left id on its right or my right id on its left
