@@ -170,11 +170,12 @@ def timed_jobs(cx, run, k):
     return cx.allreduce(t1 - t0, "max")
 
 
-def committed_profile(name):
+def committed_profile(name, sharded=False):
     """rocprof average (ms) of kernel `name` and PMC traffic per launch from
-    the committed summaries of this same command (profiles/<tag>_*)"""
+    the committed summaries of this same command (profiles/<tag>_*): the
+    single-GPU bench command, or (sharded) the sharded one with one rank"""
     out = {}
-    for kind in ("train", "sharded"):  # single-GPU bench command, then the sharded one
+    for kind in (("sharded",) if sharded else ("train",)):
         p = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_{kind}_kernel_stats.csv")
         if "avg_ms_rocprof" in out or not os.path.exists(p):
             continue
@@ -190,10 +191,12 @@ def committed_profile(name):
     if os.path.exists(p):
         with open(p) as f:
             tr = json.load(f)
-        if name in tr:
-            out["traffic"] = tr[name]["traffic_bytes_per_launch"]
+        # (kernels both commands run carry "@sharded" for the sharded one)
+        key = name + "@sharded" if sharded and name + "@sharded" in tr else name
+        if key in tr:
+            out["traffic"] = tr[key]["traffic_bytes_per_launch"]
             out["traffic_source"] = (os.path.relpath(p, ROOT) + ": FETCH_SIZE x %.1f + WRITE_SIZE, separate "
-                                     "--pmc passes of this command" % tr[name]["fetch_correction"])
+                                     "--pmc passes of this command" % tr[key]["fetch_correction"])
     return out
 
 
@@ -480,7 +483,7 @@ def main():
                                           "spec_misses")},
     })
     out.update(extra)
-    cp = committed_profile(name)
+    cp = committed_profile(name, sharded)
     out["roofline"].update({k2: v for k2, v in cp.items() if k2 != "traffic"})
     if "traffic" in cp:
         out["roofline"]["traffic"] = cp["traffic"]
@@ -492,7 +495,7 @@ def main():
     if nl and st["ms_apply_span"] > 0:
         ab = 16.0 * st["table_updates"] / nl
         aa = ab / (st["ms_apply_span"] * 1e-3) / 1e9
-        ap = committed_profile("k_bapply")
+        ap = committed_profile("k_bapply", sharded)
         out["roofline_apply"] = {"kernel": "k_bapply", "bound": "hbm", "achieved": round(aa, 1), "peak": HBM_PEAK_GBS,
                                  "unit": "GB/s", "frac": round(aa / HBM_PEAK_GBS, 4), "traffic": ap.get("traffic"),
                                  "bytes_per_launch": round(ab), "avg_ms": round(st["ms_apply_span"], 5), "launches": nl,
