@@ -312,7 +312,11 @@ def train_sharded(args, cx, out):
         out["error"] = f"a job stopped early: {sorted(set(done))} merges"
     if len(set(digests)) != 1:
         out["error"] = "merges differ across ranks"
-    extra = {"merges_identical_across_ranks": len(set(digests)) == 1, "transport": transport}
+    extra = {"merges_identical_across_ranks": len(set(digests)) == 1, "transport": transport,
+             "engine_form": ("batches (one delta sum + one record gather per batch)" if st["batches"] else
+                             "one merge per exchange")}
+    if getattr(g, "fallback_reason", None):
+        extra["transport_fallback_reason"] = g.fallback_reason
     if single is not None:
         t1 = single[0]
         extra["single_gpu_1024"] = {"ms": round(t1 * 1e3, 3), "value": round(args.size / 1e6 * merges / t1, 1)}

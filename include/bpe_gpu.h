@@ -88,6 +88,15 @@ typedef struct {
 /* number of visible GPUs */
 int bpe_gpu_device_count(int *count);
 
+/* PCI bus id of device `device` ("dddd:bb:dd.f", NUL-terminated into buf[len]):
+   the identity ranks compare before mapping each other's mailboxes */
+int bpe_gpu_device_pci(int device, char *buf, int len);
+
+/* *ok = 1 when `device` can access `peer`'s memory directly (hipDeviceCanAccessPeer;
+   1 for device == peer): checked on every pair of ranks before the P2P transport
+   maps the peers' mailboxes */
+int bpe_gpu_peer_access(int device, int peer, int *ok);
+
 /* create a context bound to device `device` (HIP ordinal) */
 int bpe_gpu_create(int device, bpe_gpu_ctx **out);
 void bpe_gpu_destroy(bpe_gpu_ctx *ctx);

@@ -33,7 +33,7 @@ EXPORTS = [
     "bpe_gpu_group_fetch_ids", "bpe_gpu_group_get_stats", "bpe_gpu_group_exchange_mode", "bpe_gpu_shard_halo", "bpe_gpu_group_kernel_profile",
     "bpe_gpu_group_create_p2p", "bpe_gpu_group_p2p_connect", "bpe_gpu_group_transport",
     "bpe_gpu_group_create_local_p2p", "bpe_gpu_ids_checksum", "bpe_gpu_group_ids_checksum", "bpe_gpu_load_fd",
-    "bpe_gpu_fetch_ids_range", "bpe_gpu_group_fetch_ids_range",
+    "bpe_gpu_fetch_ids_range", "bpe_gpu_group_fetch_ids_range", "bpe_gpu_device_pci", "bpe_gpu_peer_access",
 ]
 
 
@@ -118,6 +118,8 @@ def load():
     L.bpe_gpu_set_profile.argtypes = [vp, ctypes.c_int]
     L.bpe_gpu_event_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
     L.bpe_gpu_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+    L.bpe_gpu_device_pci.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.bpe_gpu_peer_access.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.bpe_gpu_kernel_profile.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
     L.compress.argtypes = [ctypes.c_char_p, ctypes.POINTER(u32p), ctypes.POINTER(sz)]

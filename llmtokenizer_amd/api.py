@@ -434,3 +434,19 @@ def device_count():
     n = ctypes.c_int(0)
     L.bpe_gpu_device_count(ctypes.byref(n))
     return n.value
+
+
+def device_pci(device):
+    """PCI bus id of a visible device (its identity across processes)"""
+    L = _lib.load()
+    buf = ctypes.create_string_buffer(64)
+    _lib.check(L.bpe_gpu_device_pci(int(device), buf, 64), "device_pci")
+    return buf.value.decode()
+
+
+def peer_access(device, peer):
+    """True when `device` can access `peer`'s memory directly"""
+    L = _lib.load()
+    ok = ctypes.c_int(0)
+    _lib.check(L.bpe_gpu_peer_access(int(device), int(peer), ctypes.byref(ok)), "peer_access")
+    return bool(ok.value)

@@ -1776,6 +1776,25 @@ int bpe_gpu_device_count(int *count) {
     return 0;
 }
 
+int bpe_gpu_device_pci(int device, char *buf, int len) {
+    if (!buf || len < 13) return BPE_GPU_EINVAL;
+    const hipError_t e = hipDeviceGetPCIBusId(buf, len, device);
+    if (e != hipSuccess) return fail(BPE_GPU_ENODEV, "hipDeviceGetPCIBusId", e);
+    return 0;
+}
+
+int bpe_gpu_peer_access(int device, int peer, int *ok) {
+    if (!ok) return BPE_GPU_EINVAL;
+    *ok = 0;
+    if (device == peer) {
+        *ok = 1;
+        return 0;
+    }
+    const hipError_t e = hipDeviceCanAccessPeer(ok, device, peer);
+    if (e != hipSuccess) return fail(BPE_GPU_ENODEV, "hipDeviceCanAccessPeer", e);
+    return 0;
+}
+
 int bpe_gpu_create(int device, bpe_gpu_ctx **out) {
     if (!out) return BPE_GPU_EINVAL;
     int n = 0;

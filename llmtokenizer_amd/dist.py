@@ -20,16 +20,41 @@ def rccl_group(device):
     return api.ShardGroup(device, nranks=world, rank=rank, comm_id=obj[0])
 
 
+def peer_problem(device, pcis):
+    """why this rank cannot map the other ranks' mailboxes, or None.  pcis:
+    every rank's device PCI bus id.  A peer device visible here must accept
+    direct access (hipDeviceCanAccessPeer); one not visible here (another
+    HIP_VISIBLE_DEVICES) is left to the IPC mapping itself."""
+    local = {}
+    for d in range(api.device_count()):
+        try:
+            local[api.device_pci(d).lower()] = d
+        except api.BpeError:
+            pass
+    for r, pci in enumerate(pcis):
+        peer = local.get(pci.lower())
+        if peer is None or peer == device:
+            continue
+        if not api.peer_access(device, peer):
+            return f"device {device} ({pcis[r]}) has no peer access to rank {r}'s device {peer}"
+    return None
+
+
 def p2p_group(device, max_merges, strict=True):
     """ShardGroup holding this rank's shard over P2P mailboxes; shard index ==
     rank.  max_merges bounds the merges of any train call on it.  The ranks
-    agree on success: with strict=False a failure on ANY rank (mailbox
-    allocation, IPC export or mapping) returns None on every rank."""
+    agree on success: with strict=False a failure on ANY rank (no peer access
+    between two ranks' devices, mailbox allocation, IPC export or mapping)
+    returns None on every rank, and p2p_group.last_failure says why."""
     import torch.distributed as dist
     rank, world = dist.get_rank(), dist.get_world_size()
     g, err = None, None
+    pcis = [None] * world
+    dist.all_gather_object(pcis, api.device_pci(device))
+    err = peer_problem(device, pcis)
     try:
-        g = api.ShardGroup(device, nranks=world, rank=rank, p2p_max_merges=max_merges)
+        if err is None:
+            g = api.ShardGroup(device, nranks=world, rank=rank, p2p_max_merges=max_merges)
     except api.BpeError as e:
         err = str(e)
     handles = [None] * world
@@ -45,10 +70,15 @@ def p2p_group(device, max_merges, strict=True):
     if errs:
         if g:
             g.close()
+        p2p_group.last_failure = "; ".join(errs)
         if strict:
-            raise api.BpeError("p2p group set-up failed: " + "; ".join(errs))
+            raise api.BpeError("p2p group set-up failed: " + p2p_group.last_failure)
         return None
+    p2p_group.last_failure = None
     return g
+
+
+p2p_group.last_failure = None
 
 
 def group(device, max_merges, transport=None):
@@ -61,7 +91,11 @@ def group(device, max_merges, transport=None):
     if transport != "p2p":
         raise ValueError(f"unknown transport {transport!r}")
     g = p2p_group(device, max_merges, strict=False)
-    return g if g is not None else rccl_group(device)
+    if g is not None:
+        return g
+    g = rccl_group(device)
+    g.fallback_reason = "P2P set-up failed, RCCL instead: " + str(p2p_group.last_failure)
+    return g
 
 
 def shard_range(n_total, rank, world):

@@ -216,3 +216,14 @@ def test_p2p_ranks_window_encode_vs_oracle(tmp_path):
         del os.environ["BPE_ENC_WIN"]
     assert (np.concatenate([r["ids"] for r in enc]) == want).all()
     assert all(int(r["path"][0]) == 2 for r in enc)
+
+
+def test_peer_access_checks():
+    """the P2P set-up's pre-check: the device's PCI id, peer access to itself,
+    and no problem reported for ranks on visible devices that accept access"""
+    from llmtokenizer_amd import dist as bdist
+    pci = api.device_pci(0)
+    assert len(pci) >= 12 and pci.count(":") == 2
+    assert api.peer_access(0, 0)
+    assert bdist.peer_problem(0, [pci, pci]) is None
+    assert bdist.peer_problem(0, [pci, "ffff:ff:1f.7"]) is None  # (not visible here: left to the IPC mapping)
