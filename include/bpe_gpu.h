@@ -57,7 +57,7 @@ typedef struct {
     uint64_t tracked_iters;   /* iterations with per-thread table tracking     */
     uint64_t tie_events;      /* chain-order ties resolved by emulation        */
     uint64_t edge_events;     /* D == resize threshold resolved by emulation   */
-    uint64_t rule_ties;       /* schedule-dependent ties decided by the rule   */
+    uint64_t rule_ties;       /* schedule-dependent ties decided by the rule (approximate in hot-set mode) */
     uint64_t table_grows;     /* pair-count table regrowths                    */
     uint64_t keys;            /* slots in use in the pair-count table          */
     double ms_init;           /* device-side setup (counting sort, table)      */

@@ -99,15 +99,7 @@ __device__ inline uint8_t ew_byte(const EncWinArgs &A, int64_t g) {
 // rank | batch << 16 of the pair (x, y); ~0 when the list has no such merge
 __device__ inline uint32_t ew_info(const EncWinArgs &A, uint32_t x, uint32_t y) {
     if (x < 256 && y < 256) return A.bp[(x << 8) | y];
-    uint32_t key = ((x << 16) | y) + 1u;
-#ifdef EW_TIMING_DOUBLE  // (timing experiment only: a second, dependent lookup of the same key)
-    {
-        uint32_t s = (uint32_t)mix64(key) & A.hmask;
-        unsigned long long e = A.ht[s];
-        while ((uint32_t)e != key && (uint32_t)e != 0) e = A.ht[s = (s + 1) & A.hmask];
-        key += (uint32_t)(e >> 32) == 0xDEADBEEFu;
-    }
-#endif
+    const uint32_t key = ((x << 16) | y) + 1u;
     uint32_t s = (uint32_t)mix64(key) & A.hmask;
     for (;;) {
         const unsigned long long e = A.ht[s];  // key and value in ONE 8-byte load
@@ -259,10 +251,6 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
         // rules of the header apply in batch b when mask bit b is set); a mask
         // is fetched only when its edge token changes.
         auto snapshot = [&](uint32_t Lu, uint32_t Ru) {
-#ifdef EW_TIMING_NOEDGE  // (timing experiment only: no edge tracking, results may differ)
-            s_lact = s_ract = 0;
-            return;
-#endif
             s_lact = (lunk || Lu > 0) && Lu < Ru;
             if (s_lact && tok[Lu] != s_lid) {
                 s_lid = tok[Lu];

@@ -2073,6 +2073,52 @@ int bpe_gpu_encode(bpe_gpu_ctx *c, const uint32_t *pairs, size_t n_merges) {
     return 0;
 }
 
+// passes k_dec_elen makes before the host takes over (a pass resolves one
+// level of the merge tree; real vocabularies are a few dozen deep)
+constexpr uint32_t DEC_MAX_PASSES = 64;
+
+// expansion lengths on the host, as k_dec_elen defines them: bytes 1 (NUL 0),
+// a self-referencing record its one char, a record naming an unknown id or on
+// a cycle ELEN_UNK
+void dec_elen_host(const uint32_t *pairs, uint32_t nm, uint64_t *elen) {
+    const uint32_t V = 256 + nm;
+    std::vector<uint8_t> st(V, 0);  // 0 new, 1 on the stack, 2 done
+    for (uint32_t x = 0; x < 256; x++) {
+        elen[x] = x ? 1 : 0;
+        st[x] = 2;
+    }
+    std::vector<uint32_t> stk;
+    for (uint32_t x0 = 256; x0 < V; x0++) {
+        if (st[x0] == 2) continue;
+        stk.assign(1, x0);
+        st[x0] = 1;
+        while (!stk.empty()) {
+            const uint32_t x = stk.back();
+            const uint32_t a = pairs[2 * (x - 256)], b = pairs[2 * (x - 256) + 1];
+            if (a == x) {  // self-reference: that one char (bpe.c:47-53)
+                elen[x] = (uint8_t)a ? 1 : 0;
+            } else if (a >= V || b >= V) {
+                elen[x] = ELEN_UNK;
+            } else {
+                bool pushed = false;
+                for (uint32_t y : {a, b})
+                    if (st[y] == 0) {
+                        st[y] = 1;
+                        stk.push_back(y);
+                        pushed = true;
+                        break;
+                    }
+                if (pushed) continue;
+                // both halves done or on the stack (a cycle: unresolvable)
+                elen[x] = (st[a] == 2 && st[b] == 2 && elen[a] != ELEN_UNK && elen[b] != ELEN_UNK) ? elen[a] + elen[b]
+                                                                                                  : ELEN_UNK;
+            }
+            st[x] = 2;
+            stk.pop_back();
+        }
+    }
+}
+
 int bpe_gpu_decode(bpe_gpu_ctx *c, const uint32_t *ids, size_t len, const uint32_t *pairs, size_t n_merges,
                    uint8_t *out, size_t cap, size_t *out_len) {
     if (!c || !out_len || (!ids && len) || (!pairs && n_merges)) return BPE_GPU_EINVAL;
@@ -2092,7 +2138,19 @@ int bpe_gpu_decode(bpe_gpu_ctx *c, const uint32_t *ids, size_t len, const uint32
     HIPCHK(hipMemsetAsync(d_err, 0, 8, c->st));
     if (len) HIPCHK(hipMemcpyAsync(d_ids, ids, len * 4, hipMemcpyHostToDevice, c->st));
     if (n_merges) HIPCHK(hipMemcpyAsync(d_pairs, pairs, n_merges * 8, hipMemcpyHostToDevice, c->st));
-    k_dec_elen<<<1, 1024, 0, c->st>>>(d_pairs, (uint32_t)n_merges, d_elen);
+    k_dec_elen<<<1, 1024, 0, c->st>>>(d_pairs, (uint32_t)n_merges, d_elen, DEC_MAX_PASSES, d_err + 1);
+    HIPCHK(hipGetLastError());
+    {
+        uint32_t unf = 0;
+        HIPCHK(hipMemcpyAsync(&unf, d_err + 1, 4, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        if (unf) {  // deep merge chains: the rest in one host pass (rank order + DFS for the others)
+            std::vector<uint64_t> he(V);
+            dec_elen_host(pairs, (uint32_t)n_merges, he.data());
+            HIPCHK(hipMemcpyAsync(d_elen, he.data(), (size_t)V * 8, hipMemcpyHostToDevice, c->st));
+            HIPCHK(hipStreamSynchronize(c->st));
+        }
+    }
     if (len) k_dec_check<<<1024, 256, 0, c->st>>>(d_ids, len, V, d_elen, d_err);
     HIPCHK(hipGetLastError());
     auto lens = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint64_t>(0),

@@ -935,7 +935,12 @@ struct Best {
 __device__ inline Best best_merge(Best x, Best y) {
     if (y.v > x.v) return y;
     if (y.v < x.v) return x;
-    if (x.key == y.key) return x;  // the same key twice (hot set): one holder
+    // the same key twice (hot set, a key listed again after an undone
+    // speculative apply): one holder -- when the duplicate meets a partial
+    // whose smallest key is another tied key it is counted twice, so `tie`
+    // (stats: rule_ties, C->ties) is approximate in hot mode; the choice of
+    // key (the smallest) and every merge are exact
+    if (x.key == y.key) return x;
     return Best{x.v, x.tie + y.tie, x.key < y.key ? x.key : y.key};
 }
 
@@ -2807,8 +2812,11 @@ constexpr uint64_t ELEN_UNK = ~0ull;
 // (halves created earlier) resolves in (tree depth) passes.  Records naming an
 // unknown id, and cycles, stay unresolved (ELEN_UNK): like the reference's
 // resolve_pair (bpe.c:23-92), which only fails when such a record is used.
+// At most max_passes passes (deep merge chains resolve one level per pass):
+// still changing after them, *unfinished = 1 and the host resolves the rest.
 __global__ __launch_bounds__(1024) void k_dec_elen(const uint32_t *__restrict__ pairs, uint32_t nm,
-                                                    uint64_t *__restrict__ elen) {
+                                                    uint64_t *__restrict__ elen, uint32_t max_passes,
+                                                    uint32_t *__restrict__ unfinished) {
     const uint32_t V = 256 + nm;
     __shared__ uint32_t changed;
     for (uint32_t x = threadIdx.x; x < V; x += blockDim.x) {
@@ -2820,7 +2828,11 @@ __global__ __launch_bounds__(1024) void k_dec_elen(const uint32_t *__restrict__ 
         elen[x] = a == x ? ((uint8_t)a ? 1 : 0) : ELEN_UNK;  // self-reference: that one char (bpe.c:47-53)
     }
     __syncthreads();
-    for (;;) {
+    for (uint32_t pass = 0;; pass++) {
+        if (pass == max_passes) {
+            if (threadIdx.x == 0) *unfinished = 1;
+            return;
+        }
         if (threadIdx.x == 0) changed = 0;
         __syncthreads();
         for (uint32_t x = 256 + threadIdx.x; x < V; x += blockDim.x) {

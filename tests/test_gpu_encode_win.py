@@ -52,6 +52,14 @@ def test_window_edges_any_halo(halo, monkeypatch):
         if rng.random() < 0.5:
             text = b"a" * rng.randint(1, 5000) + text + b"a" * rng.randint(0, 3000)
         merges = _random_merges(rng, sorted(set(alpha)), rng.randint(1, 600), eq=rng.choice([0.0, 0.3]))
+        if rng.random() < 0.3 and len(merges) > 2:
+            # records the plan skips: a forward reference (an id not created
+            # yet) and a pair that repeats an earlier record
+            m = merges.copy()
+            q = rng.randrange(1, len(m))
+            m[q] = [256 + len(m) - 1, m[0][1]]
+            m = np.vstack([m, m[:1]])
+            merges = m
         ids, st = _encode(text, merges)
         paths.add(st["enc_path"])
         assert (ids == O.encode(text, merges)).all(), (halo, n, len(merges))
@@ -102,17 +110,19 @@ def test_window_equals_global_replay(monkeypatch):
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_group_halo_from_neighbours(seed, monkeypatch):
-    """shards shorter than the halo: halo bytes gathered across several shards"""
+@pytest.mark.parametrize("eq", [0.0, 0.3])
+def test_group_halo_from_neighbours(seed, eq, monkeypatch):
+    """shards shorter than the halo: halo bytes gathered across several shards
+    (eq > 0: a == a runs across shard seams, the run-end and left-parity rules)"""
     monkeypatch.setenv("BPE_EW_HALO", "64")
-    rng = random.Random(900 + seed)
+    rng = random.Random(900 + seed + int(eq * 10))
     for _ in range(6):
         alpha = rng.choice([b"ab", b"abc", b"aab", bytes(range(97, 101))])
         n = rng.randint(50, 8000)
         text = bytes(rng.choice(alpha) for _ in range(n))
         k = rng.randint(2, 9)
         cuts = [0] + sorted(rng.sample(range(1, n), k - 1)) + [n]
-        merges = _random_merges(rng, sorted(set(alpha)), rng.randint(1, 200), eq=0.0)
+        merges = _random_merges(rng, sorted(set(alpha)), rng.randint(1, 200), eq=eq)
         g = api.ShardGroup(0, local_shards=k)
         g.load_split(text, cuts)
         g.encode(merges)

@@ -181,6 +181,16 @@ def test_decode_errors_and_self_reference():
     chain = np.array([[97, 97]] + [[256 + r, 256 + r] for r in range(12)], dtype=np.uint32)
     assert e.decode(np.array([256 + 12], dtype=np.uint32), chain) == b"a" * (1 << 13)
     assert e.decode(np.zeros(0, dtype=np.uint32), chain) == b""
+    # chains deeper than the device fixpoint's pass cap (64): the host finishes
+    # the lengths; errors (cycle, unknown id) deep in the chain still surface
+    deep = np.array([[97, 98]] + [[256 + r, 99 + r % 3] for r in range(299)], dtype=np.uint32)
+    ids = np.array([256 + 299, 97, 256 + 150, 256], dtype=np.uint32)
+    assert e.decode(ids, deep) == O.decode(ids, deep)
+    cyc = deep.copy()
+    cyc[100] = [256 + 200, 65]  # id 356 names a later id on the chain that leads back to it
+    with pytest.raises(api.BpeError):
+        e.decode(np.array([256 + 299], dtype=np.uint32), cyc)
+    assert e.decode(np.array([256 + 50], dtype=np.uint32), cyc) == O.decode(np.array([256 + 50]), cyc)
 
 
 def test_streaming_file_load(tmp_path):
