@@ -258,23 +258,45 @@ def train_single(args, cx, out):
     return el, merges, st, prof, got, extra
 
 
-def ingest_rate(e, size=GIB):
-    """get_file + strlen into HBM (bpe_gpu_load_fd, pinned double-buffered
-    staging) for a 1 GiB file in the page cache: the PCIe-inclusive rate
-    (never `value`: the timed jobs start from resident input)"""
+def ingest_rate(e, size=GIB, merges=1024):
+    """get_file + strlen into HBM (bpe_gpu_load_fd: pinned double-buffered
+    staging, several reader threads, byte presence gathered per chunk) for a
+    1 GiB file in the page cache: the PCIe-inclusive rate (never `value`: the
+    timed jobs start from resident input).  Then the whole compress() path on
+    the same file (bpe.h compress_ex: ingest, training, merges and ids back to
+    the host; its engine context kept from a first call) against the ingest
+    plus the same training and fetch from resident bytes."""
     import numpy as np
+    from llmtokenizer_amd import api
     path = os.path.join(tempfile.gettempdir(), "bpe_bench_ingest.bin")
     try:
+        # 1 GiB of uniform printable bytes (random_text.txt-shaped)
         np.random.default_rng(0).integers(32, 127, size, dtype=np.uint8).tofile(path)
         e.load_file(path)  # warm (staging buffers)
         t0 = time.perf_counter()
         n = e.load_file(path)
         t1 = time.perf_counter()
+        e.train(merges)
+        e.merges(), e.ids()
+        t2 = time.perf_counter()
+        e.train(merges)
+        e.merges(), e.ids()
+        t3 = time.perf_counter()
+        api.compress(path, merges)  # (creates the kept context)
+        t4 = time.perf_counter()
+        api.compress(path, merges)
+        t5 = time.perf_counter()
     finally:
         if os.path.exists(path):
             os.remove(path)
-    return {"bytes": n, "ms": round((t1 - t0) * 1e3, 2), "GB/s": round(n / (t1 - t0) / 1e9, 2),
-            "note": "file in the page cache -> HBM incl. the NUL scan, PCIe-inclusive; not part of value"}
+    ing, res, comp = t1 - t0, t3 - t2, t5 - t4
+    return {"bytes": n, "ms": round(ing * 1e3, 2), "GB/s": round(n / ing / 1e9, 2),
+            "note": "file in the page cache -> HBM incl. the NUL scan, PCIe-inclusive; not part of value",
+            "compress": {"merges": merges, "ms": round(comp * 1e3, 2),
+                         "resident_train_fetch_ms": round(res * 1e3, 2),
+                         "ratio_to_ingest_plus_resident": round(comp / (ing + res), 3),
+                         "note": "compress_ex(path) = ingest + training + merges and ids to the host, vs the "
+                                 "ingest plus the same training and fetch from resident bytes"}}
 
 
 def train_sharded(args, cx, out):

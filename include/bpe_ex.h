@@ -45,6 +45,11 @@ uint32_t *bpe_encode_bytes(const uint8_t *bytes, size_t n, dyn_arr_t *pair_arr, 
 /* statistics of the last compress/compress_ex/bpe_train_bytes/bpe_encode_bytes */
 int bpe_last_stats(bpe_gpu_stats *out);
 
+/* compress / compress_ex / bpe_train_bytes / bpe_encode_bytes / decompress keep
+ * one engine context per device between calls (its device memory pool and
+ * pinned staging are reused; BPE_KEEP_CONTEXT=0 turns this off): free them */
+void bpe_release_engines(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,7 +20,7 @@ EXPORTS = [
     "hash_table_search", "hash_table_clear", "hash_table_merge",
     # bpe_ex.h
     "compress_ex", "bpe_train_bytes", "bpe_encode_bytes", "bpe_last_stats",
-    "bpe_train_bytes_devices", "compress_multi",
+    "bpe_train_bytes_devices", "compress_multi", "bpe_release_engines",
     # bpe_gpu.h
     "bpe_gpu_device_count", "bpe_gpu_create", "bpe_gpu_destroy", "bpe_gpu_load", "bpe_gpu_synth",
     "bpe_gpu_train", "bpe_gpu_fetch_merges", "bpe_gpu_fetch_ids", "bpe_gpu_encode", "bpe_gpu_decode",

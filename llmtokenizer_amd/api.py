@@ -9,6 +9,7 @@ libbpe_amd.so on the GPU; errors raise BpeError (the C layer returns NULL).
 """
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -49,8 +50,14 @@ def _merges_to_arr(merges):
 
 
 def _take_ids(ptr, n):
-    ids = np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0, dtype=np.uint32)
-    ctypes.CDLL(None).free(ctypes.cast(ptr, ctypes.c_void_p))
+    """the library's malloc'd id buffer as a numpy array without a copy (a
+    multi-GB encoding): freed when the array (and every view of it) is gone"""
+    addr = ctypes.cast(ptr, ctypes.c_void_p).value
+    if not n:
+        ctypes.CDLL(None).free(ctypes.c_void_p(addr))
+        return np.zeros(0, dtype=np.uint32)
+    ids = np.ctypeslib.as_array(ptr, shape=(n,))
+    weakref.finalize(ids, ctypes.CDLL(None).free, ctypes.c_void_p(addr))
     return ids
 
 

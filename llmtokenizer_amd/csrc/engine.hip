@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <rocprim/rocprim.hpp>
@@ -285,6 +286,9 @@ struct bpe_gpu_ctx {
     std::vector<uint32_t> ew_stage;  // host image of the window encoder's tables (outlives the upload)
     uint8_t *stage[2] = {};
     hipEvent_t stage_ev[2] = {};
+    size_t bytes_cap = 0;        // capacity of h.bytes (kept across loads of the same or smaller size)
+    uint32_t *d_pres = nullptr;  // [256] byte presence gathered while bpe_gpu_load_fd streamed the corpus
+    bool pres_valid = false;     // d_pres describes the bytes loaded now
 };
 
 namespace {
@@ -1374,6 +1378,10 @@ int compact_ids(bpe_gpu_ctx *c) {
 int init_presence(bpe_gpu_ctx *c, uint32_t **d_bh) {
     int r;
     if ((r = dalloc(c, d_bh, 256))) return r;
+    if (c->pres_valid) {  // gathered chunk by chunk while the corpus streamed in (bpe_gpu_load_fd)
+        HIPCHK(hipMemcpyAsync(*d_bh, c->d_pres, 1024, hipMemcpyDeviceToDevice, c->st));
+        return 0;
+    }
     k_init_tok<false><<<1024, 256, 0, c->st>>>(c->dE, *d_bh);
     HIPCHK(hipGetLastError());
     return 0;
@@ -1815,6 +1823,7 @@ void bpe_gpu_destroy(bpe_gpu_ctx *c) {
     if (c->hprobe) hipHostFree((void *)c->hprobe);
     for (auto &e : c->ev_probe)
         if (e) (void)hipEventDestroy(e);
+    if (c->d_pres) hipFree(c->d_pres);
     if (c->d_enc_pairs) hipFree(c->d_enc_pairs);
     for (void *p : c->dscr)
         if (p) (void)hipFree(p);
@@ -1833,9 +1842,14 @@ void bpe_gpu_destroy(bpe_gpu_ctx *c) {
 static int alloc_bytes(bpe_gpu_ctx *c, size_t n) {
     if (n > 0xFFFFFFFEull) return fail(BPE_GPU_ERANGE, "corpus > 2^32-2 bytes");
     free_train(c, true);
-    if (c->h.bytes) { (void)hipFree(c->h.bytes); c->h.bytes = nullptr; }
-    HIPCHK(hipMalloc(&c->h.bytes, n + 64));  // kernels read whole 16-byte groups
-    HIPCHK(hipMemsetAsync(c->h.bytes, 0, n + 64, c->st));
+    c->pres_valid = false;
+    if (!c->h.bytes || c->bytes_cap < n + 64) {  // (a buffer at least this large is kept)
+        if (c->h.bytes) { (void)hipFree(c->h.bytes); c->h.bytes = nullptr; }
+        HIPCHK(hipMalloc(&c->h.bytes, n + 64));
+        c->bytes_cap = n + 64;
+    }
+    // kernels read whole 16-byte groups / words past n: zero padding
+    HIPCHK(hipMemsetAsync(c->h.bytes + n, 0, 64, c->st));
     c->n0 = n;
     c->loaded = true;
     return 0;
@@ -1957,16 +1971,58 @@ int bpe_gpu_fetch_merges(bpe_gpu_ctx *c, uint32_t *pairs, size_t cap, size_t *co
     return 0;
 }
 
+// device -> host copy of `bytes` into pageable host memory: through the
+// context's two pinned 64-MiB staging buffers, the DMA of chunk k + 1
+// overlapping several threads' copy of chunk k into dst (a plain
+// hipMemcpy to pageable memory stages through the runtime at ~10 GB/s, and
+// one thread page-faulting a fresh multi-GB buffer is slower still)
+int d2h_staged(bpe_gpu_ctx *c, void *dst, const void *src, size_t bytes) {
+    constexpr size_t CH = 64u << 20;
+    if (bytes < (8u << 20)) {
+        HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipStreamSynchronize(c->st));
+        return 0;
+    }
+    for (int k = 0; k < 2; k++) {
+        if (!c->stage[k]) HIPCHK(hipHostMalloc((void **)&c->stage[k], CH, hipHostMallocDefault));
+        if (!c->stage_ev[k]) HIPCHK(hipEventCreateWithFlags(&c->stage_ev[k], hipEventDisableTiming));
+    }
+    const int nthr = std::max(1, std::min(32, getenv_int("BPE_LOAD_THREADS", 16)));
+    const size_t nch = (bytes + CH - 1) / CH;
+    auto issue = [&](size_t k) -> int {
+        const size_t off = k * CH, len = std::min(CH, bytes - off);
+        HIPCHK(hipMemcpyAsync(c->stage[k & 1], (const uint8_t *)src + off, len, hipMemcpyDeviceToHost, c->st));
+        HIPCHK(hipEventRecord(c->stage_ev[k & 1], c->st));
+        return 0;
+    };
+    int r;
+    if ((r = issue(0))) return r;
+    std::vector<std::thread> pool;
+    for (size_t k = 0; k < nch; k++) {
+        if (k + 1 < nch && (r = issue(k + 1))) return r;  // (its buffer's chunk k - 1 was copied out)
+        HIPCHK(hipEventSynchronize(c->stage_ev[k & 1]));
+        const size_t off = k * CH, len = std::min(CH, bytes - off);
+        const size_t step = ((len + nthr - 1) / nthr + 4095) & ~(size_t)4095;
+        const uint8_t *from = c->stage[k & 1];
+        uint8_t *to = (uint8_t *)dst + off;
+        pool.clear();
+        for (int t = 1; t < nthr; t++) {
+            const size_t lo = std::min(len, (size_t)t * step), hi = std::min(len, lo + step);
+            if (hi > lo) pool.emplace_back([=] { memcpy(to + lo, from + lo, hi - lo); });
+        }
+        memcpy(to, from, std::min(len, step));
+        for (auto &th : pool) th.join();
+    }
+    return 0;
+}
+
 int bpe_gpu_fetch_ids(bpe_gpu_ctx *c, uint32_t *ids, size_t cap, size_t *len) {
     if (!c || !len) return BPE_GPU_EINVAL;
     if (!c->ids_ready) return fail(BPE_GPU_ESTATE, "no ids: train or encode first");
     HIPCHK(hipSetDevice(c->dev));
     *len = c->ids_len;
     size_t n = std::min<size_t>(cap, c->ids_len);
-    if (n && ids) {
-        HIPCHK(hipMemcpyAsync(ids, c->h.ids_out, n * 4, hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));
-    }
+    if (n && ids) return d2h_staged(c, ids, c->h.ids_out, n * 4);
     return 0;
 }
 
@@ -1975,10 +2031,7 @@ int bpe_gpu_fetch_ids_range(bpe_gpu_ctx *c, size_t first, uint32_t *ids, size_t 
     if (!c->ids_ready) return fail(BPE_GPU_ESTATE, "no ids: train or encode first");
     if (first > c->ids_len || count > c->ids_len - first) return fail(BPE_GPU_EINVAL, "id range out of bounds");
     HIPCHK(hipSetDevice(c->dev));
-    if (count) {
-        HIPCHK(hipMemcpyAsync(ids, c->h.ids_out + first, count * 4, hipMemcpyDeviceToHost, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));
-    }
+    if (count) return d2h_staged(c, ids, c->h.ids_out + first, count * 4);
     return 0;
 }
 
@@ -2193,39 +2246,81 @@ int bpe_gpu_load_fd(bpe_gpu_ctx *c, int fd, size_t size, size_t *n_loaded) {
     const size_t want_total = std::min(size, LIMIT);
     if ((r = alloc_bytes(c, want_total))) return r;
     constexpr size_t CH = 64u << 20;
+    if (!c->d_pres) HIPCHK(hipMalloc(&c->d_pres, 1024));
+    HIPCHK(hipMemsetAsync(c->d_pres, 0, 1024, c->st));
     for (int k = 0; k < 2; k++) {
         if (!c->stage[k]) HIPCHK(hipHostMalloc((void **)&c->stage[k], CH, hipHostMallocDefault));
         if (!c->stage_ev[k]) HIPCHK(hipEventCreateWithFlags(&c->stage_ev[k], hipEventDisableTiming));
     }
+    // each chunk is read by several threads (one reader is bound by its
+    // memcpy out of the page cache, ~15 GB/s), each also scanning its part
+    // for the first NUL; the next chunk's reads overlap this chunk's copy
+    const int nthr = std::max(1, std::min(32, getenv_int("BPE_LOAD_THREADS", 16)));
+    struct Part {
+        size_t lo, want, got, nul;
+        int err;
+    };
+    std::vector<Part> parts(nthr);
+    std::vector<std::thread> pool;
     size_t off = 0;
     bool done = false;
     for (uint64_t k = 0; off < want_total && !done; k++) {
         uint8_t *buf = c->stage[k & 1];
         if (k >= 2) HIPCHK(hipEventSynchronize(c->stage_ev[k & 1]));  // its previous copy is done
         const size_t want = std::min(CH, want_total - off);
+        const size_t step = ((want + nthr - 1) / nthr + 4095) & ~(size_t)4095;
+        auto read_part = [&](Part &p) {
+            while (p.got < p.want) {
+                const ssize_t q = pread(fd, buf + p.lo + p.got, p.want - p.got, (off_t)(off + p.lo + p.got));
+                if (q < 0 && errno == EINTR) continue;
+                if (q < 0) {
+                    p.err = errno;
+                    return;
+                }
+                if (q == 0) break;  // the file shrank: it ends here
+                p.got += (size_t)q;
+            }
+            const void *z = memchr(buf + p.lo, 0, p.got);
+            p.nul = z ? (size_t)((const uint8_t *)z - (buf + p.lo)) : SIZE_MAX;
+        };
+        for (int t = 0; t < nthr; t++) {
+            const size_t lo = std::min(want, (size_t)t * step);
+            parts[t] = Part{lo, std::min(want, lo + step) - lo, 0, SIZE_MAX, 0};
+        }
+        pool.clear();
+        for (int t = 1; t < nthr; t++)
+            if (parts[t].want) pool.emplace_back(read_part, std::ref(parts[t]));
+        read_part(parts[0]);
+        for (auto &th : pool) th.join();
         size_t got = 0;
-        while (got < want) {
-            const ssize_t q = pread(fd, buf + got, want - got, (off_t)(off + got));
-            if (q < 0 && errno == EINTR) continue;
-            if (q < 0) {
-                const int e = errno;
+        for (const Part &p : parts) {
+            if (p.err) {
                 (void)hipStreamSynchronize(c->st);
                 c->n0 = 0;
                 const int rc = fail(BPE_GPU_EIO, "read");
-                errno = e;
+                errno = p.err;
                 return rc;
             }
-            if (q == 0) { done = true; break; }  // the file shrank: stop at its end
-            got += (size_t)q;
         }
-        const void *nul = memchr(buf, 0, got);
-        if (nul) {
-            got = (size_t)((const uint8_t *)nul - buf);
-            done = true;
+        for (const Part &p : parts) {  // in file order: the first NUL or short read ends the text
+            if (p.nul != SIZE_MAX) {
+                got = p.lo + p.nul;
+                done = true;
+                break;
+            }
+            got = p.lo + p.got;
+            if (p.got < p.want) {
+                done = true;
+                break;
+            }
         }
         if (got) {
             HIPCHK(hipMemcpyAsync(c->h.bytes + off, buf, got, hipMemcpyHostToDevice, c->st));
             HIPCHK(hipEventRecord(c->stage_ev[k & 1], c->st));
+            // the chunk's byte presence while the next chunk is read (the
+            // training init then skips its presence pass)
+            k_presence_range<<<256, 256, 0, c->st>>>(c->h.bytes + off, got, c->d_pres);
+            HIPCHK(hipGetLastError());
         }
         off += got;
     }
@@ -2242,7 +2337,10 @@ int bpe_gpu_load_fd(bpe_gpu_ctx *c, int fd, size_t size, size_t *n_loaded) {
             return fail(BPE_GPU_ERANGE, "corpus > 2^32-2 bytes before its first NUL");
         }
     }
+    HIPCHK(hipMemsetAsync(c->h.bytes + off, 0, 64, c->st));  // (the padding past a NUL-cut text)
+    HIPCHK(hipStreamSynchronize(c->st));
     c->n0 = off;
+    c->pres_valid = true;
     *n_loaded = off;
     return 0;
 }

@@ -1905,6 +1905,33 @@ __global__ void k_init_cross(const Eng *__restrict__ E, uint32_t *__restrict__ t
 
 
 // ------------------------------------------------------------- init kernels
+// byte presence of one 16-byte aligned range [p, p + n) into present (OR):
+// bpe_gpu_load_fd runs it on each chunk as it lands, so the training init
+// needs no presence pass of its own over a streamed corpus
+__global__ __launch_bounds__(256) void k_presence_range(const uint8_t *__restrict__ p, uint64_t n,
+                                                        uint32_t *__restrict__ present) {
+    __shared__ uint32_t seen[256];
+    seen[threadIdx.x] = 0;
+    __syncthreads();
+    const uint4 *v = reinterpret_cast<const uint4 *>(p);
+    const uint64_t nv = n / 16;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 q = v[i];
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {  // (benign same-value races)
+            seen[w[k] & 0xFF] = 1;
+            seen[(w[k] >> 8) & 0xFF] = 1;
+            seen[(w[k] >> 16) & 0xFF] = 1;
+            seen[w[k] >> 24] = 1;
+        }
+    }
+    if (blockIdx.x == 0)
+        for (uint64_t i = nv * 16 + threadIdx.x; i < n; i += blockDim.x) seen[p[i]] = 1;
+    __syncthreads();
+    if (seen[threadIdx.x] && !present[threadIdx.x]) atomicOr(&present[threadIdx.x], 1u);
+}
+
 
 // per-(tile, part) histogram of byte-pair rank keys; LDS u32 bins.
 // 16 pair positions per thread from one uint4 load (+1 byte of the next).

@@ -15,6 +15,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <time.h>
 #include <unistd.h>
 
 static bpe_gpu_stats g_last_stats;
@@ -194,11 +196,60 @@ static void report(const char *what, int rc)
     fprintf(stderr, "bpe: %s failed: %s (%s)\n", what, bpe_gpu_strerror(rc), bpe_gpu_last_error());
 }
 
+/* One engine context per device is kept between calls (its HBM buffer pool,
+ * corpus buffer and pinned staging are reused, so a second compress() pays
+ * the ingest and the training, not the set-up); BPE_KEEP_CONTEXT=0 makes
+ * every call create and destroy its own, bpe_release_engines() frees the kept
+ * ones.  A context in use by one thread is taken out of the cache, so
+ * concurrent calls on one device simply create another. */
+#define ENGINE_CACHE 64
+static pthread_mutex_t g_engine_mu = PTHREAD_MUTEX_INITIALIZER;
+static bpe_gpu_ctx *g_engines[ENGINE_CACHE];
+
+static int keep_engines(void)
+{
+    const char *v = getenv("BPE_KEEP_CONTEXT");
+    return !v || atoi(v) != 0;
+}
+
 static int open_engine(int device, bpe_gpu_ctx **ctx)
 {
+    *ctx = NULL;
+    if (device >= 0 && device < ENGINE_CACHE && keep_engines()) {
+        pthread_mutex_lock(&g_engine_mu);
+        *ctx = g_engines[device];
+        g_engines[device] = NULL;
+        pthread_mutex_unlock(&g_engine_mu);
+        if (*ctx) return 0;
+    }
     int rc = bpe_gpu_create(device, ctx);
     if (rc) report("GPU context (an MI355X is required; there is no CPU path)", rc);
     return rc;
+}
+
+/* back into the cache after a successful call, else destroyed */
+static void close_engine(int device, bpe_gpu_ctx *ctx, int ok)
+{
+    if (!ctx) return;
+    if (ok && device >= 0 && device < ENGINE_CACHE && keep_engines()) {
+        pthread_mutex_lock(&g_engine_mu);
+        if (!g_engines[device]) {
+            g_engines[device] = ctx;
+            ctx = NULL;
+        }
+        pthread_mutex_unlock(&g_engine_mu);
+    }
+    bpe_gpu_destroy(ctx);
+}
+
+void bpe_release_engines(void)
+{
+    pthread_mutex_lock(&g_engine_mu);
+    for (int d = 0; d < ENGINE_CACHE; d++) {
+        bpe_gpu_destroy(g_engines[d]);
+        g_engines[d] = NULL;
+    }
+    pthread_mutex_unlock(&g_engine_mu);
 }
 
 /* merges (pairs) -> a reference-shaped merge list */
@@ -231,31 +282,64 @@ static uint32_t *arr_to_pairs(dyn_arr_t *arr, size_t *k)
     return pairs;
 }
 
+/* a multi-GB id buffer is first touched by the fetch's copy threads: ask for
+ * transparent huge pages (512x fewer page faults where THP is in "madvise" mode) */
+static uint32_t *alloc_ids(size_t n)
+{
+    const size_t bytes = (n ? n : 1) * sizeof(uint32_t);
+    uint32_t *p = malloc(bytes);
+    if (p && bytes >= ((size_t)64 << 20)) {
+        const uintptr_t lo = ((uintptr_t)p + 4095) & ~(uintptr_t)4095, hi = ((uintptr_t)p + bytes) & ~(uintptr_t)4095;
+        if (hi > lo) (void)madvise((void *)lo, hi - lo, MADV_HUGEPAGE);
+    }
+    return p;
+}
+
+/* BPE_DEBUG: wall-clock phases of compress / train_loaded on stderr */
+static double wall_ms(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec / 1e6;
+}
+
+static void phase(const char *what, double *t)
+{
+    if (!getenv("BPE_DEBUG")) return;
+    const double now = wall_ms();
+    fprintf(stderr, "bpe: %s %.2f ms\n", what, now - *t);
+    *t = now;
+}
+
 /* train on the corpus loaded into ctx, fetch merges + ids; destroys ctx */
-static dyn_arr_t *train_loaded(bpe_gpu_ctx *ctx, long max_merges, uint32_t **encoding, size_t *len)
+static dyn_arr_t *train_loaded(bpe_gpu_ctx *ctx, int device, long max_merges, uint32_t **encoding, size_t *len)
 {
     dyn_arr_t *arr = NULL;
     uint32_t *pairs = NULL, *ids = NULL;
     size_t k = 0, n_ids = 0, got = 0;
     int rc;
+    double t = wall_ms();
     if ((rc = bpe_gpu_train(ctx, max_merges, &k))) { report("train", rc); goto fail; }
+    phase("train", &t);
     pairs = malloc((k ? k : 1) * 2 * sizeof(uint32_t));
     if (!pairs) goto fail;
     if ((rc = bpe_gpu_fetch_merges(ctx, pairs, k, &got))) { report("fetch merges", rc); goto fail; }
     if ((rc = bpe_gpu_fetch_ids(ctx, NULL, 0, &n_ids))) { report("fetch ids", rc); goto fail; }
-    ids = malloc((n_ids ? n_ids : 1) * sizeof(uint32_t));
+    ids = alloc_ids(n_ids);
     if (!ids) goto fail;
     if ((rc = bpe_gpu_fetch_ids(ctx, ids, n_ids, &n_ids))) { report("fetch ids", rc); goto fail; }
+    phase("fetch merges + ids", &t);
     arr = pairs_to_arr(pairs, k);
     if (!arr) goto fail;
+    phase("merge list", &t);
     bpe_gpu_get_stats(ctx, &g_last_stats);
-    bpe_gpu_destroy(ctx);
+    close_engine(device, ctx, 1);
     free(pairs);
     *encoding = ids;
     *len = n_ids;
     return arr;
 fail:
-    bpe_gpu_destroy(ctx);
+    close_engine(device, ctx, 0);
     free(pairs);
     free(ids);
     *encoding = NULL;
@@ -271,12 +355,12 @@ dyn_arr_t *bpe_train_bytes(const uint8_t *bytes, size_t n, long max_merges, int 
     int rc;
     if ((rc = open_engine(device, &ctx)) || (rc = bpe_gpu_load(ctx, bytes, n))) {
         if (ctx) report("load", rc);
-        bpe_gpu_destroy(ctx);
+        close_engine(device, ctx, 0);
         *encoding = NULL;
         *len = 0;
         return NULL;
     }
-    return train_loaded(ctx, max_merges, encoding, len);
+    return train_loaded(ctx, device, max_merges, encoding, len);
 }
 
 /* ------------------------------------------------- one process, N devices */
@@ -483,17 +567,20 @@ dyn_arr_t *compress_ex(const char *path, long max_merges, int device, uint32_t *
     }
     bpe_gpu_ctx *ctx = NULL;
     size_t n = 0;
+    double t = wall_ms();
     int rc = open_engine(device, &ctx);
+    phase("engine", &t);
     if (!rc && (rc = bpe_gpu_load_fd(ctx, fileno(f), (size_t)size, &n))) {
         if (rc == BPE_GPU_EIO) perror("fread");
         else report("load", rc);
     }
     fclose(f);
     if (rc) {
-        bpe_gpu_destroy(ctx);
+        close_engine(device, ctx, 0);
         return NULL;
     }
-    return train_loaded(ctx, max_merges, encoding, len);
+    phase("ingest", &t);
+    return train_loaded(ctx, device, max_merges, encoding, len);
 }
 
 dyn_arr_t *compress(const char *path, uint32_t **encoding, size_t *len)
@@ -533,7 +620,7 @@ uint32_t *bpe_encode_bytes(const uint8_t *bytes, size_t n, dyn_arr_t *pair_arr, 
     if ((rc = bpe_gpu_load(ctx, bytes, n))) { report("load", rc); goto done; }
     if ((rc = bpe_gpu_encode(ctx, pairs, k))) { report("encode", rc); goto done; }
     if ((rc = bpe_gpu_fetch_ids(ctx, NULL, 0, &n_ids))) { report("fetch ids", rc); goto done; }
-    ids = malloc((n_ids ? n_ids : 1) * sizeof(uint32_t));
+    ids = alloc_ids(n_ids);
     if (ids && (rc = bpe_gpu_fetch_ids(ctx, ids, n_ids, &n_ids))) {
         report("fetch ids", rc);
         free(ids);
@@ -544,7 +631,7 @@ uint32_t *bpe_encode_bytes(const uint8_t *bytes, size_t n, dyn_arr_t *pair_arr, 
         bpe_gpu_get_stats(ctx, &g_last_stats);
     }
 done:
-    bpe_gpu_destroy(ctx);
+    close_engine(device, ctx, ids != NULL);
     free(pairs);
     return ids;
 }
@@ -563,7 +650,7 @@ char *decompress(uint32_t *encoding, size_t len, dyn_arr_t *pair_arr)
     uint32_t *pairs = arr_to_pairs(pair_arr, &k);
     if (!pairs) return NULL;
     char *out = NULL;
-    long dev;
+    long dev = -1;
     bpe_gpu_ctx *ctx = NULL;
     if (env_int("BPE_DEVICE", 0, &dev) || open_engine((int)dev, &ctx)) goto done;
     int rc = bpe_gpu_decode(ctx, encoding, len, pairs, k, NULL, 0, &out_len);
@@ -582,7 +669,7 @@ char *decompress(uint32_t *encoding, size_t len, dyn_arr_t *pair_arr)
     }
     out[out_len] = '\0';
 done:
-    bpe_gpu_destroy(ctx);
+    close_engine((int)dev, ctx, out != NULL);
     free(pairs);
     return out;
 }
