@@ -1127,27 +1127,69 @@ __global__ __launch_bounds__(256) void k_hot_hist(const Eng *__restrict__ E) {
 // Rebuild, pass 2 (one block): the threshold -- the lowest bin edge that keeps
 // the listed keys within HOT_TARGET (or the top bin alone); hot_fill = keys
 // that will be listed (> HOT_LIMIT / 2: the host falls back to the level
-// summaries).  Zeroes the histogram for the next rebuild.
+// summaries).  Zeroes the histogram for the next rebuild.  Walking the bins
+// down from the top, a nonempty bin is taken while the keys at or above it
+// stay within the target (the top nonempty bin always): so the chosen bin is
+// the lowest nonempty one whose inclusive suffix sum is <= target, found with
+// a block suffix scan (each thread owns PB consecutive bins) and an LDS min.
 __global__ __launch_bounds__(1024) void k_hot_pick(const Eng *__restrict__ E, Ctl *__restrict__ C) {
-    __shared__ uint32_t h[HOT_BINS];
-    for (uint32_t x = threadIdx.x; x < HOT_BINS; x += blockDim.x) {
-        h[x] = E->hot_hist[x];
-        E->hot_hist[x] = 0;
+    constexpr uint32_t PB = (HOT_BINS + 1023) / 1024;
+    __shared__ uint32_t wsum[16], sbest, stop_b;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // thread tid owns bins [HOT_BINS - (tid + 1) PB, HOT_BINS - tid PB): thread 0 the top ones
+    uint32_t c[PB], tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PB; k++) {
+        const int b = (int)HOT_BINS - 1 - (int)(tid * PB + k);  // descending
+        c[k] = b >= 2 ? E->hot_hist[b] : 0u;
+        if (b >= 0) E->hot_hist[b] = 0;
+        tot += c[k];
     }
+    if (tid == 0) {
+        sbest = HOT_BINS;
+        stop_b = 0;
+    }
+    // exclusive prefix over threads in descending-bin order = keys in higher bins
+    uint32_t incl = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    if (threadIdx.x) return;
-    uint32_t T = 0, cum = 0;
-    for (int b = (int)HOT_BINS - 1; b >= 2; b--) {
-        const uint32_t c = h[b];
-        if (!c) continue;
-        if (cum > 0 && cum + c > E->hot_target) break;
-        cum += c;
-        T = hot_bin_lo((uint32_t)b);
+    uint32_t above = incl - tot;
+    for (uint32_t w = 0; w < wv; w++) above += wsum[w];
+    const uint32_t target = E->hot_target, above0 = above;
+    uint32_t best = HOT_BINS, topb = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PB; k++) {
+        const int b = (int)HOT_BINS - 1 - (int)(tid * PB + k);
+        if (b >= 2 && c[k]) {
+            if (above + c[k] <= target) best = (uint32_t)b;  // (descending: the last such is the lowest)
+            topb = max(topb, (uint32_t)b);
+        }
+        above += c[k];
     }
-    C->hot_T = T < 2 ? 2u : T;  // no count >= 2: an empty list, k_select stops (max <= 1)
-    C->hot_fill = cum;
-    C->hot_n = 0;
-    C->hot_rebuilds++;
+    if (best < HOT_BINS) atomicMin(&sbest, best);
+    if (topb) atomicMax(&stop_b, topb);
+    __syncthreads();
+    // (no bin within the target: the top nonempty bin alone; no count >= 2:
+    // an empty list, the select stops on max <= 1)
+    const uint32_t bsel = sbest < HOT_BINS ? sbest : stop_b;
+    above = above0;
+#pragma unroll
+    for (uint32_t k = 0; k < PB; k++) {
+        const int b = (int)HOT_BINS - 1 - (int)(tid * PB + k);
+        above += c[k];
+        if (stop_b >= 2 && b == (int)bsel) C->hot_fill = above;  // keys in bins >= bsel
+    }
+    if (tid == 0) {
+        const uint32_t T = stop_b >= 2 ? hot_bin_lo(bsel) : 2u;
+        C->hot_T = T < 2 ? 2u : T;
+        if (stop_b < 2) C->hot_fill = 0;
+        C->hot_n = 0;
+        C->hot_rebuilds++;
+    }
 }
 
 // Rebuild, pass 3: list every key with count >= hot_T
