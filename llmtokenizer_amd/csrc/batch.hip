@@ -38,9 +38,9 @@
 
 namespace bpeamd {
 
-static_assert(TOPK == 32, "wave merges hold two 32-entry lists");
+static_assert(TOPK == 64, "a wave holds a list, one entry per lane");
 static_assert(BRB == 2 * (1024 / 64), "the select's 16 waves merge two partial lists each");
-static_assert(BK < 32, "member masks are 32-bit");
+static_assert(BK < 64, "member masks are 64-bit");
 #ifndef BPE_SU
 #define BPE_SU 1
 #endif
@@ -82,8 +82,7 @@ __device__ inline KV wave_sort64(KV x) {
     return x;
 }
 
-// lanes 0..31 one sorted list, lanes 32..63 another in reverse: a bitonic
-// sequence; after the merge the lanes hold the union sorted (0..31 its top)
+// a bitonic sequence over the 64 lanes, sorted (lane 0 first in argmax order)
 __device__ inline KV wave_merge64(KV x) {
     const uint32_t lane = lane_id();
 #pragma unroll
@@ -94,15 +93,18 @@ __device__ inline KV wave_merge64(KV x) {
     return x;
 }
 
+// the top 64 of two sorted lists a, b (one entry per lane): the better of
+// a[i] and b[63 - i] is the top 64 of the union as a bitonic sequence
+__device__ inline KV wave_top(const KV &a, const KV &b) {
+    const KV br = kv_shfl(b, (int)(63 - lane_id()));
+    return wave_merge64(kv_ahead(br, a) ? br : a);
+}
+
 // tree of the block's wave lists in part[w] (sorted, TOPK each): part[0] = top TOPK
 __device__ inline void block_list_tree(KV (*part)[TOPK], uint32_t nw) {
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (uint32_t s = 1; s < nw; s <<= 1) {
-        if (w % (2 * s) == 0 && w + s < nw) {
-            KV x = lane < 32 ? part[w][lane] : part[w + s][63 - lane];
-            x = wave_merge64(x);
-            if (lane < 32) part[w][lane] = x;
-        }
+        if (w % (2 * s) == 0 && w + s < nw) part[w][lane] = wave_top(part[w][lane], part[w + s][lane]);
         __syncthreads();
     }
 }
@@ -125,11 +127,9 @@ __device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bs
             if (c) x = KV{pack_val(c, (uint32_t)(key >> 32), (uint32_t)key, Bsz), key};
         }
         x = wave_sort64(x);
-        const KV r = kv_shfl(run, (int)(63 - lane));
-        if (lane >= 32) x = r;
-        run = wave_merge64(x);
+        run = wave_top(run, x);
     }
-    if (lane < TOPK) part[w][lane] = run;
+    part[w][lane] = run;
     __syncthreads();
     block_list_tree(part, nw);
     if (threadIdx.x < TOPK) out[threadIdx.x] = part[0][threadIdx.x];
@@ -162,17 +162,15 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
     const uint32_t *cgw = reinterpret_cast<const uint32_t *>(Cg);
     const uint32_t *bgw = reinterpret_cast<const uint32_t *>(Bg);
     // partial lists 2w and 2w+1 (published by the other blocks: L2-coherent loads)
-    KV x;
-    {
-        const uint32_t src = lane < 32 ? (2 * w) * TOPK + lane : (2 * w + 1) * TOPK + (63 - lane);
-        x.v = aload64(&Bg->pv[src]);
-        x.k = aload64(&Bg->pk[src]);
-    }
+    KV x, y;
+    x.v = aload64(&Bg->pv[(2 * w) * TOPK + lane]);
+    x.k = aload64(&Bg->pk[(2 * w) * TOPK + lane]);
+    y.v = aload64(&Bg->pv[(2 * w + 1) * TOPK + lane]);
+    y.k = aload64(&Bg->pk[(2 * w + 1) * TOPK + lane]);
     const uint32_t cv = tid < CW ? aload(cgw + tid) : 0u;
     const uint32_t bv = tid < BAT_HEAD_WORDS ? aload(bgw + tid) : 0u;
     const uint32_t rk = tid < 256 ? E->rank[tid] : 0u;
-    x = wave_merge64(x);
-    if (lane < 32) part[w][lane] = x;
+    part[w][lane] = wave_top(x, y);
     if (tid < CW) scw[tid] = cv;
     if (tid < BAT_HEAD_WORDS) sbw[tid] = bv;
     if (tid < 256) srank[tid] = rk;
@@ -567,23 +565,24 @@ __global__ __launch_bounds__(1024) void k_bsel(const Eng *__restrict__ E, Ctl *_
 }
 
 // ----------------------------------------------------------------- k_bscan
-constexpr uint32_t RH = 128;  // LDS role table: member ids -> (left-member mask, right-member mask)
-__device__ inline uint32_t rh_hash(uint32_t id) { return (id * 2654435761u) >> 25; }
+constexpr uint32_t RH = 256;  // LDS role table: member ids -> (left-member mask, right-member mask)
+__device__ inline uint32_t rh_hash(uint32_t id) { return (id * 2654435761u) >> 24; }
 
 struct RoleTab {
-    uint32_t id[RH], lm[RH], rm[RH];
+    uint32_t id[RH];
+    unsigned long long lm[RH], rm[RH];
     __device__ inline void put(uint32_t x, bool right, uint32_t m) {
         uint32_t s = rh_hash(x);
         for (;;) {
             const uint32_t prev = atomicCAS(&id[s], HOLE, x);
             if (prev == HOLE || prev == x) {
-                atomicOr(right ? &rm[s] : &lm[s], 1u << m);
+                atomicOr(right ? &rm[s] : &lm[s], 1ull << m);
                 return;
             }
             s = (s + 1) & (RH - 1);
         }
     }
-    __device__ inline void get(uint32_t x, uint32_t *l, uint32_t *r) const {
+    __device__ inline void get(uint32_t x, unsigned long long *l, unsigned long long *r) const {
         uint32_t s = rh_hash(x);
         for (;;) {  // at most 2 BK < RH / 2 ids
             const uint32_t v = id[s];
@@ -633,13 +632,13 @@ __device__ inline uint32_t tok_at_b(const uint32_t *__restrict__ tok, const BHal
 template <bool SH>
 __device__ inline uint32_t cover_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const uint32_t *sa,
                                     const uint32_t *sb, const BHalo &H, uint32_t p, int64_t ps, int64_t n) {
-    uint32_t lmk, rmk;
+    unsigned long long lmk, rmk;
     rt.get(p, &lmk, &rmk);
     if (!rmk) return BK;
     const int64_t pps = v_left<SH>(tok, ps);
     const uint32_t pp = tok_at_b<SH>(tok, H, pps, n);
-    for (uint32_t q = rmk; q; q &= q - 1) {
-        const uint32_t mm = __ffs(q) - 1;
+    for (unsigned long long q = rmk; q; q &= q - 1) {
+        const uint32_t mm = __ffsll(q) - 1;
         if (sa[mm] != pp) continue;
         if (sa[mm] != sb[mm]) return mm;
         uint32_t L;  // run of p ending at ps
@@ -662,13 +661,13 @@ __device__ inline uint32_t cover_of(const uint32_t *__restrict__ tok, const Role
 template <bool SH>
 __device__ inline uint32_t starts_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const uint32_t *sb,
                                      const uint32_t *sla, const BHalo &H, uint32_t q, int64_t kq, int64_t n) {
-    uint32_t lmk, rmk;
+    unsigned long long lmk, rmk;
     rt.get(q, &lmk, &rmk);
     if (!lmk) return BK;
-    const int64_t kn = v_right(kq, sla[__ffs(lmk) - 1], n);
+    const int64_t kn = v_right(kq, sla[__ffsll(lmk) - 1], n);
     const uint32_t qq = tok_at_b<SH>(tok, H, kn, n);
-    for (uint32_t t = lmk; t; t &= t - 1) {
-        const uint32_t mm = __ffs(t) - 1;
+    for (unsigned long long t = lmk; t; t &= t - 1) {
+        const uint32_t mm = __ffsll(t) - 1;
         if (sb[mm] == qq) return mm;
     }
     return BK;
@@ -1116,11 +1115,16 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             ovm = __ballot(lane < k && ov != 0);
         }
         const uint32_t sbase = in ? B->sbase[lane] : 0;
-        const uint32_t nl0 = 2 * lane < 4 * k ? E->bvnl[2 * lane] : 0, nl1 = 2 * lane + 1 < 4 * k ? E->bvnl[2 * lane + 1] : 0;
+        uint32_t nlv[4], nls = 0;  // my member's listed-id counts (ids >= DENSE) per vector
+#pragma unroll
+        for (uint32_t v = 0; v < 4; v++) {
+            nlv[v] = in ? E->bvnl[4 * lane + v] : 0u;
+            nls += nlv[v];
+        }
         const uint32_t tla = in ? E->tlen[ma] : 0, tlb = in ? E->tlen[mb] : 0;
         // exclusive prefix sum of R and max of bound over the members before me
         unsigned long long rpre = R;
-        uint32_t bpre = bnd, lpre = nl0 + nl1;
+        uint32_t bpre = bnd, lpre = nls;
         for (int o = 1; o < 64; o <<= 1) {
             const unsigned long long y = __shfl_up(rpre, o);
             const uint32_t yb = __shfl_up(bpre, o), yl = __shfl_up(lpre, o);
@@ -1153,8 +1157,14 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             ssb[lane] = sbase;
             spre[lane] = (uint32_t)rex;
         }
-        if (2 * lane < 4 * k) snl[2 * lane + 1] = lpre - nl1;
-        if (2 * lane + 1 < 4 * k) snl[2 * lane + 2] = lpre;
+        if (in) {
+            uint32_t q = lpre - nls;
+#pragma unroll
+            for (uint32_t v = 0; v < 4; v++) {
+                q += nlv[v];
+                snl[4 * lane + v + 1] = q;
+            }
+        }
         if (lane == 0) {
             snl[0] = 0;
             spre[k] = k ? rall : 0u;

@@ -112,8 +112,8 @@ struct EncBatch {
 // occurrences in the pre-batch tokens; k_bapply applies the prefix of members
 // that are provably the argmax in turn (count above every key the earlier
 // members can create) and drops the rest, which the next selection sees again.
-constexpr uint32_t TOPK = 32;   // sorted list length (partials and the merged list)
-constexpr uint32_t BK = 31;     // members per batch (one list entry stays for the strictness test)
+constexpr uint32_t TOPK = 64;   // sorted list length (partials and the merged list): one entry per lane
+constexpr uint32_t BK = 63;     // members per batch (one list entry stays for the strictness test)
 constexpr uint32_t BRB = 32;    // k_bsel reduce blocks (partial lists)
 constexpr uint32_t BREPL = 2;   // replicas of a member's dense delta accumulators
 constexpr uint32_t BSB = 256;   // k_bscan blocks (1024 threads, one per CU)
