@@ -519,14 +519,24 @@ __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat 
         }
     }
     // the last block to finish marks the rewrite done (a k_bsel launched again
-    // after a stop has nothing to redo)
+    // after a stop has nothing to redo); sharded, it also writes my edge record
+    // of the rewritten tokens (every block's stores released before its
+    // ticket, acquired by the last), which the records gather after this
+    // launch carries to the next scan's halo
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) last = atomicAdd(&B->ra_done, 1u) == nA - 1;
+    if (tid == 0) {
+        if (sh) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        last = __hip_atomic_fetch_add(&B->ra_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nA - 1;
+        if (last && sh) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
     __syncthreads();
-    if (last && tid == 0) {
+    if (!last) return;
+    if (tid == 0) {
         B->ra_k = 0;
         B->ra_done = 0;
     }
+    if (sh) edge_record_block(E, C);
 }
 
 __global__ __launch_bounds__(1024) void k_bsel(const Eng *__restrict__ E, Ctl *__restrict__ C) {

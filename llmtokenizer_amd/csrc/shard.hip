@@ -264,8 +264,8 @@ int launch_group_bstep(bpe_gpu_group *g) {
     for (bpe_gpu_ctx *c : g->cs) k_bscan<true><<<BSB, SCAN_T, 0, g->st>>>(c->dE, c->dC);
     if ((r = ex_bsum(g))) return r;
     for (bpe_gpu_ctx *c : g->cs) k_bapply<true><<<BAPPLY_B, 1024, 0, g->st>>>(c->dE, c->dC);
+    // (k_bsel's last rewrite block writes the edge record of the new tokens)
     for (bpe_gpu_ctx *c : g->cs) k_bsel<<<BRB + BAPPLY_A, 1024, 0, g->st>>>(c->dE, c->dC);
-    for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 1);  // (after the rewrite)
     HIPCHK(hipGetLastError());
     return ex_records(g, g->d_ptrs);
 }
