@@ -298,7 +298,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 const unsigned long long y = __shfl_up(pre, o);
                 if ((int)lane >= o) pre += y;
             }
-            const unsigned long long over = __ballot(lane > 0 && lane < k && pre > E->n0);
+            const unsigned long long over = __ballot(lane > 0 && lane < k && pre > B->stage_cap);
             uint32_t why_end = endwhy == 8 ? 0 : endwhy;
             // sharded: every shard must form the same batch, so a shard whose
             // staging overflows scans nothing from that member on and flags it

@@ -247,6 +247,7 @@ struct bpe_gpu_ctx {
     uint32_t sharded = 0, shard = 0, nshards = 1;
     uint32_t xfused = 0;                   // fused sharded step (P2P group, shard.hip)
     uint32_t sbatch = 0;                   // sharded training in batches (shard.hip, batch.hip)
+    uint64_t stage_cap = 0;                // batch occurrence staging positions (Bat::stage_cap's source)
     const P2P *xp2p = nullptr;             // its exchange descriptor (device)
     unsigned long long xtimeout = 0;       // its wait bound (wall-clock ticks)
     Eng h{};
@@ -478,6 +479,11 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         // z = 0 mod d (tests drive the drop path with it)
         const uint32_t dt = (uint32_t)getenv_int("BPE_BATCH_DROP_TEST", 0);
         if (dt) HIPCHK(hipMemcpyAsync(&h.bat->drop_test, &dt, 4, hipMemcpyHostToDevice, c->st));
+        // BPE_BATCH_STAGE=p: only p staging positions (tests drive the overflow
+        // cut -- sharded: the flag in the exchange and the re-formed batch)
+        c->stage_cap = n0;
+        if (const char *t = getenv("BPE_BATCH_STAGE")) c->stage_cap = std::min<uint64_t>(n0, std::max(1ll, atoll(t)));
+        HIPCHK(hipMemcpyAsync(&h.bat->stage_cap, &c->stage_cap, 8, hipMemcpyHostToDevice, c->st));
         HIPCHK(hipStreamSynchronize(c->st));  // (dt is on the stack)
     }
     h.ntiles = (n0 + CTILE - 1) / CTILE;

@@ -124,7 +124,8 @@ struct Bat {
     unsigned long long dD;            // distinct-pair delta of the applied batch
     unsigned long long nbatch, ndrop, nretry;  // batches applied; members dropped by the verification; batches re-formed
     unsigned long long why[8];        // what ended each batch's formation (BPE_DEBUG report)
-    uint32_t drop_test, pad1, pad2, pad3;  // > 0: members j >= 1 with (z0 + j) % drop_test == 0 fail (tests)
+    uint32_t drop_test, pad1;              // > 0: members j >= 1 with (z0 + j) % drop_test == 0 fail (tests)
+    unsigned long long stage_cap;          // occurrence staging positions (n0; BPE_BATCH_STAGE lowers it: tests)
     // device wall-clock spans (first block entry, complemented, and last block
     // exit of this batch's k_bscan / k_bapply; folded by the select) and
     // their sums; table updates role B made

@@ -83,6 +83,18 @@ def test_dropped_members_match_oracle():
     assert dropped > 0
 
 
+def test_staging_cut_matches_oracle(monkeypatch):
+    """BPE_BATCH_STAGE: a small occurrence staging area ends batch formation
+    where the members' candidate lists stop fitting (never before the first)"""
+    monkeypatch.setenv("BPE_BATCH_STAGE", "100")
+    batches = merges = 0
+    for seed in (506, 507):
+        st = _check(synth_bytes(seed, 120000), 500)
+        batches += st["batches"]
+        merges += st["merges"]
+    assert merges > batches > 0
+
+
 @pytest.mark.parametrize("seed,n,mm", [(501, 1 << 20, 500), (502, 300000, 2000), (503, 60000, -1)])
 def test_batches_match_oracle_uniform(seed, n, mm):
     data = synth_bytes(seed, n)

@@ -146,3 +146,23 @@ def test_rccl_group_single_rank():
     e.train(300)
     _assert_same(g.merges(), g.all_ids(), e.merges(), e.ids(), "rccl")
     print("graph captured:", g.graph_captured())
+
+
+@pytest.mark.parametrize("knob", ["drop", "stage"])
+def test_group_batch_failures_vs_oracle_rule(knob, monkeypatch, engine_mode):
+    """sharded batches that fail and are formed again: members dropped by the
+    verification (BPE_BATCH_DROP_TEST) and a staging area some shards overflow
+    (BPE_BATCH_STAGE: the shard's flag travels in the exchange, every shard
+    re-forms the batch shorter) -- merges and ids still the oracle's"""
+    if engine_mode != "batch":
+        pytest.skip("batch engine only")
+    monkeypatch.setenv("BPE_BATCH_DROP_TEST" if knob == "drop" else "BPE_BATCH_STAGE", "3" if knob == "drop" else "40")
+    rng = random.Random(77 if knob == "drop" else 78)
+    for seed in range(3):
+        data = synth_bytes(990 + seed, 150000)
+        cuts = _split(len(data), 4, rng)
+        m, ids, g = _group_train(data, cuts, 400)
+        om, oi, _ = O.train(data, 400, O.RULE)
+        _assert_same(m, ids, om, oi, (knob, seed))
+        st = g.stats()
+        assert st["batch_retries"] > 0, st
