@@ -48,6 +48,15 @@ static_assert(BK < 64, "member masks are 64-bit");
 #define BPE_RU 4
 #endif
 constexpr uint32_t SU = BPE_SU;  // k_bscan candidates per thread per round (1: measured fastest, 85 vs 91 ms at 4)
+#ifndef BPE_FR
+#define BPE_FR 4
+#endif
+// k_bscan rounds staged in LDS per flush (one block barrier pair per flush;
+// 1 GiB x 8192: 1 -> 75.6 ms, 2 -> 72.5, 4 -> 71.8)
+constexpr uint32_t FR = BPE_FR;
+#ifndef BPE_SCAN_PF
+#define BPE_SCAN_PF 1
+#endif
 constexpr uint32_t RU = BPE_RU;  // rewrite occurrences per thread per round
 
 // debug timeline of a batch (BPE_DEBUG_TS; E->dbgts rows indexed by batch)
@@ -252,7 +261,9 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             const uint32_t hsh = murmur_pair(u, v);
             const uint32_t clast = __shfl(c, (int)(nl ? nl - 1 : 0));
             bool order_ok = true;
-            for (uint32_t p = 1; p < TOPK; p++) {  // (uniform loop; readlane needs every lane)
+            const bool tie_next = lane < nl && !(c > (lane + 1 < nl ? cnext : 0u));
+            const bool check = __ballot(!stable && lane > 0 && lane < BK && tie_next) != 0;  // (wave-uniform)
+            for (uint32_t p = 1; check && p < TOPK; p++) {  // (uniform loop; readlane needs every lane)
                 const uint32_t cp = __builtin_amdgcn_readlane((int)c, (int)p);
                 const uint32_t hp = __builtin_amdgcn_readlane((int)hsh, (int)p);
                 const unsigned long long kp =
@@ -428,8 +439,49 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
 // Role A of the batch k_bapply applied last (blocks [BRB, grid)): its
 // members' spans in tok[], their occurrence lists copied into the pool.
 // Nothing the selection reads depends on it; the next k_bscan does.
+// Role A of one member for occurrences [elo, ehi) of its staged list: the
+// new token's span in tok[] (id at its start, end code at its end slot,
+// HOLE in between) and the occurrence copied into the pool; this block is
+// bidm of the nbm blocks on the member.  L1: my last token's start (sharded)
+__device__ inline void rewrite_occ(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat *__restrict__ B, uint32_t z,
+                                   uint32_t la, uint32_t lb, uint32_t base, uint32_t obase, uint32_t elo, uint32_t ehi,
+                                   uint32_t bidm, uint32_t nbm, uint64_t L1) {
+    uint32_t *tok = E->tok;
+    const uint64_t n = E->n0;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t e0 = elo + bidm * blockDim.x * RU; e0 < ehi; e0 += nbm * blockDim.x * RU) {
+        uint32_t pos[RU];
+        uint16_t tg[RU];
+#pragma unroll
+        for (uint32_t u = 0; u < RU; u++) {
+            const uint32_t e = e0 + u * blockDim.x + tid;
+            pos[u] = e < ehi ? E->ids_out[base + e] : 0u;
+            tg[u] = e < ehi ? E->btag[base + e] : (uint16_t)0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < RU; u++) {
+            const uint32_t e = e0 + u * blockDim.x + tid;
+            if (e >= ehi) continue;
+            const uint64_t i = pos[u], j = i + la, kq = j + lb;
+            tok[i] = z;
+            if (j < n) {  // (sharded: else b starts in a later shard, which retires it)
+                if (kq - 1 - i > E->end_max) B->ra_err = 5;  // (the select's staged control block would drop C->err)
+                if (kq - 1 == j) {
+                    tok[j] = end_code(kq - 1 - i);
+                } else {
+                    tok[j] = HOLE;
+                    if (kq - 1 < n) tok[kq - 1] = end_code(kq - 1 - i);
+                }
+                if (j == L1) C->L1new = (uint32_t)i;  // my last token moved
+            }
+            E->occ[obase + e] = (uint32_t)i;
+            E->occnb[obase + e] = tg[u];
+        }
+    }
+}
+
 __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat *__restrict__ B) {
-    __shared__ uint32_t sz[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], ablk[BK + 1];
+    __shared__ uint32_t sz[BK], sla[BK], slb[BK], sR[BK], slo[BK], ssb[BK], spre[BK + 1], ablk[BK + 1];
     __shared__ uint32_t sk, stop_, am, last;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t nA = gridDim.x - BRB, bid = blockIdx.x - BRB;
@@ -437,9 +489,11 @@ __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat 
         const uint32_t k = aload(&B->ra_k);
         const bool in = lane < k;
         const uint32_t R = in ? B->ra_R[lane] : 0u;
-        const uint32_t tot = k ? B->ra_pre[k] : 0u;
-        // blocks in proportion to the occurrences (>= 1 per member)
-        const uint32_t nb = in ? 1 + (uint32_t)(tot ? (uint64_t)(nA - k) * R / tot : 0) : 0;
+        const uint32_t lo = in ? B->ra_lo[lane] : 0u;  // (k_bapply rewrote [0, lo))
+        unsigned long long tot = R - lo;
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        // blocks in proportion to the occurrences left (>= 1 per member)
+        const uint32_t nb = in ? 1 + (uint32_t)(tot ? (uint64_t)(nA - k) * (R - lo) / tot : 0) : 0;
         uint32_t nbp = nb;
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(nbp, o);
@@ -450,6 +504,7 @@ __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat 
             sla[lane] = B->ra_la[lane];
             slb[lane] = B->ra_lb[lane];
             sR[lane] = R;
+            slo[lane] = lo;
             ssb[lane] = B->ra_sbase[lane];
             spre[lane] = B->ra_pre[lane];
             ablk[lane] = nbp - nb;
@@ -484,40 +539,9 @@ __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat 
             C->F1 = (uint32_t)(end < n ? end : n);
         }
     }
-    if (m < k) {
-        const uint64_t L1 = sh ? C->L1 : ~0ull;
-        const uint32_t z = sz[m], la = sla[m], lb = slb[m], Rm = sR[m], base = ssb[m], obase = stop_ + spre[m];
-        const uint32_t bidm = bid - ablk[m], nbm = ablk[m + 1] - ablk[m];
-        for (uint32_t e0 = bidm * blockDim.x * RU; e0 < Rm; e0 += nbm * blockDim.x * RU) {
-            uint32_t pos[RU];
-            uint16_t tg[RU];
-#pragma unroll
-            for (uint32_t u = 0; u < RU; u++) {
-                const uint32_t e = e0 + u * blockDim.x + tid;
-                pos[u] = e < Rm ? E->ids_out[base + e] : 0u;
-                tg[u] = e < Rm ? E->btag[base + e] : (uint16_t)0;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < RU; u++) {
-                const uint32_t e = e0 + u * blockDim.x + tid;
-                if (e >= Rm) continue;
-                const uint64_t i = pos[u], j = i + la, kq = j + lb;
-                tok[i] = z;
-                if (j < n) {  // (sharded: else b starts in a later shard, which retires it)
-                    if (kq - 1 - i > E->end_max) B->ra_err = 5;  // (the select's staged control block would drop C->err)
-                    if (kq - 1 == j) {
-                        tok[j] = end_code(kq - 1 - i);
-                    } else {
-                        tok[j] = HOLE;
-                        if (kq - 1 < n) tok[kq - 1] = end_code(kq - 1 - i);
-                    }
-                    if (j == L1) C->L1new = (uint32_t)i;  // my last token moved
-                }
-                E->occ[obase + e] = (uint32_t)i;
-                E->occnb[obase + e] = tg[u];
-            }
-        }
-    }
+    if (m < k)
+        rewrite_occ(E, C, B, sz[m], sla[m], slb[m], ssb[m], stop_ + spre[m], slo[m], sR[m], bid - ablk[m],
+                    ablk[m + 1] - ablk[m], sh ? C->L1 : ~0ull);
     // the last block to finish marks the rewrite done (a k_bsel launched again
     // after a stop has nothing to redo); sharded, it also writes my edge record
     // of the rewritten tokens (every block's stores released before its
@@ -698,8 +722,8 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     ts_mark(E, bi, BT_SCAN_IN, true);
     if (threadIdx.x == 0) atomicMax(&B->sc_in, ~wall_clock64());
     __shared__ uint32_t s[4][DENSE];
-    __shared__ uint32_t list[SCAN_T * SU];  // this round's occurrences (position, tag), flushed per round
-    __shared__ uint16_t ltag[SCAN_T * SU];
+    __shared__ uint32_t list[SCAN_T * SU * FR];  // the rounds' occurrences (position, tag), flushed every FR rounds
+    __shared__ uint16_t ltag[SCAN_T * SU * FR];
     __shared__ uint32_t lcount, gbase, list_n, covc, sm, sk, sz0, bRs;
     __shared__ uint32_t gcnt[2];
     __shared__ uint32_t sa[BK], sb[BK], sla[BK];
@@ -769,21 +793,36 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         // SU candidates per thread per round, in stages, so that their chains of
         // dependent gathers overlap; the round's occurrences are staged in LDS
         // and leave with one global atomic per block
-        for (uint32_t e0 = bid * SCAN_T * SU; e0 < len; e0 += nblk * SCAN_T * SU) {  // uniform trip count
+        // the next round's list entries are loaded while this round runs
+        const uint32_t stride = nblk * SCAN_T * SU;
+        uint32_t nent[SU];
+        uint16_t ntg[SU];
+        auto fetch = [&](uint32_t f0) {
+#pragma unroll
+            for (uint32_t u = 0; u < SU; u++) {
+                const uint32_t e = f0 + u * SCAN_T + tid;
+                nent[u] = 0;
+                ntg[u] = 0xFFFFu;
+                if (e < len) {
+                    nent[u] = mode == 0 ? E->plist[off + e] : E->occ[off + e];
+                    if (mode) ntg[u] = E->occnb[off + e];
+                }
+            }
+        };
+        fetch(bid * SCAN_T * SU);
+        uint32_t round = 0;
+        for (uint32_t e0 = bid * SCAN_T * SU; e0 < len; e0 += stride) {  // uniform trip count
             uint32_t ent[SU];
             uint16_t etg[SU];
             bool val[SU];
+            if (!BPE_SCAN_PF) fetch(e0);
 #pragma unroll
             for (uint32_t u = 0; u < SU; u++) {
-                const uint32_t e = e0 + u * SCAN_T + tid;
-                val[u] = e < len;
-                ent[u] = 0;
-                etg[u] = 0xFFFFu;
-                if (val[u]) {
-                    ent[u] = mode == 0 ? E->plist[off + e] : E->occ[off + e];
-                    if (mode) etg[u] = E->occnb[off + e];
-                }
+                val[u] = e0 + u * SCAN_T + tid < len;
+                ent[u] = nent[u];
+                etg[u] = ntg[u];
             }
+            if (BPE_SCAN_PF && e0 + stride < len) fetch(e0 + stride);
             int64_t ii[SU], jj[SU];
             TokWin W[SU];
 #pragma unroll
@@ -874,21 +913,23 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     ltag[slot] = nb_tag(lfin, rfin);
                 }
             }
-            // flush the round's list: one global atomic per block
-            __syncthreads();
-            if (tid == 0) {
-                const uint32_t c = lcount;
-                gbase = c ? atomicAdd(Rm, c) : 0u;
-                bRs += c;
-                lcount = 0;
-                list_n = c;
+            // flush the staged rounds' list: one global atomic per block
+            if (++round % FR == 0 || e0 + stride >= len) {  // (uniform)
+                __syncthreads();
+                if (tid == 0) {
+                    const uint32_t c = lcount;
+                    gbase = c ? atomicAdd(Rm, c) : 0u;
+                    bRs += c;
+                    lcount = 0;
+                    list_n = c;
+                }
+                __syncthreads();
+                for (uint32_t q = tid; q < list_n; q += SCAN_T) {
+                    occz[gbase + q] = list[q];
+                    tagz[gbase + q] = ltag[q];
+                }
+                __syncthreads();
             }
-            __syncthreads();
-            for (uint32_t q = tid; q < list_n; q += SCAN_T) {
-                occz[gbase + q] = list[q];
-                tagz[gbase + q] = ltag[q];
-            }
-            __syncthreads();
         }
     } else {
         // a == b (a batch of its own): the thread holding a run's first token
@@ -1092,14 +1133,18 @@ __device__ inline uint64_t hinsert_c(const Eng *E, uint32_t u, uint32_t v, uint3
 // follow from each atomic's old value).
 // SH: the occurrence counts, bounds, deltas and staging-overflow flags come
 // summed over the shards from the exchange buffer (xbat), cleared as read.
+// Blocks [roleB_blocks, grid) rewrite the first B->ra_split / 256 of every
+// verified member's occurrences beside the table updates (k_bsel's rewrite
+// blocks do the rest beside the selection).
 template <bool SH>
-__global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+__global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleB_blocks) {
     if (C->stop) return;
     Bat *B = E->bat;
     const uint32_t bi = bat_idx(E);
     ts_mark(E, bi, BT_APPLY_IN, true);
     if (threadIdx.x == 0) atomicMax(&B->ap_in, ~wall_clock64());
     __shared__ uint32_t sa[BK], sb[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], snl[BK * 4 + 1], sRg[BK];
+    __shared__ uint32_t scut[BK], ablk[BK + 1];
     __shared__ uint32_t sk, sj, sz0;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     // prologue, wave 0, lane q = member q: the verified prefix, prefix sums of
@@ -1158,6 +1203,23 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             js = 0;
         }
         const uint32_t rall = (uint32_t)__shfl(rpre, (int)(k ? k - 1 : 0));
+        // the first part of each verified member's rewrite runs here, in
+        // blocks in proportion to it (>= 1 per member)
+        const uint32_t nA1 = gridDim.x - roleB_blocks;
+        const uint32_t cut = (in && lane < js && nA1) ? (uint32_t)((uint64_t)R * B->ra_split / 256) : 0u;
+        unsigned long long ctot = cut;
+        for (int o = 32; o > 0; o >>= 1) ctot += __shfl_xor(ctot, o);
+        const uint32_t nb1 = lane < js ? 1 + (uint32_t)(ctot ? (uint64_t)(nA1 > js ? nA1 - js : 0) * cut / ctot : 0) : 0;
+        uint32_t nbp1 = nb1;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(nbp1, o);
+            if ((int)lane >= o) nbp1 += y;
+        }
+        if (lane < js) {
+            scut[lane] = cut;
+            ablk[lane] = nbp1 - nb1;
+        }
+        if (lane == 0) ablk[js] = nA1;
         if (in) {
             sa[lane] = ma;
             sb[lane] = mb;
@@ -1187,6 +1249,19 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     ts_mark(E, bi, BT_APPLY_PRO, false);
     ts_mark(E, bi, BT_APPLY_A, false);  // (role A runs in k_bsel)
     const uint32_t k = sk, js = sj, z0 = sz0;
+    if (blockIdx.x >= roleB_blocks) {  // role A, first part (block-uniform)
+        __shared__ uint32_t am;
+        const uint32_t bid = blockIdx.x - roleB_blocks;
+        if (tid == 0) am = BK;
+        __syncthreads();
+        if (tid < js && bid >= ablk[tid] && bid < ablk[tid + 1]) am = tid;
+        __syncthreads();
+        const uint32_t m = am;
+        if (m < js && scut[m])
+            rewrite_occ(E, C, B, z0 + m, sla[m], slb[m], ssb[m], C->occ_top + spre[m], 0, scut[m], bid - ablk[m],
+                        ablk[m + 1] - ablk[m], E->sharded ? C->L1 : ~0ull);
+        return;
+    }
     if (blockIdx.x == 0) {
         // bookkeeping and the role-A descriptor for k_bsel's rewrite blocks
         const uint32_t top = C->occ_top;
@@ -1200,6 +1275,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             B->ra_la[tid] = sla[tid];
             B->ra_lb[tid] = slb[tid];
             B->ra_R[tid] = sR[tid];
+            B->ra_lo[tid] = scut[tid];
             B->ra_sbase[tid] = ssb[tid];
             B->ra_pre[tid] = spre[tid];
         }
@@ -1223,7 +1299,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         }
     }
     // role B
-    const uint32_t nB = gridDim.x, bidB = blockIdx.x;
+    const uint32_t nB = roleB_blocks, bidB = blockIdx.x;
     const uint32_t Wd = SH ? z0 + k : min(DENSE, z0 + k);
     const uint32_t per = SH ? xbat_member_words(Wd) : 1 + 4 * Wd;
     const uint32_t dense_total = k * per;
@@ -1335,7 +1411,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     }
     ts_mark(E, bi, BT_APPLY_B, false, true);
 }
-template __global__ void k_bapply<false>(const Eng *, Ctl *);
-template __global__ void k_bapply<true>(const Eng *, Ctl *);
+template __global__ void k_bapply<false>(const Eng *, Ctl *, uint32_t);
+template __global__ void k_bapply<true>(const Eng *, Ctl *, uint32_t);
 
 }  // namespace bpeamd

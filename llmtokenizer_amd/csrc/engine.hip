@@ -93,6 +93,12 @@ bool HOT_ON = !getenv("BPE_HOT") || atoi(getenv("BPE_HOT")) != 0;
 // batch's token rewrite, beside the selection), 1024 threads each;
 // BPE_BGRID="a,b" overrides them (a: rewrite blocks, b: table blocks) for tuning runs
 uint32_t BAPPLY_A = 224, BAPPLY_B = 256;
+// k_bapply's own rewrite blocks (the first BPE_RA_SPLIT / 256 of every
+// member's occurrences, beside the table updates): 0 or >= BK (one per member).
+// Off by default: at 1 GiB x 8192 the split cost 2-4 ms of the 72 ms loop
+// (BPE_RA_BLOCKS=96 with BPE_RA_SPLIT 64/96/128 -> 74.0/74.5/75.5 ms; the
+// table blocks wait behind the rewrite blocks), identical merges and ids
+uint32_t BAPPLY_RA = 0;
 constexpr uint32_t BATCHES_PER_GRAPH = 8;
 // ids >= DENSE of the batch delta vectors: per (member, vector) one slot per
 // id, so runs with a larger vocabulary cap than this stay on one merge per pair
@@ -104,6 +110,10 @@ struct BatchInit {
             if (sscanf(g, "%u,%u", &a, &b) == 2 && a >= BK && b >= 1 && a + b <= 2048) {  // (>= 1 role-A block per member)
                 BAPPLY_A = a; BAPPLY_B = b;
             }
+        }
+        if (const char *g = getenv("BPE_RA_BLOCKS")) {
+            const unsigned r = (unsigned)atoi(g);
+            if (r == 0 || (r >= BK && r <= 1024)) BAPPLY_RA = r;
         }
     }
 } batch_init;
@@ -479,12 +489,15 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         // z = 0 mod d (tests drive the drop path with it)
         const uint32_t dt = (uint32_t)getenv_int("BPE_BATCH_DROP_TEST", 0);
         if (dt) HIPCHK(hipMemcpyAsync(&h.bat->drop_test, &dt, 4, hipMemcpyHostToDevice, c->st));
+        // k_bapply's share of the rewrite (1/256; BPE_RA_SPLIT: tuning)
+        const uint32_t split = BAPPLY_RA ? (uint32_t)std::min(256, std::max(0, getenv_int("BPE_RA_SPLIT", 96))) : 0u;
+        HIPCHK(hipMemcpyAsync(&h.bat->ra_split, &split, 4, hipMemcpyHostToDevice, c->st));
         // BPE_BATCH_STAGE=p: only p staging positions (tests drive the overflow
         // cut -- sharded: the flag in the exchange and the re-formed batch)
         c->stage_cap = n0;
         if (const char *t = getenv("BPE_BATCH_STAGE")) c->stage_cap = std::min<uint64_t>(n0, std::max(1ll, atoll(t)));
         HIPCHK(hipMemcpyAsync(&h.bat->stage_cap, &c->stage_cap, 8, hipMemcpyHostToDevice, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));  // (dt is on the stack)
+        HIPCHK(hipStreamSynchronize(c->st));  // (dt, split are on the stack)
     }
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
@@ -670,7 +683,7 @@ void launch_argmax_inputs(bpe_gpu_ctx *c) {
 // one batch: scan, verify + apply, select the next (batch.hip)
 void launch_batch(bpe_gpu_ctx *c) {
     k_bscan<false><<<BSB, SCAN_T, 0, c->st>>>(c->dE, c->dC);
-    k_bapply<false><<<BAPPLY_B, 1024, 0, c->st>>>(c->dE, c->dC);
+    k_bapply<false><<<BAPPLY_B + BAPPLY_RA, 1024, 0, c->st>>>(c->dE, c->dC, BAPPLY_B);
     k_bsel<<<BRB + BAPPLY_A, 1024, 0, c->st>>>(c->dE, c->dC);
 }
 

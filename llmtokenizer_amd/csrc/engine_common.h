@@ -146,6 +146,8 @@ struct Bat {
     uint32_t ra_k, ra_top, ra_done, ra_err;  // members (0: nothing pending), pool offset, blocks finished, error
     uint32_t ra_z[BK], ra_la[BK], ra_lb[BK], ra_R[BK], ra_sbase[BK], ra_pre[BK + 1];
     uint32_t ra_xl, ra_xlb;           // sharded: my first token, retired (its b's length), or HOLE
+    uint32_t ra_lo[BK];               // occurrences k_bapply's role-A blocks rewrote already (the first ones)
+    uint32_t ra_split, pad6;          // k_bapply's share of the rewrite, in 1/256 (BPE_RA_SPLIT)
 };
 
 // Sharded batches: the words one batch exchanges (summed over the shards):

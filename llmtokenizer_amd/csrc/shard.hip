@@ -263,7 +263,7 @@ int launch_group_bstep(bpe_gpu_group *g) {
     int r;
     for (bpe_gpu_ctx *c : g->cs) k_bscan<true><<<BSB, SCAN_T, 0, g->st>>>(c->dE, c->dC);
     if ((r = ex_bsum(g))) return r;
-    for (bpe_gpu_ctx *c : g->cs) k_bapply<true><<<BAPPLY_B, 1024, 0, g->st>>>(c->dE, c->dC);
+    for (bpe_gpu_ctx *c : g->cs) k_bapply<true><<<BAPPLY_B + BAPPLY_RA, 1024, 0, g->st>>>(c->dE, c->dC, BAPPLY_B);
     // (k_bsel's last rewrite block writes the edge record of the new tokens)
     for (bpe_gpu_ctx *c : g->cs) k_bsel<<<BRB + BAPPLY_A, 1024, 0, g->st>>>(c->dE, c->dC);
     HIPCHK(hipGetLastError());
