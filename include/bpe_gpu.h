@@ -83,6 +83,11 @@ typedef struct {
     uint64_t table_updates;   /* training, batches: pair-table updates of the applies */
     double ms_scan_span;      /* training, batches: average k_bscan span (device wall clock) */
     double ms_apply_span;     /* training, batches: average k_bapply span (device wall clock) */
+    uint64_t track_exact;     /* tracked iterations: exact (thread, pair) passes run */
+    uint64_t track_skipped;   /* tracked iterations whose exact pass the distinct-count
+                                 bounds proved unnecessary (no per-thread table grows) */
+    uint64_t track_violations;/* BPE_TRACK=2 check runs: skipped passes the exact one
+                                 contradicts (must stay 0)                         */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */

@@ -46,7 +46,8 @@ class GpuStats(ctypes.Structure):
                                                      "count_pass_span", "hot_rebuilds", "hot_mode", "hot_scanned",
                                                      "enc_path", "enc_windows", "relists", "batches",
                                                      "batch_dropped", "batch_retries", "table_updates")] + \
-        [(n, ctypes.c_double) for n in ("ms_scan_span", "ms_apply_span")]
+        [(n, ctypes.c_double) for n in ("ms_scan_span", "ms_apply_span")] + \
+        [(n, ctypes.c_uint64) for n in ("track_exact", "track_skipped", "track_violations")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

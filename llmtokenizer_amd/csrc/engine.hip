@@ -73,6 +73,19 @@ struct GridInit {
         }
     }
 } grid_init;
+// tracked iterations (n < 2^21 tokens: ~10^2 occurrences per merge) launch
+// smaller grids; BPE_TGRID="scan,rescan1,applyA,applyB" overrides them
+uint32_t TSCAN_BLOCKS = 128, TRESCAN1_BLOCKS = 128, TAPPLY_A = 32, TAPPLY_B = 32;
+struct TGridInit {
+    TGridInit() {
+        if (const char *g = getenv("BPE_TGRID")) {
+            unsigned s = 0, r = 0, a = 0, b = 0;
+            if (sscanf(g, "%u,%u,%u,%u", &s, &r, &a, &b) == 4 && s >= 1 && s <= 1024 && r >= 1 && a >= 1 && b >= 1) {
+                TSCAN_BLOCKS = s; TRESCAN1_BLOCKS = r; TAPPLY_A = a; TAPPLY_B = b;
+            }
+        }
+    }
+} tgrid_init;
 constexpr uint32_t ENC_APPLY_BLOCKS = 1024;
 // speculative one-shard graph (k_rescan_spec): rescan blocks of 1024 threads,
 // then the predicted merge's scan blocks.  BPE_SPEC=0 disables it;
@@ -411,6 +424,11 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.xfused = c->sharded && c->xfused && !encode;
     h.end_max = END_MAX;
     if (const char *t = getenv("BPE_END_MAX")) h.end_max = std::min<uint64_t>(END_MAX, std::max(1ll, atoll(t)));
+    // tracked iterations: the exact (thread, pair) pass only when a bound on a
+    // thread's distinct pairs reaches its growth threshold (BPE_TRACK=0: every
+    // iteration, 2: both, each skip verified -- tests)
+    h.track_ub = 1;
+    if (const char *t = getenv("BPE_TRACK")) h.track_ub = (uint32_t)std::min(2, std::max(0, atoi(t)));
     h.xtimeout = c->xtimeout;
     h.xstride = (uint32_t)(((4ull * h.vcap + 2) + 63) & ~63ull);
     if (c->sharded) {
@@ -635,8 +653,9 @@ void launch_stats(bpe_gpu_ctx *c) {
 }
 
 // edges: + the block that writes the shard's edge record (sharded training)
-void launch_summaries(bpe_gpu_ctx *c, bool edges = false) {
-    k_rescan1<<<RESCAN1_BLOCKS + (edges ? 1 : 0), 256, 0, c->st>>>(c->dE, c->dC, edges ? 1 : 0);
+void launch_summaries(bpe_gpu_ctx *c, bool edges = false, bool track = false, uint32_t blocks = 0) {
+    k_rescan1<<<(blocks ? blocks : RESCAN1_BLOCKS) + (edges ? 1 : 0) + (track ? 1 : 0), 256, 0, c->st>>>(
+        c->dE, c->dC, (edges ? RS_EDGES : 0) | (track ? RS_TRACK : 0));
     if (c->h.hcap / L1W > SELECT_L1_MAX) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
 }
 
@@ -687,20 +706,30 @@ void launch_batch(bpe_gpu_ctx *c) {
     k_bsel<<<BRB + BAPPLY_A, 1024, 0, c->st>>>(c->dE, c->dC);
 }
 
+// tracked phases run the fused speculative graph too when the distinct-count
+// bounds replace the per-iteration exact pass (its K1 carries the track block)
+bool fused_graph(const bpe_gpu_ctx *c, bool tracked) { return c->h.spec_on && (!tracked || c->h.track_ub == 1); }
+
 void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
-    if (c->h.spec_on && !tracked) {
+    if (fused_graph(c, tracked)) {
         // fused speculative graph: entered with the current merge applied
         // (by the previous k_fused, or the host after a stop)
-        k_rescan_spec<<<SPEC_RB + SPEC_SB, SCAN_T, 0, c->st>>>(c->dE, c->dC, SPEC_RB);
+        const uint32_t trk = c->h.track_ub == 1 && !c->fast && c->n0 < TRACK_LIMIT ? 1 : 0;
+        k_rescan_spec<<<SPEC_RB + SPEC_SB + trk, SCAN_T, 0, c->st>>>(c->dE, c->dC, SPEC_RB, trk);
         // (the hot set needs no level-2 pass; a fall-back recaptures the graph)
         if (c->h.hcap / L1W > SELECT_L1_MAX && !c->h.hot) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
         k_fused<<<1 + FUSED_A + FUSED_B, 1024, 0, c->st>>>(c->dE, c->dC, FUSED_A, nullptr);
         return;
     }
-    k_scan<false><<<SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
-    k_apply<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
-    if (tracked) launch_stats(c);
-    launch_summaries(c);
+    k_scan<false><<<tracked ? TSCAN_BLOCKS : SCAN_BLOCKS, SCAN_T, 0, c->st>>>(c->dE, c->dC);
+    if (tracked) k_apply<<<TAPPLY_A + TAPPLY_B, 256, 0, c->st>>>(c->dE, c->dC, TAPPLY_A);
+    else k_apply<<<APPLY_A + APPLY_B, 256, 0, c->st>>>(c->dE, c->dC, APPLY_A);
+    // tracked: the distinct-count bounds beside the rescan; the exact pass in
+    // the graph only without bounds (or to check them), else on STOP_STATS
+    const uint32_t tu = c->h.track_ub;
+    if (tracked && tu == 0) launch_stats(c);
+    launch_summaries(c, false, tracked && tu != 0, tracked ? TRESCAN1_BLOCKS : 0);
+    if (tracked && tu == 2) launch_stats(c);
     k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
 }
 
@@ -1184,7 +1213,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
                 }
                 break;
             } else {
-                const bool tracked = !c->h.fast && C.n_live < TRACK_LIMIT;
+                const bool tracked = !c->h.fast && C.n_live < TRACK_LIMIT && !fused_graph(c, true);
                 g = tracked ? &c->g_tracked : &c->g_plain;
                 if (!*g && (r = capture(c, g, tracked, false))) return r;
                 last_graph = tracked ? 1 : 0;
@@ -1221,8 +1250,10 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             if ((r = push_ctl(c))) return r;
             launch_stats(c);
             launch_summaries(c);
-            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, SEL_TRACKED);
+            // (the fused graph goes on: a plain selection arms its prediction)
+            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, fused_graph(c, true) ? SEL_PLAIN : SEL_TRACKED);
             HIPCHK(hipGetLastError());
+            need_scan = true;
             break;
         case STOP_GROW: {
             C.stop = STOP_NONE;
@@ -1230,7 +1261,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             if ((r = push_ctl(c))) return r;
             if ((r = grow_table(c, c->h.hcap * 4))) return r;
             if ((r = hot_rebuild(c))) return r;  // (slots moved)
-            if ((r = select_next(c, !c->h.fast && C.n_live < TRACK_LIMIT))) return r;
+            if ((r = select_next(c, !c->h.fast && C.n_live < TRACK_LIMIT && !fused_graph(c, true)))) return r;
             need_scan = !c->h.batch;
             break;
         }
@@ -1250,11 +1281,29 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             if ((r = select_next(c, false))) return r;
             need_scan = !c->h.batch;
             break;
+        case STOP_STATS:  // a per-thread table may grow: the exact pass, then the same selection
+            C.stop = STOP_NONE;
+            if ((r = push_ctl(c))) return r;
+            launch_stats(c);
+            k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, fused_graph(c, true) ? SEL_PLAIN : SEL_TRACKED);
+            HIPCHK(hipGetLastError());
+            need_scan = true;
+            break;
         case STOP_EVENT: {
+            if (!C.stat_exact) {
+                // the resolver reads the (thread, pair) set of this counting
+                // phase: the bounds skipped its exact pass, run it now
+                C.stop = STOP_NONE;
+                if ((r = push_ctl(c))) return r;
+                launch_stats(c);
+                HIPCHK(hipGetLastError());
+                if ((r = pull_ctl(c))) return r;
+            }
             uint32_t u = 0, v = 0;
             if ((r = res.resolve(&u, &v))) return r;
             k_commit<<<1, 1, 0, c->st>>>(c->dE, c->dC, u, v);
             HIPCHK(hipGetLastError());
+            need_scan = true;  // (the fused graph: scanned and applied by launch_redo)
             break;
         }
         default:
@@ -1936,7 +1985,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->hot_fallback = false;
     c->relists = 0;
     if ((r = hot_rebuild(c))) return r;
-    if ((r = select_next(c, tracked))) return r;
+    if ((r = select_next(c, tracked && !fused_graph(c, true)))) return r;
     HIPCHK(hipStreamSynchronize(c->st));
     const double t1 = now_ms();
     if ((r = drive(c, false, 0))) return r;
@@ -1964,6 +2013,9 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.hot_scanned = C.hot_scanned;
     c->stats.hot_mode = c->h.hot ? 1 : c->hot_fallback ? 2 : 0;
     c->stats.relists = c->relists;
+    c->stats.track_exact = C.track_exact;
+    c->stats.track_skipped = C.track_skip;
+    c->stats.track_violations = C.track_viol;
     if ((r = batch_stats(c))) return r;
     if (c->h.dbgts) print_timeline(c, C.z);
     if (getenv("BPE_DEBUG"))

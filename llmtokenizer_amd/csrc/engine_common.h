@@ -35,6 +35,7 @@ constexpr uint32_t NTHR = 16;            // reference THREAD_NO (bpe.c:409)
 constexpr uint64_t CHUNK = 65536;        // reference CHUNK_SIZE (bpe.c:423)
 constexpr uint64_t DYN_LIMIT = CHUNK * NTHR;     // n >= this: chunked counting
 constexpr uint64_t TRACK_LIMIT = 2 * DYN_LIMIT;  // per-thread history tracked below this
+constexpr uint64_t TRACK_MIN_N = 4096;  // tracked phases with fewer tokens always take the exact pass
 constexpr uint64_t MERGED_B0 = 65536;    // reference MERGED_TABLE_BUCKET_NUM (bpe.c:611)
 constexpr uint64_t THREAD_B0 = 256;      // reference PER_THREAD_TABLE_BUCKET_NUM (bpe.c:610)
 constexpr uint32_t L1W = 1024;           // slots per level-1 summary block
@@ -61,6 +62,7 @@ enum : uint32_t {
     STOP_REDO = 8,     // speculative graph: the predicted next merge was wrong, host scans
     STOP_HOT = 9,      // hot-set argmax: the set no longer holds the maximum (or grew): host rebuilds it
     STOP_RELIST = 10,  // the byte-pair position lists went stale: host rebuilds them (k_relist_*)
+    STOP_STATS = 11,   // tracked iteration: a per-thread table may grow, host runs the exact pass (k_stat_*)
 };
 
 // Hot-set argmax (Eng::hot, untracked one-shard training): the keys whose count
@@ -245,6 +247,10 @@ struct Eng {
     // longest token span (end distance) an end code may hold: END_MAX, or less
     // for tests (BPE_END_MAX) that drive the over-long-token error paths
     uint64_t end_max;
+    // tracked iterations: 0 the exact (thread, pair) pass every iteration, 1 only
+    // when a distinct-count bound reaches a growth threshold (default), 2 both
+    // (check: every skipped pass is verified against the exact one; BPE_TRACK)
+    uint32_t track_ub;
 };
 
 // Control block.  Everything up to Dp is owned by k_select, which stages it in
@@ -281,6 +287,17 @@ struct Ctl {
     uint32_t s_len, spec, sRp[2];
     uint32_t hot_T, hot_fill;         // hot-set threshold; keys the last rebuild listed
     uint32_t relist_c0, relist_o0;    // counters[4] / [5] (low words) at the last byte-pair list rebuild
+    // tracked iterations: bounds on the per-thread distinct counts between
+    // exact (thread, pair) passes (kernels.hip track_block, Eng::track_ub)
+    uint32_t stat_need;               // the track block asks for the exact pass (k_select: STOP_STATS)
+    uint32_t stat_exact;              // the k_stat_* pass ran for the current counting phase
+    uint32_t stat_valid;              // tP / tUB describe the stat_nt-token phase (static split)
+    uint32_t stat_skip;               // the track block proved this phase needs no exact pass
+    uint32_t trk_on, trk_pad;         // an exact pass ran: tracked iterations entered (no STOP_MODE)
+    uint32_t tP[NTHR];              // position of the first token of thread t's pair range (t >= 1)
+    uint32_t tUB[NTHR];               // upper bound on thread t's distinct pairs
+    unsigned long long stat_nt;       // tokens of the phase tP / tUB describe
+    unsigned long long track_exact, track_skip, track_viol;  // exact passes, proven skips, check-mode violations
     // ---- tail: written by k_apply / k_rescan_spec (see above)
     unsigned long long Dp[2];   // D delta of the merge applied with parity p (finish_iteration folds it)
     unsigned long long nkeys;   // pair-table slots in use
