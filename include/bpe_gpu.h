@@ -88,6 +88,8 @@ typedef struct {
                                  bounds proved unnecessary (no per-thread table grows) */
     uint64_t track_violations;/* BPE_TRACK=2 check runs: skipped passes the exact one
                                  contradicts (must stay 0)                         */
+    uint64_t track_light;     /* tracked iterations: on-device exact counts of only the
+                                 threads whose bound reached a growth threshold   */
 } bpe_gpu_stats;
 
 /* number of visible GPUs */

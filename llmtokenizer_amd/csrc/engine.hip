@@ -526,6 +526,15 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.skey, h.scap))) return r;
     if ((r = dalloc(c, &h.scnt, h.scap))) return r;
     if ((r = dalloc(c, &h.sfirst, h.scap))) return r;
+    // k_stat_light's generation-tagged set (tracked corpora; ids in 22 bits)
+    h.lcap = 0;
+    h.lkey = h.lfirst = nullptr;
+    if (!encode && !c->sharded && !c->fast && n0 < TRACK_LIMIT && h.vcap <= (1u << 22) && h.track_ub != 0) {
+        h.lcap = pow2_at_least(std::max<uint64_t>(1024, 2 * n0));
+        if ((r = dalloc(c, &h.lkey, h.lcap))) return r;                // generation 0: empty
+        if ((r = dalloc(c, &h.lfirst, h.lcap, false))) return r;
+        HIPCHK(hipMemsetAsync(h.lfirst, 0xFF, h.lcap * 8, c->st));
+    }
     // pair table
     if (!encode) {
         // keys (distinct pairs ever seen): merge t adds at most 2 (256 + t)
@@ -716,6 +725,7 @@ void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
         // (by the previous k_fused, or the host after a stop)
         const uint32_t trk = c->h.track_ub == 1 && !c->fast && c->n0 < TRACK_LIMIT ? 1 : 0;
         k_rescan_spec<<<SPEC_RB + SPEC_SB + trk, SCAN_T, 0, c->st>>>(c->dE, c->dC, SPEC_RB, trk);
+        if (trk && c->h.lcap) k_stat_light<<<LIGHT_B, 1024, 0, c->st>>>(c->dE, c->dC);
         // (the hot set needs no level-2 pass; a fall-back recaptures the graph)
         if (c->h.hcap / L1W > SELECT_L1_MAX && !c->h.hot) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
         k_fused<<<1 + FUSED_A + FUSED_B, 1024, 0, c->st>>>(c->dE, c->dC, FUSED_A, nullptr);
@@ -729,6 +739,7 @@ void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
     const uint32_t tu = c->h.track_ub;
     if (tracked && tu == 0) launch_stats(c);
     launch_summaries(c, false, tracked && tu != 0, tracked ? TRESCAN1_BLOCKS : 0);
+    if (tracked && tu != 0 && c->h.lcap) k_stat_light<<<LIGHT_B, 1024, 0, c->st>>>(c->dE, c->dC);
     if (tracked && tu == 2) launch_stats(c);
     k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
 }
@@ -1283,6 +1294,11 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             break;
         case STOP_STATS:  // a per-thread table may grow: the exact pass, then the same selection
             C.stop = STOP_NONE;
+            if (c->h.lcap && C.lgen >= 0xFFFEu) {  // k_stat_light's generations ran out: a clean set
+                HIPCHK(hipMemsetAsync(c->h.lkey, 0, c->h.lcap * 8, c->st));
+                HIPCHK(hipMemsetAsync(c->h.lfirst, 0xFF, c->h.lcap * 8, c->st));
+                C.lgen = 0;
+            }
             if ((r = push_ctl(c))) return r;
             launch_stats(c);
             k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, fused_graph(c, true) ? SEL_PLAIN : SEL_TRACKED);
@@ -2016,6 +2032,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.track_exact = C.track_exact;
     c->stats.track_skipped = C.track_skip;
     c->stats.track_violations = C.track_viol;
+    c->stats.track_light = C.track_light;
     if ((r = batch_stats(c))) return r;
     if (c->h.dbgts) print_timeline(c, C.z);
     if (getenv("BPE_DEBUG"))

@@ -251,6 +251,10 @@ struct Eng {
     // when a distinct-count bound reaches a growth threshold (default), 2 both
     // (check: every skipped pass is verified against the exact one; BPE_TRACK)
     uint32_t track_ub;
+    // k_stat_light's (thread, pair) set: key (gen << 48 | t << 44 | a << 22 | b),
+    // first position ((0xFFFF - gen) << 48 | position); lcap == 0: no light pass
+    unsigned long long *lkey, *lfirst;
+    uint64_t lcap;
 };
 
 // Control block.  Everything up to Dp is owned by k_select, which stages it in
@@ -293,11 +297,16 @@ struct Ctl {
     uint32_t stat_exact;              // the k_stat_* pass ran for the current counting phase
     uint32_t stat_valid;              // tP / tUB describe the stat_nt-token phase (static split)
     uint32_t stat_skip;               // the track block proved this phase needs no exact pass
-    uint32_t trk_on, trk_pad;         // an exact pass ran: tracked iterations entered (no STOP_MODE)
+    uint32_t trk_on;                  // an exact pass ran: tracked iterations entered (no STOP_MODE)
+    uint32_t phase_open;              // the track block opened this phase (Bstart = the sizes before it)
+    uint32_t light_mask, lgen;        // threads whose D_t k_stat_light counts (stat_need == 2); its table generation
+    uint32_t lticket, lpad;           // k_stat_light blocks done
+    uint32_t ldt[NTHR];               // k_stat_light: distinct pairs of the masked threads
     uint32_t tP[NTHR];              // position of the first token of thread t's pair range (t >= 1)
     uint32_t tUB[NTHR];               // upper bound on thread t's distinct pairs
     unsigned long long stat_nt;       // tokens of the phase tP / tUB describe
     unsigned long long track_exact, track_skip, track_viol;  // exact passes, proven skips, check-mode violations
+    unsigned long long track_light;   // k_stat_light passes (exact D_t of the threads whose bound reached 0.3 B)
     // ---- tail: written by k_apply / k_rescan_spec (see above)
     unsigned long long Dp[2];   // D delta of the merge applied with parity p (finish_iteration folds it)
     unsigned long long nkeys;   // pair-table slots in use

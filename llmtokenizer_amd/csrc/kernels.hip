@@ -2857,17 +2857,25 @@ __global__ void k_stat_final(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     }
     C->last_c[t] = last >= 0 ? (uint32_t)last : 0xFFFFFFFFu;
     C->follows[t] = follows;
-    C->Bstart[t] = C->Bcur[t];
-    const uint64_t Bf = thread_cascade(C->Bcur[t], C->Dt[t], follows);
+    // the sizes before this counting phase: taken by the track block when it
+    // opened the phase (k_stat_light may have grown them since: idempotent)
+    const uint64_t B0 = C->phase_open ? C->Bstart[t] : C->Bcur[t];
+    const uint64_t Bprev = C->Bcur[t];
+    C->Bstart[t] = B0;
+    const uint64_t Bf = thread_cascade(B0, C->Dt[t], follows);
     C->Bfin[t] = Bf;
     C->Bcur[t] = Bf;
     // the bound state of track_block: exact from here, or (check mode, the
-    // track block skipped this phase) verified against the exact pass
+    // track block skipped this phase) verified against the exact pass: D_t
+    // within its bound (equal to it where k_stat_light counted it), the sizes
+    // the bounds / the light pass left, the carried range boundaries
     const bool stat_ok = n >= TRACK_MIN_N && n < DYN_LIMIT;
     const uint32_t P = stat_ok && t > 0 ? E->cpos[(uint64_t)t * (n / NTHR)] : 0u;
     const bool skipped = C->stat_skip != 0;
     if (E->track_ub == 2 && skipped) {
-        const bool bad = C->Dt[t] > C->tUB[t] || Bf != C->Bstart[t] || (t > 0 && P != C->tP[t]);
+        const bool lit = (C->light_mask >> t) & 1u;
+        const bool bad = C->Dt[t] > C->tUB[t] || (lit && C->Dt[t] != C->tUB[t]) || Bf != Bprev ||
+                         (t > 0 && P != C->tP[t]);
         if (bad) atomicAdd(&C->track_viol, 1ull);
     } else {
         C->tUB[t] = C->Dt[t];
@@ -3009,32 +3017,171 @@ __device__ void track_block(const Eng *__restrict__ E, Ctl *__restrict__ C) {
         }
         __syncthreads();
     }
-    if (tid == 0) {
-        bool need = sfail != 0;
+    // wave 0, lane t < 16: thread t's bound; D_t <= bound < 0.3 B: no insert
+    // call grows its table.  Threads whose bound reaches 0.3 B get their exact
+    // D_t from k_stat_light (the whole exact pass when anything was unusual)
+    if (wv == 0) {
+        const bool fail = sfail != 0;
+        const uint32_t t = lane;
         const uint64_t per = nnew / NTHR;
-        for (uint32_t t = 0; t < NTHR && !need; t++) {
+        bool needt = false;
+        uint32_t u32 = 0;
+        uint64_t Bc = 0;
+        if (t < NTHR) {
+            Bc = C->Bcur[t];
             const long long dl = t > 0 ? sdel[t] : 0, dr = t + 1 < NTHR ? sdel[t + 1] : 0;
             uint64_t u = (uint64_t)C->tUB[t] + chg[t] + (uint64_t)(dl < 0 ? -dl : dl) + (uint64_t)(dr < 0 ? -dr : dr);
             const uint64_t pairs = t + 1 < NTHR ? per : nnew - 1 - (NTHR - 1) * per;
-            if (u > pairs) u = pairs;
-            ub[t] = (uint32_t)u;
-            need = (double)u >= 0.3 * (double)C->Bcur[t];  // D_t <= u < 0.3 B: no insert call grows the table
+            if (!fail && u > pairs) u = pairs;
+            u32 = (uint32_t)min<uint64_t>(u, 0xFFFFFFFFull);
+            needt = (double)u >= 0.3 * (double)Bc;
         }
-        if (need) {
-            C->stat_need = 1;
-            C->stat_skip = 0;
-        } else {
-            for (uint32_t t = 0; t < NTHR; t++) {
-                C->tUB[t] = ub[t];
+        const uint32_t mask = (uint32_t)__ballot(needt) & ((1u << NTHR) - 1u);
+        const uint32_t lg = C->lgen;
+        const bool light = !fail && mask && E->lcap && E->track_ub != 0 && lg < 0xFFFEu;
+        const bool full = fail || (mask && !light);
+        if (t < NTHR) {
+            C->Bstart[t] = Bc;  // the phase's starting sizes (k_stat_final / k_stat_light grow from them)
+            if (!full) {
+                C->tUB[t] = u32;
                 C->tP[t] = sPn[t];
-                C->Bstart[t] = C->Bfin[t] = C->Bcur[t];
+                C->Bfin[t] = Bc;
+                if (light) C->ldt[t] = 0;
             }
-            C->stat_nt = nnew;
-            C->stat_exact = 0;
-            C->stat_skip = 1;
-            C->counters[1]++;
-            C->track_skip++;
         }
+        if (lane == 0) {
+            C->phase_open = 1;
+            C->light_mask = light ? mask : 0u;
+            if (full) {
+                C->stat_need = 1;
+                C->stat_skip = 0;
+            } else {
+                C->stat_nt = nnew;
+                C->stat_exact = 0;
+                C->stat_skip = 1;
+                C->counters[1]++;
+                C->track_skip += mask ? 0ull : 1ull;
+                if (light) {
+                    C->stat_need = 2;
+                    C->lgen = lg + 1;
+                    C->lticket = 0;
+                }
+            }
+        }
+    }
+}
+
+// Exact D_t (and the follows flag) of the threads whose bound reached its
+// growth threshold (Ctl::light_mask), between the two kernels of a merge:
+// their pair ranges [tP[t], tP[t + 1]) -- carried exactly by the track block --
+// go into a generation-tagged (thread, pair) set (no clearing: a slot of an
+// older generation counts as empty), and the last block applies the table
+// growth (thread_cascade from the phase's starting size).  The resolver's full
+// pass (k_stat_*) still runs at tie events.
+constexpr uint32_t LIGHT_B = 128;
+constexpr unsigned long long LKEY_MASK = (1ull << 48) - 1ull;
+
+__device__ inline unsigned long long lkey48(uint32_t t, uint32_t u, uint32_t v) {
+    return ((unsigned long long)t << 44) | ((unsigned long long)u << 22) | v;
+}
+
+// slot of key48 in generation gen (claim it when absent: *fresh = true)
+__device__ inline int64_t light_slot(const Eng *E, unsigned long long key48, uint32_t gen, bool insert, bool *fresh) {
+    const uint64_t m = E->lcap - 1;
+    uint64_t s = mix64(key48) & m;
+    const unsigned long long want = ((unsigned long long)gen << 48) | key48;
+    for (uint64_t p = 0; p <= m;) {
+        unsigned long long v = __hip_atomic_load(&E->lkey[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 48) == gen) {
+            if (v == want) return (int64_t)s;
+            s = (s + 1) & m;
+            p++;
+            continue;
+        }
+        if (!insert) return -1;  // (an empty slot ends the probe)
+        const unsigned long long prev = atomicCAS(&E->lkey[s], v, want);
+        if (prev == v) {
+            *fresh = true;
+            return (int64_t)s;
+        }
+        // another thread took the slot meanwhile: look at it again
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(1024) void k_stat_light(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    if (C->stop || C->stat_need != 2) return;
+    __shared__ uint32_t cnt[NTHR], sP[NTHR + 1];
+    __shared__ uint32_t last, bad;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t mask = C->light_mask, gen = C->lgen;
+    const uint64_t n0 = E->n0;
+    if (tid < NTHR) {
+        cnt[tid] = 0;
+        sP[tid] = tid ? C->tP[tid] : 0u;
+    }
+    if (tid == 0) {
+        sP[NTHR] = (uint32_t)n0;
+        bad = 0;
+    }
+    __syncthreads();
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x, g0 = (uint64_t)blockIdx.x * blockDim.x + tid;
+    for (uint32_t t = 0; t < NTHR; t++) {
+        if (!((mask >> t) & 1u)) continue;
+        for (uint64_t p = sP[t] + g0; p < sP[t + 1]; p += gs) {
+            const uint32_t x = E->tok[p];
+            if (!is_id(x)) continue;
+            const uint64_t q = p + E->tlen[x];
+            if (q >= n0) continue;  // the last token: no pair
+            bool fresh = false;
+            const int64_t s = light_slot(E, lkey48(t, x, E->tok[q]), gen, true, &fresh);
+            if (s < 0) {
+                bad = 1;
+                continue;
+            }
+            if (fresh) atomicAdd(&cnt[t], 1u);
+            atomicMin(&E->lfirst[s], ((unsigned long long)(0xFFFFu - gen) << 48) | p);
+        }
+    }
+    __syncthreads();
+    if (tid < NTHR && cnt[tid]) atomicAdd(&C->ldt[tid], cnt[tid]);
+    if (tid == 0 && bad) atomicOr(&C->light_mask, 1u << 31);  // (table full: the full pass instead)
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) last = atomicAdd(&C->lticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last || tid >= 64) return;
+    __threadfence();
+    const uint32_t t = tid;
+    const uint32_t lm = __hip_atomic_load(&C->light_mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lm >> 31) {
+        if (t == 0) C->stat_need = 1;
+        return;
+    }
+    if (t < NTHR && ((mask >> t) & 1u)) {
+        // the last pair of the range: its left token is the token before the
+        // next range's first one (thread 15: the second-to-last token)
+        auto start_of = [&](uint64_t e) -> uint64_t {  // start of the token covering position e
+            const uint32_t w = E->tok[e];
+            return is_id(w) ? e : e - (w & ~END_FLAG);
+        };
+        uint64_t lp = start_of((uint64_t)sP[t + 1] - 1);
+        if (t == NTHR - 1) lp = start_of(lp - 1);
+        const uint32_t u = E->tok[lp], v = E->tok[lp + E->tlen[u]];
+        bool fr = false;
+        const int64_t s = light_slot(E, lkey48(t, u, v), gen, false, &fr);
+        const unsigned long long f =
+            s >= 0 ? __hip_atomic_load(&E->lfirst[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0ull;
+        const uint32_t follows = s >= 0 && (f & LKEY_MASK) != lp;  // the last key was counted before
+        const uint32_t Dt = __hip_atomic_load(&C->ldt[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t Bf = thread_cascade(C->Bstart[t], Dt, follows);
+        C->Bfin[t] = Bf;
+        C->Bcur[t] = Bf;
+        C->tUB[t] = Dt;
+    }
+    if (t == 0) {
+        C->stat_need = 0;
+        C->track_light++;
     }
 }
 

@@ -50,8 +50,11 @@ def test_bounds_checked_against_exact_pass(name, data, m, monkeypatch):
     assert s1["tracked_iters"] == s0["tracked_iters"]
     # the bounds skip most exact passes (the point of them)
     assert s1["track_skipped"] > 0 and s1["track_exact"] < s0["track_exact"], (s0, s1)
+    if name == "configs1":  # the on-device exact counts ran (and were checked in mode 2)
+        assert s1["track_light"] > 0 and s2["track_light"] > 0
     print(name, "exact passes", s0["track_exact"], "->", s1["track_exact"], "skipped", s1["track_skipped"],
-          "predictions held / missed", s1["spec_hits"], s1["spec_misses"])
+          "light", s1["track_light"], "(check mode", s2["track_light"], ") predictions held / missed",
+          s1["spec_hits"], s1["spec_misses"])
 
 
 _CHILD = """
