@@ -92,6 +92,26 @@ typedef struct {
                                  threads whose bound reached a growth threshold   */
 } bpe_gpu_stats;
 
+/* Per-merge record (training): the structured per-iteration metrics the
+   reference only prints (bpe.c:560).  Off by default; when on, every committed
+   merge writes one record on the device (no host round trip).  The batch
+   engine commits several merges per kernel chain: its records share the
+   batch's pre-batch D and token count.                                      */
+typedef struct {
+    uint32_t count;           /* occurrences of the merged pair (the argmax count) */
+    uint32_t ties;            /* one-merge engine: keys sharing its (count, bucket); batches: 0 */
+    uint32_t batch;           /* batch engine: the batch that committed it; else the merge index */
+    uint32_t batch_pos;       /* its position in that batch (0: one-merge engine)  */
+    uint64_t distinct_pairs;  /* D when it was selected                            */
+    uint64_t tokens;          /* tokens when it was selected                       */
+    double t_us;              /* device wall clock at its selection, us after the first record's */
+} bpe_gpu_merge_rec;
+
+/* records for the next trainings on ctx (on != 0), up to 2^20 merges */
+int bpe_gpu_set_merge_log(bpe_gpu_ctx *ctx, int on);
+/* the last training's records: *count = records held; out may be NULL */
+int bpe_gpu_fetch_merge_log(bpe_gpu_ctx *ctx, bpe_gpu_merge_rec *out, size_t cap, size_t *count);
+
 /* number of visible GPUs */
 int bpe_gpu_device_count(int *count);
 

@@ -24,7 +24,7 @@ EXPORTS = [
     # bpe_gpu.h
     "bpe_gpu_device_count", "bpe_gpu_create", "bpe_gpu_destroy", "bpe_gpu_load", "bpe_gpu_synth",
     "bpe_gpu_train", "bpe_gpu_fetch_merges", "bpe_gpu_fetch_ids", "bpe_gpu_encode", "bpe_gpu_decode",
-    "bpe_gpu_get_stats", "bpe_gpu_device_tokens", "bpe_gpu_kernel_profile", "bpe_gpu_set_profile", "bpe_gpu_event_profile",
+    "bpe_gpu_get_stats", "bpe_gpu_set_merge_log", "bpe_gpu_fetch_merge_log", "bpe_gpu_device_tokens", "bpe_gpu_kernel_profile", "bpe_gpu_set_profile", "bpe_gpu_event_profile",
     "bpe_gpu_strerror",
     "bpe_gpu_last_error", "bpe_gpu_train_ex",
     # bpe_gpu.h: sharded training
@@ -51,6 +51,13 @@ class GpuStats(ctypes.Structure):
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class MergeRec(ctypes.Structure):
+    """bpe_gpu.h bpe_gpu_merge_rec"""
+    _fields_ = [("count", ctypes.c_uint32), ("ties", ctypes.c_uint32), ("batch", ctypes.c_uint32),
+                ("batch_pos", ctypes.c_uint32), ("distinct_pairs", ctypes.c_uint64), ("tokens", ctypes.c_uint64),
+                ("t_us", ctypes.c_double)]
 
 
 class DynArr(ctypes.Structure):
@@ -113,6 +120,8 @@ def load():
     L.bpe_gpu_encode.argtypes = [vp, vp, sz]
     L.bpe_gpu_decode.argtypes = [vp, vp, sz, vp, sz, vp, sz, ctypes.POINTER(sz)]
     L.bpe_gpu_get_stats.argtypes = [vp, ctypes.POINTER(GpuStats)]
+    L.bpe_gpu_set_merge_log.argtypes = [vp, ctypes.c_int]
+    L.bpe_gpu_fetch_merge_log.argtypes = [vp, ctypes.POINTER(MergeRec), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
     L.bpe_gpu_ids_checksum.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     L.bpe_gpu_group_ids_checksum.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
                                              ctypes.POINTER(ctypes.c_uint64)]

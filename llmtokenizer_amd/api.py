@@ -258,6 +258,21 @@ class Engine:
         _lib.check(self.L.bpe_gpu_get_stats(self.ctx, ctypes.byref(st)), "stats")
         return st.as_dict()
 
+    def set_merge_log(self, on=True):
+        """per-merge records for the next trainings (bpe_gpu_set_merge_log)"""
+        _lib.check(self.L.bpe_gpu_set_merge_log(self.ctx, 1 if on else 0), "set_merge_log")
+
+    def merge_log(self):
+        """the last training's per-merge records (count, ties, batch, batch_pos,
+        distinct_pairs, tokens, t_us) as a numpy structured array"""
+        n = ctypes.c_size_t(0)
+        _lib.check(self.L.bpe_gpu_fetch_merge_log(self.ctx, None, 0, ctypes.byref(n)), "fetch_merge_log")
+        recs = (_lib.MergeRec * max(n.value, 1))()
+        _lib.check(self.L.bpe_gpu_fetch_merge_log(self.ctx, recs, n.value, ctypes.byref(n)), "fetch_merge_log")
+        dt = np.dtype([(f, np.uint32 if t is ctypes.c_uint32 else np.uint64 if t is ctypes.c_uint64 else np.float64)
+                       for f, t in _lib.MergeRec._fields_])
+        return np.frombuffer(bytes(recs), dtype=dt, count=n.value).copy()
+
     def ids_checksum(self, base=0):
         """position-keyed checksum of the ids in HBM (bpe_gpu_ids_checksum)"""
         s = ctypes.c_uint64()

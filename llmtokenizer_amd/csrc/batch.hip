@@ -1269,6 +1269,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             const uint32_t md = C->merges_done;
             E->merges[2 * (md + tid)] = sa[tid];
             E->merges[2 * (md + tid) + 1] = sb[tid];
+            log_merge(E, md + tid, B->cnt[tid], 0, (uint32_t)B->nbatch, tid, C->D, C->n_live);
             E->occ_off[z0 + tid] = top + spre[tid];
             E->occ_len[z0 + tid] = sR[tid];
             B->ra_z[tid] = z0 + tid;

@@ -267,6 +267,7 @@ struct bpe_gpu_ctx {
     bool own_stream = true;
     // run configuration (set before setup_run)
     uint32_t fast = 0;                     // schedule-free tie rule everywhere
+    bool mlog_on = false;                  // per-merge records (bpe_gpu_set_merge_log)
     uint32_t sharded = 0, shard = 0, nshards = 1;
     uint32_t xfused = 0;                   // fused sharded step (P2P group, shard.hip)
     uint32_t sbatch = 0;                   // sharded training in batches (shard.hip, batch.hip)
@@ -526,6 +527,13 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.skey, h.scap))) return r;
     if ((r = dalloc(c, &h.scnt, h.scap))) return r;
     if ((r = dalloc(c, &h.sfirst, h.scap))) return r;
+    // per-merge records (bpe_gpu_set_merge_log)
+    h.mlog = nullptr;
+    h.mlog_cap = 0;
+    if (c->mlog_on && !encode) {
+        h.mlog_cap = std::min<uint64_t>(std::max<uint32_t>(mcap, 1), MLOG_MAX);
+        if ((r = dalloc(c, &h.mlog, MLOG_WORDS * h.mlog_cap))) return r;
+    }
     // k_stat_light's generation-tagged set (tracked corpora; ids in 22 bits)
     h.lcap = 0;
     h.lkey = h.lfirst = nullptr;
@@ -2472,6 +2480,39 @@ int bpe_gpu_ids_checksum(bpe_gpu_ctx *c, uint64_t base, uint64_t *sum) {
 int bpe_gpu_get_stats(bpe_gpu_ctx *c, bpe_gpu_stats *st) {
     if (!c || !st) return BPE_GPU_EINVAL;
     *st = c->stats;
+    return 0;
+}
+
+int bpe_gpu_set_merge_log(bpe_gpu_ctx *c, int on) {
+    if (!c) return BPE_GPU_EINVAL;
+    c->mlog_on = on != 0;
+    return 0;
+}
+
+int bpe_gpu_fetch_merge_log(bpe_gpu_ctx *c, bpe_gpu_merge_rec *out, size_t cap, size_t *count) {
+    if (!c || !count) return BPE_GPU_EINVAL;
+    const size_t have = c->h.mlog && !c->h.encode ? (size_t)std::min<uint64_t>(c->merges_done, c->h.mlog_cap) : 0;
+    *count = have;
+    const size_t n = out ? std::min(cap, have) : 0;
+    if (!n) return 0;
+    HIPCHK(hipSetDevice(c->dev));
+    std::vector<unsigned long long> w((size_t)MLOG_WORDS * n);
+    HIPCHK(hipMemcpyAsync(w.data(), c->h.mlog, w.size() * 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    int khz = 0;
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
+    const double tick_us = 1000.0 / (khz > 0 ? khz : 100000);
+    const unsigned long long t0 = w[4];
+    for (size_t i = 0; i < n; i++) {
+        const unsigned long long *r = &w[(size_t)MLOG_WORDS * i];
+        out[i].count = (uint32_t)r[0];
+        out[i].ties = (uint32_t)(r[0] >> 32);
+        out[i].batch = (uint32_t)r[1];
+        out[i].batch_pos = (uint32_t)(r[1] >> 32);
+        out[i].distinct_pairs = r[2];
+        out[i].tokens = r[3];
+        out[i].t_us = (double)(long long)(r[4] - t0) * tick_us;
+    }
     return 0;
 }
 

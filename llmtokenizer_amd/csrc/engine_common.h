@@ -255,7 +255,13 @@ struct Eng {
     // first position ((0xFFFF - gen) << 48 | position); lcap == 0: no light pass
     unsigned long long *lkey, *lfirst;
     uint64_t lcap;
+    // per-merge record (bpe_gpu_set_merge_log; null: off): MLOG_WORDS words per
+    // merge -- count | ties << 32, batch | position << 32, D, tokens, wall clock
+    unsigned long long *mlog;
+    uint64_t mlog_cap;
 };
+constexpr uint32_t MLOG_WORDS = 5;
+constexpr uint64_t MLOG_MAX = 1ull << 20;  // merges a log holds (40 MB)
 
 // Control block.  Everything up to Dp is owned by k_select, which stages it in
 // LDS and writes it back whole; the tail section is written by k_apply and

@@ -1350,6 +1350,20 @@ __global__ __launch_bounds__(256) void k_rescan2(const Eng *__restrict__ E, Ctl 
     }
 }
 
+// per-merge record (SURVEY section 5 metrics; Eng::mlog, off by default): the
+// merged pair's count and ties, its batch and position in it, D and the tokens
+// when it was selected, the device wall clock
+__device__ inline void log_merge(const Eng *E, uint32_t md, uint32_t cnt, uint32_t ties, uint32_t batch, uint32_t pos,
+                                 uint64_t D, uint64_t n) {
+    if (!E->mlog || md >= E->mlog_cap) return;
+    unsigned long long *r = E->mlog + (uint64_t)MLOG_WORDS * md;
+    r[0] = cnt | ((unsigned long long)ties << 32);
+    r[1] = batch | ((unsigned long long)pos << 32);
+    r[2] = D;
+    r[3] = n;
+    r[4] = wall_clock64();
+}
+
 // set up iteration for merge (u, v) -> z; returns via Ctl.  rank / poff: the
 // byte-rank and byte-pair offset tables (k_select passes LDS copies).
 __device__ inline void commit_merge(const Eng *E, Ctl *C, uint32_t u, uint32_t v, const uint32_t *rank = nullptr,
@@ -1364,6 +1378,7 @@ __device__ inline void commit_merge(const Eng *E, Ctl *C, uint32_t u, uint32_t v
     if (!E->encode) {
         E->merges[2 * md] = u;
         E->merges[2 * md + 1] = v;
+        log_merge(E, md, (uint32_t)(C->W >> 32), C->ties, md, 0, C->D, C->n_live);
     }
     C->merges_done = md + 1;
     const bool valid = u < z && v < z;  // ids must already exist
@@ -1473,6 +1488,7 @@ __device__ inline void select_tail(const Eng *__restrict__ E, Ctl *C, Ctl *Cg, T
     if (arm) cand_of(E, pa, pb, true, rank, poff, &pm, &po, &pl);
     E->merges[2 * md] = u;
     E->merges[2 * md + 1] = v;
+    log_merge(E, md, cnt, r.tie, md, 0, D, C->n_live);
     C->a = u;
     C->b = v;
     C->z = z;

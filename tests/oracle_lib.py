@@ -33,6 +33,7 @@ def lib():
         L.oracle_train.restype = ctypes.c_long
         L.oracle_train_bytes.restype = ctypes.c_long
         L.oracle_encode.restype = ctypes.c_size_t
+        L.oracle_encode_heap.restype = ctypes.c_size_t
         L.oracle_decode.restype = ctypes.c_size_t
         L.oracle_decoded_len.restype = ctypes.c_size_t
         L.oracle_murmur_pair.restype = ctypes.c_uint32
@@ -79,6 +80,18 @@ def encode(data: bytes, merges: np.ndarray) -> np.ndarray:
     ids = np.zeros(max(buf.size, 1), dtype=np.uint32)
     n = L.oracle_encode(_ptr(buf), ctypes.c_size_t(buf.size), _ptr(m),
                         ctypes.c_size_t(m.size // 2), _ptr(ids))
+    return ids[:n].copy()
+
+
+def encode_heap(data: bytes, merges: np.ndarray) -> np.ndarray:
+    """oracle_encode's result in O(n log n) (smallest rank first over a token
+    list): the bench's CPU encode baseline"""
+    L = lib()
+    buf = np.frombuffer(data, dtype=np.uint8).copy()
+    m = np.ascontiguousarray(merges, dtype=np.uint32).reshape(-1)
+    ids = np.zeros(max(buf.size, 1), dtype=np.uint32)
+    n = L.oracle_encode_heap(_ptr(buf), ctypes.c_size_t(buf.size), _ptr(m),
+                             ctypes.c_size_t(m.size // 2), _ptr(ids))
     return ids[:n].copy()
 
 
