@@ -32,7 +32,9 @@ def main():
         g.synth(q, 3, (total if q == k - 1 else a + step) - a, a)
     g.encode(m)
     st = g.stats()
-    print({x: st[x] for x in ("ms_total", "ms_init", "ms_train", "iterations", "candidates", "occurrences")})
+    d = {x: st[x] for x in ("ms_total", "ms_init", "ms_train", "iterations", "candidates", "occurrences", "enc_path")}
+    d["ids_checksum"] = "%016x" % g.ids_checksum()[0]
+    print(d)
 
 
 if __name__ == "__main__":
