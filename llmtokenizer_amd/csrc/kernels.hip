@@ -3094,7 +3094,9 @@ __device__ void track_block(const Eng *__restrict__ E, Ctl *__restrict__ C) {
 // older generation counts as empty), and the last block applies the table
 // growth (thread_cascade from the phase's starting size).  The resolver's full
 // pass (k_stat_*) still runs at tie events.
-constexpr uint32_t LIGHT_B = 128;
+// (its grid launches with every merge and mostly exits at once: a small one;
+// BPE_LIGHT_B overrides it for tuning runs)
+uint32_t LIGHT_B = getenv("BPE_LIGHT_B") ? (uint32_t)std::max(1, atoi(getenv("BPE_LIGHT_B"))) : 32u;
 constexpr unsigned long long LKEY_MASK = (1ull << 48) - 1ull;
 
 __device__ inline unsigned long long lkey48(uint32_t t, uint32_t u, uint32_t v) {
