@@ -731,9 +731,9 @@ void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
     if (fused_graph(c, tracked)) {
         // fused speculative graph: entered with the current merge applied
         // (by the previous k_fused, or the host after a stop)
-        const uint32_t trk = c->h.track_ub == 1 && !c->fast && c->n0 < TRACK_LIMIT ? 1 : 0;
+        // + the track block and the light blocks (tracked corpora)
+        const uint32_t trk = c->h.track_ub == 1 && !c->fast && c->n0 < TRACK_LIMIT ? 1 + (c->h.lcap ? LIGHT_B : 0) : 0;
         k_rescan_spec<<<SPEC_RB + SPEC_SB + trk, SCAN_T, 0, c->st>>>(c->dE, c->dC, SPEC_RB, trk);
-        if (trk && c->h.lcap) k_stat_light<<<LIGHT_B, 1024, 0, c->st>>>(c->dE, c->dC);
         // (the hot set needs no level-2 pass; a fall-back recaptures the graph)
         if (c->h.hcap / L1W > SELECT_L1_MAX && !c->h.hot) k_rescan2<<<RESCAN2_BLOCKS, 256, 0, c->st>>>(c->dE, c->dC);
         k_fused<<<1 + FUSED_A + FUSED_B, 1024, 0, c->st>>>(c->dE, c->dC, FUSED_A, nullptr);
@@ -1252,7 +1252,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             return 0;
         case STOP_ERROR:
             return fail(C.err == 5 ? BPE_GPU_ERANGE : BPE_GPU_EINTERNAL,
-                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than an end code holds (2^31 - 3 bytes)" : "thread-stat table full");
+                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than an end code holds (2^31 - 3 bytes)" : C.err == 7 ? "tracked iterations: the light pass waited for the track block in vain" : "thread-stat table full");
         case STOP_REDO:  // missed prediction: k_select committed the real merge
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;

@@ -306,7 +306,8 @@ struct Ctl {
     uint32_t trk_on;                  // an exact pass ran: tracked iterations entered (no STOP_MODE)
     uint32_t phase_open;              // the track block opened this phase (Bstart = the sizes before it)
     uint32_t light_mask, lgen;        // threads whose D_t k_stat_light counts (stat_need == 2); its table generation
-    uint32_t lticket, lpad;           // k_stat_light blocks done
+    uint32_t lticket;                 // k_stat_light blocks done
+    uint32_t lgo;                     // fused graph: the track block's word to K1's light blocks, (z << 2) | 1 run / 2 none
     uint32_t ldt[NTHR];               // k_stat_light: distinct pairs of the masked threads
     uint32_t tP[NTHR];              // position of the first token of thread t's pair range (t >= 1)
     uint32_t tUB[NTHR];               // upper bound on thread t's distinct pairs

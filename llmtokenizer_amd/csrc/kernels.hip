@@ -994,6 +994,7 @@ constexpr uint32_t SUM_ONE_RT = 4;         // summaries <= 4 x 1024 entries: red
 // one wave per dirty level-1 block (256 slots, 4 per lane)
 __device__ void edge_record_block(const Eng *__restrict__ E, Ctl *__restrict__ C);
 __device__ void track_block(const Eng *__restrict__ E, Ctl *__restrict__ C);
+__device__ void light_body(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t bid, uint32_t nblk);
 
 // edges = 1 (sharded training): one extra block writes this shard's edge
 // record (it only needs k_apply's span writes) beside the rescans
@@ -1246,15 +1247,46 @@ __device__ inline void spec_descriptor(Ctl *C, const Snap &S) {
     }
 }
 
-// track = 1: the last block updates the per-thread distinct-count bounds of
-// the tokens the last apply left (tracked phases; it returns at once otherwise)
+// track = T > 0: after the scan blocks, one block updates the per-thread
+// distinct-count bounds of the tokens the last apply left (tracked phases; it
+// returns at once otherwise), then T - 1 blocks count the exact D_t of the
+// threads whose bound reached its growth threshold (light_body) once the
+// track block says so -- in the same kernel, so a merge that needs no light
+// pass pays no kernel for it.  The track block is dispatched before them, so
+// their wait (bounded, on Ctl::lgo tagged with the merge's z) always ends.
 __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ E, Ctl *__restrict__ C,
                                                          uint32_t rblocks, uint32_t track) {
     const Snap S = snap(C);
     if (blockIdx.x == 0 && threadIdx.x == 0) spec_descriptor(C, S);
     if (S.stop) return;
-    if (track && blockIdx.x == gridDim.x - 1) {
+    const uint32_t tb = gridDim.x - track;  // the track block (when track > 0)
+    const uint32_t tag = (S.z & 0x3FFFFFFFu) << 2;
+    if (track && blockIdx.x == tb) {
         track_block(E, C);
+        __syncthreads();
+        if (threadIdx.x == 0 && track > 1)
+            __hip_atomic_store(&C->lgo, tag | (C->stat_need == 2 ? 1u : 2u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (track > 1 && blockIdx.x > tb) {
+        __shared__ uint32_t go;
+        if (threadIdx.x == 0) {
+            const unsigned long long t0 = wall_clock64();
+            uint32_t v;
+            for (;;) {
+                v = __hip_atomic_load(&C->lgo, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if ((v & ~3u) == tag) break;
+                if (wall_clock64() - t0 > 100000000ull) {  // ~1 s: the track block never spoke
+                    v = 2u;
+                    C->err = 7;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            go = (v & 3u) == 1u;
+        }
+        __syncthreads();
+        if (go) light_body(E, C, blockIdx.x - tb - 1, track - 1);
         return;
     }
     ts_mark(E, S.z, TS_K1_IN, true);
@@ -1266,7 +1298,7 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ 
         scan_exit_stamp(E, blockIdx.x);
         ts_mark(E, S.z, TS_K1_RESCAN, false, true);
     } else if (S.spec) {
-        scan_body<false, true>(E, C, S, blockIdx.x - rblocks, gridDim.x - rblocks - (track ? 1 : 0));
+        scan_body<false, true>(E, C, S, blockIdx.x - rblocks, gridDim.x - rblocks - track);
         ts_mark(E, S.z, TS_K1_SCAN, false, true);
     } else {
         scan_exit_stamp(E, blockIdx.x);
@@ -3127,8 +3159,7 @@ __device__ inline int64_t light_slot(const Eng *E, unsigned long long key48, uin
     return -1;
 }
 
-__global__ __launch_bounds__(1024) void k_stat_light(const Eng *__restrict__ E, Ctl *__restrict__ C) {
-    if (C->stop || C->stat_need != 2) return;
+__device__ void light_body(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t bid, uint32_t nblk) {
     __shared__ uint32_t cnt[NTHR], sP[NTHR + 1];
     __shared__ uint32_t last, bad;
     const uint32_t tid = threadIdx.x;
@@ -3143,7 +3174,7 @@ __global__ __launch_bounds__(1024) void k_stat_light(const Eng *__restrict__ E, 
         bad = 0;
     }
     __syncthreads();
-    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x, g0 = (uint64_t)blockIdx.x * blockDim.x + tid;
+    const uint64_t gs = (uint64_t)nblk * blockDim.x, g0 = (uint64_t)bid * blockDim.x + tid;
     for (uint32_t t = 0; t < NTHR; t++) {
         if (!((mask >> t) & 1u)) continue;
         for (uint64_t p = sP[t] + g0; p < sP[t + 1]; p += gs) {
@@ -3166,7 +3197,7 @@ __global__ __launch_bounds__(1024) void k_stat_light(const Eng *__restrict__ E, 
     if (tid == 0 && bad) atomicOr(&C->light_mask, 1u << 31);  // (table full: the full pass instead)
     __threadfence();
     __syncthreads();
-    if (tid == 0) last = atomicAdd(&C->lticket, 1u) == gridDim.x - 1;
+    if (tid == 0) last = atomicAdd(&C->lticket, 1u) == nblk - 1;
     __syncthreads();
     if (!last || tid >= 64) return;
     __threadfence();
@@ -3201,6 +3232,12 @@ __global__ __launch_bounds__(1024) void k_stat_light(const Eng *__restrict__ E, 
         C->stat_need = 0;
         C->track_light++;
     }
+}
+
+// the light pass as a kernel of its own (the unfused tracked graph)
+__global__ __launch_bounds__(1024) void k_stat_light(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+    if (C->stop || C->stat_need != 2) return;
+    light_body(E, C, blockIdx.x, gridDim.x);
 }
 
 // synthetic corpus (llmtokenizer_amd/synth.py), bytes [off, off+n)
