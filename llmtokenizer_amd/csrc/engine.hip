@@ -1490,6 +1490,18 @@ void launch_hist_span(bpe_gpu_ctx *c, size_t lds, uint32_t ntl, uint32_t *d_hist
     k_pair_hist_span<R><<<ntl, 1024, lds, c->st>>>(c->dE, d_hist, tile, lo, S);
 }
 
+template <uint32_t R>
+void launch_hist_pk(bpe_gpu_ctx *c, size_t lds, uint32_t ntl, uint32_t *d_hist, uint64_t tile, uint32_t lo,
+                    uint32_t S) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_hist_pk<R>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    // sub-tile between folds: PK_SUB(R) keeps every 16-bit bin below 2^16;
+    // BPE_HIST_PK_SUB (tuning only, multiple of 32 K) may overflow on skewed input
+    uint64_t sub = PK_SUB(R);
+    if (const char *t = getenv("BPE_HIST_PK_SUB")) sub = std::max<uint64_t>(32768, strtoull(t, nullptr, 0) & ~32767ull);
+    k_pair_hist_pk<R><<<ntl, 1024, lds, c->st>>>(c->dE, d_hist, tile, lo, S, sub);
+}
+
 // init phase 2: byte ranks (from the presence vector `bh`, nonzero = present),
 // token lengths, tok[] = bytes, counting sort of byte-pair positions by rank key
 int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint32_t> *unrank_out,
@@ -1534,11 +1546,23 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
             // 1 GiB: 1 copy 0.380 ms, 2 copies 0.368, 4 copies (one block per CU) 0.418)
             uint32_t R = 2;
             while (R > 1 && ((size_t)R * S * S + 256) * 4 > HIST_LDS_MAX) R >>= 1;
+            // packed 16-bit copies (k_pair_hist_pk): R = 4 or 8
+            uint32_t PK = 0;
+            if (const char *t = getenv("BPE_HIST_PK")) PK = (uint32_t)atoi(t);  // tuning
             if (const char *t = getenv("BPE_HIST_R")) R = std::min<uint32_t>(R, (uint32_t)atoi(t));  // tuning
-            const size_t lds = ((size_t)R * S * S + 256) * 4;
-            if (R >= 2) launch_hist_span<2>(c, lds, ntl, d_hist, tile, lo, S);
-            else launch_hist_span<1>(c, lds, ntl, d_hist, tile, lo, S);
-            c->stats.count_pass_span = R;
+            const size_t W = ((size_t)S * S + 1) / 2;
+            if (PK == 8 && (8 * W + 256) * 4 <= 160 * 1024) {
+                launch_hist_pk<8>(c, (8 * W + 256) * 4, ntl, d_hist, tile, lo, S);
+                c->stats.count_pass_span = 108;
+            } else if (PK == 4 && (4 * W + 256) * 4 <= HIST_LDS_MAX) {
+                launch_hist_pk<4>(c, (4 * W + 256) * 4, ntl, d_hist, tile, lo, S);
+                c->stats.count_pass_span = 104;
+            } else {
+                const size_t lds = ((size_t)R * S * S + 256) * 4;
+                if (R >= 2) launch_hist_span<2>(c, lds, ntl, d_hist, tile, lo, S);
+                else launch_hist_span<1>(c, lds, ntl, d_hist, tile, lo, S);
+                c->stats.count_pass_span = R;
+            }
         }
         else k_pair_hist<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
         HIPCHK(hipEventRecord(e1, c->st));

@@ -2198,6 +2198,118 @@ __global__ __launch_bounds__(1024) void k_pair_hist_span(const Eng *__restrict__
 template __global__ void k_pair_hist_span<1>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
 template __global__ void k_pair_hist_span<2>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
 
+// Packed form of k_pair_hist_span: 16-bit bins, two to a word, so R = 4 or 8
+// interleaved copies fit the LDS (lane class rl = lane mod R adds
+// 1 << 16 * (bin & 1) to word (bin >> 1) * R + rl: the 32 lanes of a bank
+// group split over R classes of 32 / R lanes, each class over 32 / R banks).
+// A 16-bit bin holds one class's adds to it for at most PK_SUB(R) / R pairs
+// (32768), so each block takes its tile in sub-tiles of PK_SUB(R) pairs and
+// after each one folds the copies into per-thread u32 accumulators (thread t
+// owns words t, t + T, ...) and clears them.  At the end the accumulators go
+// back into the LDS as plain u32 bins (R * S * S / 2 >= S * S words) and are
+// written out in rank-key order as k_pair_hist_span does.
+constexpr uint32_t PK_WORDS_MAX = (SPAN_MAX * SPAN_MAX + 1) / 2;  // words of one packed copy
+__host__ __device__ constexpr uint64_t PK_SUB(uint32_t R) { return 32768ull * R; }
+
+template <uint32_t R>
+__device__ __forceinline__ void pk_count4(uint32_t *h, uint32_t w, uint32_t next, uint32_t S, uint32_t off,
+                                          uint32_t lim, uint32_t rl) {
+    const uint32_t b[5] = {w & 0xFF, (w >> 8) & 0xFF, (w >> 16) & 0xFF, w >> 24, next & 0xFF};
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        if (j < lim) {
+            const uint32_t bin = b[j] * S + b[j + 1] - off;
+            atomicAdd(&h[(bin >> 1) * R + rl], 1u << ((bin & 1) << 4));
+        }
+    }
+}
+
+template <uint32_t R>
+__global__ __launch_bounds__(1024) void k_pair_hist_pk(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
+                                                       uint64_t tile, uint32_t lo, uint32_t S, uint64_t sub) {
+    extern __shared__ uint32_t hdyn[];
+    constexpr uint32_t T = 1024, NACC = (PK_WORDS_MAX + T - 1) / T;
+    const uint32_t A = E->A, AA = A * A, SS = S * S, W = (SS + 1) / 2;
+    uint32_t *h = hdyn, *ur = hdyn + R * W;
+    const uint32_t tl = blockIdx.x, lane = threadIdx.x & 63, rl = lane & (R - 1);
+    for (uint32_t i = threadIdx.x; i < R * W; i += T) h[i] = 0;
+    for (uint32_t x = threadIdx.x; x < 256; x += T) {
+        const uint32_t r = E->rank[x];
+        if (r != HOLE) ur[r] = x;
+    }
+    uint32_t acc[2 * NACC];
+#pragma unroll
+    for (uint32_t j = 0; j < 2 * NACC; j++) acc[j] = 0;
+    __syncthreads();
+    const uint64_t n0 = E->n0;
+    const uint64_t s = (uint64_t)tl * tile, e = min(n0 - 1, s + tile);  // pair positions [s, e), tile % 1024 == 0
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(E->bytes);
+    const uint8_t *bytes = E->bytes;
+    const uint32_t off = lo * S + lo;
+    const uint64_t nw = T / 64, nwords = (n0 + 3) / 4;
+    for (uint64_t ss = s; ss < e; ss += sub) {  // block-uniform
+        const uint64_t se = min(e, ss + sub), kb1 = (se + 1023) / 1024;
+        for (uint64_t kb = ss / 1024 + (threadIdx.x >> 6); kb < kb1; kb += 2 * nw) {  // wave-uniform
+            const uint64_t kc = kb + nw;
+            uint32_t wa[4], wb[4];
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) {
+                const uint64_t ia = kb * 256 + 64 * q + lane, ib = kc * 256 + 64 * q + lane;
+                wa[q] = ia < nwords ? src[ia] : 0u;
+                wb[q] = kc < kb1 && ib < nwords ? src[ib] : 0u;
+            }
+#pragma unroll
+            for (uint32_t half = 0; half < 2; half++) {
+                const uint64_t k = half ? kc : kb;
+                if (half && k >= kb1) break;
+                const uint32_t *w = half ? wb : wa;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++) {
+                    const uint64_t p = (k * 256 + 64 * q + lane) * 4;
+                    uint32_t nxt = __shfl_down(w[q], 1);
+                    if (q < 3) {
+                        const uint32_t f = __shfl(w[q + 1], 0);
+                        if (lane == 63) nxt = f;
+                    } else if (lane == 63) {
+                        nxt = (k + 1) * 1024 < n0 ? bytes[(k + 1) * 1024] : 0;
+                    }
+                    if (p < se) pk_count4<R>(h, w[q], nxt, S, off, (uint32_t)min<uint64_t>(4, se - p), rl);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < NACC; j++) {
+            const uint32_t m = threadIdx.x + j * T;
+            if (m < W) {
+#pragma unroll
+                for (uint32_t r = 0; r < R; r++) {
+                    const uint32_t v = h[m * R + r];
+                    acc[2 * j] += v & 0xFFFF;
+                    acc[2 * j + 1] += v >> 16;
+                    h[m * R + r] = 0;
+                }
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < NACC; j++) {
+        const uint32_t m = threadIdx.x + j * T;
+        if (m < W) {
+            h[2 * m] = acc[2 * j];
+            h[2 * m + 1] = acc[2 * j + 1];
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < AA; k += T) {
+        const uint32_t x = ur[k / A] - lo, y = ur[k % A] - lo;
+        hist[(uint64_t)tl * AA + k] = h[x * S + y];
+    }
+}
+template __global__ void k_pair_hist_pk<4>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t, uint64_t);
+template __global__ void k_pair_hist_pk<8>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t, uint64_t);
+
 // Init phase 1: the set of byte values present (only presence is needed to
 // rank them), plus tok[] = bytes when TOK (inputs too short for the counting
 // sort, whose first pass k_sort_a writes tok[] otherwise).  Grid-stride over
