@@ -2414,6 +2414,27 @@ __global__ __launch_bounds__(256) void k_pair_colscan(uint32_t *__restrict__ his
 constexpr uint32_t RELIST_MAXAA = 12288;  // keys per LDS histogram (A <= 110)
 constexpr uint32_t RELIST_T = 1024;
 
+// f(x, y, i) for every live byte pair (tok[i], tok[i + 1]), lo <= i < hi:
+// each lane reads 4 consecutive slots with one 16-byte load (lo % 4 == 0; a
+// block's waves cover 16 KB per round) and takes the slot after them from the
+// next lane (lane 63 loads it).  tok[] has 8 slots of slack past n0 > hi.
+template <class F>
+__device__ __forceinline__ void relist_walk(const uint32_t *__restrict__ tok, uint64_t lo, uint64_t hi, F f) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wbase = lo + 4ull * (threadIdx.x & ~63u);
+    for (uint64_t k = 0; wbase + k < hi; k += 4ull * RELIST_T) {  // wave-uniform
+        const uint64_t i0 = wbase + k + 4 * lane;
+        uint4 v = make_uint4(HOLE, HOLE, HOLE, HOLE);
+        if (i0 <= hi) v = *reinterpret_cast<const uint4 *>(tok + i0);
+        uint32_t nx = __shfl_down(v.x, 1);
+        if (lane == 63) nx = i0 + 4 <= hi ? tok[i0 + 4] : HOLE;
+        const uint32_t t[5] = {v.x, v.y, v.z, v.w, nx};
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++)
+            if (i0 + j < hi && t[j] < 256 && t[j + 1] < 256) f(t[j], t[j + 1], i0 + j);
+    }
+}
+
 __global__ __launch_bounds__(RELIST_T) void k_relist_hist(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
                                                           uint64_t tile) {
     extern __shared__ uint32_t rh[];  // [A * A]
@@ -2423,11 +2444,7 @@ __global__ __launch_bounds__(RELIST_T) void k_relist_hist(const Eng *__restrict_
     if (threadIdx.x < 256) srank[threadIdx.x] = E->rank[threadIdx.x];
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * tile, hi = min(E->n0 - 1, lo + tile);
-    const uint32_t *__restrict__ tok = E->tok;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += RELIST_T) {
-        const uint32_t x = tok[i], y = tok[i + 1];
-        if (x < 256 && y < 256) atomicAdd(&rh[srank[x] * A + srank[y]], 1u);
-    }
+    relist_walk(E->tok, lo, hi, [&](uint32_t x, uint32_t y, uint64_t) { atomicAdd(&rh[srank[x] * A + srank[y]], 1u); });
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < AA; k += RELIST_T) hist[(uint64_t)blockIdx.x * AA + k] = rh[k];
 }
@@ -2442,12 +2459,10 @@ __global__ __launch_bounds__(RELIST_T) void k_relist_scatter(const Eng *__restri
     if (threadIdx.x < 256) srank[threadIdx.x] = E->rank[threadIdx.x];
     __syncthreads();
     const uint64_t lo = (uint64_t)blockIdx.x * tile, hi = min(E->n0 - 1, lo + tile);
-    const uint32_t *__restrict__ tok = E->tok;
     uint32_t *__restrict__ plist = E->plist;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += RELIST_T) {
-        const uint32_t x = tok[i], y = tok[i + 1];
-        if (x < 256 && y < 256) plist[atomicAdd(&cur[srank[x] * A + srank[y]], 1u)] = (uint32_t)i;
-    }
+    relist_walk(E->tok, lo, hi, [&](uint32_t x, uint32_t y, uint64_t i) {
+        plist[atomicAdd(&cur[srank[x] * A + srank[y]], 1u)] = (uint32_t)i;
+    });
 }
 
 // exclusive scan of in[0..n) into out[0..n], out[n] = total; one block of

@@ -1,7 +1,9 @@
 """BASELINE configs at their full sizes on one MI355X (SURVEY.md 8(d) "parity
 at scale").  The oracle cannot train 1 GiB x 8192 merges end to end, so:
 
-  configs[2]  1 GiB x 8192 merges: spot checks -- the GPU's token array after
+  configs[2]  1 GiB x 8192 merges: the final ids equal the oracle's replace
+              passes on 256 KiB windows (start, middle, end); spot checks --
+              the GPU's token array after
               t merges is copied back and the CPU restatement recounts every
               pair and picks the next merge (oracle_next_merge, RULE order =
               the reference's own at >= 2^20 tokens); it must be merge t of the
@@ -71,7 +73,25 @@ def test_config2_1g_8192_merges_spot_checks():
     st = e.stats()
     csum = e.ids_checksum()
     n_out = st["n_out"]
+    # the training ids against the oracle's sequential replace passes
+    # (bpe.c:760-779) on 256 KiB windows at the start, middle and end of the
+    # corpus: positions and ids of every token inside each window
+    ids = e.ids()
     e.close()
+    el = _elen(M)
+    ends = np.cumsum(el[ids].astype(np.uint32), dtype=np.int64)
+    assert ends[-1] == GIB
+    W = 256 << 10
+    for lo in (0, GIB // 2 + 4321, GIB - W):
+        hi = lo + W
+        a = int(np.searchsorted(ends, lo, side="right"))  # first token ending after lo
+        b = int(np.searchsorted(ends, hi, side="right"))
+        gp = ends[a:b + 1] - el[ids[a:b + 1]]
+        gi = ids[a:b + 1]
+        keep = (gp >= lo) & (gp + el[gi] <= hi)
+        opos, oids = _oracle_window(M, el, lo, hi, seed=2, n=GIB)
+        assert (gp[keep] == opos).all() and (gi[keep] == oids).all(), lo
+    del ids, ends
     # the encoder replaying the learned list lands on the training ids
     x = api.Engine(0)
     x.synth(2, GIB)
@@ -186,11 +206,12 @@ def _shard_tail(g, k, E, el, T):
     return ends - el[tail], tail
 
 
-def _oracle_window(M, el, lo, hi, margin=32 << 10):
+def _oracle_window(M, el, lo, hi, margin=32 << 10, seed=3, n=None):
     """(positions, ids) of the tokens inside [lo, hi) when the oracle encodes
     [lo - margin, hi + margin) alone (the margin absorbs its chunk edges)"""
     c0 = max(0, lo - margin)
-    oids = O.encode(synth_bytes(3, hi + margin - c0, lo=c0), M)
+    c1 = hi + margin if n is None else min(n, hi + margin)
+    oids = O.encode(synth_bytes(seed, c1 - c0, lo=c0), M)
     pos = c0 + np.concatenate([[0], np.cumsum(el[oids], dtype=np.int64)[:-1]])
     keep = (pos >= lo) & (pos + el[oids] <= hi)
     return pos[keep], oids[keep]
