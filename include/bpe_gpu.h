@@ -69,7 +69,8 @@ typedef struct {
     uint64_t l1_rescanned;    /* level-1 summary blocks rescanned                 */
     uint64_t spec_hits;       /* next merges found by the speculative scan        */
     uint64_t spec_misses;     /* mispredicted next merges (host re-scan)          */
-    uint64_t count_pass_span; /* >0: the count pass ran in span form (k_pair_hist_span), value = LDS histogram copies */
+    uint64_t count_pass_span; /* >0: the count pass ran in span form (k_pair_hist_span), value = LDS histogram copies
+                                 (100 + copies: the packed 16-bit form k_pair_hist_pk, BPE_HIST_PK) */
     uint64_t hot_rebuilds;    /* hot-set argmax: full-table rebuilds of the listed keys */
     uint64_t hot_mode;        /* 0 level summaries, 1 hot set, 2 hot set given up mid-run */
     uint64_t hot_scanned;     /* hot-set entries reduced, summed over the merges */
