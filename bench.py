@@ -134,7 +134,23 @@ class Ctx:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29517")
             torch.cuda.set_device(self.local)
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            # gloo prints its mesh set-up ("[Gloo] Rank r is connected to ...")
+            # on stdout, where the driver reads the one JSON line: send fd 1 to
+            # stderr while the group connects, then flush C stdio before restoring
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+                dist.barrier()
+            finally:
+                try:
+                    import ctypes
+                    ctypes.CDLL(None).fflush(None)
+                except OSError:
+                    pass
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):
