@@ -418,15 +418,25 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
     }
 }
 
-// ids of window w (staged at w * core) to out + off[w], widened to u32
+// ids of window w (staged at w * core) to out + off[w], widened to u32: the
+// few ids before out's next 16-byte boundary one per lane, the rest four per
+// lane as one 16-byte store (the u16 reads stay coalesced across the lanes)
 __global__ __launch_bounds__(256) void k_ew_gather(const uint16_t *__restrict__ stage, const uint32_t *__restrict__ cnt,
                                                    const unsigned long long *__restrict__ off, uint64_t nwin,
                                                    uint32_t core, uint32_t *__restrict__ out) {
     for (uint64_t w = blockIdx.x; w < nwin; w += gridDim.x) {
         const uint32_t n = cnt[w];
+        const uint64_t o = off[w];
         const uint16_t *src = stage + w * core;
-        uint32_t *dst = out + off[w];
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+        uint32_t *dst = out + o;
+        const uint32_t h = min(n, (uint32_t)((4 - (o & 3)) & 3));  // ids before the boundary
+        if (threadIdx.x < h) dst[threadIdx.x] = src[threadIdx.x];
+        const uint32_t nq = (n - h) / 4;
+        for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
+            const uint32_t i = h + 4 * q;
+            *reinterpret_cast<uint4 *>(dst + i) = make_uint4(src[i], src[i + 1], src[i + 2], src[i + 3]);
+        }
+        for (uint32_t i = h + 4 * nq + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
     }
 }
 
