@@ -2225,7 +2225,7 @@ __device__ __forceinline__ void pk_count4(uint32_t *h, uint32_t w, uint32_t next
 }
 
 template <uint32_t R>
-__global__ __launch_bounds__(1024) void k_pair_hist_pk(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pair_hist_pk(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
                                                        uint64_t tile, uint32_t lo, uint32_t S, uint64_t sub) {
     extern __shared__ uint32_t hdyn[];
     constexpr uint32_t T = 1024, NACC = (PK_WORDS_MAX + T - 1) / T;
