@@ -46,8 +46,10 @@ uint32_t *bpe_encode_bytes(const uint8_t *bytes, size_t n, dyn_arr_t *pair_arr, 
 int bpe_last_stats(bpe_gpu_stats *out);
 
 /* compress / compress_ex / bpe_train_bytes / bpe_encode_bytes / decompress keep
- * one engine context per device between calls (its device memory pool and
- * pinned staging are reused; BPE_KEEP_CONTEXT=0 turns this off): free them */
+ * one engine context per device between calls.  By default its device memory
+ * is given back when the call returns (bpe_gpu_trim: only the stream and the
+ * pinned host staging stay); BPE_KEEP_CONTEXT=1 keeps the HBM pool too,
+ * BPE_KEEP_CONTEXT=0 creates and destroys a context per call.  Free them: */
 void bpe_release_engines(void);
 
 #ifdef __cplusplus

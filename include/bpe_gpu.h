@@ -113,6 +113,22 @@ int bpe_gpu_set_merge_log(bpe_gpu_ctx *ctx, int on);
 /* the last training's records: *count = records held; out may be NULL */
 int bpe_gpu_fetch_merge_log(bpe_gpu_ctx *ctx, bpe_gpu_merge_rec *out, size_t cap, size_t *count);
 
+/* Run events of the last training, in order: each entry is
+   (kind << 56) | merges committed before the event.  The hot-set rebuild at
+   the start of a run is recorded with 0 merges.  *count = events held. */
+enum {
+    BPE_GPU_EV_RELIST = 1,       /* byte-pair position lists rebuilt from the live tokens */
+    BPE_GPU_EV_HOT_REBUILD = 2,  /* hot set (listed keys with count >= hot_T) rebuilt */
+    BPE_GPU_EV_TABLE_GROW = 3,   /* pair-count table regrown (x4) */
+    BPE_GPU_EV_MODE = 4          /* hot set given up for the level summaries / tracked phase */
+};
+int bpe_gpu_fetch_events(bpe_gpu_ctx *ctx, uint64_t *out, size_t cap, size_t *count);
+
+/* Free the context's device memory (buffer pool, corpus, scratch) but keep
+   the stream, events and pinned host staging, so the next load on it pays no
+   stream / staging set-up.  The context must be loaded again before use. */
+int bpe_gpu_trim(bpe_gpu_ctx *ctx);
+
 /* number of visible GPUs */
 int bpe_gpu_device_count(int *count);
 

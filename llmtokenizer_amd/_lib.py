@@ -1,6 +1,7 @@
 """ctypes binding of libbpe_amd.so (the C-ABI in include/bpe.h, bpe_ex.h,
 bpe_gpu.h).  The library is built in-tree (make / __graft_entry__.build()) and
 loaded from this package directory; there is no Python or CPU fallback."""
+import atexit
 import ctypes
 import os
 
@@ -34,6 +35,7 @@ EXPORTS = [
     "bpe_gpu_group_create_p2p", "bpe_gpu_group_p2p_connect", "bpe_gpu_group_transport",
     "bpe_gpu_group_create_local_p2p", "bpe_gpu_ids_checksum", "bpe_gpu_group_ids_checksum", "bpe_gpu_load_fd",
     "bpe_gpu_fetch_ids_range", "bpe_gpu_group_fetch_ids_range", "bpe_gpu_device_pci", "bpe_gpu_peer_access",
+    "bpe_gpu_fetch_events", "bpe_gpu_trim",
 ]
 
 
@@ -162,7 +164,14 @@ def load():
     L.dyn_arr_set.argtypes = [ctypes.POINTER(DynArr), sz, vp]
     L.dyn_arr_set.restype = ctypes.c_bool
     L.bpe_last_stats.argtypes = [ctypes.POINTER(GpuStats)]
+    L.bpe_gpu_fetch_events.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), sz, ctypes.POINTER(sz)]
+    L.bpe_gpu_trim.argtypes = [vp]
+    L.bpe_release_engines.argtypes = []
+    L.bpe_release_engines.restype = None
     _LIB = L
+    # the C library keeps one (trimmed) engine context per device between
+    # compress() calls: give it back before the interpreter exits
+    atexit.register(L.bpe_release_engines)
     return L
 
 

@@ -61,6 +61,12 @@ def _take_ids(ptr, n):
     return ids
 
 
+def release_engines():
+    """free the engine contexts compress() & co. keep between calls
+    (bpe_ex.h bpe_release_engines; also run at interpreter exit)"""
+    _lib.load().bpe_release_engines()
+
+
 def last_stats():
     st = GpuStats()
     _lib.load().bpe_last_stats(ctypes.byref(st))
@@ -278,6 +284,22 @@ class Engine:
         s = ctypes.c_uint64()
         _lib.check(self.L.bpe_gpu_ids_checksum(self.ctx, int(base), ctypes.byref(s)), "ids_checksum")
         return s.value
+
+    EVENT_KINDS = {1: "relist", 2: "hot_rebuild", 3: "table_grow", 4: "mode"}
+
+    def events(self):
+        """run events of the last training (bpe_gpu_fetch_events): a list of
+        (kind, merges committed before it), kind in EVENT_KINDS' values"""
+        n = ctypes.c_size_t(0)
+        _lib.check(self.L.bpe_gpu_fetch_events(self.ctx, None, 0, ctypes.byref(n)), "fetch_events")
+        buf = (ctypes.c_uint64 * max(n.value, 1))()
+        _lib.check(self.L.bpe_gpu_fetch_events(self.ctx, buf, n.value, ctypes.byref(n)), "fetch_events")
+        return [(self.EVENT_KINDS.get(buf[i] >> 56, str(buf[i] >> 56)), buf[i] & ((1 << 56) - 1))
+                for i in range(n.value)]
+
+    def trim(self):
+        """give the context's device memory back (bpe_gpu_trim); load again before use"""
+        _lib.check(self.L.bpe_gpu_trim(self.ctx), "trim")
 
     def set_profile(self, on=True):
         _lib.check(self.L.bpe_gpu_set_profile(self.ctx, 1 if on else 0), "set_profile")

@@ -1157,11 +1157,13 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         const uint32_t R = in ? B->R[lane] : 0, cnt = in ? B->cnt[lane] : 0;
         uint32_t bnd = in && !SH ? B->bound[lane] : 0;
         unsigned long long ovm = 0;  // SH: members some shard could not stage
+        uint32_t Rg = R;             // occurrences over all shards (the live-token count is global)
         if (SH) {
             uint32_t *xm = E->xbat + BK + (uint64_t)lane * xbat_member_words(z0 + k);
             // (every block's prologue reads these words: the next select clears them)
             if (in) {
                 const uint32_t rg = xm[0];
+                Rg = rg;
                 bnd = xm[1];
                 if (blockIdx.x == 0) B->Rg[lane] = rg;
                 sRg[lane] = rg;
@@ -1190,11 +1192,21 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             }
         }
         const unsigned long long rex = rpre - R;                            // occurrences of the members before me
+        // the same over all shards: C->n_live counts every shard's tokens
+        unsigned long long rexg = rex;
+        if (SH) {
+            unsigned long long g = Rg;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned long long y = __shfl_up(g, o);
+                if ((int)lane >= o) g += y;
+            }
+            rexg = g - Rg;
+        }
         const uint32_t pm = __shfl_up(bpre, 1);                              // max bound of the members before me
         // member q is the argmax after the members before it: its count beats
         // every key they can create, and the run is still untracked then
         const bool fail = in && lane > 0 &&
-                          (!(pm < cnt) || (dt && (z0 + lane) % dt == 0) || (!E->fast && live0 - rex < TRACK_LIMIT) ||
+                          (!(pm < cnt) || (dt && (z0 + lane) % dt == 0) || (!E->fast && live0 - rexg < TRACK_LIMIT) ||
                            (ovm & ((2ull << lane) - 1ull)) != 0);
         const unsigned long long fm = __ballot(fail);
         uint32_t js = fm ? (uint32_t)__ffsll(fm) - 1 : k;

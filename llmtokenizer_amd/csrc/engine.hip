@@ -292,6 +292,7 @@ struct bpe_gpu_ctx {
     hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr, g_batch = nullptr;
     bool hot_fallback = false;  // the hot set was given up for the level summaries
     uint32_t relists = 0;       // byte-pair list rebuilds of the current run
+    std::vector<uint64_t> events;  // run events of the current run (bpe_gpu_fetch_events)
     std::vector<hipGraphExec_t> retired;  // replaced graphs, destroyed with the run
     bpe_gpu_stats stats{};
     // profile of the dominant kernel: HIP events captured around every k_scan
@@ -355,6 +356,11 @@ int dalloc(bpe_gpu_ctx *c, T **p, size_t count, bool zero = true) {
         if (e != hipSuccess) return fail(BPE_GPU_EHIP, "hipMemsetAsync", e);
     }
     return 0;
+}
+
+// a run event (bpe_gpu_fetch_events): kind in the top byte, merges committed before it below
+void note_event(bpe_gpu_ctx *c, uint32_t kind, uint64_t merges) {
+    c->events.push_back(((uint64_t)kind << 56) | (merges & ((1ull << 56) - 1)));
 }
 
 void free_train(bpe_gpu_ctx *c, bool release = false) {
@@ -430,6 +436,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     // iteration, 2: both, each skip verified -- tests)
     h.track_ub = 1;
     if (const char *t = getenv("BPE_TRACK")) h.track_ub = (uint32_t)std::min(2, std::max(0, atoi(t)));
+    h.light_wait = 100000000ull;
+    if (const char *t = getenv("BPE_LIGHT_WAIT_TICKS")) h.light_wait = strtoull(t, nullptr, 10);
     h.xtimeout = c->xtimeout;
     h.xstride = (uint32_t)(((4ull * h.vcap + 2) + 63) & ~63ull);
     if (c->sharded) {
@@ -1260,6 +1268,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             break;
         case STOP_MODE:
             C.stop = STOP_NONE;
+            note_event(c, BPE_GPU_EV_MODE, C.merges_done);
             if (c->h.hot) {  // tracked iterations select from the level summaries
                 c->h.hot = 0;
                 c->h.batch = 0;
@@ -1276,6 +1285,8 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             break;
         case STOP_GROW: {
             C.stop = STOP_NONE;
+            note_event(c, BPE_GPU_EV_TABLE_GROW, C.merges_done);
+            note_event(c, BPE_GPU_EV_HOT_REBUILD, C.merges_done);
             C.full = 1;
             if ((r = push_ctl(c))) return r;
             if ((r = grow_table(c, c->h.hcap * 4))) return r;
@@ -1286,6 +1297,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
         }
         case STOP_RELIST:
             C.stop = STOP_NONE;
+            note_event(c, BPE_GPU_EV_RELIST, C.merges_done);
             C.relist_c0 = (uint32_t)C.counters[4];
             C.relist_o0 = (uint32_t)C.counters[5];
             if ((r = push_ctl(c))) return r;
@@ -1295,6 +1307,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             break;
         case STOP_HOT:
             C.stop = STOP_NONE;
+            note_event(c, BPE_GPU_EV_HOT_REBUILD, C.merges_done);
             if ((r = push_ctl(c))) return r;
             if ((r = hot_rebuild(c))) return r;
             if ((r = select_next(c, false))) return r;
@@ -2032,6 +2045,8 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     if (tracked) launch_stats(c);
     c->hot_fallback = false;
     c->relists = 0;
+    c->events.clear();
+    if (c->h.hot) note_event(c, BPE_GPU_EV_HOT_REBUILD, 0);
     if ((r = hot_rebuild(c))) return r;
     if ((r = select_next(c, tracked && !fused_graph(c, true)))) return r;
     HIPCHK(hipStreamSynchronize(c->st));
@@ -2537,6 +2552,33 @@ int bpe_gpu_fetch_merge_log(bpe_gpu_ctx *c, bpe_gpu_merge_rec *out, size_t cap, 
         out[i].tokens = r[3];
         out[i].t_us = (double)(long long)(r[4] - t0) * tick_us;
     }
+    return 0;
+}
+
+int bpe_gpu_fetch_events(bpe_gpu_ctx *c, uint64_t *out, size_t cap, size_t *count) {
+    if (!c || !count) return BPE_GPU_EINVAL;
+    *count = c->events.size();
+    if (out) std::copy_n(c->events.begin(), std::min(cap, c->events.size()), out);
+    return 0;
+}
+
+int bpe_gpu_trim(bpe_gpu_ctx *c) {
+    if (!c) return BPE_GPU_EINVAL;
+    HIPCHK(hipSetDevice(c->dev));
+    free_train(c, true);  // (synchronises the stream first)
+    if (c->h.bytes) (void)hipFree(c->h.bytes);
+    c->h.bytes = nullptr;
+    c->bytes_cap = 0;
+    c->n0 = 0;
+    c->loaded = false;
+    c->pres_valid = false;
+    for (int k = 0; k < 10; k++) {
+        if (c->dscr[k]) (void)hipFree(c->dscr[k]);
+        c->dscr[k] = nullptr;
+        c->dscr_cap[k] = 0;
+    }
+    if (c->d_enc_pairs) (void)hipFree(c->d_enc_pairs);
+    c->d_enc_pairs = nullptr;
     return 0;
 }
 

@@ -251,6 +251,9 @@ struct Eng {
     // when a distinct-count bound reaches a growth threshold (default), 2 both
     // (check: every skipped pass is verified against the exact one; BPE_TRACK)
     uint32_t track_ub;
+    // wall-clock ticks the light blocks of K1 wait for the track block before
+    // leaving the merge to the exact pass (BPE_LIGHT_WAIT_TICKS; ~1 s)
+    unsigned long long light_wait;
     // k_stat_light's (thread, pair) set: key (gen << 48 | t << 44 | a << 22 | b),
     // first position ((0xFFFF - gen) << 48 | position); lcap == 0: no light pass
     unsigned long long *lkey, *lfirst;

@@ -1253,7 +1253,9 @@ __device__ inline void spec_descriptor(Ctl *C, const Snap &S) {
 // threads whose bound reached its growth threshold (light_body) once the
 // track block says so -- in the same kernel, so a merge that needs no light
 // pass pays no kernel for it.  The track block is dispatched before them, so
-// their wait (bounded, on Ctl::lgo tagged with the merge's z) always ends.
+// their wait (on Ctl::lgo tagged with the merge's z) normally ends at once; it
+// is bounded (Eng::light_wait), and a block that gives up leaves the merge to
+// the exact pass (STOP_STATS) instead of failing the run.
 __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ E, Ctl *__restrict__ C,
                                                          uint32_t rblocks, uint32_t track) {
     const Snap S = snap(C);
@@ -1276,9 +1278,13 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ 
             for (;;) {
                 v = __hip_atomic_load(&C->lgo, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 if ((v & ~3u) == tag) break;
-                if (wall_clock64() - t0 > 100000000ull) {  // ~1 s: the track block never spoke
+                if (wall_clock64() - t0 > E->light_wait) {
+                    // the track block did not speak in time (a busy or shared
+                    // GPU, a serialising profiler): no light pass here.  If the
+                    // track block asks for one (stat_need == 2) it then stays
+                    // unanswered -- no block is the last one -- so k_select
+                    // raises STOP_STATS and the host runs the exact pass.
                     v = 2u;
-                    C->err = 7;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);

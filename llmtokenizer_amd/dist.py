@@ -50,9 +50,14 @@ def p2p_group(device, max_merges, strict=True):
     rank, world = dist.get_rank(), dist.get_world_size()
     g, err = None, None
     pcis = [None] * world
-    dist.all_gather_object(pcis, api.device_pci(device))
-    err = peer_problem(device, pcis)
+    try:  # (every rank reaches every all_gather_object below, whatever fails)
+        mine = api.device_pci(device)
+    except api.BpeError as e:
+        mine, err = "", str(e)
+    dist.all_gather_object(pcis, mine)
     try:
+        if err is None:
+            err = peer_problem(device, pcis)
         if err is None:
             g = api.ShardGroup(device, nranks=world, rank=rank, p2p_max_merges=max_merges)
     except api.BpeError as e:

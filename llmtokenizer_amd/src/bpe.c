@@ -196,20 +196,25 @@ static void report(const char *what, int rc)
     fprintf(stderr, "bpe: %s failed: %s (%s)\n", what, bpe_gpu_strerror(rc), bpe_gpu_last_error());
 }
 
-/* One engine context per device is kept between calls (its HBM buffer pool,
- * corpus buffer and pinned staging are reused, so a second compress() pays
- * the ingest and the training, not the set-up); BPE_KEEP_CONTEXT=0 makes
- * every call create and destroy its own, bpe_release_engines() frees the kept
- * ones.  A context in use by one thread is taken out of the cache, so
- * concurrent calls on one device simply create another. */
+/* One engine context per device is kept between calls.  By default it is
+ * trimmed when a call returns (bpe_gpu_trim: its HBM -- buffer pool, corpus,
+ * scratch -- goes back to the device; the stream and the pinned staging stay),
+ * so the reference's "compress frees everything" holds for device memory.
+ * BPE_KEEP_CONTEXT=1 keeps the HBM pool too (a second compress() of the same
+ * size pays no allocation), BPE_KEEP_CONTEXT=0 creates and destroys a context
+ * per call; bpe_release_engines() frees the kept ones.  A context in use by
+ * one thread is taken out of the cache, so concurrent calls on one device
+ * simply create another. */
 #define ENGINE_CACHE 64
 static pthread_mutex_t g_engine_mu = PTHREAD_MUTEX_INITIALIZER;
 static bpe_gpu_ctx *g_engines[ENGINE_CACHE];
 
+/* 0 destroy per call, 1 keep trimmed (default), 2 keep with its HBM pool */
 static int keep_engines(void)
 {
     const char *v = getenv("BPE_KEEP_CONTEXT");
-    return !v || atoi(v) != 0;
+    if (!v) return 1;
+    return atoi(v) == 0 ? 0 : atoi(v) == 1 ? 2 : 1;
 }
 
 static int open_engine(int device, bpe_gpu_ctx **ctx)
@@ -231,7 +236,9 @@ static int open_engine(int device, bpe_gpu_ctx **ctx)
 static void close_engine(int device, bpe_gpu_ctx *ctx, int ok)
 {
     if (!ctx) return;
-    if (ok && device >= 0 && device < ENGINE_CACHE && keep_engines()) {
+    const int keep = keep_engines();
+    if (ok && keep == 1 && bpe_gpu_trim(ctx)) ok = 0;
+    if (ok && device >= 0 && device < ENGINE_CACHE && keep) {
         pthread_mutex_lock(&g_engine_mu);
         if (!g_engines[device]) {
             g_engines[device] = ctx;

@@ -5,6 +5,7 @@
 
 int bpe_gpu_create(int device, bpe_gpu_ctx **out) { (void)device; if (out) *out = NULL; return BPE_GPU_ENODEV; }
 void bpe_gpu_destroy(bpe_gpu_ctx *ctx) { (void)ctx; }
+int bpe_gpu_trim(bpe_gpu_ctx *ctx) { (void)ctx; return BPE_GPU_ENODEV; }
 int bpe_gpu_load(bpe_gpu_ctx *c, const uint8_t *b, size_t n) { (void)c; (void)b; (void)n; return BPE_GPU_ENODEV; }
 int bpe_gpu_load_fd(bpe_gpu_ctx *c, int fd, size_t s, size_t *n) { (void)c; (void)fd; (void)s; (void)n; return BPE_GPU_ENODEV; }
 int bpe_gpu_train(bpe_gpu_ctx *c, long m, size_t *n) { (void)c; (void)m; (void)n; return BPE_GPU_ENODEV; }

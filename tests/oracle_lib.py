@@ -39,6 +39,7 @@ def lib():
         L.oracle_murmur_pair.restype = ctypes.c_uint32
         L.oracle_murmur_pair.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_next_merge.restype = ctypes.c_int
+        L.oracle_next_merge_mt.restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -113,16 +114,18 @@ def murmur_pair(a: int, b: int) -> int:
     return lib().oracle_murmur_pair(a, b)
 
 
-def next_merge(ids: np.ndarray, V: int):
+def next_merge(ids: np.ndarray, V: int, threads: int = 1):
     """The merge the reference picks next on the token sequence `ids` (full
     recount; RULE tie order = the reference's own for >= 2^20 tokens).
-    Returns (a, b, count, D, B_final) or None when training would stop."""
+    Returns (a, b, count, D, B_final) or None when training would stop.
+    threads > 1 shares the dense count table (V <= 16384) between threads."""
     L = lib()
     ids = np.ascontiguousarray(ids, dtype=np.uint32)
     a, b = ctypes.c_uint32(), ctypes.c_uint32()
     c, D, B = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-    r = L.oracle_next_merge(_ptr(ids), ctypes.c_size_t(ids.size), ctypes.c_uint32(V), ctypes.byref(a),
-                            ctypes.byref(b), ctypes.byref(c), ctypes.byref(D), ctypes.byref(B))
+    r = L.oracle_next_merge_mt(_ptr(ids), ctypes.c_size_t(ids.size), ctypes.c_uint32(V), ctypes.c_int(threads),
+                               ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(D),
+                               ctypes.byref(B))
     if r < 0:
         raise MemoryError("oracle_next_merge")
     return (a.value, b.value, c.value, D.value, B.value) if r == 1 else None

@@ -1,7 +1,10 @@
 """BASELINE configs at their full sizes on one MI355X (SURVEY.md 8(d) "parity
 at scale").  The oracle cannot train 1 GiB x 8192 merges end to end, so:
 
-  configs[2]  1 GiB x 8192 merges: the final ids equal the oracle's replace
+  configs[2]  1 GiB x 8192 merges: every merge of the batch engine equals the
+              one-merge engine's (merges, counts, ids), CPU recounts at
+              checkpoints every 512 merges and around each relist / hot-set
+              rebuild; the final ids equal the oracle's replace
               passes on 256 KiB windows (start, middle, end); spot checks --
               the GPU's token array after
               t merges is copied back and the CPU restatement recounts every
@@ -111,6 +114,105 @@ def test_config2_1g_8192_merges_spot_checks():
         assert (nm[0], nm[1]) == tuple(M[t].tolist()), (t, nm, M[t])
         del ids
     t3.close()
+
+
+# configs[2] as the round-3 bench line recorded it (profiles/r3_bench_final.json)
+C2_MERGES_MD5 = "ec83a657060eed3e2e21d3653cab2392"
+C2_IDS_CHECKSUM = 0xEA3C70245637EC3F
+
+
+def _train_c2(monkeypatch, batch, log=True):
+    monkeypatch.setenv("BPE_BATCH", batch)
+    e = api.Engine(0)
+    try:
+        e.set_merge_log(log)
+        e.synth(2, GIB)
+        assert e.train(8192) == 8192
+        return e.merges(), e.ids_checksum(), e.merge_log(), e.stats(), e.events()
+    finally:
+        e.close()
+
+
+@pytest.fixture(scope="module")
+def c2_run():
+    """the batch engine's configs[2] job with per-merge records and run events"""
+    mp = pytest.MonkeyPatch()
+    try:
+        yield _train_c2(mp, "1")
+    finally:
+        mp.undo()
+
+
+def test_config2_every_merge_batch_equals_one_merge_engine(c2_run, monkeypatch):
+    """All 8192 merges of configs[2] at full size: the batch engine (several
+    merges per scan/apply, formation rules of DESIGN 1.0) == the one-merge
+    engine (one exact argmax per merge, bpe.c:669-783 restated), merge for
+    merge, with the same counts and the same final ids -- and both equal the
+    round-3 bench line's md5 / ids checksum."""
+    M, csum, log, st, ev = c2_run
+    assert hashlib.md5(M.tobytes()).hexdigest() == C2_MERGES_MD5
+    assert csum == C2_IDS_CHECKSUM
+    assert st["batches"] > 0 and log.size == 8192
+    M1, csum1, log1, st1, _ = _train_c2(monkeypatch, "0")
+    assert st1["batches"] == 0
+    assert (M1 == M).all()
+    assert csum1 == csum
+    assert (log1["count"] == log["count"]).all()
+    # the one-merge engine's records carry D and the token count before every
+    # merge; the batch engine's first member of each batch the same
+    first = log["batch_pos"] == 0
+    assert (log1["distinct_pairs"][first] == log["distinct_pairs"][first]).all()
+    assert (log1["tokens"][first] == log["tokens"][first]).all()
+
+
+def _c2_checkpoints(log, ev):
+    """merge indices t (batch starts: the records there carry the state after
+    exactly t merges) every 512 merges, and just before / after every relist
+    and hot-set rebuild of the run"""
+    starts = np.flatnonzero(log["batch_pos"] == 0)
+    starts = starts[starts > 0]
+    pick = set()
+    for t in range(512, 8192, 512):
+        j = int(np.searchsorted(starts, t))
+        if j < starts.size:
+            pick.add(int(starts[j]))
+    for kind, m in ev:
+        if kind in ("relist", "hot_rebuild") and 0 < m < 8192:
+            j = int(np.searchsorted(starts, m))  # starts[j] == m: the batch after the event
+            for q in (j - 1, j, j + 1):
+                if 0 <= q < starts.size:
+                    pick.add(int(starts[q]))
+    return sorted(pick)
+
+
+@pytest.mark.parametrize("part", range(4))
+def test_config2_recount_checkpoints(c2_run, part):
+    """CPU recounts of the GPU's token array after t merges (t every 512, and
+    around each relist / hot-set rebuild): the merge the reference would pick
+    next (full recount, oracle_next_merge) is merge t of the run, and the
+    merge records' count and D there equal the recount's."""
+    M, _, log, st, ev = c2_run
+    kinds = [k for k, _ in ev]
+    assert st["relists"] == kinds.count("relist") and st["relists"] >= 1
+    assert st["hot_rebuilds"] >= 1 and "hot_rebuild" in kinds
+    pts = _c2_checkpoints(log, ev)
+    assert len(pts) >= 15
+    mine = pts[part::4]
+    e = api.Engine(0)
+    try:
+        e.synth(2, GIB)
+        for t in mine:
+            assert e.train(t) == t
+            ids = e.ids()
+            assert ids.size == int(log["tokens"][t])
+            nm = O.next_merge(ids, 256 + t, threads=16)
+            del ids
+            assert nm is not None, t
+            a, b, cnt, D, _ = nm
+            assert (a, b) == tuple(M[t].tolist()), (t, nm, M[t])
+            assert cnt == int(log["count"][t]) and D == int(log["distinct_pairs"][t]), (t, nm, log[t])
+    finally:
+        e.close()
 
 
 def test_config3_1g_eight_shards_equals_single_engine():

@@ -99,3 +99,18 @@ def test_tie_events_after_skipped_passes_vs_oracle(seed, n, monkeypatch):
     assert (ids == oids).all()
     assert st["track_skipped"] > 0
     assert st["tie_events"] + st["edge_events"] > 0, st
+
+
+def test_light_pass_wait_timeout_falls_back_to_exact_pass(monkeypatch):
+    """K1's light blocks wait (bounded) for the track block of the same grid.
+    With the bound forced to zero ticks (BPE_LIGHT_WAIT_TICKS=0) a block that
+    does not see the track block's word at once leaves the merge to the exact
+    pass (STOP_STATS) instead of failing the run: same merges and ids."""
+    data = synth_bytes(1, 1 << 20)
+    m0, i0, s0 = _train(data, 1024, 1, monkeypatch)
+    monkeypatch.setenv("BPE_LIGHT_WAIT_TICKS", "0")
+    m1, i1, s1 = _train(data, 1024, 1, monkeypatch)
+    assert (m1 == m0).all() and (i1 == i0).all()
+    assert s1["track_violations"] == 0
+    # every light pass that timed out ran as an exact pass instead
+    assert s1["track_light"] + s1["track_exact"] >= s0["track_light"] + s0["track_exact"], (s0, s1)
