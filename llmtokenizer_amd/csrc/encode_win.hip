@@ -1,8 +1,9 @@
 // encode_win.hip -- window-local encoder (BASELINE configs[4]); included by engine.hip.
 //
 // Same semantics as encode.hip (the reference's replace pass, bpe.c:760-779,
-// applied merge by merge in rank order) and the same commuting batches of
-// merges, but each workgroup replays ALL batches on one window of the byte
+// applied merge by merge in rank order) and batches of commuting merges
+// (engine.hip ew_plan: the list layered by its conflict chains, ids relabeled
+// to the replay order and mapped back in k_ew_gather), but each workgroup replays ALL batches on one window of the byte
 // stream held in LDS: HBM sees the bytes streamed in and the ids streamed
 // out, plus L2-resident rank lookups for the pairs merges create.  The global
 // batched replay (encode.hip) pays several random DRAM sectors per
@@ -418,25 +419,28 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
     }
 }
 
-// ids of window w (staged at w * core) to out + off[w], widened to u32: the
+// ids of window w (staged at w * core) to out + off[w], widened to u32 and
+// mapped back to merge-list ids (unmap, when the plan reordered the list): the
 // few ids before out's next 16-byte boundary one per lane, the rest four per
 // lane as one 16-byte store (the u16 reads stay coalesced across the lanes)
 __global__ __launch_bounds__(256) void k_ew_gather(const uint16_t *__restrict__ stage, const uint32_t *__restrict__ cnt,
                                                    const unsigned long long *__restrict__ off, uint64_t nwin,
-                                                   uint32_t core, uint32_t *__restrict__ out) {
+                                                   uint32_t core, const uint32_t *__restrict__ unmap,
+                                                   uint32_t *__restrict__ out) {
+    auto id = [&](uint16_t x) -> uint32_t { return unmap ? unmap[x] : (uint32_t)x; };
     for (uint64_t w = blockIdx.x; w < nwin; w += gridDim.x) {
         const uint32_t n = cnt[w];
         const uint64_t o = off[w];
         const uint16_t *src = stage + w * core;
         uint32_t *dst = out + o;
         const uint32_t h = min(n, (uint32_t)((4 - (o & 3)) & 3));  // ids before the boundary
-        if (threadIdx.x < h) dst[threadIdx.x] = src[threadIdx.x];
+        if (threadIdx.x < h) dst[threadIdx.x] = id(src[threadIdx.x]);
         const uint32_t nq = (n - h) / 4;
         for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
             const uint32_t i = h + 4 * q;
-            *reinterpret_cast<uint4 *>(dst + i) = make_uint4(src[i], src[i + 1], src[i + 2], src[i + 3]);
+            *reinterpret_cast<uint4 *>(dst + i) = make_uint4(id(src[i]), id(src[i + 1]), id(src[i + 2]), id(src[i + 3]));
         }
-        for (uint32_t i = h + 4 * nq + threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+        for (uint32_t i = h + 4 * nq + threadIdx.x; i < n; i += blockDim.x) dst[i] = id(src[i]);
     }
 }
 

@@ -16,6 +16,7 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <unordered_map>
 
 #include <rocprim/rocprim.hpp>
 
@@ -1701,96 +1702,175 @@ int getenv_int(const char *k, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 
-// Batches of the commuting rule (encode.hip form_batch, without its scratch
-// cap) and the window encoder's lookup tables, as one host image:
+// Batches of merges that commute exactly, and the window encoder's lookup
+// tables, as one host image:
 //   bp[65536] | ht[H] {key, value} | roles[V][2][8] (per id: batches using it left / right) | bstart[nb + 1] |
-//   beq[nb] (bytes)
+//   beq[nb] (bytes) | unmap[V] (replay id -> merge-list id; when the list was reordered)
+//
+// Two merges q < r CONFLICT (must keep their order) when r uses the id q
+// creates, an id is the left id of one and the right id of the other, one is
+// an a == a merge on an id the other uses, or they are the same pair (the
+// pairwise form of encode.hip form_batch's rule).  Any order that keeps every
+// conflicting pair in rank order replays to the same ids: a non-conflicting
+// pair of adjacent merges commutes (an `a` followed by `b` is untouched by a
+// merge of `a` with something else, a shared right id likewise, run pairing
+// only reads tokens no other merge touches).  So the list is LAYERED: each
+// merge goes into the layer after the latest layer holding a merge it
+// conflicts with -- the longest conflict chain, not the first conflict, ends a
+// batch (BASELINE configs[4]'s 32 k-merge list: 81 contiguous batches before).
+// The replay then runs in layer order with merge ids relabeled to their
+// position in it (256 + position: a merge's inputs are created in earlier
+// layers, so the relabeled list is a valid merge list and every batch is a
+// rank range again), and the id gather maps the replay ids back (unmap).
+// BPE_EW_LAYER=0: the contiguous greedy cut (the list's own order).
 struct EwPlan {
     bool ok = false;
+    bool relabeled = false;  // unmap[] is needed
     uint32_t nb = 0, H = 0;  // H: hash slots
-    size_t off_ht = 0, off_roles = 0, off_bstart = 0, off_beq = 0, words = 0;
+    size_t off_ht = 0, off_roles = 0, off_bstart = 0, off_beq = 0, off_unmap = 0, words = 0;
 };
 
 EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
     EwPlan P;
     if (m > EW_MAX_MERGES || getenv_int("BPE_ENC_WIN", 1) == 0) return P;
     const uint32_t V = 256 + (uint32_t)m;
+    const bool layered = getenv_int("BPE_EW_LAYER", 1) != 0;
+    // 1. the batch (layer) of every merge, in the list's own rank order
+    std::vector<uint32_t> batch(m);
+    uint32_t nb = 0;
+    auto valid_at = [&](uint32_t r) { return pairs[2 * r] < 256 + r && pairs[2 * r + 1] < 256 + r; };
+    if (layered) {
+        // per id: latest layer creating it / using it left / right / in an
+        // a == a merge / at all (-1: none); per pair: latest layer holding it
+        std::vector<int32_t> cre(V, -1), asl(V, -1), asr(V, -1), aeq(V, -1), any(V, -1);
+        std::unordered_map<uint64_t, int32_t> key;
+        key.reserve(2 * m);
+        int32_t top = -1;
+        for (uint32_t r = 0; r < m; r++) {
+            const uint32_t u = pairs[2 * r], v = pairs[2 * r + 1], z = 256 + r;
+            int32_t L = 0;  // (a merge that can never match goes first: it changes nothing)
+            if (valid_at(r)) {
+                const uint64_t k = ((uint64_t)u << 32) | v;
+                auto it = key.find(k);
+                int32_t dep = std::max({cre[u], cre[v], aeq[u], aeq[v], asr[u], asl[v],
+                                        it == key.end() ? -1 : it->second});
+                if (u == v) dep = std::max(dep, any[u]);
+                L = dep + 1;
+                asl[u] = std::max(asl[u], L);
+                asr[v] = std::max(asr[v], L);
+                any[u] = std::max(any[u], L);
+                any[v] = std::max(any[v], L);
+                if (u == v) aeq[u] = std::max(aeq[u], L);
+                key[k] = L;
+            }
+            cre[z] = L;
+            batch[r] = (uint32_t)L;
+            top = std::max(top, L);
+        }
+        nb = m ? (uint32_t)(top + 1) : 0;
+    } else {
+        // the contiguous greedy cut: a batch ends at the first merge that
+        // conflicts with one of its members
+        std::vector<uint8_t> fl(V, 0);
+        std::vector<uint32_t> touched;
+        std::unordered_map<uint64_t, uint32_t> firstb;
+        uint32_t b0 = 0;
+        for (uint32_t r = 0; r < m; r++) {
+            const uint32_t u = pairs[2 * r], v = pairs[2 * r + 1], z = 256 + r;
+            const bool valid = valid_at(r);
+            const uint64_t k = ((uint64_t)u << 32) | v;
+            if (r > b0) {
+                const uint8_t fu = valid ? fl[u] : 0, fv = valid ? fl[v] : 0;
+                auto it = valid ? firstb.find(k) : firstb.end();
+                const bool dep = ((fu | fv) & (UF_Z | UF_EQ)) || (fu & UF_R) || (fv & UF_L) ||
+                                 (u == v && (fu | fv)) || (it != firstb.end() && it->second == nb);
+                if (dep) {
+                    for (uint32_t id : touched) fl[id] = 0;
+                    touched.clear();
+                    nb++;
+                    b0 = r;
+                }
+            }
+            if (valid) {
+                fl[u] |= UF_L | (u == v ? UF_EQ : 0);
+                fl[v] |= UF_R;
+                touched.push_back(u);
+                touched.push_back(v);
+                firstb[k] = nb;
+            }
+            fl[z] |= UF_Z;
+            touched.push_back(z);
+            batch[r] = nb;
+        }
+        if (m) nb++;
+    }
+    if (nb > EW_MAX_BATCHES) return P;
+    // 2. replay order: by batch, rank order inside a batch (stable); the
+    // replay id of merge r is 256 + its position
+    std::vector<uint32_t> order(m), pos(m);
+    {
+        std::vector<uint32_t> fill(nb + 1, 0);
+        for (uint32_t r = 0; r < m; r++) fill[batch[r] + 1]++;
+        for (uint32_t b = 0; b < nb; b++) fill[b + 1] += fill[b];
+        for (uint32_t r = 0; r < m; r++) {
+            pos[r] = fill[batch[r]]++;
+            order[pos[r]] = r;
+        }
+    }
+    bool moved = false;
+    for (uint32_t r = 0; r < m && !moved; r++) moved = pos[r] != r;
+    auto rid = [&](uint32_t x) { return x < 256 ? x : 256 + pos[x - 256]; };
+    // 3. tables over the replay list: first position of every pair | batch << 16
+    uint32_t H = 64;
     // hash slots: at most 1/8 full, so that a lookup (most of them misses:
     // pairs a merge creates that the list does not hold) is ~1.1 dependent probes
-    uint32_t H = 64;
     const uint64_t hscale = (uint64_t)std::max(2, getenv_int("BPE_EW_HSCALE", 8));
     while (H < hscale * m) H <<= 1;
-    std::vector<uint32_t> bp(65536, ~0u), hkey(H, 0), hval(H, ~0u), batch(m);
-    std::vector<uint8_t> fl(V, 0), eq;
-    std::vector<uint32_t> touched;
-    auto slot = [&](uint32_t key) {
-        uint32_t s = (uint32_t)mix64(key) & (H - 1);
-        while (hkey[s] != 0 && hkey[s] != key) s = (s + 1) & (H - 1);
+    std::vector<uint32_t> bp(65536, ~0u), hkey(H, 0), hval(H, ~0u);
+    auto slot = [&](uint32_t k) {
+        uint32_t s = (uint32_t)mix64(k) & (H - 1);
+        while (hkey[s] != 0 && hkey[s] != k) s = (s + 1) & (H - 1);
         return s;
     };
-    uint32_t b0 = 0, nb = 0;
-    for (uint32_t r = 0; r < m; r++) {
-        const uint32_t u = pairs[2 * r], v = pairs[2 * r + 1], z = 256 + r;
-        const bool valid = u < z && v < z, byte = u < 256 && v < 256;
-        uint32_t *first = nullptr;  // the key's first rank | batch << 16 (~0: new key)
-        if (valid) {
-            if (byte) {
-                first = &bp[(u << 8) | v];
-            } else {
-                const uint32_t key = ((u << 16) | v) + 1u, s = slot(key);
-                hkey[s] = key;
-                first = &hval[s];
-            }
-        }
-        if (r > b0) {
-            const uint8_t fu = valid ? fl[u] : 0, fv = valid ? fl[v] : 0;
-            const bool dep = ((fu | fv) & (UF_Z | UF_EQ)) || (fu & UF_R) || (fv & UF_L) || (u == v && (fu | fv)) ||
-                             (first && *first != ~0u && (*first & 0xFFFFu) >= b0);
-            if (dep) {
-                for (uint32_t id : touched) fl[id] = 0;
-                touched.clear();
-                nb++;
-                b0 = r;
-            }
-        }
-        if (valid) {
-            fl[u] |= UF_L | (u == v ? UF_EQ : 0);
-            fl[v] |= UF_R;
-            touched.push_back(u);
-            touched.push_back(v);
-            if (*first == ~0u) *first = r | (nb << 16);
-        }
-        fl[z] |= UF_Z;
-        touched.push_back(z);
-        batch[r] = nb;
-    }
-    if (m) nb++;
-    if (nb > EW_MAX_BATCHES) return P;
     P.nb = nb;
     P.H = H;
+    P.relabeled = moved;
     P.off_ht = 65536;
     P.off_roles = P.off_ht + 2ull * H;  // (16-byte aligned: H >= 64)
     P.off_bstart = P.off_roles + (size_t)V * 16;
     P.off_beq = P.off_bstart + nb + 1;
-    P.words = P.off_beq + (nb + 3) / 4 + 1;
+    P.off_unmap = P.off_beq + (nb + 3) / 4 + 1;
+    P.words = P.off_unmap + V;
     img.assign(P.words, 0);
+    uint32_t *roles = img.data() + P.off_roles;
+    uint32_t *bst = img.data() + P.off_bstart;
+    uint8_t *beq = (uint8_t *)(img.data() + P.off_beq);
+    uint32_t *unmap = img.data() + P.off_unmap;
+    for (uint32_t x = 0; x < 256; x++) unmap[x] = x;
+    for (uint32_t p = m; p-- > 0;) bst[batch[order[p]]] = p;  // first position of each batch
+    bst[nb] = (uint32_t)m;
+    for (uint32_t p = 0; p < m; p++) {
+        const uint32_t r = order[p], b = batch[r];
+        unmap[256 + p] = 256 + r;
+        if (!valid_at(r)) continue;  // (never matches: not in the tables)
+        const uint32_t u = rid(pairs[2 * r]), v = rid(pairs[2 * r + 1]);
+        uint32_t *first;
+        if (u < 256 && v < 256) {
+            first = &bp[(u << 8) | v];
+        } else {
+            const uint32_t k = ((u << 16) | v) + 1u, s = slot(k);
+            hkey[s] = k;
+            first = &hval[s];
+        }
+        if (*first == ~0u) *first = p | (b << 16);
+        roles[(size_t)u * 16 + (b >> 5)] |= 1u << (b & 31);
+        roles[(size_t)v * 16 + 8 + (b >> 5)] |= 1u << (b & 31);
+        if (u == v) beq[b] = 1;
+    }
     memcpy(img.data(), bp.data(), 65536 * 4);
     for (uint32_t k = 0; k < H; k++) {
         img[P.off_ht + 2 * k] = hkey[k];
         img[P.off_ht + 2 * k + 1] = hval[k];
-    }
-    uint32_t *roles = img.data() + P.off_roles;
-    uint32_t *bst = img.data() + P.off_bstart;
-    for (uint32_t r = m; r-- > 0;) bst[batch[r]] = r;  // first rank of each batch
-    bst[nb] = (uint32_t)m;
-    uint8_t *beq = (uint8_t *)(img.data() + P.off_beq);
-    for (uint32_t r = 0; r < m; r++) {
-        const uint32_t u = pairs[2 * r], v = pairs[2 * r + 1], z = 256 + r;
-        if (!(u < z && v < z)) continue;
-        const uint32_t b = batch[r];
-        roles[(size_t)u * 16 + (b >> 5)] |= 1u << (b & 31);
-        roles[(size_t)v * 16 + 8 + (b >> 5)] |= 1u << (b & 31);
-        if (u == v) beq[batch[r]] = 1;
     }
     P.ok = true;
     return P;
@@ -1854,7 +1934,8 @@ int ew_run(bpe_gpu_ctx *c, const EwPlan &P, const uint32_t *d_img, uint32_t halo
     if ((r = dscratch(c, 4, tb, &tmp))) return r;
     HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, 0ull, nwin + 1, rocprim::plus<unsigned long long>(), c->st));
     if (nwin)
-        k_ew_gather<<<(uint32_t)std::min<uint64_t>(nwin, 8192), 256, 0, c->st>>>(stage, cnt, off, nwin, core, ids);
+        k_ew_gather<<<(uint32_t)std::min<uint64_t>(nwin, 8192), 256, 0, c->st>>>(
+            stage, cnt, off, nwin, core, P.relabeled ? d_img + P.off_unmap : nullptr, ids);
     HIPCHK(hipGetLastError());
     if (prof) {
         unsigned long long h[8 + 512];
