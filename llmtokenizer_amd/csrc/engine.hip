@@ -314,6 +314,9 @@ struct bpe_gpu_ctx {
     uint8_t *stage[2] = {};
     hipEvent_t stage_ev[2] = {};
     size_t bytes_cap = 0;        // capacity of h.bytes (kept across loads of the same or smaller size)
+    uint32_t *d_skew = nullptr;  // k_pair_skew_sample's {largest pair count, pairs sampled} (device)
+    uint32_t skew[2] = {0, 0};   // ... on the host once skew_valid
+    bool skew_valid = false;
     uint32_t *d_pres = nullptr;  // [256] byte presence gathered while bpe_gpu_load_fd streamed the corpus
     bool pres_valid = false;     // d_pres describes the bytes loaded now
 };
@@ -1481,9 +1484,13 @@ int compact_ids(bpe_gpu_ctx *c) {
 }
 
 // init phase 1: the set of byte values present (tok[] is written by k_sort_a)
+// (+ the skew probe of the count pass into words 256-257 of the same buffer)
 int init_presence(bpe_gpu_ctx *c, uint32_t **d_bh) {
     int r;
-    if ((r = dalloc(c, d_bh, 256))) return r;
+    if ((r = dalloc(c, d_bh, 256 + 2))) return r;
+    c->d_skew = *d_bh + 256;
+    c->skew_valid = false;
+    if (c->n0 >= 2) k_pair_skew_sample<<<1, 1024, 0, c->st>>>(c->h.bytes, c->n0, c->d_skew);
     if (c->pres_valid) {  // gathered chunk by chunk while the corpus streamed in (bpe_gpu_load_fd)
         HIPCHK(hipMemcpyAsync(*d_bh, c->d_pres, 1024, hipMemcpyDeviceToDevice, c->st));
         return 0;
@@ -1502,6 +1509,75 @@ void launch_hist_span(bpe_gpu_ctx *c, size_t lds, uint32_t ntl, uint32_t *d_hist
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_hist_span<R>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     k_pair_hist_span<R><<<ntl, 1024, lds, c->st>>>(c->dE, d_hist, tile, lo, S);
+}
+
+template <uint32_t R, bool SKEW>
+void launch_hist_v(bpe_gpu_ctx *c, size_t lds, uint32_t ntl, uint32_t *d_hist, uint64_t tile, uint32_t lo,
+                   uint32_t S) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_pair_hist_v<R, SKEW>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    k_pair_hist_v<R, SKEW><<<ntl, 1024, lds, c->st>>>(c->dE, d_hist, tile, lo, S);
+}
+
+template <uint32_t R>
+void launch_hist_pk(bpe_gpu_ctx *c, size_t lds, uint32_t ntl, uint32_t *d_hist, uint64_t tile, uint32_t lo,
+                    uint32_t S);
+
+// The count pass's form (stats count_pass_span): 200 + R the vector form
+// (k_pair_hist_v, R histogram copies), 300 + R its run-folding variant for
+// skewed input; R the shuffle form (k_pair_hist_span); 100 + R its packed
+// 16-bit variant (k_pair_hist_pk).  Skewed = a byte pair holds more than 1/16
+// of the sampled pairs (k_pair_skew_sample): one value repeated, two
+// alternating, a dominant space; same-address adds would serialise.
+uint32_t launch_count_pass(bpe_gpu_ctx *c, uint32_t ntl, uint32_t *d_hist, uint64_t tile, uint32_t lo, uint32_t S) {
+    int r;
+    if (!c->skew_valid && c->d_skew) {
+        if ((r = hipMemcpyAsync(c->skew, c->d_skew, 8, hipMemcpyDeviceToHost, c->st)) == hipSuccess)
+            r = hipStreamSynchronize(c->st);
+        if (r != hipSuccess) c->skew[0] = c->skew[1] = 0;
+        c->skew_valid = true;
+    }
+    bool skew = c->skew[1] > 0 && (uint64_t)c->skew[0] * 16 > c->skew[1];
+    if (const char *t = getenv("BPE_HIST_SKEW")) skew = atoi(t) != 0;  // tuning / tests
+    const char *form = getenv("BPE_HIST_FORM");                       // tuning: v (default), span, pk
+    const size_t SS = (size_t)S * S;
+    uint32_t R = 2;
+    if (const char *t = getenv("BPE_HIST_R")) R = (uint32_t)std::max(1, atoi(t));
+    if (!form || !strcmp(form, "v")) {
+        // 4 copies take one 1024-thread block per CU, 2 copies two, 1 copy more
+        R = R >= 4 ? 4 : R >= 2 ? 2 : 1;
+        while (R > 1 && ((size_t)R * SS + 256) * 4 > (R == 4 ? 160 * 1024 : HIST_LDS_MAX)) R >>= 1;
+        const size_t lds = ((size_t)R * SS + 256) * 4;
+        if (skew) {
+            if (R == 4) launch_hist_v<4, true>(c, lds, ntl, d_hist, tile, lo, S);
+            else if (R == 2) launch_hist_v<2, true>(c, lds, ntl, d_hist, tile, lo, S);
+            else launch_hist_v<1, true>(c, lds, ntl, d_hist, tile, lo, S);
+            return 300 + R;
+        }
+        if (R == 4) launch_hist_v<4, false>(c, lds, ntl, d_hist, tile, lo, S);
+        else if (R == 2) launch_hist_v<2, false>(c, lds, ntl, d_hist, tile, lo, S);
+        else launch_hist_v<1, false>(c, lds, ntl, d_hist, tile, lo, S);
+        return 200 + R;
+    }
+    const size_t W = (SS + 1) / 2;
+    if (!strcmp(form, "pk")) {
+        if (R >= 8 && (8 * W + 256) * 4 <= 160 * 1024) {
+            launch_hist_pk<8>(c, (8 * W + 256) * 4, ntl, d_hist, tile, lo, S);
+            return 108;
+        }
+        if ((4 * W + 256) * 4 <= HIST_LDS_MAX) {
+            launch_hist_pk<4>(c, (4 * W + 256) * 4, ntl, d_hist, tile, lo, S);
+            return 104;
+        }
+    }
+    // the shuffle form: copies while two blocks still fit a CU (measured, 1 GiB:
+    // 1 copy 0.380 ms, 2 copies 0.368, 4 copies (one block per CU) 0.418)
+    R = std::min<uint32_t>(R, 2);
+    while (R > 1 && ((size_t)R * SS + 256) * 4 > HIST_LDS_MAX) R >>= 1;
+    const size_t lds = ((size_t)R * SS + 256) * 4;
+    if (R >= 2) launch_hist_span<2>(c, lds, ntl, d_hist, tile, lo, S);
+    else launch_hist_span<1>(c, lds, ntl, d_hist, tile, lo, S);
+    return R;
 }
 
 template <uint32_t R>
@@ -1555,29 +1631,7 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
         HIPCHK(hipEventRecord(e0, c->st));
-        if (span) {
-            // copies of the LDS histogram: 2 while two blocks still fit a CU (measured,
-            // 1 GiB: 1 copy 0.380 ms, 2 copies 0.368, 4 copies (one block per CU) 0.418)
-            uint32_t R = 2;
-            while (R > 1 && ((size_t)R * S * S + 256) * 4 > HIST_LDS_MAX) R >>= 1;
-            // packed 16-bit copies (k_pair_hist_pk): R = 4 or 8
-            uint32_t PK = 0;
-            if (const char *t = getenv("BPE_HIST_PK")) PK = (uint32_t)atoi(t);  // tuning
-            if (const char *t = getenv("BPE_HIST_R")) R = std::min<uint32_t>(R, (uint32_t)atoi(t));  // tuning
-            const size_t W = ((size_t)S * S + 1) / 2;
-            if (PK == 8 && (8 * W + 256) * 4 <= 160 * 1024) {
-                launch_hist_pk<8>(c, (8 * W + 256) * 4, ntl, d_hist, tile, lo, S);
-                c->stats.count_pass_span = 108;
-            } else if (PK == 4 && (4 * W + 256) * 4 <= HIST_LDS_MAX) {
-                launch_hist_pk<4>(c, (4 * W + 256) * 4, ntl, d_hist, tile, lo, S);
-                c->stats.count_pass_span = 104;
-            } else {
-                const size_t lds = ((size_t)R * S * S + 256) * 4;
-                if (R >= 2) launch_hist_span<2>(c, lds, ntl, d_hist, tile, lo, S);
-                else launch_hist_span<1>(c, lds, ntl, d_hist, tile, lo, S);
-                c->stats.count_pass_span = R;
-            }
-        }
+        if (span) c->stats.count_pass_span = launch_count_pass(c, ntl, d_hist, tile, lo, S);
         else k_pair_hist<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
         HIPCHK(hipEventRecord(e1, c->st));
         HIPCHK(hipEventSynchronize(e1));
@@ -1622,9 +1676,13 @@ int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_
     uint32_t *d_bh;
     int r;
     if ((r = init_presence(c, &d_bh))) return r;
-    std::vector<uint32_t> bh(256);
-    HIPCHK(hipMemcpyAsync(bh.data(), d_bh, 1024, hipMemcpyDeviceToHost, c->st));
+    std::vector<uint32_t> bh(256 + 2);
+    HIPCHK(hipMemcpyAsync(bh.data(), d_bh, bh.size() * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    c->skew[0] = bh[256];
+    c->skew[1] = bh[257];
+    c->skew_valid = true;
+    bh.resize(256);
     return init_sort(c, bh, unrank_out, d_tot_out);
 }
 

@@ -2204,6 +2204,164 @@ __global__ __launch_bounds__(1024) void k_pair_hist_span(const Eng *__restrict__
 template __global__ void k_pair_hist_span<1>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
 template __global__ void k_pair_hist_span<2>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
 
+// Vector form of the span count pass (round 4, the default): each lane takes
+// 16 consecutive bytes as one uint4 plus the dword after them (its byte 0 ends
+// the lane's 16th pair) -- a second load instead of a cross-lane shuffle, so no
+// LDS permute sits between the bin adds and nothing in the loop waits on the
+// LDS queue (the shuffle form drained it every 4 pairs: lgkmcnt(0) before each
+// permute's result), and the 16 adds of a lane issue back to back, branch-free
+// on every full 1-KB block.  Bins as in k_pair_hist_span: R interleaved copies,
+// lane class rl = lane mod R.
+// SKEW: a lane first folds runs of equal bins in a two-entry cache (evicting
+// the entry with the smaller count), so one value repeated, two alternating, or
+// a dominant pair cost one add per run instead of one per pair; the host picks
+// it when a sample of the corpus has a dominant pair (k_pair_skew_sample).
+// byte address of pair k's bin: b_k * (S R 4) + (b_{k+1} * R 4 + base4)
+// -- one 24-bit multiply-add per pair on a per-byte term (v_mad_u32_u24; a
+// full 32-bit multiply is a quarter-rate instruction)
+template <uint32_t R, bool SKEW>
+__device__ __forceinline__ void hv_lane16(uint32_t *h, const uint32_t x[4], uint32_t nx, uint32_t SR4, uint32_t base4) {
+    uint32_t b[17], q[17];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        b[4 * j] = x[j] & 0xFF;
+        b[4 * j + 1] = (x[j] >> 8) & 0xFF;
+        b[4 * j + 2] = (x[j] >> 16) & 0xFF;
+        b[4 * j + 3] = x[j] >> 24;
+    }
+    b[16] = nx & 0xFF;
+#pragma unroll
+    for (uint32_t j = 1; j < 17; j++) q[j] = b[j] * (R * 4) + base4;
+    char *hb = reinterpret_cast<char *>(h);
+    auto bin = [&](uint32_t k) { return __umul24(b[k], SR4) + q[k + 1]; };
+    auto add = [&](uint32_t off, uint32_t v) { atomicAdd(reinterpret_cast<uint32_t *>(hb + off), v); };
+    if (!SKEW) {
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) add(bin(k), 1u);
+    } else {
+        uint32_t c0 = bin(0), n0 = 1, c1 = ~0u, n1 = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < 16; k++) {
+            const uint32_t i = bin(k);
+            if (i == c0) {
+                n0++;
+            } else if (i == c1) {
+                n1++;
+            } else if (n1 <= n0) {
+                if (n1) add(c1, n1);
+                c1 = i;
+                n1 = 1;
+            } else {
+                add(c0, n0);
+                c0 = i;
+                n0 = 1;
+            }
+        }
+        add(c0, n0);
+        if (n1) add(c1, n1);
+    }
+}
+
+template <uint32_t R, bool SKEW>
+__global__ __launch_bounds__(1024) void k_pair_hist_v(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
+                                                      uint64_t tile, uint32_t lo, uint32_t S) {
+    extern __shared__ uint32_t hdyn[];
+    const uint32_t A = E->A, AA = A * A, SS = S * S;
+    uint32_t *h = hdyn, *ur = hdyn + R * SS;
+    const uint32_t tl = blockIdx.x, T = blockDim.x, lane = threadIdx.x & 63;
+    for (uint32_t i = threadIdx.x; i < R * SS; i += T) h[i] = 0;
+    for (uint32_t x = threadIdx.x; x < 256; x += T) {
+        const uint32_t r = E->rank[x];
+        if (r != HOLE) ur[r] = x;
+    }
+    __syncthreads();
+    const uint64_t n0 = E->n0;
+    const uint64_t s = (uint64_t)tl * tile, e = min(n0 - 1, s + tile);  // pair positions [s, e), tile % 1024 == 0
+    const uint4 *src4 = reinterpret_cast<const uint4 *>(E->bytes);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(E->bytes);
+    const uint8_t *bytes = E->bytes;
+    // word index of pair (x, y): x * S * R + y * R + (lane class - (lo * S + lo) * R)   (mod 2^32)
+    const uint32_t SR = S * R, base = (lane & (R - 1)) - (lo * S + lo) * R, SR4 = SR * 4, base4 = base * 4;
+    const uint64_t nw = T / 64, kb0 = s / 1024, kfull = e / 1024, kb1 = (e + 1023) / 1024;
+    // full blocks [kb0, kfull): every pair position < e, the dword after a
+    // lane's 16 bytes ends at most 3 bytes past e <= n0 - 1 (64 bytes of padding)
+    for (uint64_t kb = kb0 + (threadIdx.x >> 6); kb < kfull; kb += 2 * nw) {  // wave-uniform
+        const uint64_t kc = kb + nw;
+        const bool two = kc < kfull;
+        const uint4 qa = src4[kb * 64 + lane];
+        const uint32_t na = src[kb * 256 + 4 * lane + 4];
+        uint4 qb = make_uint4(0, 0, 0, 0);
+        uint32_t nb = 0;
+        if (two) {
+            qb = src4[kc * 64 + lane];
+            nb = src[kc * 256 + 4 * lane + 4];
+        }
+        const uint32_t xa[4] = {qa.x, qa.y, qa.z, qa.w};
+        hv_lane16<R, SKEW>(h, xa, na, SR4, base4);
+        if (two) {
+            const uint32_t xb[4] = {qb.x, qb.y, qb.z, qb.w};
+            hv_lane16<R, SKEW>(h, xb, nb, SR4, base4);
+        }
+    }
+    // the partial last block (last tile only): byte by byte
+    if (kfull < kb1 && (threadIdx.x >> 6) == (kfull - kb0) % nw) {
+        for (uint32_t k = 0; k < 16; k++) {
+            const uint64_t p = kfull * 1024 + 16 * lane + k;
+            if (p < e) atomicAdd(&h[(uint32_t)bytes[p] * SR + (uint32_t)bytes[p + 1] * R + base], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < AA; k += T) {
+        const uint32_t x = ur[k / A] - lo, y = ur[k % A] - lo;
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < R; r++) v += h[(x * S + y) * R + r];
+        hist[(uint64_t)tl * AA + k] = v;
+    }
+}
+template __global__ void k_pair_hist_v<1, false>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
+template __global__ void k_pair_hist_v<2, false>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
+template __global__ void k_pair_hist_v<4, false>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
+template __global__ void k_pair_hist_v<1, true>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
+template __global__ void k_pair_hist_v<2, true>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
+template __global__ void k_pair_hist_v<4, true>(const Eng *, uint32_t *, uint64_t, uint32_t, uint32_t);
+
+// Skew probe of the corpus (one block, before the count pass): the byte pairs
+// inside SKEW_SAMPLES dwords spread evenly over it, counted in 16-bit LDS bins
+// (two to a word); out[0] = the largest count, out[1] = pairs sampled.
+constexpr uint32_t SKEW_SAMPLES = 16384;
+__global__ __launch_bounds__(1024) void k_pair_skew_sample(const uint8_t *__restrict__ bytes, uint64_t n0,
+                                                           uint32_t *__restrict__ out) {
+    __shared__ uint32_t h[32768];
+    __shared__ uint32_t smax, stot;
+    for (uint32_t i = threadIdx.x; i < 32768; i += blockDim.x) h[i] = 0;
+    if (threadIdx.x == 0) smax = stot = 0;
+    __syncthreads();
+    const uint64_t nwords = n0 / 4;  // whole dwords only
+    const uint32_t ns = (uint32_t)min<uint64_t>(SKEW_SAMPLES, nwords);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(bytes);
+    uint32_t mine = 0;
+    for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x) {
+        const uint32_t w = src[(uint64_t)j * nwords / ns];
+#pragma unroll
+        for (uint32_t k = 0; k < 3; k++) {
+            const uint32_t key = (w >> (8 * k)) & 0xFFFF;
+            atomicAdd(&h[key >> 1], 1u << ((key & 1) << 4));
+        }
+        mine += 3;
+    }
+    atomicAdd(&stot, mine);
+    __syncthreads();
+    uint32_t m = 0;
+    for (uint32_t i = threadIdx.x; i < 32768; i += blockDim.x) m = max(m, max(h[i] & 0xFFFF, h[i] >> 16));
+    atomicMax(&smax, m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[0] = smax;
+        out[1] = stot;
+    }
+}
+
 // Packed form of k_pair_hist_span: 16-bit bins, two to a word, so R = 4 or 8
 // interleaved copies fit the LDS (lane class rl = lane mod R adds
 // 1 << 16 * (bin & 1) to word (bin >> 1) * R + rl: the 32 lanes of a bank

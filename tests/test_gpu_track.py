@@ -112,5 +112,7 @@ def test_light_pass_wait_timeout_falls_back_to_exact_pass(monkeypatch):
     m1, i1, s1 = _train(data, 1024, 1, monkeypatch)
     assert (m1 == m0).all() and (i1 == i0).all()
     assert s1["track_violations"] == 0
-    # every light pass that timed out ran as an exact pass instead
-    assert s1["track_light"] + s1["track_exact"] >= s0["track_light"] + s0["track_exact"], (s0, s1)
+    # the light passes that timed out ran as exact passes instead (an exact
+    # pass resets the bounds, so there are fewer of them than light ones)
+    assert s0["track_light"] > 0 and s1["track_light"] < s0["track_light"], (s0, s1)
+    assert s1["track_exact"] > s0["track_exact"], (s0, s1)

@@ -11,7 +11,7 @@ cp /tmp/bpe_m32k.npy $OUT/m32k.npy
 for rep in 1 2; do
     for lay in 1 0; do
         echo "layer=$lay rep $rep" >> $LOG
-        BPE_EW_LAYER=$lay timeout -k 10 120 python3 tools/enc_prof.py enc >> $LOG 2>&1 || exit 1
+        ENC_REPS=3 BPE_EW_LAYER=$lay timeout -k 10 120 python3 tools/enc_prof.py enc >> $LOG 2>&1 || exit 1
     done
 done
 echo done >> $LOG

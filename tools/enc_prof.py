@@ -30,11 +30,14 @@ def main():
     for q in range(k):
         a = q * step
         g.synth(q, 3, (total if q == k - 1 else a + step) - a, a)
-    g.encode(m)
-    st = g.stats()
-    d = {x: st[x] for x in ("ms_total", "ms_init", "ms_train", "iterations", "candidates", "occurrences", "enc_path")}
-    d["ids_checksum"] = "%016x" % g.ids_checksum()[0]
-    print(d)
+    for rep in range(int(os.environ.get("ENC_REPS", "1"))):  # (the first pays the allocations)
+        g.encode(m)
+        st = g.stats()
+        d = {x: st[x] for x in ("ms_total", "ms_init", "ms_train", "iterations", "candidates", "occurrences",
+                                "enc_path")}
+        d["ids_checksum"] = "%016x" % g.ids_checksum()[0]
+        d["rep"] = rep
+        print(d, flush=True)
 
 
 if __name__ == "__main__":
