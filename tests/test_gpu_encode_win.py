@@ -147,3 +147,35 @@ def test_goldens_through_window_path():
         assert ids.size == fx["ids_len"] and G.ids_md5(ids) == fx["ids_md5"], fx["name"]
         n += st["enc_path"] == 1
     assert n > 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_layered_plan_equals_greedy_cut(seed, monkeypatch):
+    """ew_plan layers the merge list by its conflict chains and replays it in
+    layer order with relabeled ids (BPE_EW_LAYER=1, default); the contiguous
+    greedy cut (=0) keeps the list's order.  Same ids as each other and as the
+    oracle's sequential passes, and never more batches."""
+    rng = random.Random(seed)
+    text = synth_bytes(40 + seed, 200_000)
+    tr = api.Engine(0)
+    tr.load(text)
+    tr.train(1500)
+    trained = tr.merges()
+    tr.close()
+    alpha = bytes(range(97, 101))
+    small = bytes(rng.choice(alpha) for _ in range(60_000))
+    lists = [(text, trained), (small, _random_merges(rng, sorted(set(alpha)), 900, eq=0.2))]
+    # plus records the plan skips: a forward reference and a repeated pair
+    m = lists[1][1].copy()
+    m[5] = [256 + len(m) - 1, m[0][1]]
+    lists.append((small, np.vstack([m, m[:3]])))
+    for data, merges in lists:
+        want = O.encode(data, merges)
+        got = {}
+        for lay in ("1", "0"):
+            monkeypatch.setenv("BPE_EW_LAYER", lay)
+            ids, st = _encode(data, merges)
+            assert st["enc_path"] in (1, 3)
+            assert (ids == want).all(), lay
+            got[lay] = st["iterations"]
+        assert got["1"] <= got["0"], got
