@@ -1659,8 +1659,12 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
         // until the first merge)
         if (tile > (1ull << SORT_LOCAL_BITS)) return fail(BPE_GPU_EINTERNAL, "sort tile exceeds 2^24 positions");
         uint32_t *d_tmp = h.occ;
-        k_sort_a<<<ntl, SORT_T, 0, c->st>>>(c->dE, d_hist, tile, d_tmp);
-        k_sort_b<<<1024 * (1024 / SORT_T), SORT_T, 0, c->st>>>(c->dE, d_hist, d_tot, ntl, tile, d_tmp);
+        // pass B sorts groups of G tiles as one unit (entries hold positions
+        // relative to the group: G * tile <= 2^24); BPE_SORT_G caps G (tuning)
+        uint32_t G = (uint32_t)std::max<uint64_t>(1, (1ull << SORT_LOCAL_BITS) / tile);
+        G = std::min<uint32_t>(G, (uint32_t)std::max(1, getenv_int("BPE_SORT_G", 16)));
+        k_sort_a<<<ntl, SORT_T, 0, c->st>>>(c->dE, d_hist, tile, G, d_tmp);
+        k_sort_b<<<1024 * (1024 / SORT_T), SORT_T, 0, c->st>>>(c->dE, d_hist, d_tot, ntl, tile, G, d_tmp);
         HIPCHK(hipGetLastError());
     } else {
         HIPCHK(hipMemsetAsync(h.poff, 0, 4ull * (AA + 1), c->st));
