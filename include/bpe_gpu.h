@@ -69,8 +69,9 @@ typedef struct {
     uint64_t l1_rescanned;    /* level-1 summary blocks rescanned                 */
     uint64_t spec_hits;       /* next merges found by the speculative scan        */
     uint64_t spec_misses;     /* mispredicted next merges (host re-scan)          */
-    uint64_t count_pass_span; /* >0: the count pass ran in span form (k_pair_hist_span), value = LDS histogram copies
-                                 (100 + copies: the packed 16-bit form k_pair_hist_pk, BPE_HIST_PK) */
+    uint64_t count_pass_span; /* >0: the count pass ran in span form, its histogram copies R and kernel:
+                                 200 + R k_pair_hist_v (default), 300 + R its run-folding variant for
+                                 skewed corpora, R k_pair_hist_span, 100 + R k_pair_hist_pk (BPE_HIST_FORM) */
     uint64_t hot_rebuilds;    /* hot-set argmax: full-table rebuilds of the listed keys */
     uint64_t hot_mode;        /* 0 level summaries, 1 hot set, 2 hot set given up mid-run */
     uint64_t hot_scanned;     /* hot-set entries reduced, summed over the merges */
@@ -91,6 +92,11 @@ typedef struct {
                                  contradicts (must stay 0)                         */
     uint64_t track_light;     /* tracked iterations: on-device exact counts of only the
                                  threads whose bound reached a growth threshold   */
+    uint64_t batch_end[8];    /* training, batches: what ended each batch's formation --
+                                 [0] the list (64 keys, 63 members) [1] merge cap / count <= 1 /
+                                 hot threshold [2] unused [3] a key listed twice [4] a tie whose
+                                 order the batch could change [5] a member that does not commute
+                                 with an earlier one [6] pair-table margin [7] occurrence staging */
 } bpe_gpu_stats;
 
 /* Per-merge record (training): the structured per-iteration metrics the

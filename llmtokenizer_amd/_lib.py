@@ -49,7 +49,9 @@ class GpuStats(ctypes.Structure):
                                                      "enc_path", "enc_windows", "relists", "batches",
                                                      "batch_dropped", "batch_retries", "table_updates")] + \
         [(n, ctypes.c_double) for n in ("ms_scan_span", "ms_apply_span")] + \
-        [(n, ctypes.c_uint64) for n in ("track_exact", "track_skipped", "track_violations", "track_light")]
+        [(n, ctypes.c_uint64) for n in ("track_exact", "track_skipped", "track_violations", "track_light")] + \
+        [(n, ctypes.c_uint64) for n in ("end_list", "end_count", "end_unused", "end_dup", "end_tie", "end_conflict",
+                                         "end_table", "end_staging")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1437,6 +1437,7 @@ int batch_stats(bpe_gpu_ctx *c) {
     c->stats.batch_dropped = hb.ndrop;
     c->stats.batch_retries = hb.nretry;
     c->stats.table_updates = hb.nupd;
+    for (int k = 0; k < 8; k++) c->stats.batch_end[k] = hb.why[k];
     if (hb.nspan) {
         int khz = 0;
         (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);

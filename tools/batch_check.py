@@ -30,4 +30,5 @@ print(json.dumps({"batch": os.environ.get("BPE_BATCH", "1"), "merges": int(st["m
                   "us_per_merge": round(st["ms_train"] * 1e3 / max(1, st["merges"]), 2),
                   "batches": int(st["batches"]), "dropped": int(st["batch_dropped"]),
                   "candidates": int(st["candidates"]), "occurrences": int(st["occurrences"]),
-                  "hot_rebuilds": int(st["hot_rebuilds"]), "n_out": int(st["n_out"])}))
+                  "hot_rebuilds": int(st["hot_rebuilds"]), "n_out": int(st["n_out"]), "relists": int(st["relists"]),
+                  "end": {k[4:]: int(st[k]) for k in st if k.startswith("end_") and k != "end_unused"}}))
