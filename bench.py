@@ -59,6 +59,13 @@ GIB = 1 << 30
 PROFILE_TAG = "r3"     # profiles/<tag>_train_kernel_stats.csv, <tag>_pmc_traffic.json (tools/gpu_profile.sh)
 
 
+def count_pass_kernel(form):
+    """the count pass's kernel from bpe_gpu_stats.count_pass_span"""
+    if not form:
+        return "k_pair_hist"
+    return {2: "k_pair_hist_v", 3: "k_pair_hist_v<skew>", 1: "k_pair_hist_pk", 0: "k_pair_hist_span"}[form // 100]
+
+
 def cpu_baseline(seed, size, merges):
     """Reference trainer on a bounded sample (first `size` bytes of the same
     corpus).  Falls back to the oracle port (1 thread) if _ref is absent."""
@@ -529,10 +536,11 @@ def main():
                      "note": ("batch scan: one random token-window gather per candidate (8 B algorithmic, a "
                               "128-B line moved), bound by the random-line rate" if name == "k_bscan" else
                               "per-merge kernel: dependent random gathers, latency-bound")},
-        "roofline_count_pass": {"kernel": "k_pair_hist_span" if st["count_pass_span"] else "k_pair_hist",
+        "roofline_count_pass": {"kernel": count_pass_kernel(st["count_pass_span"]),
                                 "bound": "hbm", "achieved": round(cp_achieved, 1), "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": round(cp_achieved / HBM_PEAK_GBS, 4),
                                 "bytes_per_launch": cp_bytes, "avg_ms": round(cp_ms, 4),
+                                "form": int(st["count_pass_span"]),
                                 "note": "histogram of byte-pair rank keys: 1 B/token read, bins in LDS "
                                         "(SURVEY 8(d)); the initial ids are written by k_sort_a"},
         "breakdown_ms": {"init": round(st["ms_init"], 3), "loop": round(st["ms_train"], 3),
@@ -541,7 +549,8 @@ def main():
                                           "rule_ties", "table_grows", "keys", "candidates", "occurrences",
                                           "hot_rebuilds", "hot_mode", "hot_scanned", "relists", "batches",
                                           "batch_dropped", "batch_retries", "table_updates", "spec_hits",
-                                          "spec_misses")},
+                                          "spec_misses", "select_launches")},
+        "batch_end": {k2[4:]: st[k2] for k2 in st if k2.startswith("end_") and k2 != "end_unused"},
     })
     out.update(extra)
     cp = committed_profile(name, sharded)
@@ -562,6 +571,20 @@ def main():
                                  "bytes_per_launch": round(ab), "avg_ms": round(st["ms_apply_span"], 5), "launches": nl,
                                  "avg_ms_rocprof": ap.get("avg_ms_rocprof"), "rocprof_summary": ap.get("rocprof_summary"),
                                  "note": "16 B per pair-table update (random key probe + count); random-line bound"}
+    # the batch select k_bsel: the hot set reduced (16 B per listed key: slot,
+    # count, key) beside the previous batch's token rewrite (12 B per
+    # occurrence: the id, the end code, the pool entry)
+    if st["select_launches"] and st["ms_select_span"] > 0:
+        sb = (16.0 * st["hot_scanned"] + 12.0 * st["occurrences"]) / st["select_launches"]
+        sa = sb / (st["ms_select_span"] * 1e-3) / 1e9
+        sp = committed_profile("k_bsel", sharded)
+        out["roofline_select"] = {"kernel": "k_bsel", "bound": "hbm", "achieved": round(sa, 1), "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": round(sa / HBM_PEAK_GBS, 4), "traffic": sp.get("traffic"),
+                                  "bytes_per_launch": round(sb), "avg_ms": round(st["ms_select_span"], 5),
+                                  "launches": st["select_launches"], "avg_ms_rocprof": sp.get("avg_ms_rocprof"),
+                                  "rocprof_summary": sp.get("rocprof_summary"),
+                                  "note": "hot-set reduce (16 B/key) + the previous batch's rewrite (12 B per "
+                                          "occurrence, one dirtied sector each); device wall clock per launch"}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.cpu_size, args.cpu_merges)
     if enc is not None:

@@ -97,6 +97,9 @@ typedef struct {
                                  hot threshold [2] unused [3] a key listed twice [4] a tie whose
                                  order the batch could change [5] a member that does not commute
                                  with an earlier one [6] pair-table margin [7] occurrence staging */
+    double ms_select_span;    /* training, batches: average k_bsel span (the selection beside the
+                                 previous batch's token rewrite; device wall clock) */
+    uint64_t select_launches; /* ... over this many k_bsel launches */
 } bpe_gpu_stats;
 
 /* Per-merge record (training): the structured per-iteration metrics the

@@ -563,13 +563,24 @@ __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat 
     if (sh) edge_record_block(E, C);
 }
 
+__device__ inline void sel_exit_stamp(Bat *B) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(&B->sl_out, wall_clock64());
+}
+
 __global__ __launch_bounds__(1024) void k_bsel(const Eng *__restrict__ E, Ctl *__restrict__ C) {
     Bat *B = E->bat;
+    if (threadIdx.x == 0) atomicMax(&B->sl_in, ~wall_clock64());
     if (blockIdx.x >= BRB) {  // (whether or not this selection stops)
         bat_rewrite(E, C, B);
+        sel_exit_stamp(B);
         return;
     }
-    if (C->stop) return;
+    if (C->stop) {
+        sel_exit_stamp(B);
+        return;
+    }
     const uint32_t bi = bat_idx(E);
     ts_mark(E, bi, BT_SEL_IN, true);
     const uint64_t Bsz = summary_B(C->D + B->dD);  // D after the batch applied last
@@ -594,8 +605,8 @@ __global__ __launch_bounds__(1024) void k_bsel(const Eng *__restrict__ E, Ctl *_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (!last) return;
-    bselect_block(E, C, B, n, bi);
+    if (last) bselect_block(E, C, B, n, bi);
+    sel_exit_stamp(B);
 }
 
 // ----------------------------------------------------------------- k_bscan
@@ -1138,8 +1149,13 @@ __device__ inline uint64_t hinsert_c(const Eng *E, uint32_t u, uint32_t v, uint3
 // blocks do the rest beside the selection).
 template <bool SH>
 __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl *__restrict__ C, uint32_t roleB_blocks) {
-    if (C->stop) return;
     Bat *B = E->bat;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && B->sl_out) {  // the k_bsel launched before this batch's scan
+        B->sl_ticks += B->sl_out - ~B->sl_in;
+        B->nsl++;
+        B->sl_in = B->sl_out = 0;
+    }
+    if (C->stop) return;
     const uint32_t bi = bat_idx(E);
     ts_mark(E, bi, BT_APPLY_IN, true);
     if (threadIdx.x == 0) atomicMax(&B->ap_in, ~wall_clock64());

@@ -1438,6 +1438,14 @@ int batch_stats(bpe_gpu_ctx *c) {
     c->stats.batch_retries = hb.nretry;
     c->stats.table_updates = hb.nupd;
     for (int k = 0; k < 8; k++) c->stats.batch_end[k] = hb.why[k];
+    {
+        unsigned long long t[2] = {0, 0};  // (sl_ticks, nsl: outside the head copied above)
+        HIPCHK(hipMemcpy(t, &c->h.bat->sl_ticks, 16, hipMemcpyDeviceToHost));
+        int khz = 0;
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
+        c->stats.select_launches = t[1];
+        if (khz > 0 && t[1]) c->stats.ms_select_span = (double)t[0] / t[1] / khz;
+    }
     if (hb.nspan) {
         int khz = 0;
         (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);

@@ -150,6 +150,10 @@ struct Bat {
     uint32_t ra_xl, ra_xlb;           // sharded: my first token, retired (its b's length), or HOLE
     uint32_t ra_lo[BK];               // occurrences k_bapply's role-A blocks rewrote already (the first ones)
     uint32_t ra_split, pad6;          // k_bapply's share of the rewrite, in 1/256 (BPE_RA_SPLIT)
+    // k_bsel's device wall-clock span (first block entry, complemented; last
+    // block exit), folded by the next k_bapply (outside the select's staged
+    // head, which it writes back whole); launches folded
+    unsigned long long sl_in, sl_out, sl_ticks, nsl;
 };
 
 // Sharded batches: the words one batch exchanges (summed over the shards):
