@@ -653,6 +653,20 @@ __device__ inline void vadd_b(uint32_t (*s)[DENSE], const Eng *E, uint32_t m, in
     if (v == V_DL || v == V_DR) atomicAdd(&gcnt[v], 1u);
 }
 
+// sharded: one add of member m, vector v, id x into the exchange (dense
+// below Wx, else my list of ids >= DENSE, which k_bpack packs)
+__device__ inline void xadd(const Eng *E, uint32_t *xo, uint32_t Wx, uint32_t m, int v, uint32_t x) {
+    if (x < Wx) {
+        atomicAdd(&xo[2 + v * Wx + x], 1u);
+        return;
+    }
+    const uint64_t base = ((uint64_t)m * 4 + v) * E->bvs;
+    if (atomicAdd(&E->bvec[base + (x - DENSE)], 1u) == 0) {
+        const uint32_t p = atomicAdd(&E->bvnl[m * 4 + v], 1u);
+        E->bvlist[base + p] = x;
+    }
+}
+
 // Sharded batches: the tokens just outside my shard (HL[m]: m-th token left
 // of my first token, HR[m]: right of my last one) and, per member, the a==b
 // run state at my edges (hlr: how many of its a precede my first token, myi:
@@ -1022,7 +1036,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     }
     __syncthreads();
     ts_mark(E, bi, BT_SCAN_CAND, false, true);
-    const uint32_t Wx = z0 + k;  // SH: ids per delta vector in the exchange
+    const uint32_t Wx = xbat_vw(z0 + k);  // SH: ids per dense delta vector in the exchange
     uint32_t *xm = SH ? E->xbat + BK + (uint64_t)m * xbat_member_words(Wx) : nullptr;
     if (SH && blockIdx.x == 0 && tid == 0) {
         // Shard edges (thread 0 of block 0, beside the other blocks' flushes).
@@ -1052,8 +1066,8 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                         lfin = z0 + cv;
                         bnd = 2;
                     } else {
-                        atomicAdd(&xo[2 + V_DL * Wx + p], 1u);
-                        atomicAdd(&xo[2 + V_IL * Wx + p], 1u);
+                        xadd(E, xo, Wx, mm, V_DL, p);
+                        xadd(E, xo, Wx, mm, V_IL, p);
                     }
                 }
                 const uint32_t q = H.HR[1];
@@ -1061,8 +1075,8 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 if (q != HOLE) {
                     const uint32_t st = starts_of<SH>(tok, rt, sb, sla, H, q, n + 1, n);
                     if (st < BK) rfin = z0 + st;
-                    atomicAdd(&xo[2 + V_DR * Wx + q], 1u);
-                    atomicAdd(&xo[2 + V_IR * Wx + rfin], 1u);
+                    xadd(E, xo, Wx, mm, V_DR, q);
+                    xadd(E, xo, Wx, mm, V_IR, rfin);
                 }
                 (void)zz;
                 const uint32_t g = atomicAdd(&B->R[mm], 1u);  // (its staging slice has one slot to spare)
@@ -1118,6 +1132,70 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
 template __global__ void k_bscan<false>(const Eng *, const Ctl *);
 template __global__ void k_bscan<true>(const Eng *, const Ctl *);
 
+// ----------------------------------------------------------------- k_bpack
+// Sharded batches with ids >= DENSE (after k_bscan, before the exchange): my
+// members' (id, delta) lists of those ids, which the scan kept in bvec /
+// bvlist, packed into xsp_out in member order as (member * 4 + vector) << 24 |
+// id, delta; bvec cleared as read (k_bsel clears bvnl).  Entries beyond
+// xsp_cap: the first member whose lists do not fit is flagged in xbat[] like a
+// staging overflow (summed over the shards), so every shard fails the batch
+// there and the select forms it again shorter.
+__global__ __launch_bounds__(256) void k_bpack(const Eng *__restrict__ E, const Ctl *__restrict__ C) {
+    if (C->stop) return;
+    const Bat *B = E->bat;
+    __shared__ uint32_t pre[BK * 4 + 1];
+    __shared__ uint32_t written;
+    const uint32_t k = B->k, tid = threadIdx.x, nmv = 4 * k;
+    if (tid < 64) {  // exclusive prefix of the list lengths, 4 (member, vector) lists per lane
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            c[j] = 4 * tid + j < nmv ? E->bvnl[4 * tid + j] : 0u;
+            sum += c[j];
+        }
+        uint32_t incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if ((int)tid >= o) incl += y;
+        }
+        uint32_t r = incl - sum;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+            if (4 * tid + j <= nmv) pre[4 * tid + j] = r;
+            r += c[j];
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const uint32_t cap = E->xsp_cap;
+        uint32_t mo = 0;
+        while (mo < k && pre[4 * (mo + 1)] <= cap) mo++;
+        written = pre[4 * mo];
+        if (blockIdx.x == 0) {
+            if (mo < k) atomicAdd(&E->xbat[mo], 1u);
+            E->xsp_out[0] = written;
+        }
+    }
+    __syncthreads();
+    const uint32_t total = pre[nmv], w = written;
+    for (uint32_t q = blockIdx.x * blockDim.x + tid; q < total; q += gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = nmv;  // the list holding entry q: pre[lo] <= q < pre[lo + 1]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (pre[mid] <= q) lo = mid;
+            else hi = mid;
+        }
+        const uint64_t base = (uint64_t)lo * E->bvs;
+        const uint32_t x = E->bvlist[base + (q - pre[lo])];
+        const uint32_t val = E->bvec[base + (x - DENSE)];
+        E->bvec[base + (x - DENSE)] = 0;
+        if (q < w) {
+            E->xsp_out[2 + 2 * (uint64_t)q] = (lo << 24) | x;
+            E->xsp_out[3 + 2 * (uint64_t)q] = val;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- k_bapply
 __device__ inline uint64_t hinsert_c(const Eng *E, uint32_t u, uint32_t v, uint32_t *nins) {
     const unsigned long long key = (((unsigned long long)u << 32) | v) + 1ull;
@@ -1162,6 +1240,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     __shared__ uint32_t sa[BK], sb[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], snl[BK * 4 + 1], sRg[BK];
     __shared__ uint32_t scut[BK], ablk[BK + 1];
     __shared__ uint32_t sk, sj, sz0;
+    __shared__ uint32_t ssp[P2P_MAXR_B + 1];  // SH: prefix of the shards' list lengths
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     // prologue, wave 0, lane q = member q: the verified prefix, prefix sums of
     // the occurrences and of the listed-id counts, role A's blocks per member
@@ -1172,6 +1251,15 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         const uint32_t ma = in ? B->a[lane] : 0, mb = in ? B->b[lane] : 0;
         const uint32_t R = in ? B->R[lane] : 0, cnt = in ? B->cnt[lane] : 0;
         uint32_t bnd = in && !SH ? B->bound[lane] : 0;
+        if (SH && lane == 0) {  // every shard's list of ids >= DENSE (gathered): prefix of their lengths
+            uint32_t acc = 0;
+            ssp[0] = 0;
+            for (uint32_t q = 0; q < E->nshards && E->xsp_in; q++) {
+                acc += E->xsp_in[(uint64_t)q * E->xsp_stride];
+                ssp[q + 1] = acc;
+            }
+            if (!E->xsp_in) ssp[1] = 0;
+        }
         unsigned long long ovm = 0;  // SH: members some shard could not stage
         uint32_t Rg = R;             // occurrences over all shards (the live-token count is global)
         if (SH) {
@@ -1329,10 +1417,11 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     }
     // role B
     const uint32_t nB = roleB_blocks, bidB = blockIdx.x;
-    const uint32_t Wd = SH ? z0 + k : min(DENSE, z0 + k);
+    const uint32_t Wd = min(DENSE, z0 + k);
     const uint32_t per = SH ? xbat_member_words(Wd) : 1 + 4 * Wd;
     const uint32_t dense_total = k * per;
-    const uint32_t total = dense_total + (SH ? 0u : snl[k * 4]);
+    const uint32_t nsh = SH ? (E->xsp_in ? E->nshards : 1u) : 0u;
+    const uint32_t total = dense_total + (SH ? ssp[nsh] : snl[k * 4]);
     const uint32_t hotT = C->hot_T;
     const bool hot = E->hot != 0;
     long long dD = 0;
@@ -1372,6 +1461,17 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                     if (c) *pr = 0;
                 }
             }
+        } else if (SH && t < total) {
+            // the shards' lists of ids >= DENSE: (member-vector << 24 | id, delta)
+            const uint32_t q = t - dense_total;
+            uint32_t sh = 0;
+            while (q >= ssp[sh + 1]) sh++;
+            const uint32_t *en = E->xsp_in + (uint64_t)sh * E->xsp_stride + 2 + 2 * (uint64_t)(q - ssp[sh]);
+            const uint32_t mv = en[0] >> 24;
+            m = mv / 4;
+            cat = mv % 4;
+            x = en[0] & 0xFFFFFFu;
+            val = en[1];
         } else if (t < total) {
             const uint32_t q = t - dense_total;
             uint32_t mv = 0;

@@ -403,6 +403,17 @@ int push_ctl(bpe_gpu_ctx *c) {
 
 int getenv_int(const char *k, int dflt);
 
+// sharded batches with ids >= DENSE: (id, delta) entries a shard may send per
+// batch (BPE_XSP_CAP: tests force the overflow path with it) and the words of
+// one shard's packed list ([n, -, 2 cap], a multiple of 4)
+// (at least one member's worth: 4 vectors of the vcap - DENSE ids, so that the
+// batch's first member, which the verification never drops, always fits)
+void xsp_layout(uint64_t vcap, uint32_t *cap, uint32_t *stride) {
+    const uint64_t one = vcap > DENSE ? 4 * (vcap - DENSE) : 1;
+    *cap = (uint32_t)std::max<uint64_t>(one, (uint64_t)std::min(1 << 22, std::max(1, getenv_int("BPE_XSP_CAP", 1 << 20))));
+    *stride = (2 + 2 * *cap + 3) / 4 * 4;
+}
+
 // allocate the per-run structures (sizes depend on the merge cap)
 int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     free_train(c);
@@ -501,8 +512,11 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     }
     // batched training (batch.hip): the hot set's one-shard runs
     // (BPE_BATCH=0: one merge per kernel pair, the speculative graph; read per run)
-    h.batch = getenv_int("BPE_BATCH", 1) && h.hot && h.vcap <= BATCH_VCAP_MAX && (!c->sharded || h.vcap <= DENSE) ? 1 : 0;
+    h.batch = getenv_int("BPE_BATCH", 1) && h.hot && h.vcap <= BATCH_VCAP_MAX && (!c->sharded || c->sbatch) ? 1 : 0;
     h.xbat = nullptr;
+    h.xsp_out = h.xsp_in = nullptr;
+    h.xsp_cap = 0;
+    h.xsp_stride = 0;
     h.bat = nullptr;
     h.btag = nullptr;
     h.bvecd = h.bvec = h.bvlist = h.bvnl = nullptr;
@@ -516,6 +530,12 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         if ((r = dalloc(c, &h.bvnl, (size_t)BK * 4))) return r;
         // sharded: the batch exchange (zero between batches; a multiple of 4 words)
         if (c->sharded && (r = dalloc(c, &h.xbat, (xbat_words(BK, h.vcap) + 3) / 4 * 4))) return r;
+        if (c->sharded && h.vcap > DENSE) {
+            // ids >= DENSE: per batch and shard up to xsp_cap (id, delta) entries
+            xsp_layout(h.vcap, &h.xsp_cap, &h.xsp_stride);
+            if ((r = dalloc(c, &h.xsp_out, h.xsp_stride))) return r;
+            if ((r = dalloc(c, &h.xsp_in, (size_t)c->nshards * h.xsp_stride))) return r;
+        }
         // BPE_BATCH_DROP_TEST=d: the verification drops members j >= 1 of id
         // z = 0 mod d (tests drive the drop path with it)
         const uint32_t dt = (uint32_t)getenv_int("BPE_BATCH_DROP_TEST", 0);

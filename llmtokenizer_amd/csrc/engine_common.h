@@ -119,6 +119,7 @@ constexpr uint32_t BK = 63;     // members per batch (one list entry stays for t
 constexpr uint32_t BRB = 32;    // k_bsel reduce blocks (partial lists)
 constexpr uint32_t BREPL = 2;   // replicas of a member's dense delta accumulators
 constexpr uint32_t BSB = 256;   // k_bscan blocks (1024 threads, one per CU)
+constexpr uint32_t P2P_MAXR_B = 16;  // shards of a sharded batch run (BPE_GPU_P2P_MAX_RANKS; the gathered lists)
 
 struct Bat {
     uint32_t k, z0, applied, jstar;   // members; id of member 0; an apply ran (the select folds it); applied prefix
@@ -159,7 +160,11 @@ struct Bat {
 // Sharded batches: the words one batch exchanges (summed over the shards):
 // [BK] staging-overflow flags, then per member [R, bound, DL, DR, IL, IR] with
 // the four delta vectors dense over the ids < z0 + k (the batch's W)
-__host__ __device__ inline uint32_t xbat_member_words(uint32_t W) { return 2 + 4 * W; }
+// sharded batches: a member's exchange words are R, bound and its four delta
+// vectors dense over the ids below min(W, DENSE); larger ids travel as (id,
+// delta) lists (xsp_*, k_bpack)
+__host__ __device__ inline uint32_t xbat_vw(uint32_t W) { return W < DENSE ? W : DENSE; }
+__host__ __device__ inline uint32_t xbat_member_words(uint32_t W) { return 2 + 4 * xbat_vw(W); }
 __host__ __device__ inline uint32_t xbat_words(uint32_t k, uint32_t W) { return BK + k * xbat_member_words(W); }
 
 // Device-resident descriptor: every kernel takes a pointer to it, so tables can
@@ -248,6 +253,11 @@ struct Eng {
     uint32_t *bvlist;     // [BK][4][bvs]
     uint32_t *bvnl;       // [BK][4] list lengths
     uint32_t *xbat;       // sharded batches: the exchange buffer (xbat_words), zero between batches
+    // sharded batches with ids >= DENSE: my (member-vector << 24 | id, delta)
+    // list of them ([0] entries, [1] unused, then pairs; xsp_cap entries at
+    // most), and every shard's list gathered ([nshards][xsp_stride] words)
+    uint32_t *xsp_out, *xsp_in;
+    uint32_t xsp_cap, xsp_stride;
     // longest token span (end distance) an end code may hold: END_MAX, or less
     // for tests (BPE_END_MAX) that drive the over-long-token error paths
     uint64_t end_max;

@@ -2004,6 +2004,18 @@ __global__ __launch_bounds__(256) void k_xbsum(uint32_t *const *__restrict__ buf
     }
 }
 
+// one device: every shard's packed list of ids >= DENSE (src[i]: [n, -, 2n
+// words]) into dst[q] + i * stride of every shard q; grid K * K * 8
+__global__ __launch_bounds__(256) void k_xspgather(uint32_t *const *__restrict__ src, uint32_t *const *__restrict__ dst,
+                                                   uint32_t nb, uint32_t stride) {
+    const uint32_t pr = blockIdx.x / 8, ch = blockIdx.x % 8, q = pr / nb, i = pr % nb;
+    if (q >= nb) return;
+    const uint32_t words = 2 + 2 * src[i][0];
+    const uint32_t per = (words + 7) / 8;
+    for (uint32_t t = ch * per + threadIdx.x; t < min(words, (ch + 1) * per); t += blockDim.x)
+        dst[q][(uint64_t)i * stride + t] = src[i][t];
+}
+
 __global__ void k_xgather(uint32_t *const *__restrict__ src, uint32_t *const *__restrict__ dst, uint32_t nb,
                           uint32_t words) {
     for (uint32_t t = threadIdx.x; t < nb * words; t += blockDim.x)

@@ -30,8 +30,9 @@ constexpr uint32_t MB_FLAG1 = 16 * P2P_MAXR; // [rank * 16]: gather channel flag
 constexpr uint32_t MB_DATA1 = 32 * P2P_MAXR; // [2][P2P_MAXR][EDGE_WORDS]
 constexpr uint32_t MB_DATA0 = MB_DATA1 + 2 * P2P_MAXR * EDGE_WORDS;  // [2][W][c0]
 // (words 4..7: group_total's scratch)
-enum { XS_SEQ0 = 0, XS_PUSH0 = 1, XS_SEQ1 = 2, XS_ERR = 3, XS_TMP = 4, XS_SEQB = 8, XS_PUSHB = 9, XS_PEER = 16 };
-constexpr uint32_t XS_WORDS = XS_PEER + P2P_MAXR;  // g->xs
+enum { XS_SEQ0 = 0, XS_PUSH0 = 1, XS_SEQ1 = 2, XS_ERR = 3, XS_TMP = 4, XS_SEQB = 8, XS_PUSHB = 9, XS_SEQ2 = 10,
+       XS_PUSH2 = 11, XS_PEER = 16, XS_PEER2 = XS_PEER + P2P_MAXR };
+constexpr uint32_t XS_WORDS = XS_PEER2 + P2P_MAXR;  // g->xs
 constexpr uint32_t P2P_ERR_BIT = 16;  // Ctl::err bit of a timed-out exchange
 
 struct P2P {
@@ -42,6 +43,9 @@ struct P2P {
     uint32_t *xs;                // my counters: seq0, pushes0, seq1, err (plain device memory)
     uint32_t *err;               // extra error word (the training run's Ctl::err) or null
     unsigned long long timeout;  // wall-clock ticks a wait may take
+    // channel 2 (sharded batches with ids >= DENSE: the packed (id, delta)
+    // lists): at word off2 of every mailbox, [P2P_MAXR * 16 flags][2][W][stride2]
+    uint32_t off2, stride2;
 };
 
 __device__ inline uint32_t sys_load(const uint32_t *p) {
@@ -179,6 +183,48 @@ __global__ __launch_bounds__(256) void k_p2p_bsum(const P2P *__restrict__ X, uin
         X->xs[XS_SEQB] = sb;
         __hip_atomic_fetch_add(X->xs + XS_PUSH0, W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (k_p2p_sum's count)
     }
+}
+
+// Gather channel 2 (sharded batches with ids >= DENSE): every rank's packed
+// list (xsp_out: [n, -, 2n words of (id, delta)]) into dst + r * dstride on
+// every rank r.  Grid W x PSLICE2: block b pushes slice b / W of my list to
+// rank (me + b) % W (the last of my slices to land there stores my flag), and
+// once every rank's flag is in, copies a share of the W lists out.  Only the
+// list's own words move (its length is in its first word).
+constexpr uint32_t PSLICE2 = 8;
+
+__global__ __launch_bounds__(256) void k_p2p_vgather(const P2P *__restrict__ X, const uint32_t *__restrict__ src,
+                                                     uint32_t *__restrict__ dst, uint32_t dstride) {
+    const uint32_t W = X->W, me = X->rank, tid = threadIdx.x, G = gridDim.x;
+    const uint32_t seq = X->xs[XS_SEQ2] + 1u, par = seq & 1u;
+    const uint32_t p = (me + blockIdx.x) % W, sl = blockIdx.x / W, ns = G / W;
+    const uint32_t nv = (2 + 2 * src[0] + 3) / 4;  // (the slot stride is a multiple of 4 words)
+    const uint32_t per = (nv + ns - 1) / ns;
+    uint32_t *d = X->mb[p] + X->off2 + 16 * P2P_MAXR + ((uint64_t)par * W + me) * X->stride2;
+    for (uint32_t i = sl * per + tid; i < min(nv, (sl + 1) * per); i += blockDim.x)
+        sys_store4(d + 4 * i, reinterpret_cast<const uint4 *>(src)[i]);
+    p2p_release_point();
+    if (tid == 0) {
+        if (X->fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        const uint32_t landed = __hip_atomic_fetch_add(X->xs + XS_PEER2 + p, 1u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        if (landed == ns * seq)  // my last slice for rank p: my flag there
+            __hip_atomic_store(X->mb[p] + X->off2 + 16 * me, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_add(X->xs + XS_PUSH2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned long long t0 = wall_clock64();
+    if (tid < W) p2p_wait(X, X->mb[me] + X->off2 + 16 * tid, seq, t0);
+    else if (tid == 64) p2p_wait(X, X->xs + XS_PUSH2, G * seq, t0);  // every block pushed: src may change
+    if (X->fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __syncthreads();
+    // block b copies chunk b / W of rank b % W's list
+    const uint32_t r = blockIdx.x % W, ch = blockIdx.x / W;
+    const uint32_t *s = X->mb[me] + X->off2 + 16 * P2P_MAXR + ((uint64_t)par * W + r) * X->stride2;
+    const uint32_t words = 2 + 2 * sys_load(s);
+    const uint32_t cper = (words + ns - 1) / ns;
+    for (uint32_t i = ch * cper + tid; i < min(words, (ch + 1) * cper); i += blockDim.x)
+        dst[(uint64_t)r * dstride + i] = sys_load(s + i);
+    if (blockIdx.x == 0 && tid == 0) X->xs[XS_SEQ2] = seq;  // (every block read seq before it pushed)
 }
 
 // Gather channel: dst[r * EDGE_WORDS + w] := rank r's src[w].  One wave.

@@ -259,10 +259,34 @@ int ex_bsum(bpe_gpu_group *g) {
 // next batch (beside its own token rewrite), and the shards' new edge
 // records are gathered for the next scan's halo.  Two exchanges per batch of
 // up to BK merges instead of two per merge.
+// the batch's lists of ids >= DENSE: every shard's packed list on every shard
+int ex_sparse(bpe_gpu_group *g) {
+    bpe_gpu_ctx *c0 = g->cs[0];
+    const uint32_t stride = c0->h.xsp_stride;
+    if (g->p2p) {
+        k_p2p_vgather<<<g->hp.W * PSLICE2, 256, 0, g->st>>>(g->d_p2p, c0->h.xsp_out, c0->h.xsp_in, stride);
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
+    if (g->rccl) {
+        ncclResult_t e = g->rccl->allGather(c0->h.xsp_out, c0->h.xsp_in, stride, ncclUint32, g->comm, g->st);
+        if (e != ncclSuccess) return rccl_fail(g->rccl, "ncclAllGather", e);
+        return 0;
+    }
+    const uint32_t K = (uint32_t)g->cs.size();
+    k_xspgather<<<K * K * 8, 256, 0, g->st>>>(g->d_ptrs + 4 * K, g->d_ptrs + 5 * K, K, stride);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int launch_group_bstep(bpe_gpu_group *g) {
     int r;
+    const bool sparse = g->cs[0]->h.xsp_out != nullptr;
     for (bpe_gpu_ctx *c : g->cs) k_bscan<true><<<BSB, SCAN_T, 0, g->st>>>(c->dE, c->dC);
+    if (sparse)  // (before the sum: a list that overflows flags its member in xbat)
+        for (bpe_gpu_ctx *c : g->cs) k_bpack<<<64, 256, 0, g->st>>>(c->dE, c->dC);
     if ((r = ex_bsum(g))) return r;
+    if (sparse && (r = ex_sparse(g))) return r;
     for (bpe_gpu_ctx *c : g->cs) k_bapply<true><<<BAPPLY_B + BAPPLY_RA, 1024, 0, g->st>>>(c->dE, c->dC, BAPPLY_B);
     // (k_bsel's last rewrite block writes the edge record of the new tokens)
     for (bpe_gpu_ctx *c : g->cs) k_bsel<<<BRB + BAPPLY_A, 1024, 0, g->st>>>(c->dE, c->dC);
@@ -545,7 +569,12 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         // batches: schedule-free ties (sharded runs always), dense exchange
         // vectors over the whole vocabulary, a mailbox slot that holds them
         const uint64_t vc = 256 + cap;
-        c->sbatch = getenv_int("BPE_BATCH", 1) && vc <= DENSE && (!g->p2p || xbat_words(BK, (uint32_t)vc) <= g->hp.c0);
+        // (ids >= DENSE travel as per-shard lists: at most P2P_MAXR_B shards,
+        // and a P2P mailbox with the list channel)
+        uint32_t xcap, xstride;
+        xsp_layout(vc, &xcap, &xstride);
+        c->sbatch = getenv_int("BPE_BATCH", 1) && (!g->p2p || xbat_words(BK, (uint32_t)vc) <= g->hp.c0) &&
+                    (vc <= DENSE || (g->nshards <= P2P_MAXR_B && (!g->p2p || g->hp.stride2 >= xstride)));
         c->xfused = g->p2p && K == 1 && FUSED_SH && !c->sbatch;
         c->xtimeout = g->hp.timeout;
         c->xp2p = c->xfused ? g->d_p2p : nullptr;
@@ -556,7 +585,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     // pointer tables for the one-device exchange
     if (local_mode(g)) {
         if (!g->d_ptrs) {
-            HIPCHK(hipMalloc(&g->d_ptrs, 4ull * K * sizeof(uint32_t *)));
+            HIPCHK(hipMalloc(&g->d_ptrs, 6ull * K * sizeof(uint32_t *)));
             HIPCHK(hipMalloc(&g->d_ptrs_tmp, (size_t)K * sizeof(uint32_t *)));
         }
         std::vector<uint32_t *> t;
@@ -564,6 +593,8 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         for (auto *c : g->cs) t.push_back(c->h.myrec);
         for (auto *c : g->cs) t.push_back(c->h.erec);
         for (auto *c : g->cs) t.push_back(c->h.xbat);  // (batch runs)
+        for (auto *c : g->cs) t.push_back(c->h.xsp_out);  // (batch runs, ids >= DENSE)
+        for (auto *c : g->cs) t.push_back(c->h.xsp_in);
         if ((r = upload_table(g, g->d_ptrs, t))) return r;
     }
     // 1. global byte alphabet
@@ -893,7 +924,7 @@ int group_encode(bpe_gpu_group *g, const uint32_t *pairs, size_t n_merges) {
     }
     if (local_mode(g)) {
         if (!g->d_ptrs) {
-            HIPCHK(hipMalloc(&g->d_ptrs, 4ull * K * sizeof(uint32_t *)));
+            HIPCHK(hipMalloc(&g->d_ptrs, 6ull * K * sizeof(uint32_t *)));
             HIPCHK(hipMalloc(&g->d_ptrs_tmp, (size_t)K * sizeof(uint32_t *)));
         }
         std::vector<uint32_t *> t;
@@ -1048,9 +1079,14 @@ static int group_create_p2p(int device, int nranks, int rank, long max_merges, u
     // exchange (xbat_words: BK members' vectors)
     const uint64_t vc = 256 + (uint64_t)max_merges;
     uint64_t c0 = std::max<uint64_t>(65536, 4 * vc + 2);
-    if (vc <= DENSE) c0 = std::max<uint64_t>(c0, xbat_words(BK, (uint32_t)vc));
+    c0 = std::max<uint64_t>(c0, xbat_words(BK, (uint32_t)std::min<uint64_t>(vc, DENSE)));
     c0 = (c0 + 3) / 4 * 4;
-    const size_t bytes = ((size_t)MB_DATA0 + 2ull * nranks * c0) * 4;
+    // channel 2: the batches' lists of ids >= DENSE
+    uint32_t xcap = 0, xstride = 0;
+    if (vc > DENSE) xsp_layout(vc, &xcap, &xstride);
+    const uint64_t off2 = (uint64_t)MB_DATA0 + 2ull * nranks * c0;
+    const uint64_t words2 = xstride ? 16ull * P2P_MAXR + 2ull * nranks * xstride : 0;
+    const size_t bytes = (size_t)(off2 + words2) * 4;
     // uncached (peers on other devices write it while my kernels poll it);
     // kept out of the allocator after use (uc_take / uc_give).
     // BPE_P2P_LOCAL_UNCACHED=0: in-process groups take plain memory (A/B)
@@ -1077,6 +1113,8 @@ static int group_create_p2p(int device, int nranks, int rank, long max_merges, u
     g->hp.W = (uint32_t)nranks;
     g->hp.rank = (uint32_t)rank;
     g->hp.c0 = (uint32_t)c0;
+    g->hp.off2 = (uint32_t)off2;
+    g->hp.stride2 = xstride;
     g->hp.xs = g->xs;
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;

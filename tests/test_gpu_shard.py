@@ -166,3 +166,30 @@ def test_group_batch_failures_vs_oracle_rule(knob, monkeypatch, engine_mode):
         _assert_same(m, ids, om, oi, (knob, seed))
         st = g.stats()
         assert st["batch_retries"] > 0, st
+
+
+@pytest.mark.parametrize("cap", [None, "1"])
+def test_batches_beyond_dense_ids_equal_single_engine(cap, engine_mode, monkeypatch):
+    """Sharded batches with a vocabulary above DENSE (8192) ids: deltas of
+    ids >= 8192 travel as per-shard (id, delta) lists (k_bpack, gathered by
+    the exchange) instead of the dense vectors.  cap = 1: every list capacity
+    at its minimum (one member's worth), so batches overflow and re-form
+    shorter.  Merges and ids == the single engine's."""
+    if cap:
+        monkeypatch.setenv("BPE_XSP_CAP", cap)
+    data = synth_bytes(960, 6 << 20)
+    m = 9000
+    e = api.Engine(0)
+    e.load(data)
+    e.train(m, fast=True)
+    em, ei = e.merges(), e.ids()
+    e.close()
+    assert em.shape[0] == m
+    gm, gi, g = _group_train(data, [0, 1 << 20, (3 << 20) + 7, 6 << 20], m)
+    st = g.stats()
+    g.close()
+    _assert_same(gm, gi, em, ei, ("beyond DENSE", cap))
+    if engine_mode == "batch":
+        assert st["batches"] > 0
+        if cap:
+            assert st["batch_retries"] > 0, st
