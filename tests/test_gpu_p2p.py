@@ -227,3 +227,24 @@ def test_peer_access_checks():
     assert api.peer_access(0, 0)
     assert bdist.peer_problem(0, [pci, pci]) is None
     assert bdist.peer_problem(0, [pci, "ffff:ff:1f.7"]) is None  # (not visible here: left to the IPC mapping)
+
+
+def test_p2p_ranks_batches_beyond_dense_ids(tmp_path, monkeypatch):
+    """2 ranks, a vocabulary above 8192 ids: sharded batches send the deltas
+    of ids >= 8192 as (id, delta) lists through the mailbox list channel
+    (k_p2p_vgather); merges and ids == the one-device group == the single
+    engine"""
+    monkeypatch.setenv("BPE_BATCH", "1")
+    n, mm = 6 << 20, 9000
+    cuts = [0, (2 << 20) + 5, n]
+    res = _run_ranks(tmp_path, 2, "train", f"synth:987:{n}", mm, cuts)
+    data = synth_bytes(987, n)
+    e = api.Engine(0)
+    e.load(data)
+    e.train(mm, fast=True)
+    em, ei = e.merges(), e.ids()
+    e.close()
+    for r in res:
+        assert r["merges"].shape == em.shape and (r["merges"] == em).all()
+    assert (np.concatenate([r["ids"] for r in res]) == ei).all()
+    assert res[0]["stats"][3] > 0  # batches ran
