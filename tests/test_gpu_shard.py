@@ -131,19 +131,20 @@ def test_group_reference_goldens(name, k):
     G.check(fx, g.merges(), g.all_ids())
 
 
-def test_rccl_group_single_rank():
+@pytest.mark.parametrize("n,mm", [(3 << 20, 300), (6 << 20, 9000)])
+def test_rccl_group_single_rank(n, mm):
     """RCCL plumbing on one GPU: unique id, communicator, collectives in the
-    captured per-merge graph; result equals the one-device group"""
-    n = 3 << 20
+    captured per-merge graph; result equals the one-device group (9000
+    merges: the allgather of the lists of ids >= 8192 as well)"""
     data = synth_bytes(980, n)
     cid = api.comm_id()
     assert len(cid) == 128
     g = api.ShardGroup(0, nranks=1, rank=0, comm_id=cid)
     g.load(0, data)
-    g.train(300)
+    g.train(mm)
     e = api.Engine(0)
     e.load(data)
-    e.train(300)
+    e.train(mm, fast=True)
     _assert_same(g.merges(), g.all_ids(), e.merges(), e.ids(), "rccl")
     print("graph captured:", g.graph_captured())
 
