@@ -131,8 +131,8 @@ __device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bs
         KV x = kv_empty();
         if (i < n) {
             const uint32_t slot = E->hot_slot[i];
-            const uint32_t c = E->hcnt[slot];
-            const unsigned long long key = E->hkey[slot] - 1;
+            const uint32_t c = E->hcnt[(uint64_t)(slot) * E->hcs];
+            const unsigned long long key = E->hkey[(uint64_t)(slot) * E->hks] - 1;
             if (c) x = KV{pack_val(c, (uint32_t)(key >> 32), (uint32_t)key, Bsz), key};
         }
         x = wave_sort64(x);
@@ -1202,7 +1202,7 @@ __device__ inline uint64_t hinsert_c(const Eng *E, uint32_t u, uint32_t v, uint3
     const uint64_t msk = E->hcap - 1;
     uint64_t s = mix64(key) & msk;
     for (uint64_t p = 0; p <= msk; p++) {
-        const unsigned long long prev = atomicCAS(&E->hkey[s], 0ull, key);
+        const unsigned long long prev = atomicCAS(&E->hkey[(uint64_t)(s) * E->hks], 0ull, key);
         if (prev == 0) {
             *nins += 1;
             return s;
@@ -1498,7 +1498,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             if (slot == ~0ull) {
                 C->err = d > 0 ? 2 : 1;
             } else {
-                const uint32_t old = atomicAdd(&E->hcnt[slot], (uint32_t)d);
+                const uint32_t old = atomicAdd(&E->hcnt[(uint64_t)(slot) * E->hcs], (uint32_t)d);
                 const uint32_t nw = old + (uint32_t)d;
                 dD += (long long)(nw != 0) - (long long)(old != 0);
                 hot_in = hot && d > 0 && nw >= hotT && old < hotT;

@@ -183,8 +183,8 @@ __device__ inline int64_t stat_find(const Eng *E, uint64_t cap, uint32_t t, uint
 // keys of the pair table with count == M
 __global__ void k_res_collect(const Eng *E, uint32_t M, uint32_t *out, uint32_t *n, uint32_t cap) {
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < E->hcap; s += (uint64_t)gridDim.x * blockDim.x) {
-        if (E->hcnt[s] != M) continue;
-        const unsigned long long k = E->hkey[s] - 1;
+        if (E->hcnt[(uint64_t)(s) * E->hcs] != M) continue;
+        const unsigned long long k = E->hkey[(uint64_t)(s) * E->hks] - 1;
         const uint32_t p = atomicAdd(n, 1u);
         if (p < cap) {
             out[2 * p] = (uint32_t)(k >> 32);
@@ -596,8 +596,17 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         h.hcap = 1ull << 16;
     }
     const uint64_t nL1 = h.hcap / L1W, nL2 = (nL1 + L2W - 1) / L2W;
-    if ((r = dalloc(c, &h.hkey, h.hcap))) return r;
-    if ((r = dalloc(c, &h.hcnt, h.hcap))) return r;
+    // the pair table: 16-byte slots {key, count} by default (BPE_TAB_IL=0: two arrays)
+    if (getenv_int("BPE_TAB_IL", 1)) {
+        if ((r = dalloc(c, &h.hkey, 2 * h.hcap))) return r;
+        h.hcnt = reinterpret_cast<uint32_t *>(h.hkey) + 2;
+        h.hks = 2;
+        h.hcs = 4;
+    } else {
+        if ((r = dalloc(c, &h.hkey, h.hcap))) return r;
+        if ((r = dalloc(c, &h.hcnt, h.hcap))) return r;
+        h.hks = h.hcs = 1;
+    }
     if ((r = dalloc(c, &h.l1best, nL1))) return r;
     if ((r = dalloc(c, &h.l1key, nL1))) return r;
     if ((r = dalloc(c, &h.l1tie, nL1))) return r;
@@ -632,12 +641,18 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
     unsigned long long *okey = h.hkey;
     uint32_t *ocnt = h.hcnt;
     const uint64_t ocap = h.hcap;
+    const uint32_t oks = h.hks, ocs = h.hcs;
+    const bool il = h.hks == 2;  // (the layout stays)
     unsigned long long *nkey;
-    uint32_t *ncnt;
-    HIPCHK(hipMalloc(&nkey, ncap * sizeof(unsigned long long)));
-    HIPCHK(hipMalloc(&ncnt, ncap * sizeof(uint32_t)));
-    HIPCHK(hipMemsetAsync(nkey, 0, ncap * sizeof(unsigned long long), c->st));
-    HIPCHK(hipMemsetAsync(ncnt, 0, ncap * sizeof(uint32_t), c->st));
+    uint32_t *ncnt = nullptr;
+    HIPCHK(hipMalloc(&nkey, ncap * sizeof(unsigned long long) * (il ? 2 : 1)));
+    HIPCHK(hipMemsetAsync(nkey, 0, ncap * sizeof(unsigned long long) * (il ? 2 : 1), c->st));
+    if (il) {
+        ncnt = reinterpret_cast<uint32_t *>(nkey) + 2;
+    } else {
+        HIPCHK(hipMalloc(&ncnt, ncap * sizeof(uint32_t)));
+        HIPCHK(hipMemsetAsync(ncnt, 0, ncap * sizeof(uint32_t), c->st));
+    }
     const uint64_t nL1 = ncap / L1W, nL2 = (nL1 + L2W - 1) / L2W;
     const uint64_t nlist = nL1 + 4ull * DENSE + 4ull * h.vcap + 64;
     unsigned long long *l1b, *l1k, *l2b, *l2k, *l1v, *l1q, *l2v, *l2q;
@@ -654,8 +669,8 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
     HIPCHK(hipMalloc(&l2l, nlist * 4));
     HIPCHK(hipMalloc(&l2v, nL2 * 8));
     HIPCHK(hipMalloc(&l2q, nL2 * 8));
-    void *olds[] = {h.hkey, h.hcnt, h.l1best, h.l1key, h.l1tie, h.l1list, h.l2best, h.l2key, h.l2tie, h.l2list,
-                    h.l1v2, h.l1k2, h.l2v2, h.l2k2};
+    void *olds[] = {h.hkey, il ? nullptr : h.hcnt, h.l1best, h.l1key, h.l1tie, h.l1list, h.l2best, h.l2key, h.l2tie,
+                    h.l2list, h.l1v2, h.l1k2, h.l2v2, h.l2k2};
     h.hkey = nkey; h.hcnt = ncnt; h.hcap = ncap;
     h.l1best = l1b; h.l1key = l1k; h.l1tie = l1t; h.l1list = l1l; h.l1v2 = l1v; h.l1k2 = l1q;
     h.l1cap = nlist;
@@ -664,10 +679,11 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
     if ((r = push_desc(c))) return r;
     c->hC->nkeys = 0;
     HIPCHK(hipMemcpyAsync(&c->dC->nkeys, &c->hC->nkeys, sizeof(unsigned long long), hipMemcpyHostToDevice, c->st));
-    k_rehash<<<1024, 256, 0, c->st>>>(c->dE, c->dC, okey, ocnt, ocap);
+    k_rehash<<<1024, 256, 0, c->st>>>(c->dE, c->dC, okey, ocnt, ocap, oks, ocs);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));
     for (void *p : olds) {
+        if (!p) continue;
         for (size_t k = 0; k < c->train_allocs.size(); k++)
             if (c->train_allocs[k].first == p) {
                 c->train_allocs.erase(c->train_allocs.begin() + k);
@@ -675,10 +691,11 @@ int grow_table(bpe_gpu_ctx *c, uint64_t ncap) {
             }
         (void)hipFree(p);
     }
-    const size_t sizes[] = {ncap * 8, ncap * 4, nL1 * 8, nL1 * 8, nL1 * 4, 2 * nlist * 4, nL2 * 8, nL2 * 8, nL2 * 4, nlist * 4,
-                            nL1 * 8, nL1 * 8, nL2 * 8, nL2 * 8};
-    void *news[] = {nkey, ncnt, l1b, l1k, l1t, l1l, l2b, l2k, l2t, l2l, l1v, l1q, l2v, l2q};
-    for (int k = 0; k < 14; k++) c->train_allocs.push_back({news[k], sizes[k]});
+    const size_t sizes[] = {ncap * 8 * (il ? 2 : 1), ncap * 4, nL1 * 8, nL1 * 8, nL1 * 4, 2 * nlist * 4, nL2 * 8, nL2 * 8,
+                            nL2 * 4, nlist * 4, nL1 * 8, nL1 * 8, nL2 * 8, nL2 * 8};
+    void *news[] = {nkey, il ? nullptr : ncnt, l1b, l1k, l1t, l1l, l2b, l2k, l2t, l2l, l1v, l1q, l2v, l2q};
+    for (int k = 0; k < 14; k++)
+        if (news[k]) c->train_allocs.push_back({news[k], sizes[k]});
     c->stats.table_grows++;
     // the iteration graphs read every table pointer through the device
     // descriptor; only the level-2 summary launch depends on the size, so

@@ -192,8 +192,11 @@ struct Eng {
     uint32_t *vecd;       // [2][REPL][4][DENSE] replicated dense accumulators (ids < DENSE), 2 parities
     // pair-count table: open addressing on (a,b), never deletes (count may hit 0)
     uint64_t hcap;        // power of two
-    unsigned long long *hkey;  // key + 1, 0 = empty
-    uint32_t *hcnt;
+    unsigned long long *hkey;  // key + 1, 0 = empty: slot s at hkey[s * hks]
+    uint32_t *hcnt;            // its count at hcnt[s * hcs]
+    // strides: 1 / 1 two arrays; 2 / 4 one array of 16-byte slots {key, count,
+    // -} (BPE_TAB_IL=1): a probe and its count update touch one line, not two
+    uint32_t hks, hcs;
     // max summaries: level 1 = 256 slots, level 2 = 256 level-1 entries;
     // best packed value, number of keys holding it, smallest such key
     unsigned long long *l1best, *l1key;

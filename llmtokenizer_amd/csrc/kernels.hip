@@ -534,7 +534,7 @@ __device__ inline uint64_t hfind(const Eng *E, uint32_t u, uint32_t v) {
     const uint64_t m = E->hcap - 1;
     uint64_t s = mix64(key) & m;
     for (uint64_t p = 0; p <= m; p++) {
-        const unsigned long long k = E->hkey[s];
+        const unsigned long long k = E->hkey[(uint64_t)(s) * E->hks];
         if (k == key) return s;
         if (k == 0) return ~0ull;
         s = (s + 1) & m;
@@ -549,10 +549,10 @@ __device__ inline uint64_t hinsert(const Eng *E, Ctl *C, uint32_t u, uint32_t v,
     const uint64_t m = E->hcap - 1;
     uint64_t s = mix64(key) & m;
     for (uint64_t p = 0; p <= m; p++) {
-        unsigned long long k = __hip_atomic_load(&E->hkey[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long k = __hip_atomic_load(&E->hkey[(uint64_t)(s) * E->hks], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (k == key) return s;
         if (k == 0) {
-            unsigned long long prev = atomicCAS(&E->hkey[s], 0ull, key);
+            unsigned long long prev = atomicCAS(&E->hkey[(uint64_t)(s) * E->hks], 0ull, key);
             if (prev == 0) {
                 if (nins) *nins += 1;
                 else atomicAdd(&C->nkeys, 1ull);
@@ -572,8 +572,8 @@ __device__ inline uint64_t hfind_b(const Eng *E, uint32_t u, uint32_t v, bool *h
     const unsigned long long key = (((unsigned long long)u << 32) | v) + 1ull;
     const uint64_t m = E->hcap - 1;
     const uint64_t s0 = mix64(key) & m;
-    const unsigned long long k0 = E->hkey[s0];
-    const uint32_t c0 = E->hcnt[s0];
+    const unsigned long long k0 = E->hkey[(uint64_t)(s0) * E->hks];
+    const uint32_t c0 = E->hcnt[(uint64_t)(s0) * E->hcs];
     const unsigned long long b0 = E->l1v2[s0 / L1W];
     if (k0 == key) {
         *hit = true;
@@ -584,7 +584,7 @@ __device__ inline uint64_t hfind_b(const Eng *E, uint32_t u, uint32_t v, bool *h
     if (k0 == 0) return ~0ull;
     uint64_t s = (s0 + 1) & m;
     for (uint64_t p = 1; p <= m; p++) {
-        const unsigned long long k = E->hkey[s];
+        const unsigned long long k = E->hkey[(uint64_t)(s) * E->hks];
         if (k == key) return s;
         if (k == 0) return ~0ull;
         s = (s + 1) & m;
@@ -604,7 +604,7 @@ __device__ inline uint64_t hinsert_b(const Eng *E, uint32_t u, uint32_t v, uint3
     // not a load followed by a CAS -- role B's keys with d > 0 are new ones
     for (uint64_t p = 0; p <= m; p++) {
         const unsigned long long b2 = E->l1v2[s / L1W];
-        const unsigned long long prev = atomicCAS(&E->hkey[s], 0ull, key);
+        const unsigned long long prev = atomicCAS(&E->hkey[(uint64_t)(s) * E->hks], 0ull, key);
         if (prev == 0) {
             *nins += 1;
             *fresh = true;
@@ -824,11 +824,11 @@ __device__ inline void apply_body(const Eng *__restrict__ E, Ctl *__restrict__ C
                     C->err = d > 0 ? 2 : 1;  // k_select stops on it
                 } else {
                     blk = (uint32_t)(slot / L1W);
-                    const uint32_t old = fresh ? fold : E->hcnt[slot];
+                    const uint32_t old = fresh ? fold : E->hcnt[(uint64_t)(slot) * E->hcs];
                     const unsigned long long bv2 = fresh ? fbv2 : E->l1v2[blk];  // loaded beside the count
 
                     const uint32_t nw = (uint32_t)((long long)old + d);
-                    E->hcnt[slot] = nw;
+                    E->hcnt[(uint64_t)(slot) * E->hcs] = nw;
                     dD += (long long)(nw != 0) - (long long)(old != 0);
                     if (hot) {
                         // a rise to >= hot_T lists the key (once: counts only rise
@@ -1045,8 +1045,8 @@ __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__r
 #pragma unroll
             for (uint32_t q = 0; q < HQ; q++) {
                 const uint64_t slot = (uint64_t)blk * L1W + (h * HQ + q) * 64 + lane;
-                cnt[q] = E->hcnt[slot];
-                key[q] = E->hkey[slot];
+                cnt[q] = E->hcnt[(uint64_t)(slot) * E->hcs];
+                key[q] = E->hkey[(uint64_t)(slot) * E->hks];
             }
 #pragma unroll
             for (uint32_t q = 0; q < HQ; q++) {
@@ -1080,8 +1080,8 @@ __device__ void hot_reduce_body(const Eng *__restrict__ E, Ctl *__restrict__ C, 
     Top2 mine = top2_one(0, 0, ~0ull);
     for (uint32_t i = bid * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
         const uint32_t slot = E->hot_slot[i];
-        const uint32_t c = E->hcnt[slot];
-        const unsigned long long k = E->hkey[slot] - 1;
+        const uint32_t c = E->hcnt[(uint64_t)(slot) * E->hcs];
+        const unsigned long long k = E->hkey[(uint64_t)(slot) * E->hks] - 1;
         if (c) mine = top2_merge(mine, top2_one(pack_val(c, (uint32_t)(k >> 32), (uint32_t)k, B), 1, k));
     }
     mine = wave_top2(mine);
@@ -1112,14 +1112,23 @@ __global__ __launch_bounds__(256) void k_hot_hist(const Eng *__restrict__ E) {
     __shared__ uint32_t h[HOT_BINS];
     for (uint32_t x = threadIdx.x; x < HOT_BINS; x += blockDim.x) h[x] = 0;
     __syncthreads();
-    const uint64_t n4 = E->hcap / 4;
-    const uint4 *c4 = reinterpret_cast<const uint4 *>(E->hcnt);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint4 q = c4[i];
-        if (q.x >= 2) atomicAdd(&h[hot_bin(q.x)], 1u);
-        if (q.y >= 2) atomicAdd(&h[hot_bin(q.y)], 1u);
-        if (q.z >= 2) atomicAdd(&h[hot_bin(q.z)], 1u);
-        if (q.w >= 2) atomicAdd(&h[hot_bin(q.w)], 1u);
+    if (E->hcs == 4) {  // 16-byte slots {key, count, -}: one uint4 per slot
+        const uint4 *c4 = reinterpret_cast<const uint4 *>(E->hkey);
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E->hcap;
+             i += (uint64_t)gridDim.x * blockDim.x) {
+            const uint32_t c = c4[i].z;
+            if (c >= 2) atomicAdd(&h[hot_bin(c)], 1u);
+        }
+    } else {
+        const uint64_t n4 = E->hcap / 4;
+        const uint4 *c4 = reinterpret_cast<const uint4 *>(E->hcnt);
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
+            const uint4 q = c4[i];
+            if (q.x >= 2) atomicAdd(&h[hot_bin(q.x)], 1u);
+            if (q.y >= 2) atomicAdd(&h[hot_bin(q.y)], 1u);
+            if (q.z >= 2) atomicAdd(&h[hot_bin(q.z)], 1u);
+            if (q.w >= 2) atomicAdd(&h[hot_bin(q.w)], 1u);
+        }
     }
     __syncthreads();
     for (uint32_t x = threadIdx.x; x < HOT_BINS; x += blockDim.x)
@@ -1201,7 +1210,7 @@ __global__ __launch_bounds__(256) void k_hot_collect(const Eng *__restrict__ E, 
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t end = (n + stride - 1) / stride * stride;  // uniform trip count (wave_append)
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride) {
-        const bool in = i < n && E->hcnt[i] >= T;
+        const bool in = i < n && E->hcnt[(uint64_t)(i) * E->hcs] >= T;
         const uint32_t p = wave_append(in, &C->hot_n);
         if (in && p < HOT_CAP) E->hot_slot[p] = (uint32_t)i;
     }
@@ -2917,20 +2926,21 @@ __global__ void k_init_counts(const Eng *__restrict__ E, Ctl *__restrict__ C, co
     const uint32_t u = unrank[k / E->A], v = unrank[k % E->A];
     const uint64_t slot = hinsert(E, C, u, v);
     if (slot == ~0ull) { C->err = 2; C->stop = STOP_ERROR; return; }
-    E->hcnt[slot] = c;
+    E->hcnt[(uint64_t)(slot) * E->hcs] = c;
     atomicAdd(&C->D, 1ull);
 }
 
 // regrow: re-insert every key of the old table
 __global__ void k_rehash(const Eng *__restrict__ E, Ctl *__restrict__ C, const unsigned long long *__restrict__ okey,
-                         const uint32_t *__restrict__ ocnt, uint64_t ocap) {
+                         const uint32_t *__restrict__ ocnt, uint64_t ocap, uint32_t oks, uint32_t ocs) {
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ocap; s += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned long long k = okey[s];
+        const unsigned long long k = okey[s * oks];
         if (!k) continue;
-        if (!ocnt[s]) continue;  // zero-count keys are dropped on regrowth
+        const uint32_t oc = ocnt[s * ocs];
+        if (!oc) continue;  // zero-count keys are dropped on regrowth
         const uint64_t slot = hinsert(E, C, (uint32_t)((k - 1) >> 32), (uint32_t)(k - 1));
         if (slot == ~0ull) { C->err = 2; C->stop = STOP_ERROR; return; }
-        E->hcnt[slot] = ocnt[s];
+        E->hcnt[(uint64_t)(slot) * E->hcs] = oc;
     }
 }
 

@@ -151,3 +151,20 @@ def test_batch_equals_one_merge_engine_64m():
         outs.append((cs, lines[1], int(nb), int(nm)))
     assert outs[0][0] == outs[1][0] and outs[0][1] == outs[1][1], outs
     assert outs[0][2] > 0 and outs[1][2] == 0 and outs[0][3] == 1500, outs
+
+
+def test_table_layouts_agree_on_batches(monkeypatch):
+    """the batch engine with the pair table as 16-byte {key, count} slots
+    (default) and as two arrays (BPE_TAB_IL=0): same merges, same ids"""
+    data = synth_bytes(77, 24 << 20)
+    out = []
+    for il in ("1", "0"):
+        monkeypatch.setenv("BPE_TAB_IL", il)
+        e = api.Engine(0)
+        e.load(data)
+        assert e.train(2500) == 2500
+        st = e.stats()
+        out.append((e.merges(), e.ids_checksum(), st["batches"]))
+        e.close()
+    assert (out[0][0] == out[1][0]).all() and out[0][1] == out[1][1]
+    assert out[0][2] > 0

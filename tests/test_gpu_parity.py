@@ -138,11 +138,14 @@ def test_1g_properties_after_many_merges():
     assert dec == synth_bytes(2, len(dec))
 
 
-def test_table_regrowth_matches_presized(monkeypatch):
+@pytest.mark.parametrize("il", ["1", "0"])
+def test_table_regrowth_matches_presized(il, monkeypatch):
     """The pair table is sized so that typical runs never regrow; a forced
     small table (BPE_TABLE_SLOTS) drives the regrowth path (host round trip,
     rehash, full summary rebuild, graph recapture) and must give the same
-    merges and ids as the presized run and the oracle."""
+    merges and ids as the presized run and the oracle.  Both table layouts:
+    16-byte {key, count} slots (BPE_TAB_IL=1, default) and two arrays (0)."""
+    monkeypatch.setenv("BPE_TAB_IL", il)
     data = synth_bytes(905, 1 << 20)
     e = api.Engine(0)
     e.load(data)
