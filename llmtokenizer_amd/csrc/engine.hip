@@ -596,8 +596,11 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         h.hcap = 1ull << 16;
     }
     const uint64_t nL1 = h.hcap / L1W, nL2 = (nL1 + L2W - 1) / L2W;
-    // the pair table: 16-byte slots {key, count} by default (BPE_TAB_IL=0: two arrays)
-    if (getenv_int("BPE_TAB_IL", 1)) {
+    // the pair table: two arrays (keys, counts); BPE_TAB_IL=1: 16-byte slots
+    // {key, count} so that a probe and its count update touch one line -- the
+    // same loop time on configs[2] (69.4-70.4 vs 69.5-70.0 ms) and +1.2 ms of
+    // init (a 4 GB table to clear and histogram instead of 3 GB), so off
+    if (getenv_int("BPE_TAB_IL", 0)) {
         if ((r = dalloc(c, &h.hkey, 2 * h.hcap))) return r;
         h.hcnt = reinterpret_cast<uint32_t *>(h.hkey) + 2;
         h.hks = 2;

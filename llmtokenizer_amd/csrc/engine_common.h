@@ -194,8 +194,8 @@ struct Eng {
     uint64_t hcap;        // power of two
     unsigned long long *hkey;  // key + 1, 0 = empty: slot s at hkey[s * hks]
     uint32_t *hcnt;            // its count at hcnt[s * hcs]
-    // strides: 1 / 1 two arrays; 2 / 4 one array of 16-byte slots {key, count,
-    // -} (BPE_TAB_IL=1): a probe and its count update touch one line, not two
+    // strides: 1 / 1 two arrays (default); 2 / 4 one array of 16-byte slots
+    // {key, count, -} (BPE_TAB_IL=1): a probe and its count update touch one line
     uint32_t hks, hcs;
     // max summaries: level 1 = 256 slots, level 2 = 256 level-1 entries;
     // best packed value, number of keys holding it, smallest such key

@@ -410,9 +410,16 @@ int drive_group(bpe_gpu_group *g) {
         for (bpe_gpu_ctx *c : g->cs)
             if ((r = pull_ctl(c))) return r;
         const Ctl &C0 = *g->cs[0]->hC;
-        for (bpe_gpu_ctx *c : g->cs)
-            if (c->hC->stop != C0.stop || c->hC->merges_done != C0.merges_done || c->hC->D != C0.D)
-                return fail(BPE_GPU_EINTERNAL, "shards diverged");
+        for (size_t q = 0; q < g->cs.size(); q++) {
+            const Ctl &Cq = *g->cs[q]->hC;
+            if (Cq.stop != C0.stop || Cq.merges_done != C0.merges_done || Cq.D != C0.D) {
+                char msg[256];
+                snprintf(msg, sizeof msg, "shards diverged (shard %zu vs 0: stop %u/%u err %u/%u merges %llu/%llu D %llu/%llu)",
+                         q, Cq.stop, C0.stop, Cq.err, C0.err, (unsigned long long)Cq.merges_done,
+                         (unsigned long long)C0.merges_done, (unsigned long long)Cq.D, (unsigned long long)C0.D);
+                return fail(BPE_GPU_EINTERNAL, msg);
+            }
+        }
         if (fused && ran_fused && C0.stop != STOP_NONE && C0.stop != STOP_ERROR) {
             // the fused graph stopped: revert the speculative apply that ran
             // beside the stopping selection (if any), clear the other parity

@@ -154,8 +154,8 @@ def test_batch_equals_one_merge_engine_64m():
 
 
 def test_table_layouts_agree_on_batches(monkeypatch):
-    """the batch engine with the pair table as 16-byte {key, count} slots
-    (default) and as two arrays (BPE_TAB_IL=0): same merges, same ids"""
+    """the batch engine with the pair table as two arrays (default) and as
+    16-byte {key, count} slots (BPE_TAB_IL=1): same merges, same ids"""
     data = synth_bytes(77, 24 << 20)
     out = []
     for il in ("1", "0"):

@@ -144,7 +144,7 @@ def test_table_regrowth_matches_presized(il, monkeypatch):
     small table (BPE_TABLE_SLOTS) drives the regrowth path (host round trip,
     rehash, full summary rebuild, graph recapture) and must give the same
     merges and ids as the presized run and the oracle.  Both table layouts:
-    16-byte {key, count} slots (BPE_TAB_IL=1, default) and two arrays (0)."""
+    two arrays (default) and 16-byte {key, count} slots (BPE_TAB_IL=1)."""
     monkeypatch.setenv("BPE_TAB_IL", il)
     data = synth_bytes(905, 1 << 20)
     e = api.Engine(0)
