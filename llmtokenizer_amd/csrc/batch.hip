@@ -245,9 +245,13 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             const uint32_t u = (uint32_t)(e.k >> 32), v = (uint32_t)e.k, c = (uint32_t)(e.v >> 32);
             // ties with the next key keep their pre-batch order when the members
             // before it cannot move B_final: a member adds or zeroes at most
-            // 2 min(ids, count) + 1 keys (its neighbours' pairs and its own)
+            // 2 min(ids, count) + 1 keys (its neighbours' pairs and its own),
+            // where the ids a neighbour can be are the A byte values present and
+            // the merged ids up to this batch's last (not all 256 byte values:
+            // text has ~95, which early in a run is most of the bound)
             const uint32_t cprev = (uint32_t)(__shfl(e.v, (int)(lane ? lane - 1 : 0)) >> 32);
-            unsigned long long span = lane > 0 && lane <= nl ? min(2ull * (256ull + md + BK), 2ull * cprev) + 1 : 0ull;
+            unsigned long long span =
+                lane > 0 && lane <= nl ? min(2ull * ((unsigned long long)E->A + md + BK), 2ull * cprev) + 1 : 0ull;
             for (int o = 1; o < 64; o <<= 1) {
                 const unsigned long long y = __shfl_up(span, o);
                 if ((int)lane >= o) span += y;
