@@ -358,6 +358,16 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->blk0[lane] = bpre - nb + (lane > bigm ? extra : 0);
                 ctl[lane] = tl;
             }
+            if (E->dbg_form) {  // (diagnostics: the formation's state where the batch ended)
+                const unsigned long long spk = __shfl(span, (int)(k < 64 ? k : 63));
+                const uint32_t ck = __shfl(c, (int)(k < 64 ? k : 63)), cn = __shfl(cnext, (int)(k < 64 ? k : 63));
+                const uint32_t ok = __shfl((uint32_t)order_ok, (int)(k < 64 ? k : 63));
+                if (lane == 0)
+                    printf("form md %u k %u why %u D %llu span %llu B %llu lo %llu hi %llu trunc %d c %u next %u last %u "
+                           "order %u\n", md, k, endwhy, D, spk, (unsigned long long)Bsz,
+                           (unsigned long long)summary_B(D > spk ? D - spk : 0), (unsigned long long)summary_B(D + spk),
+                           (int)truncated, ck, cn, clast, ok);
+            }
             if (lane == 0) {
                 B->sbase[k] = (uint32_t)stage_end;
                 B->blk0[k] = BSB;

@@ -218,6 +218,7 @@ struct Eng {
     uint32_t *aux;        // per-slot scratch for the resolver (first thread)
     unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
     unsigned long long *dbgts;      // [TS_SLOTS][TS_N] per-merge block timeline (BPE_DEBUG_TS) or null
+    uint32_t dbg_form;              // BPE_DEBUG_FORM=1: k_bsel prints why each batch's formation ended
     uint32_t *hprobe;     // host-mapped stop probe: k_select writes the stop code when it stops
                           // (the host keeps the next graph queued while the probe reads 0)
     uint32_t fast;        // 1: schedule-free tie rule everywhere (no tracking)
