@@ -20,7 +20,7 @@ e.train(mm, fast=True)
 em = e.merges()
 e.close()
 cuts = [0] + [n * q // K + 7 * q for q in range(1, K)] + [n]
-for m in (8000, 8100, 8200, 8500, mm):
+for m in [int(x) for x in os.environ.get("DBG_M", "8000,8100,8200,8500").split(",")] + [mm]:
     g = api.ShardGroup(0, local_shards=K)
     g.load_split(data, cuts)
     try:
