@@ -358,13 +358,13 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->blk0[lane] = bpre - nb + (lane > bigm ? extra : 0);
                 ctl[lane] = tl;
             }
-            if (E->dbg_form) {  // (diagnostics: the formation's state where the batch ended)
+            if (E->dbg_form && md + 1 >= E->dbg_form) {  // (diagnostics: the formation's state where the batch ended; from merge BPE_DEBUG_FORM - 1)
                 const unsigned long long spk = __shfl(span, (int)(k < 64 ? k : 63));
                 const uint32_t ck = __shfl(c, (int)(k < 64 ? k : 63)), cn = __shfl(cnext, (int)(k < 64 ? k : 63));
                 const uint32_t ok = __shfl((uint32_t)order_ok, (int)(k < 64 ? k : 63));
                 if (lane == 0)
-                    printf("form md %u k %u why %u D %llu span %llu B %llu lo %llu hi %llu trunc %d c %u next %u last %u "
-                           "order %u\n", md, k, endwhy, D, spk, (unsigned long long)Bsz,
+                    printf("form shard %u md %u k %u why %u D %llu span %llu B %llu lo %llu hi %llu trunc %d c %u next %u last %u "
+                           "order %u\n", E->shard, md, k, endwhy, D, spk, (unsigned long long)Bsz,
                            (unsigned long long)summary_B(D > spk ? D - spk : 0), (unsigned long long)summary_B(D + spk),
                            (int)truncated, ck, cn, clast, ok);
             }
@@ -1328,6 +1328,8 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                            (ovm & ((2ull << lane) - 1ull)) != 0);
         const unsigned long long fm = __ballot(fail);
         uint32_t js = fm ? (uint32_t)__ffsll(fm) - 1 : k;
+        if (E->dbg_form && C->merges_done + 1 >= E->dbg_form && blockIdx.x == 0 && lane == 0)
+            printf("verify shard %u z0 %u k %u js %u ovm %llx R0 %u Rg0 %u\n", E->shard, z0, k, js, ovm, R, Rg);
         if (js < k) {  // re-form the batch with the verified prefix; apply nothing
             if (lane == 0) B->retry = js;
             js = 0;
@@ -1511,6 +1513,9 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             const uint64_t slot = d > 0 ? hinsert_c(E, u, v, &nins) : hfind(E, u, v);
             if (slot == ~0ull) {
                 C->err = d > 0 ? 2 : 1;
+                if (E->dbg_form)
+                    printf("apply shard %u z0 %u k %u js %u: no key (%u, %u) for member %u cat %u delta %lld (x %u t %u)\n",
+                           E->shard, z0, k, js, u, v, m, cat, d, x, t);
             } else {
                 const uint32_t old = atomicAdd(&E->hcnt[(uint64_t)(slot) * E->hcs], (uint32_t)d);
                 const uint32_t nw = old + (uint32_t)d;

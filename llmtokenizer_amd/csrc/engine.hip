@@ -270,6 +270,8 @@ struct bpe_gpu_ctx {
     uint32_t fast = 0;                     // schedule-free tie rule everywhere
     bool mlog_on = false;                  // per-merge records (bpe_gpu_set_merge_log)
     uint32_t sharded = 0, shard = 0, nshards = 1;
+    uint64_t ntot = 0;                     // sharded: the group's tokens (the replicated pair table is sized
+                                           // for them, alike on every shard: its capacity steers stops and batches)
     uint32_t xfused = 0;                   // fused sharded step (P2P group, shard.hip)
     uint32_t sbatch = 0;                   // sharded training in batches (shard.hip, batch.hip)
     uint64_t stage_cap = 0;                // batch occurrence staging positions (Bat::stage_cap's source)
@@ -586,7 +588,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         // to ~10 k merges never regrow (a regrowth is a host round trip, a
         // rehash and a graph recapture)
         const uint64_t mm = mcap;
-        const uint64_t keys = std::min<uint64_t>(n0, 65536 + 512 * mm + mm * mm);
+        const uint64_t keys = std::min<uint64_t>(c->sharded && c->ntot ? c->ntot : n0, 65536 + 512 * mm + mm * mm);
         uint64_t want = std::max<uint64_t>(2 * keys, 4ull * (65536 + 16ull * (256 + std::min<uint64_t>(mcap, 4096))));
         want = std::min<uint64_t>(want, 1ull << 28);
         // BPE_TABLE_SLOTS: initial size override (tests drive the regrowth path with it)

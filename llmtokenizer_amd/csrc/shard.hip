@@ -573,6 +573,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         c->sharded = 1;
         c->shard = g->shard0 + k;
         c->nshards = g->nshards;
+        c->ntot = ntot;
         // batches: schedule-free ties (sharded runs always), dense exchange
         // vectors over the whole vocabulary, a mailbox slot that holds them
         const uint64_t vc = 256 + cap;
