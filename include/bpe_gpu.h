@@ -100,6 +100,10 @@ typedef struct {
     double ms_select_span;    /* training, batches: average k_bsel span (the selection beside the
                                  previous batch's token rewrite; device wall clock) */
     uint64_t select_launches; /* ... over this many k_bsel launches */
+    uint64_t tie_verified;    /* training, batches: batches with a member admitted on a tie order that
+                                 holds only if the earlier members zero few keys (checked in k_bapply) */
+    uint64_t tie_failed;      /* ... of them re-formed shorter (the check failed) */
+    uint64_t keys_zeroed;     /* training, batches: pair keys the applied batches took to count 0 */
 } bpe_gpu_stats;
 
 /* Per-merge record (training): the structured per-iteration metrics the

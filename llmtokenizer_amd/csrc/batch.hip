@@ -58,6 +58,11 @@ constexpr uint32_t FR = BPE_FR;
 #define BPE_SCAN_PF 1
 #endif
 constexpr uint32_t RU = BPE_RU;  // rewrite occurrences per thread per round
+// verified tie order: k_bapply's blocks taking part in its phase barrier (the
+// rest exit; 1024-thread blocks, one per CU: half the CUs must be resident) and
+// the bound on that barrier's wait (wall-clock ticks, 100 MHz: 0.5 s)
+constexpr uint32_t TIE_B = 128;
+constexpr unsigned long long TIE_WAIT_TICKS = 50000000ull;
 
 // debug timeline of a batch (BPE_DEBUG_TS; E->dbgts rows indexed by batch)
 enum { BT_SCAN_IN = 0, BT_SCAN_CAND, BT_SCAN_OUT, BT_APPLY_IN, BT_APPLY_PRO, BT_APPLY_A, BT_APPLY_B, BT_SEL_IN,
@@ -146,6 +151,16 @@ __device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bs
 }
 
 constexpr uint32_t BAT_HEAD_WORDS = offsetof(Bat, pv) / 4;
+
+// every level B = B_sz 2^e in [lo, hi] has its bit (e + 5) in mask
+__device__ inline bool tie_levels_ok(uint64_t lo, uint64_t hi, uint64_t Bsz, uint32_t mask) {
+    const int zsz = __builtin_ctzll(Bsz);
+    for (uint64_t Bx = lo; Bx <= hi; Bx <<= 1) {
+        const int lv = __builtin_ctzll(Bx) - zsz + 5;
+        if (lv < 0 || lv >= 8 || !((mask >> lv) & 1u)) return false;
+    }
+    return true;
+}
 
 // The selection (the last reduce block): folds the batch applied last into the
 // control block, runs the reference's stop rules on the argmax, forms the next
@@ -258,13 +273,21 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             }
             const uint64_t Blo = summary_B(D > span ? D - span : 0), Bhi = summary_B(D + span);
             const bool stable = Blo == Bsz && Bhi == Bsz;
+            // D only falls by the keys the members zero (their own and a few
+            // neighbour pairs): with a guess of those from the batches so far,
+            // the lower end of the reachable B is usually B_sz; k_bapply counts
+            // the keys really zeroed and checks that guess (verified members)
+            const unsigned long long zg = 16ull + (unsigned long long)B->zrate * lane;
+            const uint64_t Blo_o = summary_B(D > zg ? D - zg : 0);
             const uint32_t cnext = __shfl(c, (int)(lane < 63 ? lane + 1 : 63));
             // otherwise keys of one count keep my order against them under every
             // B the members before me can reach (bucket = murmur & (B - 1), then
-            // the key): checked against the listed keys of my count after me
+            // the key): checked against the listed keys of my count after me, as
+            // a mask of the levels B = B_sz 2^e (bit e + 5) where it holds
             const uint32_t hsh = murmur_pair(u, v);
             const uint32_t clast = __shfl(c, (int)(nl ? nl - 1 : 0));
-            bool order_ok = true;
+            const int zsz = __builtin_ctzll(Bsz);
+            uint32_t tmask = 0xFFu;
             const bool tie_next = lane < nl && !(c > (lane + 1 < nl ? cnext : 0u));
             const bool check = __ballot(!stable && lane > 0 && lane < BK && tie_next) != 0;  // (wave-uniform)
             for (uint32_t p = 1; check && p < TOPK; p++) {  // (uniform loop; readlane needs every lane)
@@ -276,15 +299,21 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 if (p > lane && p < nl && cp == c)
                     for (uint64_t Bx = Blo; Bx <= Bhi; Bx <<= 1) {
                         const uint64_t bj = hsh & (Bx - 1), bp = hp & (Bx - 1);
-                        if (!(bj < bp || (bj == bp && e.k < kp))) order_ok = false;
+                        const int lv = __builtin_ctzll(Bx) - zsz + 5;
+                        if (!(bj < bp || (bj == bp && e.k < kp)) && lv >= 0 && lv < 8) tmask &= ~(1u << lv);
                     }
             }
+            if (truncated && c == clast) tmask &= 1u << 5;  // (keys past the list keep their order under B_sz only)
+            const bool tie_rel = !stable && ((truncated && c == clast) || tie_next);
+            const bool cons_ok = tie_levels_ok(Blo, Bhi, Bsz, tmask);
+            const bool opt_ok = tie_levels_ok(Blo_o, Bhi, Bsz, tmask);
+            bool pend = false;
             uint32_t why = 0;  // 0: qualifies
             if (lane >= nl || lane >= BK) why = 8;  // past the list (reported as "list")
             else if (lane > 0) {
                 if (e.k == kprev) why = 3;  // the same key listed twice (the one-merge engine's undo): end here
                 else if (md + lane >= E->mcap || c <= 1 || (hotT > 2 && c < hotT)) why = 1;
-                else if (!stable && ((truncated && c == clast) || (!(c > (lane + 1 < nl ? cnext : 0u)) && !order_ok)))
+                else if (tie_rel && !cons_ok && !(opt_ok && E->tie_verify))
                     why = 4;  // (a tie whose order the batch could change, or one running past the list)
                 else if (C->nkeys + 4ull * (256ull + md + lane + 2) * (lane + 1) >= E->hcap / 2) why = 6;
             }
@@ -294,9 +323,11 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 const uint32_t up = __builtin_amdgcn_readlane((int)u, (int)p), vp = __builtin_amdgcn_readlane((int)v, (int)p);
                 if (!why && p < lane && (u == vp || v == up)) why = 5;
             }
+            if (lane > 0 && !why && tie_rel && !cons_ok) pend = true;  // admitted on the guess: k_bapply verifies
             const unsigned long long badm = __ballot(why != 0);
             k = badm ? (uint32_t)__ffsll(badm) - 1 : 64;  // lane 0 always qualifies
             if (retry && retry < k) k = retry;  // the last batch failed there (nothing changed since)
+            const unsigned long long pm = __ballot(pend && lane < k);
             const uint32_t endwhy = __shfl(why, (int)(k < 64 ? k : 0));
             // candidate lists and token lengths, one lane per member
             uint32_t mode = 1, off = 0, len = 0, tl = 0;
@@ -356,23 +387,28 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->R[lane] = 0;
                 B->bound[lane] = 0;
                 B->blk0[lane] = bpre - nb + (lane > bigm ? extra : 0);
+                B->tmask[lane] = (uint8_t)tmask;
+                B->tspan[lane] = (uint32_t)min(span, 0xFFFFFFFFull);
                 ctl[lane] = tl;
             }
             if (E->dbg_form && md + 1 >= E->dbg_form) {  // (diagnostics: the formation's state where the batch ended; from merge BPE_DEBUG_FORM - 1)
                 const unsigned long long spk = __shfl(span, (int)(k < 64 ? k : 63));
                 const uint32_t ck = __shfl(c, (int)(k < 64 ? k : 63)), cn = __shfl(cnext, (int)(k < 64 ? k : 63));
-                const uint32_t ok = __shfl((uint32_t)order_ok, (int)(k < 64 ? k : 63));
+                const uint32_t ok = __shfl(tmask, (int)(k < 64 ? k : 63));
                 if (lane == 0)
                     printf("form shard %u md %u k %u why %u D %llu span %llu B %llu lo %llu hi %llu trunc %d c %u next %u last %u "
-                           "order %u\n", E->shard, md, k, endwhy, D, spk, (unsigned long long)Bsz,
+                           "mask %x pend %llx zrate %u\n", E->shard, md, k, endwhy, D, spk, (unsigned long long)Bsz,
                            (unsigned long long)summary_B(D > spk ? D - spk : 0), (unsigned long long)summary_B(D + spk),
-                           (int)truncated, ck, cn, clast, ok);
+                           (int)truncated, ck, cn, clast, ok, pm, B->zrate);
             }
             if (lane == 0) {
                 B->sbase[k] = (uint32_t)stage_end;
                 B->blk0[k] = BSB;
                 B->sumlen = (uint32_t)sumlen;
                 B->over = ovm < k ? ovm : BK;
+                B->tpend = pm ? (uint32_t)__ffsll(pm) - 1 : BK;
+                B->ztot = 0;
+                B->tbar = 0;
                 B->why[why_end]++;
                 if (ties > 1) C->counters[2]++;
             }
@@ -385,6 +421,9 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             }
             B->sc_in = B->sc_out = B->ap_in = B->ap_out = 0;
             if (applied) {
+                // the formation's guess of the keys a member zeroes: twice the
+                // run's average so far, + 2
+                B->zrate = (uint32_t)min(2ull * B->nzero / (md ? md : 1u) + 2ull, 1ull << 20);
                 C->merges_done = md;
                 C->occ_top += (uint32_t)rs;
                 C->n_live = n_live;
@@ -1338,7 +1377,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         // the first part of each verified member's rewrite runs here, in
         // blocks in proportion to it (>= 1 per member)
         const uint32_t nA1 = gridDim.x - roleB_blocks;
-        const uint32_t cut = (in && lane < js && nA1) ? (uint32_t)((uint64_t)R * B->ra_split / 256) : 0u;
+        const uint32_t cut = (in && lane < js && nA1 && !(B->tpend < js)) ? (uint32_t)((uint64_t)R * B->ra_split / 256) : 0u;
         unsigned long long ctot = cut;
         for (int o = 32; o > 0; o >>= 1) ctot += __shfl_xor(ctot, o);
         const uint32_t nb1 = lane < js ? 1 + (uint32_t)(ctot ? (uint64_t)(nA1 > js ? nA1 - js : 0) * cut / ctot : 0) : 0;
@@ -1394,10 +1433,173 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                         ablk[m + 1] - ablk[m], E->sharded ? C->L1 : ~0ull);
         return;
     }
+    // role B: the verified members' deltas into the pair table.  With a member
+    // the formation admitted on its tie-order guess (B->tpend < js): the
+    // decrements first (entries kept), a barrier of the first TIE_B blocks,
+    // the check against the keys those decrements zeroed (D can only have
+    // fallen by them before any member's turn; every block checks alike), then
+    // the increments -- or, if a member fails, the decrements reverted and the
+    // batch re-formed before it.  Every entry is cleared either way.
+    const bool tie = B->tpend < js;
+    const uint32_t nB = tie ? min(roleB_blocks, TIE_B) : roleB_blocks, bidB = blockIdx.x;
+    if (bidB >= nB) return;
+    const uint32_t Wd = min(DENSE, z0 + k);
+    const uint32_t per = SH ? xbat_member_words(Wd) : 1 + 4 * Wd;
+    const uint32_t dense_total = k * per;
+    const uint32_t nsh = SH ? (E->xsp_in ? E->nshards : 1u) : 0u;
+    const uint32_t total = dense_total + (SH ? ssp[nsh] : snl[k * 4]);
+    const uint32_t hotT = C->hot_T;
+    const bool hot = E->hot != 0;
+    long long dD = 0, dD1 = 0;
+    uint32_t nins = 0, nupd = 0, nzero = 0;
+    // mode 0: every entry; 1: the decrements, entries kept; 2: the increments;
+    // 3: the decrements reverted (2 and 3 clear every entry)
+    auto pass = [&](uint32_t mode) {
+        const bool clear = mode != 1;
+        for (uint32_t t0 = bidB * blockDim.x; t0 < total; t0 += nB * blockDim.x) {  // uniform per block
+            const uint32_t t = t0 + tid;
+            uint32_t m = BK, cat = 0, x = 0, val = 0;
+            if (SH && t < dense_total) {
+                // [R, bound, DL, DR, IL, IR] per member (R and bound were read by the prologue)
+                m = t / per;
+                const uint32_t r = t % per;
+                if (r == 0) {
+                    cat = 4;
+                    val = sRg[m];
+                } else if (r >= 2) {
+                    cat = (r - 2) / Wd;
+                    x = (r - 2) % Wd;
+                    uint32_t *pw = E->xbat + BK + (uint64_t)m * per + r;
+                    val = *pw;
+                    if (clear && val) *pw = 0;
+                }
+            } else if (t < dense_total) {
+                m = t / per;
+                const uint32_t r = t % per;
+                if (r == 0) {
+                    cat = 4;
+                    val = sR[m];
+                } else {
+                    cat = (r - 1) / Wd;
+                    x = (r - 1) % Wd;
+                    uint32_t *p0 = E->bvecd + ((uint64_t)(m * BREPL) * 4 + cat) * DENSE + x;
+#pragma unroll
+                    for (uint32_t rr = 0; rr < BREPL; rr++) {
+                        uint32_t *pr = p0 + (uint64_t)rr * 4 * DENSE;
+                        const uint32_t c = *pr;
+                        val += c;
+                        if (clear && c) *pr = 0;
+                    }
+                }
+            } else if (SH && t < total) {
+                // the shards' lists of ids >= DENSE: (member-vector << 24 | id, delta)
+                const uint32_t q = t - dense_total;
+                uint32_t sh = 0;
+                while (q >= ssp[sh + 1]) sh++;
+                const uint32_t *en = E->xsp_in + (uint64_t)sh * E->xsp_stride + 2 + 2 * (uint64_t)(q - ssp[sh]);
+                const uint32_t mv = en[0] >> 24;
+                m = mv / 4;
+                cat = mv % 4;
+                x = en[0] & 0xFFFFFFu;
+                val = en[1];
+            } else if (t < total) {
+                const uint32_t q = t - dense_total;
+                uint32_t mv = 0;
+                while (q >= snl[mv + 1]) mv++;
+                m = mv / 4;
+                cat = mv % 4;
+                const uint64_t base = (uint64_t)mv * E->bvs;
+                x = E->bvlist[base + (q - snl[mv])];
+                val = E->bvec[base + (x - DENSE)];
+                if (clear) E->bvec[base + (x - DENSE)] = 0;
+            }
+            bool hot_in = false;
+            uint32_t hslot = 0;
+            const bool dec = cat == 4 || cat == V_DL || cat == V_DR;
+            if (m < js && val != 0 && (mode == 0 || (mode == 2 ? !dec : dec))) {
+                const uint32_t a = sa[m], b = sb[m], z = z0 + m;
+                uint32_t u, v;
+                long long d;
+                if (cat == 4) { u = a; v = b; d = -(long long)val; }
+                else if (cat == V_DL) { u = x; v = a; d = -(long long)val; }
+                else if (cat == V_DR) { u = b; v = x; d = -(long long)val; }
+                else if (cat == V_IL) { u = x; v = z; d = val; }
+                else { u = z; v = x; d = val; }
+                if (mode == 3) d = -d;  // (the key exists: it was decremented)
+                const uint64_t slot = d > 0 && mode != 3 ? hinsert_c(E, u, v, &nins) : hfind(E, u, v);
+                if (slot == ~0ull) {
+                    C->err = d > 0 ? 2 : 1;
+                    if (E->dbg_form)
+                        printf("apply shard %u z0 %u k %u js %u: no key (%u, %u) for member %u cat %u delta %lld (x %u t %u)\n",
+                               E->shard, z0, k, js, u, v, m, cat, d, x, t);
+                } else {
+                    const uint32_t old = atomicAdd(&E->hcnt[(uint64_t)(slot) * E->hcs], (uint32_t)d);
+                    const uint32_t nw = old + (uint32_t)d;
+                    const long long dd = (long long)(nw != 0) - (long long)(old != 0);
+                    if (mode == 1) dD1 += dd;
+                    else if (mode != 3) dD += dd;
+                    if (d < 0 && nw == 0 && old != 0) nzero++;
+                    hot_in = hot && d > 0 && mode != 3 && nw >= hotT && old < hotT;
+                    hslot = (uint32_t)slot;
+                    nupd++;
+                }
+            }
+            if (hot) {
+                const uint32_t hp = wave_append(hot_in, &C->hot_n);
+                if (hot_in && hp < HOT_CAP) E->hot_slot[hp] = hslot;
+            }
+        }
+    };
+    __shared__ uint32_t sjf, szb[16];
+    uint32_t jf = js;  // the applied prefix
+    if (!tie) {
+        pass(0);
+    } else {
+        pass(1);
+        uint32_t zb = nzero;
+        for (int o = 32; o > 0; o >>= 1) zb += __shfl_xor(zb, o);
+        if ((tid & 63) == 0) szb[tid >> 6] = zb;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t zt = 0;
+            for (uint32_t w = 0; w < blockDim.x / 64; w++) zt += szb[w];
+            if (zt) atomicAdd(&B->ztot, zt);
+            __hip_atomic_fetch_add(&B->tbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long t0 = wall_clock64();
+            while (__hip_atomic_load(&B->tbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < nB) {
+                if (wall_clock64() - t0 > TIE_WAIT_TICKS) {  // (bounded: an error, never a hang)
+                    C->err = 9;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        if (tid < 64) {  // lane = member: its tie order under every B its turn can see
+            // (BPE_TIE_TEST: tests pretend every key was zeroed, so the check fails and the revert runs)
+            const uint32_t Z = E->tie_verify > 1 ? 0xFFFFFFFFu
+                                                 : __hip_atomic_load(&B->ztot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long D0 = C->D;
+            const uint64_t Bsz = C->B, lo = summary_B(D0 > Z ? D0 - Z : 0);
+            const bool f = lane >= 1 && lane < js &&
+                           !tie_levels_ok(lo, summary_B(D0 + B->tspan[lane]), Bsz, B->tmask[lane]);
+            const unsigned long long fm = __ballot(f);
+            if (lane == 0) sjf = fm ? (uint32_t)__ffsll(fm) - 1 : js;
+        }
+        __syncthreads();
+        if (sjf < js) {
+            pass(3);
+            jf = 0;
+            nzero = 0;
+        } else {
+            pass(2);
+            dD += dD1;
+        }
+    }
     if (blockIdx.x == 0) {
         // bookkeeping and the role-A descriptor for k_bsel's rewrite blocks
         const uint32_t top = C->occ_top;
-        if (tid < js) {
+        if (tid < jf) {
             const uint32_t md = C->merges_done;
             E->merges[2 * (md + tid)] = sa[tid];
             E->merges[2 * (md + tid) + 1] = sb[tid];
@@ -1413,12 +1615,12 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             B->ra_pre[tid] = spre[tid];
         }
         if (tid == 0) {
-            B->ra_pre[js] = spre[js];
+            B->ra_pre[jf] = spre[jf];
             B->ra_top = top;
             uint32_t xl = HOLE, xlb = 0;
             if (SH) {
                 const uint32_t xm = B->xl_m;
-                if (xm < js) {
+                if (xm < jf) {
                     xl = C->F1;
                     xlb = slb[xm];
                 }
@@ -1426,135 +1628,47 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             B->ra_xl = xl;
             B->ra_xlb = xlb;
             B->ra_done = 0;
-            B->ra_k = js;
-            B->jstar = js;
+            B->ra_k = jf;
+            B->jstar = jf;
             B->applied = 1;
-        }
-    }
-    // role B
-    const uint32_t nB = roleB_blocks, bidB = blockIdx.x;
-    const uint32_t Wd = min(DENSE, z0 + k);
-    const uint32_t per = SH ? xbat_member_words(Wd) : 1 + 4 * Wd;
-    const uint32_t dense_total = k * per;
-    const uint32_t nsh = SH ? (E->xsp_in ? E->nshards : 1u) : 0u;
-    const uint32_t total = dense_total + (SH ? ssp[nsh] : snl[k * 4]);
-    const uint32_t hotT = C->hot_T;
-    const bool hot = E->hot != 0;
-    long long dD = 0;
-    uint32_t nins = 0, nupd = 0;
-    for (uint32_t t0 = bidB * blockDim.x; t0 < total; t0 += nB * blockDim.x) {  // uniform per block
-        const uint32_t t = t0 + tid;
-        uint32_t m = BK, cat = 0, x = 0, val = 0;
-        if (SH && t < dense_total) {
-            // [R, bound, DL, DR, IL, IR] per member (R and bound were read by the prologue)
-            m = t / per;
-            const uint32_t r = t % per;
-            if (r == 0) {
-                cat = 4;
-                val = sRg[m];
-            } else if (r >= 2) {
-                cat = (r - 2) / Wd;
-                x = (r - 2) % Wd;
-                uint32_t *pw = E->xbat + BK + (uint64_t)m * per + r;
-                val = *pw;
-                if (val) *pw = 0;
-            }
-        } else if (t < dense_total) {
-            m = t / per;
-            const uint32_t r = t % per;
-            if (r == 0) {
-                cat = 4;
-                val = sR[m];
-            } else {
-                cat = (r - 1) / Wd;
-                x = (r - 1) % Wd;
-                uint32_t *p0 = E->bvecd + ((uint64_t)(m * BREPL) * 4 + cat) * DENSE + x;
-#pragma unroll
-                for (uint32_t rr = 0; rr < BREPL; rr++) {
-                    uint32_t *pr = p0 + (uint64_t)rr * 4 * DENSE;
-                    const uint32_t c = *pr;
-                    val += c;
-                    if (c) *pr = 0;
+            if (tie) {
+                B->ntie++;
+                if (jf < js) {
+                    B->ntfail++;
+                    B->retry = sjf;
                 }
             }
-        } else if (SH && t < total) {
-            // the shards' lists of ids >= DENSE: (member-vector << 24 | id, delta)
-            const uint32_t q = t - dense_total;
-            uint32_t sh = 0;
-            while (q >= ssp[sh + 1]) sh++;
-            const uint32_t *en = E->xsp_in + (uint64_t)sh * E->xsp_stride + 2 + 2 * (uint64_t)(q - ssp[sh]);
-            const uint32_t mv = en[0] >> 24;
-            m = mv / 4;
-            cat = mv % 4;
-            x = en[0] & 0xFFFFFFu;
-            val = en[1];
-        } else if (t < total) {
-            const uint32_t q = t - dense_total;
-            uint32_t mv = 0;
-            while (q >= snl[mv + 1]) mv++;
-            m = mv / 4;
-            cat = mv % 4;
-            const uint64_t base = (uint64_t)mv * E->bvs;
-            x = E->bvlist[base + (q - snl[mv])];
-            val = E->bvec[base + (x - DENSE)];
-            E->bvec[base + (x - DENSE)] = 0;
-        }
-        bool hot_in = false;
-        uint32_t hslot = 0;
-        if (m < js && val != 0) {
-            const uint32_t a = sa[m], b = sb[m], z = z0 + m;
-            uint32_t u, v;
-            long long d;
-            if (cat == 4) { u = a; v = b; d = -(long long)val; }
-            else if (cat == V_DL) { u = x; v = a; d = -(long long)val; }
-            else if (cat == V_DR) { u = b; v = x; d = -(long long)val; }
-            else if (cat == V_IL) { u = x; v = z; d = val; }
-            else { u = z; v = x; d = val; }
-            const uint64_t slot = d > 0 ? hinsert_c(E, u, v, &nins) : hfind(E, u, v);
-            if (slot == ~0ull) {
-                C->err = d > 0 ? 2 : 1;
-                if (E->dbg_form)
-                    printf("apply shard %u z0 %u k %u js %u: no key (%u, %u) for member %u cat %u delta %lld (x %u t %u)\n",
-                           E->shard, z0, k, js, u, v, m, cat, d, x, t);
-            } else {
-                const uint32_t old = atomicAdd(&E->hcnt[(uint64_t)(slot) * E->hcs], (uint32_t)d);
-                const uint32_t nw = old + (uint32_t)d;
-                dD += (long long)(nw != 0) - (long long)(old != 0);
-                hot_in = hot && d > 0 && nw >= hotT && old < hotT;
-                hslot = (uint32_t)slot;
-                nupd++;
-            }
-        }
-        if (hot) {
-            const uint32_t hp = wave_append(hot_in, &C->hot_n);
-            if (hot_in && hp < HOT_CAP) E->hot_slot[hp] = hslot;
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
         dD += __shfl_xor(dD, o);
         nins += __shfl_xor(nins, o);
         nupd += __shfl_xor(nupd, o);
+        nzero += __shfl_xor(nzero, o);
     }
     __shared__ long long sd[16];
-    __shared__ uint32_t si[16], su[16];
+    __shared__ uint32_t si[16], su[16], sz[16];
     if ((tid & 63) == 0) {
         sd[tid >> 6] = dD;
         si[tid >> 6] = nins;
         su[tid >> 6] = nupd;
+        sz[tid >> 6] = nzero;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         long long t = 0;
-        unsigned long long ni = 0, nu = 0;
+        unsigned long long ni = 0, nu = 0, nz = 0;
         for (uint32_t w = 0; w < blockDim.x / 64; w++) {
             t += sd[w];
             ni += si[w];
             nu += su[w];
+            nz += sz[w];
         }
         if (t != 0) atomicAdd(&B->dD, (unsigned long long)t);
         if (ni != 0) atomicAdd(&C->nkeys, ni);
         if (nu != 0) atomicAdd(&B->nupd, nu);
+        if (nz != 0) atomicAdd(&B->nzero, nz);
         atomicMax(&B->ap_out, wall_clock64());
     }
     ts_mark(E, bi, BT_APPLY_B, false, true);

@@ -478,6 +478,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.scan_tend, STAMPS))) return r;
     h.dbgts = nullptr;
     h.dbg_form = (uint32_t)getenv_int("BPE_DEBUG_FORM", 0);
+    h.tie_verify = (uint32_t)getenv_int("BPE_TIE_VERIFY", 1);
+    if (h.tie_verify && getenv_int("BPE_TIE_TEST", 0)) h.tie_verify = 2;  // (tests: every verification fails)
     if (getenv("BPE_DEBUG_TS") && !encode && (r = dalloc(c, &h.dbgts, (size_t)TS_SLOTS * TS_N))) return r;
     h.spec_on = SPEC_ON && !encode && (!c->sharded || h.xfused);
     h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? 1 + SPEC_RB + SPEC_SB : 0);
@@ -1307,7 +1309,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             return 0;
         case STOP_ERROR:
             return fail(C.err == 5 ? BPE_GPU_ERANGE : BPE_GPU_EINTERNAL,
-                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than an end code holds (2^31 - 3 bytes)" : C.err == 7 ? "tracked iterations: the light pass waited for the track block in vain" : "thread-stat table full");
+                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than an end code holds (2^31 - 3 bytes)" : C.err == 7 ? "tracked iterations: the light pass waited for the track block in vain" : C.err == 9 ? "batch apply: the tie-verification barrier timed out" : "thread-stat table full");
         case STOP_REDO:  // missed prediction: k_select committed the real merge
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;
@@ -1481,6 +1483,9 @@ int batch_stats(bpe_gpu_ctx *c) {
     c->stats.batch_retries = hb.nretry;
     c->stats.table_updates = hb.nupd;
     for (int k = 0; k < 8; k++) c->stats.batch_end[k] = hb.why[k];
+    c->stats.tie_verified = hb.ntie;
+    c->stats.tie_failed = hb.ntfail;
+    c->stats.keys_zeroed = hb.nzero;
     {
         unsigned long long t[2] = {0, 0};  // (sl_ticks, nsl: outside the head copied above)
         HIPCHK(hipMemcpy(t, &c->h.bat->sl_ticks, 16, hipMemcpyDeviceToHost));
@@ -1500,8 +1505,10 @@ int batch_stats(bpe_gpu_ctx *c) {
     if (c->h.dbgts) print_batch_timeline(c, hb.nbatch + hb.nretry);
     if (getenv("BPE_DEBUG"))
         fprintf(stderr, "batches %llu, dropped %llu, re-formed %llu; formation ended by: list %llu, cap/count/hot_T %llu, a==b %llu, "
-                "duplicate %llu, tie %llu, conflict %llu, table margin %llu, staging %llu\n", hb.nbatch, hb.ndrop, hb.nretry,
-                hb.why[0], hb.why[1], hb.why[2], hb.why[3], hb.why[4], hb.why[5], hb.why[6], hb.why[7]);
+                "duplicate %llu, tie %llu, conflict %llu, table margin %llu, staging %llu; tie-verified %llu (re-formed %llu); "
+                "keys zeroed %llu\n", hb.nbatch, hb.ndrop, hb.nretry,
+                hb.why[0], hb.why[1], hb.why[2], hb.why[3], hb.why[4], hb.why[5], hb.why[6], hb.why[7], hb.ntie, hb.ntfail,
+                hb.nzero);
     return 0;
 }
 

@@ -682,6 +682,9 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     for (int k = 0; k < 8; k++) g->stats.batch_end[k] = s0.batch_end[k];
     g->stats.ms_select_span = s0.ms_select_span;
     g->stats.select_launches = s0.select_launches;
+    g->stats.tie_verified = s0.tie_verified;
+    g->stats.tie_failed = s0.tie_failed;
+    g->stats.keys_zeroed = s0.keys_zeroed;
     g->stats.ms_scan_span = s0.ms_scan_span;
     g->stats.ms_apply_span = s0.ms_apply_span;
     g->stats.hot_rebuilds = g->cs[0]->hC->hot_rebuilds;

@@ -215,12 +215,51 @@ def test_config2_recount_checkpoints(c2_run, part):
         e.close()
 
 
-def test_config3_1g_eight_shards_equals_single_engine():
+C3_MERGES_MD5 = "b58e334e1360ca73030996c9cdfe044a"  # 1 GiB x 1024 (train_1024), every engine form
+C3_IDS_CHECKSUM = 0x9EB1D5D726D3C952
+
+
+@pytest.mark.parametrize("mode", ["verify", "forced_fail", "off"])
+def test_verified_tie_order_1g_1024(mode, monkeypatch):
+    """Members admitted on a tie order that holds only if the earlier members
+    zero few keys (k_bapply: decrements, count of zeroed keys, check, then
+    increments or revert): the same merges and ids as without them (off), with
+    the check passing (verify) and with every check failing (forced_fail:
+    decrements reverted, batch re-formed before the member)."""
+    monkeypatch.setenv("BPE_TIE_VERIFY", "0" if mode == "off" else "1")
+    if mode == "forced_fail":
+        monkeypatch.setenv("BPE_TIE_TEST", "1")
+    e = api.Engine(0)
+    try:
+        e.synth(2, GIB)
+        assert e.train(1024) == 1024
+        st = e.stats()
+        assert hashlib.md5(e.merges().tobytes()).hexdigest() == C3_MERGES_MD5
+        assert e.ids_checksum() == C3_IDS_CHECKSUM
+    finally:
+        e.close()
+    print(mode, {k: st[k] for k in ("batches", "batch_retries", "tie_verified", "tie_failed", "keys_zeroed", "end_tie")})
+    if mode == "verify":
+        assert st["tie_verified"] > 0 and st["tie_failed"] == 0
+    elif mode == "forced_fail":
+        assert st["tie_failed"] > 0 and st["tie_failed"] == st["tie_verified"] and st["batch_retries"] >= st["tie_failed"]
+    else:
+        assert st["tie_verified"] == 0
+
+
+@pytest.mark.parametrize("ties", ["verify", "forced_fail"])
+def test_config3_1g_eight_shards_equals_single_engine(ties, monkeypatch):
+    """8 shards of the 1 GiB corpus == the single engine; forced_fail: every
+    tie-order check of the sharded batches fails (BPE_TIE_TEST), so each shard
+    reverts the same decrements and re-forms the same batch"""
     e = api.Engine(0)
     e.synth(2, GIB)
     assert e.train(1024) == 1024
     M, csum, n_out = e.merges(), e.ids_checksum(), e.stats()["n_out"]
     e.close()
+    assert hashlib.md5(M.tobytes()).hexdigest() == C3_MERGES_MD5 and csum == C3_IDS_CHECKSUM
+    if ties == "forced_fail":
+        monkeypatch.setenv("BPE_TIE_TEST", "1")
     g = api.ShardGroup(0, local_shards=8)
     step = GIB // 8
     for q in range(8):
@@ -229,7 +268,10 @@ def test_config3_1g_eight_shards_equals_single_engine():
     assert (g.merges() == M).all()
     s, n = g.ids_checksum()
     assert n == n_out and s == csum
+    st = g.stats()
     g.close()
+    assert st["tie_verified"] > 0
+    assert (st["tie_failed"] > 0) == (ties == "forced_fail")
 
 
 def test_config3_reference_golden_at_eight_shards():
