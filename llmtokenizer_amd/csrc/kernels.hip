@@ -2711,65 +2711,25 @@ __device__ inline uint32_t tile_count(const uint32_t *hist, const uint32_t *tot,
 #ifndef BPE_SORT_T
 #define BPE_SORT_T 1024
 #endif
-#ifndef BPE_SORT_DIAG
-#define BPE_SORT_DIAG 0
-#endif
-#ifndef BPE_SORT_EU
-#define BPE_SORT_EU 4  // the copy-out loop's unroll (registers)
-#endif
-#ifndef BPE_SORT_WAVES
-#define BPE_SORT_WAVES 1
-#endif
-// waves per SIMD the sort passes are compiled for (8: two 1024-thread blocks per CU,
-// <= 64 VGPRs, but that spills; 1: no constraint)
-constexpr uint32_t SORT_WAVES = BPE_SORT_WAVES;
 constexpr uint32_t SORT_T = BPE_SORT_T, SORT_PER = 8, SORT_CH = SORT_T * SORT_PER;
 constexpr uint32_t SORT_LOCAL_BITS = 24;
 
 struct SortLds {
     uint32_t ent[SORT_CH];  // staged entries in local bin order
-    uint32_t dst[SORT_CH];  // their slots in out (the emit has no dependent LDS lookups)
+    uint8_t bin[SORT_CH];   // their bins
     uint32_t cnt[256], lstart[256], gcur[256], gstart[256];
-    uint32_t total;
-};  // 66 KB: two 1024-thread blocks per CU (the 32-wave cap allows two anyway)
-
-// before the first lds_sort_emit (the block barrier after it is the caller's)
-__device__ inline void lds_sort_init(SortLds &L) {
-    for (uint32_t x = threadIdx.x; x < 256; x += SORT_T) L.cnt[x] = 0;
-}
+};  // 44 KB: three 1024-thread blocks per CU
 
 // local counting sort of this thread's SORT_PER (bin, entry) pairs, then a
 // coalesced copy of every bin's run to out[gcur[bin] ...]; gcur advances.
-// get(k, &bin, &val) gives the thread's k-th pair (bin >= nb: no entry); it is
-// called once per phase so that no per-entry array stays live across the
-// barriers (registers: two blocks per CU need <= 64).  Four block barriers
-// per chunk: ranks | scan | staging | copy (+ the counters cleared for the
-// next chunk).
-template <class F>
-__device__ inline void lds_sort_emit(SortLds &L, F get, uint32_t nb, uint32_t *__restrict__ out) {
-#if BPE_SORT_DIAG == 1  // (timing diagnostics only: a plain coalesced copy, no sort)
-    {
-        __shared__ uint32_t base;
-        if (threadIdx.x == 0) base = L.gcur[0];
-        __syncthreads();
-#pragma unroll
-        for (uint32_t k = 0; k < SORT_PER; k++) {
-            uint32_t b, v;
-            get(k, &b, &v);
-            if (b < nb) out[base + k * SORT_T + threadIdx.x] = v;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) L.gcur[0] += SORT_CH;
-        return;
-    }
-#endif
+// bins[k] >= nb: no entry.
+__device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const uint32_t *vals, uint32_t nb,
+                                     uint32_t *__restrict__ out) {
+    for (uint32_t x = threadIdx.x; x < nb; x += SORT_T) L.cnt[x] = 0;
+    __syncthreads();
     uint32_t rank[SORT_PER];
 #pragma unroll
-    for (uint32_t k = 0; k < SORT_PER; k++) {
-        uint32_t b, v;
-        get(k, &b, &v);
-        rank[k] = b < nb ? atomicAdd(&L.cnt[b], 1u) : 0;
-    }
+    for (uint32_t k = 0; k < SORT_PER; k++) rank[k] = bins[k] < nb ? atomicAdd(&L.cnt[bins[k]], 1u) : 0;
     __syncthreads();
     if (threadIdx.x < 64) {
         // wave-parallel exclusive scan over the (<= 256) bins, 4 per lane
@@ -2797,31 +2757,23 @@ __device__ inline void lds_sort_emit(SortLds &L, F get, uint32_t nb, uint32_t *_
             }
             r += c[q];
         }
-        if (lane == 63) L.total = incl;
+        const uint32_t total = __shfl(incl, 63);
+        if (lane == 0) L.cnt[0] = total;  // total staged (cnt[] no longer needed)
     }
     __syncthreads();
-#pragma unroll BPE_SORT_EU
-    for (uint32_t k = 0; k < SORT_PER; k++) {
-        uint32_t b, v;
-        get(k, &b, &v);
-        if (b < nb) {
-            const uint32_t s = L.lstart[b] + rank[k];
-            L.ent[s] = v;
-            L.dst[s] = L.gstart[b] + rank[k];
+#pragma unroll
+    for (uint32_t k = 0; k < SORT_PER; k++)
+        if (bins[k] < nb) {
+            const uint32_t s = L.lstart[bins[k]] + rank[k];
+            L.ent[s] = vals[k];
+            L.bin[s] = (uint8_t)bins[k];
         }
-    }
     __syncthreads();
-    const uint32_t total = L.total;
-#pragma unroll BPE_SORT_EU
-    for (uint32_t k = 0; k < SORT_PER; k++) {
-        const uint32_t s = k * SORT_T + threadIdx.x;
-#if BPE_SORT_DIAG == 2  // (timing diagnostics only: the LDS sort without the stores)
-        if (s < total && L.ent[s] == 0xFFFFFFFFu) out[L.dst[s]] = 0;
-#else
-        if (s < total) out[L.dst[s]] = L.ent[s];
-#endif
+    const uint32_t total = L.cnt[0];
+    for (uint32_t s = threadIdx.x; s < total; s += SORT_T) {
+        const uint32_t bn = L.bin[s];
+        out[L.gstart[bn] + (s - L.lstart[bn])] = L.ent[s];
     }
-    for (uint32_t x = threadIdx.x; x < nb; x += SORT_T) L.cnt[x] = 0;
     __syncthreads();
 }
 
@@ -2834,7 +2786,7 @@ __device__ inline void lds_sort_emit(SortLds &L, F get, uint32_t nb, uint32_t *_
 // after a word comes from the next lane), so each widened uint4 store is one
 // contiguous 1-KB run of tok[]; the next round's words are loaded before this
 // round's LDS sort.
-__global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_WAVES, 8))) void k_sort_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
+__global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
                                                    uint64_t tile, uint32_t G, uint32_t *__restrict__ tmp) {
     static_assert(SORT_PER == 8, "two 4-byte words per lane and round");
     __shared__ SortLds L;
@@ -2842,7 +2794,6 @@ __global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_WAV
     const uint32_t A = E->A, AA = A * A;
     const uint32_t t = blockIdx.x;
     for (uint32_t x = threadIdx.x; x < 256; x += SORT_T) rk[x] = E->rank[x];
-    lds_sort_init(L);
     if (threadIdx.x < A) {  // (independent loads: unrolled so they are in flight together)
         uint32_t s0 = E->poff[threadIdx.x * A];
         const uint32_t *hr = hist + (uint64_t)t * AA + threadIdx.x * A;
@@ -2884,23 +2835,21 @@ __global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_WAV
         uint32_t nx0 = __shfl_down(x0, 1), nx1 = __shfl_down(x1, 1);
         const uint32_t f = __shfl(x1, 0);
         if (lane == 63) { nx0 = f; nx1 = b8; }
+        uint32_t bins[SORT_PER], vals[SORT_PER];
 #pragma unroll
         for (uint32_t h = 0; h < 2; h++) {
-            const uint64_t p = wb + 256 * h + 4 * lane;
-            if (p < te) store(p / 4, h ? x1 : x0);
-        }
-        // pair k of the lane: word h = k / 4, byte k % 4 and the byte after it
-        const uint32_t pl = (uint32_t)(wb - gs) + 4 * lane;  // (position - group start, < 2^24)
-        const uint32_t lim = e > wb + 4 * lane ? (uint32_t)min<uint64_t>(e - wb - 4 * lane, 1024) : 0u;
-        lds_sort_emit(L, [&](uint32_t k, uint32_t *bin, uint32_t *val) {
-            const uint32_t h = k / 4, j = k % 4;
             const uint32_t x = h ? x1 : x0, nx = h ? nx1 : nx0;
-            const uint32_t b0 = (x >> (8 * j)) & 0xFF, b1 = j < 3 ? (x >> (8 * j + 8)) & 0xFF : nx & 0xFF;
-            const uint32_t off = 256 * h + j;  // pair position - (wb + 4 lane)
-            const bool in = off < lim;
-            *bin = in ? rk[b0] : 256u;
-            *val = (rk[b1] << SORT_LOCAL_BITS) | (pl + off);
-        }, A, tmp);
+            const uint64_t p = wb + 256 * h + 4 * lane;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const uint32_t b0 = (x >> (8 * k)) & 0xFF, b1 = k < 3 ? (x >> (8 * k + 8)) & 0xFF : nx & 0xFF;
+                const bool in = p + k < e;
+                bins[4 * h + k] = in ? rk[b0] : 256u;
+                vals[4 * h + k] = in ? (rk[b1] << SORT_LOCAL_BITS) | (uint32_t)(p + k - gs) : 0u;
+            }
+            if (p < te) store(p / 4, x);
+        }
+        lds_sort_emit(L, bins, vals, A, tmp);
     }
 }
 
@@ -2911,7 +2860,7 @@ __global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_WAV
 // 8 K-entry rounds instead of ~1.4 rounds per (tile, k1) of ~11 K entries
 // (1 GiB, 1 M-position tiles: G = 16), and the unit set-up once per G tiles.
 // Entries hold their position relative to the group's start (pass A).
-__global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_WAVES, 8))) void k_sort_b(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
+__global__ __launch_bounds__(SORT_T) void k_sort_b(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
                                                    const uint32_t *__restrict__ tot, uint32_t ntl, uint64_t tile,
                                                    uint32_t G, const uint32_t *__restrict__ tmp) {
     __shared__ SortLds L;
@@ -2937,7 +2886,6 @@ __global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_WAV
         }
     };
     prefetch(blockIdx.x);
-    lds_sort_init(L);
     for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
         const uint32_t gi = u / A;
         const uint32_t gbase = (uint32_t)((uint64_t)gi * G * tile);  // positions are u32 (n0 <= 2^32 - 2)
@@ -2953,26 +2901,16 @@ __global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_WAV
         __syncthreads();
         const uint32_t lo = range[0], n = range[1];
         prefetch(u + gridDim.x);
-        // the next chunk's entries are loaded before this chunk's LDS sort
-        uint32_t wn[SORT_PER];
-        auto load = [&](uint32_t q0) {
+        for (uint32_t q0 = 0; q0 < n; q0 += SORT_CH) {
+            uint32_t bins[SORT_PER], vals[SORT_PER];
 #pragma unroll
             for (uint32_t k = 0; k < SORT_PER; k++) {
                 const uint32_t q = q0 + k * SORT_T + threadIdx.x;  // coalesced reads
-                wn[k] = q < n ? tmp[lo + q] : 0u;
+                const uint32_t w = q < n ? tmp[lo + q] : 0u;
+                bins[k] = q < n ? w >> SORT_LOCAL_BITS : 256u;
+                vals[k] = gbase + (w & LOCAL);
             }
-        };
-        load(0);
-        for (uint32_t q0 = 0; q0 < n; q0 += SORT_CH) {
-            uint32_t w[SORT_PER];
-#pragma unroll
-            for (uint32_t k = 0; k < SORT_PER; k++) w[k] = wn[k];
-            load(q0 + SORT_CH);
-            const uint32_t lim = n - q0;
-            lds_sort_emit(L, [&](uint32_t k, uint32_t *bin, uint32_t *val) {
-                *bin = k * SORT_T + threadIdx.x < lim ? w[k] >> SORT_LOCAL_BITS : 256u;
-                *val = gbase + (w[k] & LOCAL);
-            }, A, E->plist);
+            lds_sort_emit(L, bins, vals, A, E->plist);
         }
     }
 }
