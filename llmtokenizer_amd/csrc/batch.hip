@@ -58,11 +58,6 @@ constexpr uint32_t FR = BPE_FR;
 #define BPE_SCAN_PF 1
 #endif
 constexpr uint32_t RU = BPE_RU;  // rewrite occurrences per thread per round
-// verified tie order: k_bapply's blocks taking part in its phase barrier (the
-// rest exit; 1024-thread blocks, one per CU: half the CUs must be resident) and
-// the bound on that barrier's wait (wall-clock ticks, 100 MHz: 0.5 s)
-constexpr uint32_t TIE_B = 128;
-constexpr unsigned long long TIE_WAIT_TICKS = 50000000ull;
 
 // debug timeline of a batch (BPE_DEBUG_TS; E->dbgts rows indexed by batch)
 enum { BT_SCAN_IN = 0, BT_SCAN_CAND, BT_SCAN_OUT, BT_APPLY_IN, BT_APPLY_PRO, BT_APPLY_A, BT_APPLY_B, BT_SEL_IN,
@@ -409,6 +404,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->tpend = pm ? (uint32_t)__ffsll(pm) - 1 : BK;
                 B->ztot = 0;
                 B->tbar = 0;
+                B->tlog_n = 0;
                 B->why[why_end]++;
                 if (ties > 1) C->counters[2]++;
             }
@@ -1434,169 +1430,173 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         return;
     }
     // role B: the verified members' deltas into the pair table.  With a member
-    // the formation admitted on its tie-order guess (B->tpend < js): the
-    // decrements first (entries kept), a barrier of the first TIE_B blocks,
-    // the check against the keys those decrements zeroed (D can only have
-    // fallen by them before any member's turn; every block checks alike), then
-    // the increments -- or, if a member fails, the decrements reverted and the
-    // batch re-formed before it.  Every entry is cleared either way.
-    const bool tie = B->tpend < js;
-    const uint32_t nB = tie ? min(roleB_blocks, TIE_B) : roleB_blocks, bidB = blockIdx.x;
-    if (bidB >= nB) return;
+    // the formation admitted on its tie-order guess (B->tpend < js), every
+    // update also goes to an undo log and the keys the decrements zero are
+    // counted; the last block to finish checks those members' order under the
+    // B_final range that count allows (D can only have fallen by those keys
+    // before any member's turn) and, if one fails, reverts the logged updates
+    // and has the batch re-formed before it.  No block waits on another.
+    const uint32_t nB = roleB_blocks, bidB = blockIdx.x;
     const uint32_t Wd = min(DENSE, z0 + k);
     const uint32_t per = SH ? xbat_member_words(Wd) : 1 + 4 * Wd;
     const uint32_t dense_total = k * per;
     const uint32_t nsh = SH ? (E->xsp_in ? E->nshards : 1u) : 0u;
     const uint32_t total = dense_total + (SH ? ssp[nsh] : snl[k * 4]);
+    // (a batch whose entries could overflow the undo log applies nothing and
+    // is re-formed before its first such member: every block decides alike)
+    const bool lfull = B->tpend < sj && total > E->tlog_cap;
+    const bool tie = B->tpend < sj && !lfull;
+    const uint32_t jsB = lfull ? 0u : sj;
     const uint32_t hotT = C->hot_T;
     const bool hot = E->hot != 0;
-    long long dD = 0, dD1 = 0;
+    long long dD = 0;
     uint32_t nins = 0, nupd = 0, nzero = 0;
-    // mode 0: every entry; 1: the decrements, entries kept; 2: the increments;
-    // 3: the decrements reverted (2 and 3 clear every entry)
-    auto pass = [&](uint32_t mode) {
-        const bool clear = mode != 1;
-        for (uint32_t t0 = bidB * blockDim.x; t0 < total; t0 += nB * blockDim.x) {  // uniform per block
-            const uint32_t t = t0 + tid;
-            uint32_t m = BK, cat = 0, x = 0, val = 0;
-            if (SH && t < dense_total) {
-                // [R, bound, DL, DR, IL, IR] per member (R and bound were read by the prologue)
-                m = t / per;
-                const uint32_t r = t % per;
-                if (r == 0) {
-                    cat = 4;
-                    val = sRg[m];
-                } else if (r >= 2) {
-                    cat = (r - 2) / Wd;
-                    x = (r - 2) % Wd;
-                    uint32_t *pw = E->xbat + BK + (uint64_t)m * per + r;
-                    val = *pw;
-                    if (clear && val) *pw = 0;
-                }
-            } else if (t < dense_total) {
-                m = t / per;
-                const uint32_t r = t % per;
-                if (r == 0) {
-                    cat = 4;
-                    val = sR[m];
-                } else {
-                    cat = (r - 1) / Wd;
-                    x = (r - 1) % Wd;
-                    uint32_t *p0 = E->bvecd + ((uint64_t)(m * BREPL) * 4 + cat) * DENSE + x;
+    for (uint32_t t0 = bidB * blockDim.x; t0 < total; t0 += nB * blockDim.x) {  // uniform per block
+        const uint32_t t = t0 + tid;
+        uint32_t m = BK, cat = 0, x = 0, val = 0;
+        if (SH && t < dense_total) {
+            // [R, bound, DL, DR, IL, IR] per member (R and bound were read by the prologue)
+            m = t / per;
+            const uint32_t r = t % per;
+            if (r == 0) {
+                cat = 4;
+                val = sRg[m];
+            } else if (r >= 2) {
+                cat = (r - 2) / Wd;
+                x = (r - 2) % Wd;
+                uint32_t *pw = E->xbat + BK + (uint64_t)m * per + r;
+                val = *pw;
+                if (val) *pw = 0;
+            }
+        } else if (t < dense_total) {
+            m = t / per;
+            const uint32_t r = t % per;
+            if (r == 0) {
+                cat = 4;
+                val = sR[m];
+            } else {
+                cat = (r - 1) / Wd;
+                x = (r - 1) % Wd;
+                uint32_t *p0 = E->bvecd + ((uint64_t)(m * BREPL) * 4 + cat) * DENSE + x;
 #pragma unroll
-                    for (uint32_t rr = 0; rr < BREPL; rr++) {
-                        uint32_t *pr = p0 + (uint64_t)rr * 4 * DENSE;
-                        const uint32_t c = *pr;
-                        val += c;
-                        if (clear && c) *pr = 0;
-                    }
-                }
-            } else if (SH && t < total) {
-                // the shards' lists of ids >= DENSE: (member-vector << 24 | id, delta)
-                const uint32_t q = t - dense_total;
-                uint32_t sh = 0;
-                while (q >= ssp[sh + 1]) sh++;
-                const uint32_t *en = E->xsp_in + (uint64_t)sh * E->xsp_stride + 2 + 2 * (uint64_t)(q - ssp[sh]);
-                const uint32_t mv = en[0] >> 24;
-                m = mv / 4;
-                cat = mv % 4;
-                x = en[0] & 0xFFFFFFu;
-                val = en[1];
-            } else if (t < total) {
-                const uint32_t q = t - dense_total;
-                uint32_t mv = 0;
-                while (q >= snl[mv + 1]) mv++;
-                m = mv / 4;
-                cat = mv % 4;
-                const uint64_t base = (uint64_t)mv * E->bvs;
-                x = E->bvlist[base + (q - snl[mv])];
-                val = E->bvec[base + (x - DENSE)];
-                if (clear) E->bvec[base + (x - DENSE)] = 0;
-            }
-            bool hot_in = false;
-            uint32_t hslot = 0;
-            const bool dec = cat == 4 || cat == V_DL || cat == V_DR;
-            if (m < js && val != 0 && (mode == 0 || (mode == 2 ? !dec : dec))) {
-                const uint32_t a = sa[m], b = sb[m], z = z0 + m;
-                uint32_t u, v;
-                long long d;
-                if (cat == 4) { u = a; v = b; d = -(long long)val; }
-                else if (cat == V_DL) { u = x; v = a; d = -(long long)val; }
-                else if (cat == V_DR) { u = b; v = x; d = -(long long)val; }
-                else if (cat == V_IL) { u = x; v = z; d = val; }
-                else { u = z; v = x; d = val; }
-                if (mode == 3) d = -d;  // (the key exists: it was decremented)
-                const uint64_t slot = d > 0 && mode != 3 ? hinsert_c(E, u, v, &nins) : hfind(E, u, v);
-                if (slot == ~0ull) {
-                    C->err = d > 0 ? 2 : 1;
-                    if (E->dbg_form)
-                        printf("apply shard %u z0 %u k %u js %u: no key (%u, %u) for member %u cat %u delta %lld (x %u t %u)\n",
-                               E->shard, z0, k, js, u, v, m, cat, d, x, t);
-                } else {
-                    const uint32_t old = atomicAdd(&E->hcnt[(uint64_t)(slot) * E->hcs], (uint32_t)d);
-                    const uint32_t nw = old + (uint32_t)d;
-                    const long long dd = (long long)(nw != 0) - (long long)(old != 0);
-                    if (mode == 1) dD1 += dd;
-                    else if (mode != 3) dD += dd;
-                    if (d < 0 && nw == 0 && old != 0) nzero++;
-                    hot_in = hot && d > 0 && mode != 3 && nw >= hotT && old < hotT;
-                    hslot = (uint32_t)slot;
-                    nupd++;
+                for (uint32_t rr = 0; rr < BREPL; rr++) {
+                    uint32_t *pr = p0 + (uint64_t)rr * 4 * DENSE;
+                    const uint32_t c = *pr;
+                    val += c;
+                    if (c) *pr = 0;
                 }
             }
-            if (hot) {
-                const uint32_t hp = wave_append(hot_in, &C->hot_n);
-                if (hot_in && hp < HOT_CAP) E->hot_slot[hp] = hslot;
+        } else if (SH && t < total) {
+            // the shards' lists of ids >= DENSE: (member-vector << 24 | id, delta)
+            const uint32_t q = t - dense_total;
+            uint32_t sh = 0;
+            while (q >= ssp[sh + 1]) sh++;
+            const uint32_t *en = E->xsp_in + (uint64_t)sh * E->xsp_stride + 2 + 2 * (uint64_t)(q - ssp[sh]);
+            const uint32_t mv = en[0] >> 24;
+            m = mv / 4;
+            cat = mv % 4;
+            x = en[0] & 0xFFFFFFu;
+            val = en[1];
+        } else if (t < total) {
+            const uint32_t q = t - dense_total;
+            uint32_t mv = 0;
+            while (q >= snl[mv + 1]) mv++;
+            m = mv / 4;
+            cat = mv % 4;
+            const uint64_t base = (uint64_t)mv * E->bvs;
+            x = E->bvlist[base + (q - snl[mv])];
+            val = E->bvec[base + (x - DENSE)];
+            E->bvec[base + (x - DENSE)] = 0;
+        }
+        bool hot_in = false, logged = false;
+        uint32_t hslot = 0, dlog = 0;
+        if (m < jsB && val != 0) {
+            const uint32_t a = sa[m], b = sb[m], z = z0 + m;
+            uint32_t u, v;
+            long long d;
+            if (cat == 4) { u = a; v = b; d = -(long long)val; }
+            else if (cat == V_DL) { u = x; v = a; d = -(long long)val; }
+            else if (cat == V_DR) { u = b; v = x; d = -(long long)val; }
+            else if (cat == V_IL) { u = x; v = z; d = val; }
+            else { u = z; v = x; d = val; }
+            const uint64_t slot = d > 0 ? hinsert_c(E, u, v, &nins) : hfind(E, u, v);
+            if (slot == ~0ull) {
+                C->err = d > 0 ? 2 : 1;
+                if (E->dbg_form)
+                    printf("apply shard %u z0 %u k %u js %u: no key (%u, %u) for member %u cat %u delta %lld (x %u t %u)\n",
+                           E->shard, z0, k, jsB, u, v, m, cat, d, x, t);
+            } else {
+                const uint32_t old = atomicAdd(&E->hcnt[(uint64_t)(slot) * E->hcs], (uint32_t)d);
+                const uint32_t nw = old + (uint32_t)d;
+                dD += (long long)(nw != 0) - (long long)(old != 0);
+                if (d < 0 && nw == 0 && old != 0) nzero++;
+                hot_in = hot && d > 0 && nw >= hotT && old < hotT;
+                hslot = (uint32_t)slot;
+                logged = tie;
+                dlog = (uint32_t)d;
+                nupd++;
             }
         }
-    };
-    __shared__ uint32_t sjf, szb[16];
-    uint32_t jf = js;  // the applied prefix
-    if (!tie) {
-        pass(0);
-    } else {
-        pass(1);
+        if (hot) {
+            const uint32_t hp = wave_append(hot_in, &C->hot_n);
+            if (hot_in && hp < HOT_CAP) E->hot_slot[hp] = hslot;
+        }
+        if (tie) {  // (uniform) the undo log: (slot, delta)
+            const uint32_t lp = wave_append(logged, &B->tlog_n);
+            if (logged) {
+                E->tlog[2 * (uint64_t)lp] = hslot;
+                E->tlog[2 * (uint64_t)lp + 1] = dlog;
+            }
+        }
+    }
+    __shared__ uint32_t sjf, slast, szb[16];
+    uint32_t jf = jsB;  // the applied prefix
+    bool keep = !tie && blockIdx.x == 0;  // this block writes the bookkeeping
+    if (tie) {
         uint32_t zb = nzero;
         for (int o = 32; o > 0; o >>= 1) zb += __shfl_xor(zb, o);
         if ((tid & 63) == 0) szb[tid >> 6] = zb;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
             uint32_t zt = 0;
             for (uint32_t w = 0; w < blockDim.x / 64; w++) zt += szb[w];
             if (zt) atomicAdd(&B->ztot, zt);
-            __hip_atomic_fetch_add(&B->tbar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long t0 = wall_clock64();
-            while (__hip_atomic_load(&B->tbar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < nB) {
-                if (wall_clock64() - t0 > TIE_WAIT_TICKS) {  // (bounded: an error, never a hang)
-                    C->err = 9;
-                    break;
+            // (release: my log entries, table updates and zero count before the ticket)
+            slast = __hip_atomic_fetch_add(&B->tbar, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nB - 1;
+        }
+        __syncthreads();
+        if (!slast) {
+            jf = BK;  // (not mine to decide: no bookkeeping here)
+        } else {
+            keep = true;
+            if (tid < 64) {  // lane = member: its tie order under every B its turn can see
+                // (BPE_TIE_TEST: tests pretend every key was zeroed, so the check fails and the revert runs)
+                const uint32_t Z = E->tie_verify > 1 ? 0xFFFFFFFFu
+                                                     : __hip_atomic_load(&B->ztot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long D0 = C->D;
+                const uint64_t Bsz = C->B, lo = summary_B(D0 > Z ? D0 - Z : 0);
+                const bool f = lane >= 1 && lane < jsB &&
+                               !tie_levels_ok(lo, summary_B(D0 + B->tspan[lane]), Bsz, B->tmask[lane]);
+                const unsigned long long fm = __ballot(f);
+                if (lane == 0) sjf = fm ? (uint32_t)__ffsll(fm) - 1 : jsB;
+            }
+            __syncthreads();
+            if (sjf < jsB) {  // revert every logged update (this block alone: rare)
+                const uint32_t nl = __hip_atomic_load(&B->tlog_n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                long long rd = 0;
+                for (uint32_t q = tid; q < nl; q += blockDim.x) {
+                    const uint32_t slot = E->tlog[2 * (uint64_t)q], d = E->tlog[2 * (uint64_t)q + 1];
+                    const uint32_t old = atomicAdd(&E->hcnt[(uint64_t)slot * E->hcs], 0u - d);
+                    rd += (long long)(old - d != 0) - (long long)(old != 0);
                 }
-                __builtin_amdgcn_s_sleep(1);
+                dD += rd;  // (this block's sum below carries the whole revert's D change)
+                nzero = 0;
+                jf = 0;
             }
         }
-        __syncthreads();
-        if (tid < 64) {  // lane = member: its tie order under every B its turn can see
-            // (BPE_TIE_TEST: tests pretend every key was zeroed, so the check fails and the revert runs)
-            const uint32_t Z = E->tie_verify > 1 ? 0xFFFFFFFFu
-                                                 : __hip_atomic_load(&B->ztot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long D0 = C->D;
-            const uint64_t Bsz = C->B, lo = summary_B(D0 > Z ? D0 - Z : 0);
-            const bool f = lane >= 1 && lane < js &&
-                           !tie_levels_ok(lo, summary_B(D0 + B->tspan[lane]), Bsz, B->tmask[lane]);
-            const unsigned long long fm = __ballot(f);
-            if (lane == 0) sjf = fm ? (uint32_t)__ffsll(fm) - 1 : js;
-        }
-        __syncthreads();
-        if (sjf < js) {
-            pass(3);
-            jf = 0;
-            nzero = 0;
-        } else {
-            pass(2);
-            dD += dD1;
-        }
     }
-    if (blockIdx.x == 0) {
+    if (keep) {
         // bookkeeping and the role-A descriptor for k_bsel's rewrite blocks
         const uint32_t top = C->occ_top;
         if (tid < jf) {
@@ -1633,11 +1633,12 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             B->applied = 1;
             if (tie) {
                 B->ntie++;
-                if (jf < js) {
+                if (jf < jsB) {
                     B->ntfail++;
                     B->retry = sjf;
                 }
             }
+            if (lfull) B->retry = B->tpend;
         }
     }
     for (int o = 32; o > 0; o >>= 1) {

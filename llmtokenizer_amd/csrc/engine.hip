@@ -525,6 +525,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.bat = nullptr;
     h.btag = nullptr;
     h.bvecd = h.bvec = h.bvlist = h.bvnl = nullptr;
+    h.tlog = nullptr;
+    h.tlog_cap = 0;
     h.bvs = h.vcap > DENSE ? h.vcap - DENSE : 1;
     if (h.batch) {
         if ((r = dalloc(c, &h.bat, 1))) return r;
@@ -533,6 +535,9 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         if ((r = dalloc(c, &h.bvec, (size_t)BK * 4 * h.bvs))) return r;
         if ((r = dalloc(c, &h.bvlist, (size_t)BK * 4 * h.bvs, false))) return r;
         if ((r = dalloc(c, &h.bvnl, (size_t)BK * 4))) return r;
+        // verified tie order: the undo log (records of 2 words)
+        h.tlog_cap = 1u << 22;
+        if ((r = dalloc(c, &h.tlog, 2ull * h.tlog_cap, false))) return r;
         // sharded: the batch exchange (zero between batches; a multiple of 4 words)
         if (c->sharded && (r = dalloc(c, &h.xbat, (xbat_words(BK, h.vcap) + 3) / 4 * 4))) return r;
         if (c->sharded && h.vcap > DENSE) {

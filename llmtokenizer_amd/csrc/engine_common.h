@@ -143,17 +143,18 @@ struct Bat {
     uint32_t xl_m;                    // sharded: member whose occurrence (owned by the left shard) ends at
                                       // my first token (k_bscan's edge step), else BK
     // verified tie order (batch.hip): the formation admits a member whose tie
-    // order holds only if the members before it zero few keys; k_bapply applies
-    // the decrements first, counts the keys they zeroed (ztot), checks, then
-    // applies the increments or reverts the decrements
+    // order holds only if the members before it zero few keys; k_bapply logs
+    // its updates and counts the keys they zeroed (ztot); its last block checks
+    // and, if a member fails, reverts the logged updates
     uint32_t tpend;                   // first member admitted that way, else BK
     uint32_t ztot;                    // keys the batch's decrements zeroed
-    uint32_t tbar, zrate;             // k_bapply's phase barrier; the formation's zeroed-keys-per-member guess
+    uint32_t tbar, zrate;             // k_bapply's blocks finished (the last one checks); the formation's
+                                      // zeroed-keys-per-member guess
     unsigned long long ntie, ntfail, nzero;  // batches verified that way, of them re-formed; keys zeroed (all batches)
     uint8_t tmask[64];                // per member: B_final levels (bit e + 5: B = B_sz 2^e, e in [-5, 2])
                                       // under which its tie order holds
     uint32_t tspan[BK];               // per member: the formation's bound on D's rise before its turn
-    uint32_t pad4;
+    uint32_t tlog_n;                  // k_bapply's undo log: (slot, delta) records written
     unsigned long long pv[BRB * TOPK], pk[BRB * TOPK];  // k_bsel partial lists: packed value, key
     // the applied batch's token rewrite (role A), done by k_bsel's extra blocks
     // beside the selection; written by k_bapply (the select never touches it)
@@ -230,6 +231,8 @@ struct Eng {
     unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
     unsigned long long *dbgts;      // [TS_SLOTS][TS_N] per-merge block timeline (BPE_DEBUG_TS) or null
     uint32_t dbg_form;
+    uint32_t *tlog;       // batches: undo log of a verified-tie batch's table updates (slot, delta)
+    uint32_t tlog_cap;    // ... records
     uint32_t tie_verify;  // batches: admit members on the tie-order guess k_bapply verifies (BPE_TIE_VERIFY,
                           // default 1; 2 = BPE_TIE_TEST: every such check fails, the revert runs)              // BPE_DEBUG_FORM=1: k_bsel prints why each batch's formation ended
     uint32_t *hprobe;     // host-mapped stop probe: k_select writes the stop code when it stops
