@@ -27,7 +27,7 @@ The line also carries
                   algorithmic bytes per launch (8 B/candidate + 20 B/occurrence)
                   and its average span from the device wall clock, both over
                   the LAST timed job; the committed rocprofv3 summary and PMC
-                  traffic of this same command (profiles/r3_*) beside them;
+                  traffic of this same command (profiles/r4_*) beside them;
   roofline_apply  the batch apply k_bapply (table updates, 16 B each), same way;
   roofline_count_pass  the corpus-wide pair-count pass (1 B/token read; the
                   initial u32 ids are written by the counting sort's first
@@ -56,7 +56,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 GIB = 1 << 30
-PROFILE_TAG = "r3"     # profiles/<tag>_train_kernel_stats.csv, <tag>_pmc_traffic.json (tools/gpu_profile.sh)
+PROFILE_TAG = "r4"     # profiles/<tag>_train_kernel_stats.csv, <tag>_pmc_traffic.json (tools/gpu_profile.sh)
 
 
 def count_pass_kernel(form):
@@ -219,6 +219,17 @@ def committed_profile(name, sharded=False):
                     out["avg_ms_rocprof"] = round(float(r["AverageNs"]) / 1e6, 5)
                     out["rocprof_calls"] = int(r["Calls"])
                     out["rocprof_summary"] = os.path.relpath(p, ROOT)
+                    break
+    # the same profile's average over the launches >= 6 us only (direct
+    # launches queued past a stop exit at once: tools/prof_nonempty.py)
+    p = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_{'sharded' if sharded else 'train'}_kernel_nonempty.txt")
+    if os.path.exists(p):
+        with open(p) as f:
+            for line in f.readlines()[1:]:
+                parts = line.split()
+                if parts and parts[0].split("<")[0] == name:
+                    out["avg_ms_rocprof_nonempty"] = round(float(parts[5]) / 1e3, 5)
+                    out["rocprof_nonempty_launches"] = int(parts[4])
                     break
     p = os.path.join(ROOT, "profiles", f"{PROFILE_TAG}_pmc_traffic.json")
     if os.path.exists(p):
