@@ -420,27 +420,36 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
 }
 
 // ids of window w (staged at w * core) to out + off[w], widened to u32 and
-// mapped back to merge-list ids (unmap, when the plan reordered the list): the
-// few ids before out's next 16-byte boundary one per lane, the rest four per
-// lane as one 16-byte store (the u16 reads stay coalesced across the lanes)
-__global__ __launch_bounds__(256) void k_ew_gather(const uint16_t *__restrict__ stage, const uint32_t *__restrict__ cnt,
-                                                   const unsigned long long *__restrict__ off, uint64_t nwin,
-                                                   uint32_t core, const uint32_t *__restrict__ unmap,
-                                                   uint32_t *__restrict__ out) {
-    auto id = [&](uint16_t x) -> uint32_t { return unmap ? unmap[x] : (uint32_t)x; };
-    for (uint64_t w = blockIdx.x; w < nwin; w += gridDim.x) {
+// mapped back to merge-list ids (unmap, when the plan reordered the list: a
+// u16 copy of it in LDS, nv entries, loaded once per block of a persistent
+// grid).  One wave per window: the few ids before out's next 16-byte boundary
+// one per lane, the rest four per lane as one 16-byte store (the u16 reads
+// stay coalesced across the lanes).
+constexpr uint32_t EWG_T = 1024, EWG_W = EWG_T / 64;
+__global__ __launch_bounds__(EWG_T) void k_ew_gather(const uint16_t *__restrict__ stage, const uint32_t *__restrict__ cnt,
+                                                     const unsigned long long *__restrict__ off, uint64_t nwin,
+                                                     uint32_t core, const uint32_t *__restrict__ unmap, uint32_t nv,
+                                                     uint32_t *__restrict__ out) {
+    extern __shared__ uint16_t um[];
+    if (unmap) {
+        for (uint32_t i = threadIdx.x; i < nv; i += EWG_T) um[i] = (uint16_t)unmap[i];
+        __syncthreads();
+    }
+    auto id = [&](uint16_t x) -> uint32_t { return unmap ? (uint32_t)um[x] : (uint32_t)x; };
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t w = (uint64_t)blockIdx.x * EWG_W + (threadIdx.x >> 6); w < nwin; w += (uint64_t)gridDim.x * EWG_W) {
         const uint32_t n = cnt[w];
         const uint64_t o = off[w];
         const uint16_t *src = stage + w * core;
         uint32_t *dst = out + o;
         const uint32_t h = min(n, (uint32_t)((4 - (o & 3)) & 3));  // ids before the boundary
-        if (threadIdx.x < h) dst[threadIdx.x] = id(src[threadIdx.x]);
+        if (lane < h) dst[lane] = id(src[lane]);
         const uint32_t nq = (n - h) / 4;
-        for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
+        for (uint32_t q = lane; q < nq; q += 64) {
             const uint32_t i = h + 4 * q;
             *reinterpret_cast<uint4 *>(dst + i) = make_uint4(id(src[i]), id(src[i + 1]), id(src[i + 2]), id(src[i + 3]));
         }
-        for (uint32_t i = h + 4 * nq + threadIdx.x; i < n; i += blockDim.x) dst[i] = id(src[i]);
+        for (uint32_t i = h + 4 * nq + lane; i < n; i += 64) dst[i] = id(src[i]);
     }
 }
 

@@ -1853,6 +1853,7 @@ struct EwPlan {
     bool ok = false;
     bool relabeled = false;  // unmap[] is needed
     uint32_t nb = 0, H = 0;  // H: hash slots
+    uint32_t V = 0;          // ids (256 + merges): unmap[]'s entries
     size_t off_ht = 0, off_roles = 0, off_bstart = 0, off_beq = 0, off_unmap = 0, words = 0;
 };
 
@@ -1961,6 +1962,7 @@ EwPlan ew_plan(const uint32_t *pairs, size_t m, std::vector<uint32_t> &img) {
     P.nb = nb;
     P.H = H;
     P.relabeled = moved;
+    P.V = V;
     P.off_ht = 65536;
     P.off_roles = P.off_ht + 2ull * H;  // (16-byte aligned: H >= 64)
     P.off_bstart = P.off_roles + (size_t)V * 16;
@@ -2059,9 +2061,13 @@ int ew_run(bpe_gpu_ctx *c, const EwPlan &P, const uint32_t *d_img, uint32_t halo
     void *tmp;
     if ((r = dscratch(c, 4, tb, &tmp))) return r;
     HIPCHK(rocprim::exclusive_scan(tmp, tb, cnt, off, 0ull, nwin + 1, rocprim::plus<unsigned long long>(), c->st));
-    if (nwin)
-        k_ew_gather<<<(uint32_t)std::min<uint64_t>(nwin, 8192), 256, 0, c->st>>>(
-            stage, cnt, off, nwin, core, P.relabeled ? d_img + P.off_unmap : nullptr, ids);
+    if (nwin) {
+        const size_t glds = P.relabeled ? (size_t)P.V * 2 : 0;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_ew_gather), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)glds);
+        k_ew_gather<<<(uint32_t)std::min<uint64_t>((nwin + EWG_W - 1) / EWG_W, 512), EWG_T, glds, c->st>>>(
+            stage, cnt, off, nwin, core, P.relabeled ? d_img + P.off_unmap : nullptr, P.V, ids);
+    }
     HIPCHK(hipGetLastError());
     if (prof) {
         unsigned long long h[8 + 512];
