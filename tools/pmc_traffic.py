@@ -15,7 +15,7 @@ import json
 import sys
 from collections import defaultdict
 
-WIDE_STREAM = {"k_pair_hist", "k_pair_hist_span", "k_live_compact", "k_enc_win"}  # whole-line coalesced streaming reads: FETCH_SIZE x 2
+WIDE_STREAM = {"k_pair_hist", "k_pair_hist_span", "k_pair_hist_v", "k_live_compact", "k_enc_win"}  # whole-line coalesced streaming reads: FETCH_SIZE x 2
 
 
 def per_kernel(path, counter):
