@@ -103,6 +103,8 @@ bool PIPE_ON = !getenv("BPE_PIPE") || atoi(getenv("BPE_PIPE")) != 0;  // pipelin
 bool GRAPH_ON = !getenv("BPE_GRAPH") || atoi(getenv("BPE_GRAPH")) != 0;
 // BPE_HOT=0: the level summaries instead of the hot-set argmax (A/B runs)
 bool HOT_ON = !getenv("BPE_HOT") || atoi(getenv("BPE_HOT")) != 0;
+// the hot set in tracked iterations as well (BPE_HOT_TRACKED=0: the level summaries there)
+bool HOT_TRACKED = !getenv("BPE_HOT_TRACKED") || atoi(getenv("BPE_HOT_TRACKED")) != 0;
 // k_bapply blocks (the table updates) and k_bsel's extra blocks (the applied
 // batch's token rewrite, beside the selection), 1024 threads each;
 // BPE_BGRID="a,b" overrides them (a: rewrite blocks, b: table blocks) for tuning runs
@@ -485,7 +487,14 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.scan_blocks = std::max<uint32_t>(SCAN_BLOCKS, h.spec_on ? 1 + SPEC_RB + SPEC_SB : 0);
     // hot-set argmax: untracked one-shard training with the speculative graph
     // (sharded: the batch engine's runs)
-    h.hot = HOT_ON && !encode && (c->sharded ? c->sbatch != 0 : h.spec_on && (c->fast || n0 >= TRACK_LIMIT)) ? 1 : 0;
+    // (tracked iterations too, BPE_HOT_TRACKED=1: the tie events come from the
+    // same top-2 with its tie count, and the resolver collects the maximal keys
+    // from the table itself; the level summaries' per-merge rescan is K1's
+    // longest part on small corpora)
+    h.hot = HOT_ON && !encode &&
+                    (c->sharded ? c->sbatch != 0 : h.spec_on && (c->fast || n0 >= TRACK_LIMIT || HOT_TRACKED))
+                ? 1
+                : 0;
     // byte-pair list rebuilds (STOP_RELIST, opt-in with BPE_RELIST=1): they
     // cut configs[2]'s scanned candidates from 974 M to 0.48-0.53 G with
     // identical merges, but the late merges did not get faster
@@ -517,7 +526,10 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     }
     // batched training (batch.hip): the hot set's one-shard runs
     // (BPE_BATCH=0: one merge per kernel pair, the speculative graph; read per run)
-    h.batch = getenv_int("BPE_BATCH", 1) && h.hot && h.vcap <= BATCH_VCAP_MAX && (!c->sharded || c->sbatch) ? 1 : 0;
+    h.batch = getenv_int("BPE_BATCH", 1) && h.hot && h.vcap <= BATCH_VCAP_MAX && (!c->sharded || c->sbatch) &&
+                      (c->sharded || c->fast || n0 >= TRACK_LIMIT)  // (batches: untracked iterations only)
+                  ? 1
+                  : 0;
     h.xbat = nullptr;
     h.xsp_out = h.xsp_in = nullptr;
     h.xsp_cap = 0;
@@ -811,6 +823,7 @@ void launch_iteration(bpe_gpu_ctx *c, bool tracked) {
     launch_summaries(c, false, tracked && tu != 0, tracked ? TRESCAN1_BLOCKS : 0);
     if (tracked && tu != 0 && c->h.lcap) k_stat_light<<<LIGHT_B, 1024, 0, c->st>>>(c->dE, c->dC);
     if (tracked && tu == 2) launch_stats(c);
+    if (c->h.hot) k_hot_reduce<<<c->h.hot_parts, 1024, 0, c->st>>>(c->dE, c->dC);  // (hot set in tracked phases)
     k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, tracked ? SEL_TRACKED : SEL_PLAIN);
 }
 
@@ -1323,15 +1336,18 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
         case STOP_MODE:
             C.stop = STOP_NONE;
             note_event(c, BPE_GPU_EV_MODE, C.merges_done);
-            if (c->h.hot) {  // tracked iterations select from the level summaries
+            if (c->h.hot && !HOT_TRACKED) {  // tracked iterations select from the level summaries
                 c->h.hot = 0;
                 c->h.batch = 0;
                 C.full = 1;
                 if ((r = push_desc(c))) return r;
+            } else if (c->h.batch) {  // (the hot set stays; batches are for untracked iterations)
+                c->h.batch = 0;
+                if ((r = push_desc(c))) return r;
             }
             if ((r = push_ctl(c))) return r;
             launch_stats(c);
-            launch_summaries(c);
+            launch_argmax_inputs(c);
             // (the fused graph goes on: a plain selection arms its prediction)
             k_select<<<1, 1024, 0, c->st>>>(c->dE, c->dC, fused_graph(c, true) ? SEL_PLAIN : SEL_TRACKED);
             HIPCHK(hipGetLastError());
