@@ -348,14 +348,23 @@ int dalloc(bpe_gpu_ctx *c, T **p, size_t count, bool zero = true) {
         c->pool.erase(c->pool.begin() + best);
     }
     if (!*p) {
+        static const bool dbg = getenv("BPE_DEBUG_INIT") != nullptr;
+        const double ta = dbg ? now_ms() : 0.0;
         hipError_t e = hipMalloc((void **)p, bytes);
         if (e != hipSuccess) {
             // return cached memory to the device and retry once
             (void)hipGetLastError();  // the failed attempt must not stay the sticky error
+            if (dbg) fprintf(stderr, "dalloc: hipMalloc(%zu) failed, freeing a pool of %zu buffers\n", bytes, c->pool.size());
             for (auto &q : c->pool) hipFree(q.first);
             c->pool.clear();
             e = hipMalloc((void **)p, bytes);
             if (e != hipSuccess) return fail(BPE_GPU_ENOMEM, "hipMalloc", e);
+        }
+        if (dbg) {
+            size_t pooled = 0;
+            for (auto &q : c->pool) pooled += q.second;
+            fprintf(stderr, "dalloc: hipMalloc(%zu) %.2f ms (pool %zu buffers, %zu bytes)\n", bytes, now_ms() - ta,
+                    c->pool.size(), pooled);
         }
     }
     c->train_allocs.push_back({(void *)*p, bytes});
@@ -2199,7 +2208,12 @@ void bpe_gpu_destroy(bpe_gpu_ctx *c) {
 
 static int alloc_bytes(bpe_gpu_ctx *c, size_t n) {
     if (n > 0xFFFFFFFEull) return fail(BPE_GPU_ERANGE, "corpus > 2^32-2 bytes");
-    free_train(c, true);
+    // the pooled run buffers stay for a corpus of about the same size (they
+    // fit it again): freeing ~20 GB and allocating it again per load made an
+    // occasional hipMalloc take 3-4 s (measured: a 4 GB one after a re-load,
+    // about one load in six; tools/init_outlier.py)
+    const bool same = c->n0 && n <= c->n0 + c->n0 / 8 && c->n0 <= n + n / 8;
+    free_train(c, !same);
     c->pres_valid = false;
     if (!c->h.bytes || c->bytes_cap < n + 64) {  // (a buffer at least this large is kept)
         if (c->h.bytes) { (void)hipFree(c->h.bytes); c->h.bytes = nullptr; }
@@ -2259,10 +2273,18 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     if (max_merges >= 0) cap = std::min<uint64_t>(cap, (uint64_t)max_merges);
     const double t0 = now_ms();
     int r;
+    static const bool dbg_init = getenv_int("BPE_DEBUG_INIT", 0) != 0;
+    auto phase = [&](const char *what) {  // (BPE_DEBUG_INIT: host-side phase times of the init)
+        if (!dbg_init) return;
+        (void)hipStreamSynchronize(c->st);
+        fprintf(stderr, "init %s %.2f ms\n", what, now_ms() - t0);
+    };
     if ((r = setup_run(c, (uint32_t)cap, false))) return r;
+    phase("setup");
     std::vector<uint32_t> unrank;
     uint32_t *d_tot;
     if ((r = init_tokens(c, &unrank, &d_tot))) return r;
+    phase("tokens");
     uint32_t *d_unrank;
     if ((r = dalloc(c, &d_unrank, unrank.size()))) return r;
     if (!unrank.empty())
@@ -2276,7 +2298,9 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->relists = 0;
     c->events.clear();
     if (c->h.hot) note_event(c, BPE_GPU_EV_HOT_REBUILD, 0);
+    phase("counts");
     if ((r = hot_rebuild(c))) return r;
+    phase("hot set");
     if ((r = select_next(c, tracked && !fused_graph(c, true)))) return r;
     HIPCHK(hipStreamSynchronize(c->st));
     const double t1 = now_ms();

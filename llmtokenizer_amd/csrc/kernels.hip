@@ -2711,6 +2711,10 @@ __device__ inline uint32_t tile_count(const uint32_t *hist, const uint32_t *tot,
 #ifndef BPE_SORT_T
 #define BPE_SORT_T 1024
 #endif
+#ifndef BPE_SORT_A_WAVES
+#define BPE_SORT_A_WAVES 1
+#endif
+constexpr uint32_t SORT_A_WAVES = BPE_SORT_A_WAVES;  // pass A's waves per SIMD target (8: two blocks per CU)
 constexpr uint32_t SORT_T = BPE_SORT_T, SORT_PER = 8, SORT_CH = SORT_T * SORT_PER;
 constexpr uint32_t SORT_LOCAL_BITS = 24;
 
@@ -2786,7 +2790,7 @@ __device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const uin
 // after a word comes from the next lane), so each widened uint4 store is one
 // contiguous 1-KB run of tok[]; the next round's words are loaded before this
 // round's LDS sort.
-__global__ __launch_bounds__(SORT_T) void k_sort_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
+__global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_A_WAVES, 8))) void k_sort_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
                                                    uint64_t tile, uint32_t G, uint32_t *__restrict__ tmp) {
     static_assert(SORT_PER == 8, "two 4-byte words per lane and round");
     __shared__ SortLds L;
