@@ -2227,12 +2227,24 @@ static int alloc_bytes(bpe_gpu_ctx *c, size_t n) {
     return 0;
 }
 
+// the byte values present, gathered once per load (as bpe_gpu_load_fd does
+// chunk by chunk): every train() of the corpus starts from it
+static int ingest_presence(bpe_gpu_ctx *c, size_t n) {
+    if (!c->d_pres) HIPCHK(hipMalloc(&c->d_pres, 1024));
+    HIPCHK(hipMemsetAsync(c->d_pres, 0, 1024, c->st));
+    if (n) k_presence_range<<<256, 256, 0, c->st>>>(c->h.bytes, n, c->d_pres);
+    HIPCHK(hipGetLastError());
+    c->pres_valid = true;
+    return 0;
+}
+
 int bpe_gpu_load(bpe_gpu_ctx *c, const uint8_t *bytes, size_t n) {
     if (!c || (!bytes && n)) return BPE_GPU_EINVAL;
     HIPCHK(hipSetDevice(c->dev));
     int r;
     if ((r = alloc_bytes(c, n))) return r;
     if (n) HIPCHK(hipMemcpyAsync(c->h.bytes, bytes, n, hipMemcpyHostToDevice, c->st));
+    if ((r = ingest_presence(c, n))) return r;
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
 }
@@ -2244,6 +2256,7 @@ int bpe_gpu_synth(bpe_gpu_ctx *c, uint64_t seed, size_t n, uint64_t offset) {
     if ((r = alloc_bytes(c, n))) return r;
     if (n) k_synth<<<2048, 256, 0, c->st>>>(c->h.bytes, n, seed, offset);
     HIPCHK(hipGetLastError());
+    if ((r = ingest_presence(c, n))) return r;
     HIPCHK(hipStreamSynchronize(c->st));
     return 0;
 }
