@@ -763,9 +763,10 @@ void launch_summaries(bpe_gpu_ctx *c, bool edges = false, bool track = false, ui
 // HOT_LIMIT; after a table regrowth moved the slots): histogram, threshold,
 // listing.  Falls back to the level summaries for the rest of the run when the
 // keys holding the top count alone would overfill the list.
-int hot_rebuild(bpe_gpu_ctx *c) {
+int hot_rebuild(bpe_gpu_ctx *c, const uint32_t *slots = nullptr, uint32_t ns = 0) {
     if (!c->h.hot) return 0;
-    k_hot_hist<<<1024, 256, 0, c->st>>>(c->dE);
+    k_hot_hist<<<slots ? std::max<uint32_t>(1, std::min<uint32_t>(256, (ns + 255) / 256)) : 1024, 256, 0, c->st>>>(
+        c->dE, slots, ns);
     k_hot_pick<<<1, 1024, 0, c->st>>>(c->dE, c->dC);
     HIPCHK(hipGetLastError());
     uint32_t fill = 0;
@@ -787,7 +788,8 @@ int hot_rebuild(bpe_gpu_ctx *c) {
         }
         return 0;
     }
-    k_hot_collect<<<2048, 256, 0, c->st>>>(c->dE, c->dC);
+    k_hot_collect<<<slots ? std::max<uint32_t>(1, std::min<uint32_t>(256, (ns + 255) / 256)) : 2048, 256, 0, c->st>>>(
+        c->dE, c->dC, slots, ns);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -2303,7 +2305,11 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     if (!unrank.empty())
         HIPCHK(hipMemcpyAsync(d_unrank, unrank.data(), unrank.size() * 4, hipMemcpyHostToDevice, c->st));
     const uint32_t AA = c->h.A * c->h.A;
-    k_init_counts<<<(AA + 255) / 256, 256, 0, c->st>>>(c->dE, c->dC, d_tot, d_unrank);
+    // (the slots of the byte-pair keys: the first hot set is built from them,
+    // not from a pass over the whole, freshly cleared table)
+    uint32_t *d_islots;
+    if ((r = dalloc(c, &d_islots, std::max<uint32_t>(AA, 1), false))) return r;
+    k_init_counts<<<(AA + 255) / 256, 256, 0, c->st>>>(c->dE, c->dC, d_tot, d_unrank, d_islots);
     HIPCHK(hipGetLastError());
     const bool tracked = !c->fast && c->n0 < TRACK_LIMIT;
     if (tracked) launch_stats(c);
@@ -2312,7 +2318,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->events.clear();
     if (c->h.hot) note_event(c, BPE_GPU_EV_HOT_REBUILD, 0);
     phase("counts");
-    if ((r = hot_rebuild(c))) return r;
+    if ((r = hot_rebuild(c, d_islots, AA))) return r;
     phase("hot set");
     if ((r = select_next(c, tracked && !fused_graph(c, true)))) return r;
     HIPCHK(hipStreamSynchronize(c->st));

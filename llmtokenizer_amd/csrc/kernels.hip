@@ -1108,11 +1108,20 @@ __global__ __launch_bounds__(1024) void k_hot_reduce(const Eng *__restrict__ E, 
 }
 
 // Rebuild, pass 1: histogram of the counts >= 2 (hot_bin) over the whole table
-__global__ __launch_bounds__(256) void k_hot_hist(const Eng *__restrict__ E) {
+// (slots != null: only the listed slots, ~0u = none -- the byte-pair keys of
+// the init, instead of a pass over the whole table)
+__global__ __launch_bounds__(256) void k_hot_hist(const Eng *__restrict__ E, const uint32_t *__restrict__ slots,
+                                                  uint32_t ns) {
     __shared__ uint32_t h[HOT_BINS];
     for (uint32_t x = threadIdx.x; x < HOT_BINS; x += blockDim.x) h[x] = 0;
     __syncthreads();
-    if (E->hcs == 4) {  // 16-byte slots {key, count, -}: one uint4 per slot
+    if (slots) {
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += gridDim.x * blockDim.x) {
+            const uint32_t s = slots[i];
+            const uint32_t c = s != ~0u ? E->hcnt[(uint64_t)(s) * E->hcs] : 0u;
+            if (c >= 2) atomicAdd(&h[hot_bin(c)], 1u);
+        }
+    } else if (E->hcs == 4) {  // 16-byte slots {key, count, -}: one uint4 per slot
         const uint4 *c4 = reinterpret_cast<const uint4 *>(E->hkey);
         for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < E->hcap;
              i += (uint64_t)gridDim.x * blockDim.x) {
@@ -1204,15 +1213,17 @@ __global__ __launch_bounds__(1024) void k_hot_pick(const Eng *__restrict__ E, Ct
 }
 
 // Rebuild, pass 3: list every key with count >= hot_T
-__global__ __launch_bounds__(256) void k_hot_collect(const Eng *__restrict__ E, Ctl *__restrict__ C) {
+__global__ __launch_bounds__(256) void k_hot_collect(const Eng *__restrict__ E, Ctl *__restrict__ C,
+                                                     const uint32_t *__restrict__ slots, uint32_t ns) {
     const uint32_t T = C->hot_T;
-    const uint64_t n = E->hcap;
+    const uint64_t n = slots ? ns : E->hcap;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t end = (n + stride - 1) / stride * stride;  // uniform trip count (wave_append)
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride) {
-        const bool in = i < n && E->hcnt[(uint64_t)(i) * E->hcs] >= T;
+        const uint32_t s = i < n ? (slots ? slots[i] : (uint32_t)i) : ~0u;
+        const bool in = s != ~0u && E->hcnt[(uint64_t)(s) * E->hcs] >= T;
         const uint32_t p = wave_append(in, &C->hot_n);
-        if (in && p < HOT_CAP) E->hot_slot[p] = (uint32_t)i;
+        if (in && p < HOT_CAP) E->hot_slot[p] = s;
     }
 }
 
@@ -2920,17 +2931,20 @@ __global__ __launch_bounds__(SORT_T) void k_sort_b(const Eng *__restrict__ E, co
 }
 
 // initial counts: the byte-pair totals into the pair table
+// (slots != null: slot of key k, ~0u for an absent pair -- the init's hot-set build reads them)
 __global__ void k_init_counts(const Eng *__restrict__ E, Ctl *__restrict__ C, const uint32_t *__restrict__ tot,
-                              const uint32_t *__restrict__ unrank) {
+                              const uint32_t *__restrict__ unrank, uint32_t *__restrict__ slots) {
     const uint32_t AA = E->A * E->A;
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= AA) return;
     const uint32_t c = tot[k];
+    if (slots) slots[k] = ~0u;
     if (!c) return;
     const uint32_t u = unrank[k / E->A], v = unrank[k % E->A];
     const uint64_t slot = hinsert(E, C, u, v);
     if (slot == ~0ull) { C->err = 2; C->stop = STOP_ERROR; return; }
     E->hcnt[(uint64_t)(slot) * E->hcs] = c;
+    if (slots) slots[k] = (uint32_t)slot;
     atomicAdd(&C->D, 1ull);
 }
 

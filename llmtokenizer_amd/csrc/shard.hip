@@ -631,7 +631,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         if ((r = dalloc(c, &d_unrank[k], unrank.size()))) return r;
         if (!unrank.empty())
             HIPCHK(hipMemcpyAsync(d_unrank[k], unrank.data(), unrank.size() * 4, hipMemcpyHostToDevice, g->st));
-        if (AA) k_init_counts<<<(AA + 255) / 256, 256, 0, g->st>>>(c->dE, c->dC, tot[k], d_unrank[k]);
+        if (AA) k_init_counts<<<(AA + 255) / 256, 256, 0, g->st>>>(c->dE, c->dC, tot[k], d_unrank[k], nullptr);
     }
     // warm the per-merge collective once outside any graph (lazy connection setup)
     {
