@@ -553,7 +553,10 @@ def main():
                                 "bytes_per_launch": cp_bytes, "avg_ms": round(cp_ms, 4),
                                 "form": int(st["count_pass_span"]),
                                 "note": "histogram of byte-pair rank keys: 1 B/token read, bins in LDS "
-                                        "(SURVEY 8(d)); the initial ids are written by k_sort_a"},
+                                        "(SURVEY 8(d)); the initial ids are written by k_sort_a; the corpus is "
+                                        "read cold (byte presence is gathered at load since round 4; before, "
+                                        "that pass left ~1/4 of the corpus in the 256 MB MALL: 0.24-0.25 ms); "
+                                        "LDS-conflict bound (DESIGN 4)"},
         "breakdown_ms": {"init": round(st["ms_init"], 3), "loop": round(st["ms_train"], 3),
                          "total_engine": round(st["ms_total"], 3), "per_merge_us": round(st["ms_train"] * 1e3 / merges, 2)},
         "engine": {k2: st[k2] for k2 in ("n_out", "iterations", "distinct_pairs", "merged_buckets",
