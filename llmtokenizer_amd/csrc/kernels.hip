@@ -2294,6 +2294,9 @@ __device__ __forceinline__ void hv_lane16(uint32_t *h, const uint32_t x[4], uint
     }
 }
 
+#ifndef BPE_HIST_PF
+#define BPE_HIST_PF 1
+#endif
 template <uint32_t R, bool SKEW>
 __global__ __launch_bounds__(1024) void k_pair_hist_v(const Eng *__restrict__ E, uint32_t *__restrict__ hist,
                                                       uint64_t tile, uint32_t lo, uint32_t S) {
@@ -2317,6 +2320,31 @@ __global__ __launch_bounds__(1024) void k_pair_hist_v(const Eng *__restrict__ E,
     const uint64_t nw = T / 64, kb0 = s / 1024, kfull = e / 1024, kb1 = (e + 1023) / 1024;
     // full blocks [kb0, kfull): every pair position < e, the dword after a
     // lane's 16 bytes ends at most 3 bytes past e <= n0 - 1 (64 bytes of padding)
+#if BPE_HIST_PF
+    // the next round's two blocks are loaded before this round's adds (the
+    // corpus arrives cold from HBM: the adds then overlap the loads)
+    uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
+    uint32_t na = 0, nb = 0;
+    auto load = [&](uint64_t kb) {
+        if (kb < kfull) {
+            qa = src4[kb * 64 + lane];
+            na = src[kb * 256 + 4 * lane + 4];
+        }
+        if (kb + nw < kfull) {
+            qb = src4[(kb + nw) * 64 + lane];
+            nb = src[(kb + nw) * 256 + 4 * lane + 4];
+        }
+    };
+    load(kb0 + (threadIdx.x >> 6));
+    for (uint64_t kb = kb0 + (threadIdx.x >> 6); kb < kfull; kb += 2 * nw) {  // wave-uniform
+        const bool two = kb + nw < kfull;
+        const uint32_t xa[4] = {qa.x, qa.y, qa.z, qa.w}, xb[4] = {qb.x, qb.y, qb.z, qb.w};
+        const uint32_t ca = na, cb = nb;
+        load(kb + 2 * nw);
+        hv_lane16<R, SKEW>(h, xa, ca, SR4, base4);
+        if (two) hv_lane16<R, SKEW>(h, xb, cb, SR4, base4);
+    }
+#else
     for (uint64_t kb = kb0 + (threadIdx.x >> 6); kb < kfull; kb += 2 * nw) {  // wave-uniform
         const uint64_t kc = kb + nw;
         const bool two = kc < kfull;
@@ -2335,6 +2363,7 @@ __global__ __launch_bounds__(1024) void k_pair_hist_v(const Eng *__restrict__ E,
             hv_lane16<R, SKEW>(h, xb, nb, SR4, base4);
         }
     }
+#endif
     // the partial last block (last tile only): byte by byte
     if (kfull < kb1 && (threadIdx.x >> 6) == (kfull - kb0) % nw) {
         for (uint32_t k = 0; k < 16; k++) {
