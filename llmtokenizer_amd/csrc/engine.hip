@@ -1236,7 +1236,13 @@ int relist(bpe_gpu_ctx *c) {
     k_pair_colsum<<<cgrid, 256, 0, c->st>>>(d_hist, d_gsum, AA, ntl, per);
     k_pair_colscan<<<cgrid, 256, 0, c->st>>>(d_hist, d_gsum, d_tot, AA, ntl, per);
     k_scan_single<<<1, 1024, 0, c->st>>>(d_tot, h.poff, AA);
-    k_relist_scatter<<<ntl, RELIST_T, AA * 4, c->st>>>(c->dE, d_hist, tile);
+    if (getenv_int("BPE_RELIST_SCATTER", 0)) {  // (the round-3 single pass, for A/B runs)
+        k_relist_scatter<<<ntl, RELIST_T, AA * 4, c->st>>>(c->dE, d_hist, tile);
+    } else {  // the init's two-pass counting sort, pass A reading tok[] (ids_out is free between batches)
+        const uint32_t G = (uint32_t)std::min<uint64_t>(16, (1ull << 24) / tile);
+        k_relist_a<<<ntl, SORT_T, 0, c->st>>>(c->dE, d_hist, tile, G, h.ids_out);
+        k_sort_b<<<1024 * (1024 / SORT_T), SORT_T, 0, c->st>>>(c->dE, d_hist, d_tot, ntl, tile, G, h.ids_out);
+    }
     HIPCHK(hipGetLastError());
     c->relists++;
     return 0;

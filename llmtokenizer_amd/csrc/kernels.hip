@@ -2897,6 +2897,74 @@ __global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_A_W
     }
 }
 
+// Relist, pass A (round 4): tile t's live byte pairs -- a single-byte token
+// followed by one, the pairs k_relist_hist counted -- as pass A's entries
+// (second rank << 24 | position - the tile group's start) grouped by first
+// rank into the same slot ranges, so that k_sort_b finishes them into plist
+// as at init.  Replaces k_relist_scatter's 4-byte stores into A^2 streams per
+// tile (~20 live positions per key per 1 M-position tile: nothing to
+// coalesce).  A wave takes 512 consecutive slots of tok[] per round (lane L
+// holds slots 4L.. and 256 + 4L..; the slot after a lane's four comes from
+// the next lane, after the wave's 512 from one extra load).
+__global__ __launch_bounds__(SORT_T) void k_relist_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
+                                                     uint64_t tile, uint32_t G, uint32_t *__restrict__ tmp) {
+    static_assert(SORT_PER == 8, "two 4-slot groups per lane and round");
+    __shared__ SortLds L;
+    __shared__ uint32_t rk[256];
+    const uint32_t A = E->A, AA = A * A;
+    const uint32_t t = blockIdx.x;
+    for (uint32_t x = threadIdx.x; x < 256; x += SORT_T) rk[x] = E->rank[x];
+    if (threadIdx.x < A) {
+        uint32_t s0 = E->poff[threadIdx.x * A];
+        const uint32_t *hr = hist + (uint64_t)t * AA + threadIdx.x * A;
+#pragma unroll 16
+        for (uint32_t k2 = 0; k2 < A; k2++) s0 += hr[k2];
+        L.gcur[threadIdx.x] = s0;
+    }
+    __syncthreads();
+    const uint64_t n0 = E->n0;
+    const uint64_t s = (uint64_t)t * tile, e = min(n0 - 1, s + tile);  // pair positions [s, e)
+    const uint64_t gs = (uint64_t)(t / G) * G * tile;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t *tok = E->tok;
+    auto load4 = [&](uint64_t i) -> uint4 {  // slots i .. i + 3 (HOLE past the corpus)
+        if (i + 4 <= n0) return *reinterpret_cast<const uint4 *>(tok + i);
+        return make_uint4(i < n0 ? tok[i] : HOLE, i + 1 < n0 ? tok[i + 1] : HOLE, i + 2 < n0 ? tok[i + 2] : HOLE, HOLE);
+    };
+    auto fetch = [&](uint64_t wb, uint4 *x0, uint4 *x1, uint32_t *b8) {
+        const bool in = wb < e;
+        *x0 = in ? load4(wb + 4 * lane) : make_uint4(HOLE, HOLE, HOLE, HOLE);
+        *x1 = in ? load4(wb + 256 + 4 * lane) : make_uint4(HOLE, HOLE, HOLE, HOLE);
+        *b8 = in && lane == 63 && wb + 512 < n0 ? tok[wb + 512] : HOLE;
+    };
+    uint4 n0v, n1v;
+    uint32_t nb8;
+    fetch(s + wv * 512, &n0v, &n1v, &nb8);
+    for (uint64_t r0 = s; r0 < e; r0 += SORT_CH) {  // block-uniform rounds
+        const uint64_t wb = r0 + wv * 512;
+        const uint4 x0 = n0v, x1 = n1v;
+        const uint32_t b8 = nb8;
+        fetch(wb + SORT_CH, &n0v, &n1v, &nb8);
+        uint32_t nx0 = __shfl_down(x0.x, 1), nx1 = __shfl_down(x1.x, 1);
+        const uint32_t f = __shfl(x1.x, 0);
+        if (lane == 63) { nx0 = f; nx1 = b8; }
+        uint32_t bins[SORT_PER], vals[SORT_PER];
+#pragma unroll
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint4 v = h ? x1 : x0;
+            const uint32_t t5[5] = {v.x, v.y, v.z, v.w, h ? nx1 : nx0};
+            const uint64_t p = wb + 256 * h + 4 * lane;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const bool in = p + k < e && t5[k] < 256 && t5[k + 1] < 256;
+                bins[4 * h + k] = in ? rk[t5[k]] : 256u;
+                vals[4 * h + k] = in ? (rk[t5[k + 1]] << SORT_LOCAL_BITS) | (uint32_t)(p + k - gs) : 0u;
+            }
+        }
+        lds_sort_emit(L, bins, vals, A, tmp);
+    }
+}
+
 // pass B: unit (first rank k1, group of G consecutive tiles) -> plist by
 // second rank.  A k1 group's entries of consecutive tiles are consecutive in
 // tmp (tmp is laid out like plist: by k1, then tile), and so are the (k1, k2)
