@@ -373,7 +373,14 @@ def train_sharded(args, cx, out):
     g = bdist.group(cx.local, merges, args.xport)
     lo, hi = bdist.shard_range(args.size, cx.rank, cx.world)
     g.synth(0, args.seed, hi - lo, lo)
-    for _ in range(args.warmup):
+    warm = args.warmup
+    if cx.world > 1:  # (untimed) a P2P job that fails on any rank moves every rank to RCCL
+        g, ok = bdist.first_job(g, cx.local, lambda gg: gg.train(merges))
+        if not ok:
+            g.synth(0, args.seed, hi - lo, lo)
+            g.train(merges)
+        warm -= 1
+    for _ in range(max(0, warm)):
         g.train(merges)
     done = []
     el = timed_jobs(cx, lambda: done.append(g.train(merges)), args.steps)
@@ -440,7 +447,13 @@ def encode_bench(args, cx):
             a = q * step
             b = total if q == k - 1 else a + step
             g.synth(q, 3, b - a, a)
-    g.encode(merges)  # warm (pools, graphs)
+    if world > 1:  # warm (pools, graphs); a P2P failure on any rank moves every rank to RCCL
+        g, ok = bdist.first_job(g, cx.local, lambda gg: gg.encode(merges))
+        if not ok:
+            g.synth(0, 3, hi - lo, lo)
+            g.encode(merges)
+    else:
+        g.encode(merges)  # warm (pools, graphs)
     warm = group_checksum(cx, g)
     el = timed_jobs(cx, lambda: g.encode(merges), 1)
     st = g.stats()
@@ -458,6 +471,8 @@ def encode_bench(args, cx):
            "roofline": {"bound": "hbm", "achieved": round(alg / el / 1e9, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(alg / el / 1e9 / HBM_PEAK_GBS, 5),
                         "bytes": alg, "note": "whole-job algorithmic bytes (input + n_out*w) / wall"}}
+    if getattr(g, "fallback_reason", None):
+        out["transport_fallback_reason"] = g.fallback_reason
     errs = []
     if warm != got:
         errs.append("warm and timed encodes differ")

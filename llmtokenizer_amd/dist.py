@@ -103,6 +103,33 @@ def group(device, max_merges, transport=None):
     return g
 
 
+def first_job(g, device, job, make_rccl=None):
+    """Run job(g) once on every rank; the ranks agree on the outcome.  A P2P
+    group whose job failed on ANY rank (e.g. a bounded mailbox wait that timed
+    out: the cross-device xGMI path is first exercised by a multi-GPU run) is
+    closed on every rank and replaced by an RCCL group, whose fallback_reason
+    says why.  Returns (group, ok): ok False means the returned group is the
+    new one and the caller loads its shard into it and runs the job again.  A
+    failure on an RCCL group is raised (nothing to fall back to)."""
+    import torch.distributed as dist
+    err = None
+    try:
+        job(g)
+    except api.BpeError as e:
+        err = str(e)
+    errs = [None] * dist.get_world_size()
+    dist.all_gather_object(errs, err)
+    errs = [e for e in errs if e]
+    if not errs:
+        return g, True
+    if g.transport() != "p2p":
+        raise api.BpeError("sharded job failed: " + errs[0])
+    g.close()
+    g2 = (make_rccl or rccl_group)(device)
+    g2.fallback_reason = "P2P job failed, RCCL instead: " + errs[0]
+    return g2, False
+
+
 def shard_range(n_total, rank, world):
     """contiguous [lo, hi) slice of an n_total-byte corpus for `rank`"""
     step = n_total // world
