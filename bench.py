@@ -375,7 +375,8 @@ def train_sharded(args, cx, out):
     g.synth(0, args.seed, hi - lo, lo)
     warm = args.warmup
     if cx.world > 1:  # (untimed) a P2P job that fails on any rank moves every rank to RCCL
-        g, ok = bdist.first_job(g, cx.local, lambda gg: gg.train(merges))
+        g, ok = bdist.first_job(g, cx.local,
+                                lambda gg: (gg.train(merges), hashlib.md5(gg.merges().tobytes()).hexdigest()))
         if not ok:
             g.synth(0, args.seed, hi - lo, lo)
             g.train(merges)

@@ -108,18 +108,22 @@ def first_job(g, device, job, make_rccl=None):
     group whose job failed on ANY rank (e.g. a bounded mailbox wait that timed
     out: the cross-device xGMI path is first exercised by a multi-GPU run) is
     closed on every rank and replaced by an RCCL group, whose fallback_reason
-    says why.  Returns (group, ok): ok False means the returned group is the
-    new one and the caller loads its shard into it and runs the job again.  A
-    failure on an RCCL group is raised (nothing to fall back to)."""
+    says why.  job may return a digest of what every rank must agree on (the
+    merges): digests that differ count as a failure too.  Returns (group, ok):
+    ok False means the returned group is the new one and the caller loads its
+    shard into it and runs the job again.  A failure on an RCCL group is
+    raised (nothing to fall back to)."""
     import torch.distributed as dist
-    err = None
+    err, dig = None, None
     try:
-        job(g)
+        dig = job(g)
     except api.BpeError as e:
         err = str(e)
-    errs = [None] * dist.get_world_size()
-    dist.all_gather_object(errs, err)
-    errs = [e for e in errs if e]
+    outs = [None] * dist.get_world_size()
+    dist.all_gather_object(outs, (err, dig))
+    errs = [e for e, _ in outs if e]
+    if not errs and len({d for _, d in outs}) > 1:
+        errs = ["the ranks' results differ"]
     if not errs:
         return g, True
     if g.transport() != "p2p":

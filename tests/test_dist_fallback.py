@@ -26,7 +26,7 @@ class _Group:
         self.closed = True
 
 
-def _worker(rank, world, port, fail_rank, transport, q):
+def _worker(rank, world, port, fail_rank, transport, q, differ=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -39,6 +39,7 @@ def _worker(rank, world, port, fail_rank, transport, q):
             gg.jobs += 1
             if rank == fail_rank:
                 raise api.BpeError("mailbox wait timed out (test)")
+            return "md5-%d" % rank if differ else "md5"
 
         try:
             g2, ok = bdist.first_job(g, 0, job, make_rccl=lambda dev: _Group("rccl"))
@@ -49,12 +50,12 @@ def _worker(rank, world, port, fail_rank, transport, q):
         dist.destroy_process_group()
 
 
-def _run(fail_rank, transport, world=2):
+def _run(fail_rank, transport, world=2, differ=False):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fail_rank, transport, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fail_rank, transport, q, differ)) for r in range(world)]
     for p in procs:
         p.start()
     out = sorted(q.get(timeout=120) for _ in range(world))
@@ -79,3 +80,8 @@ def test_first_job_failure_on_one_rank_moves_every_rank_to_rccl(fail_rank):
 def test_first_job_failure_on_rccl_is_raised_on_every_rank():
     for rank, ok, t, closed, why, err in _run(1, "rccl"):
         assert ok is None and not closed and "sharded job failed" in err
+
+
+def test_first_job_results_that_differ_move_every_rank_to_rccl():
+    for rank, ok, t, closed, why, err in _run(-1, "p2p", differ=True):
+        assert ok is False and t == "rccl" and closed and "results differ" in why
