@@ -425,7 +425,11 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
 // grid).  One wave per window: the few ids before out's next 16-byte boundary
 // one per lane, the rest four per lane as one 16-byte store (the u16 reads
 // stay coalesced across the lanes).
+#ifndef EWG_PIPE
+#define EWG_PIPE 1
+#endif
 constexpr uint32_t EWG_T = 1024, EWG_W = EWG_T / 64;
+constexpr uint32_t EWG_U = 8;  // rounds of 4 ids per lane loaded ahead (a 1 952-byte core: <= 488 quads)
 __global__ __launch_bounds__(EWG_T) void k_ew_gather(const uint16_t *__restrict__ stage, const uint32_t *__restrict__ cnt,
                                                      const unsigned long long *__restrict__ off, uint64_t nwin,
                                                      uint32_t core, const uint32_t *__restrict__ unmap, uint32_t nv,
@@ -437,7 +441,50 @@ __global__ __launch_bounds__(EWG_T) void k_ew_gather(const uint16_t *__restrict_
     }
     auto id = [&](uint16_t x) -> uint32_t { return unmap ? (uint32_t)um[x] : (uint32_t)x; };
     const uint32_t lane = threadIdx.x & 63;
-    for (uint64_t w = (uint64_t)blockIdx.x * EWG_W + (threadIdx.x >> 6); w < nwin; w += (uint64_t)gridDim.x * EWG_W) {
+    const uint64_t stride = (uint64_t)gridDim.x * EWG_W;
+#if EWG_PIPE
+    // the next window's count and offset load while this one moves; a
+    // window's first EWG_U rounds of source ids are all loaded before any of
+    // their stores (one round trip per window instead of one per round)
+    uint64_t w = (uint64_t)blockIdx.x * EWG_W + (threadIdx.x >> 6);
+    uint32_t n = w < nwin ? cnt[w] : 0u;
+    uint64_t o = w < nwin ? off[w] : 0ull;
+    for (; w < nwin; w += stride) {
+        const uint64_t wn = w + stride;
+        const uint32_t nn = wn < nwin ? cnt[wn] : 0u;
+        const uint64_t on = wn < nwin ? off[wn] : 0ull;
+        const uint16_t *src = stage + w * core;
+        uint32_t *dst = out + o;
+        const uint32_t h = min(n, (uint32_t)((4 - (o & 3)) & 3));  // ids before the boundary
+        const uint32_t nq = (n - h) / 4;
+        uint16_t v[EWG_U][4];
+        uint16_t hv = lane < h ? src[lane] : (uint16_t)0;
+#pragma unroll
+        for (uint32_t u = 0; u < EWG_U; u++) {
+            const uint32_t q = lane + 64 * u, i = h + 4 * q;
+            if (q < nq) {
+                v[u][0] = src[i];
+                v[u][1] = src[i + 1];
+                v[u][2] = src[i + 2];
+                v[u][3] = src[i + 3];
+            }
+        }
+        if (lane < h) dst[lane] = id(hv);
+#pragma unroll
+        for (uint32_t u = 0; u < EWG_U; u++) {
+            const uint32_t q = lane + 64 * u, i = h + 4 * q;
+            if (q < nq) *reinterpret_cast<uint4 *>(dst + i) = make_uint4(id(v[u][0]), id(v[u][1]), id(v[u][2]), id(v[u][3]));
+        }
+        for (uint32_t q = lane + 64 * EWG_U; q < nq; q += 64) {  // (windows past EWG_U rounds)
+            const uint32_t i = h + 4 * q;
+            *reinterpret_cast<uint4 *>(dst + i) = make_uint4(id(src[i]), id(src[i + 1]), id(src[i + 2]), id(src[i + 3]));
+        }
+        for (uint32_t i = h + 4 * nq + lane; i < n; i += 64) dst[i] = id(src[i]);
+        n = nn;
+        o = on;
+    }
+#else
+    for (uint64_t w = (uint64_t)blockIdx.x * EWG_W + (threadIdx.x >> 6); w < nwin; w += stride) {
         const uint32_t n = cnt[w];
         const uint64_t o = off[w];
         const uint16_t *src = stage + w * core;
@@ -451,6 +498,7 @@ __global__ __launch_bounds__(EWG_T) void k_ew_gather(const uint16_t *__restrict_
         }
         for (uint32_t i = h + 4 * nq + lane; i < n; i += 64) dst[i] = id(src[i]);
     }
+#endif
 }
 
 }  // namespace bpeamd
