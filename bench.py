@@ -272,6 +272,7 @@ def train_single(args, cx, out):
         extra = {"train_1024": {"value": round(args.size / 1e6 * 1024 / t, 1), "ms": round(t * 1e3, 3),
                                 "workload": "configs[3] at N=1: 1 GiB x 1024 merges, one job",
                                 "breakdown_ms": {"init": round(s2["ms_init"], 3), "loop": round(s2["ms_train"], 3)},
+                                "batches": s2["batches"], "batch_retries": s2["batch_retries"],
                                 "ids_checksum": "%016x" % e.ids_checksum(),
                                 "merges_md5": hashlib.md5(e.merges().tobytes()).hexdigest()}}
         extra["ingest"] = ingest_rate(e)
@@ -579,7 +580,8 @@ def main():
                                           "rule_ties", "table_grows", "keys", "candidates", "occurrences",
                                           "hot_rebuilds", "hot_mode", "hot_scanned", "relists", "batches",
                                           "batch_dropped", "batch_retries", "table_updates", "spec_hits",
-                                          "spec_misses", "select_launches")},
+                                          "spec_misses", "select_launches", "keys_skipped", "skip_failed",
+                                          "tie_verified", "tie_failed")},
         "batch_end": {k2[4:]: st[k2] for k2 in st if k2.startswith("end_") and k2 != "end_unused"},
     })
     out.update(extra)

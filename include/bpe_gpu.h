@@ -104,6 +104,9 @@ typedef struct {
                                  holds only if the earlier members zero few keys (checked in k_bapply) */
     uint64_t tie_failed;      /* ... of them re-formed shorter (the check failed) */
     uint64_t keys_zeroed;     /* training, batches: pair keys the applied batches took to count 0 */
+    uint64_t keys_skipped;    /* training, batches: listed keys the applied batches skipped (they do not
+                                 commute with an earlier member; its merge lowers their count) */
+    uint64_t skip_failed;     /* ... batches re-formed because a skipped key stayed ahead of a member */
 } bpe_gpu_stats;
 
 /* Per-merge record (training): the structured per-iteration metrics the

@@ -210,6 +210,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         // (read before the lanes overwrite the member fields)
         const uint32_t olda = jst ? B->a[jst - 1] : 0, oldb = jst ? B->b[jst - 1] : 0, oldz0 = B->z0;
         const uint32_t oldsum = B->sumlen;
+        const uint32_t oldnsk = Bg->nsk;  // (outside the staged head; the formation below rewrites it)
         const uint32_t raerr = aload(&Bg->ra_err);  // a token too long for an end code (rewrite blocks)
         const bool sh = E->sharded != 0;
         unsigned long long rs = lane < jst ? B->R[lane] : 0ull;   // this shard's occurrences
@@ -302,7 +303,6 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             const bool tie_rel = !stable && ((truncated && c == clast) || tie_next);
             const bool cons_ok = tie_levels_ok(Blo, Bhi, Bsz, tmask);
             const bool opt_ok = tie_levels_ok(Blo_o, Bhi, Bsz, tmask);
-            bool pend = false;
             uint32_t why = 0;  // 0: qualifies
             if (lane >= nl || lane >= BK) why = 8;  // past the list (reported as "list")
             else if (lane > 0) {
@@ -312,23 +312,90 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                     why = 4;  // (a tie whose order the batch could change, or one running past the list)
                 else if (C->nkeys + 4ull * (256ull + md + lane + 2) * (lane + 1) >= E->hcap / 2) why = 6;
             }
-            // commuting: no earlier entry uses my left id on its right or my right id on its left
+            // the earlier entries that do not commute with me: one uses my left
+            // id on its right or my right id on its left
+            unsigned long long cm = 0;
 #pragma unroll
             for (uint32_t p = 0; p < BK; p++) {
                 const uint32_t up = __builtin_amdgcn_readlane((int)u, (int)p), vp = __builtin_amdgcn_readlane((int)v, (int)p);
-                if (!why && p < lane && (u == vp || v == up)) why = 5;
+                if (p < lane && (u == vp || v == up)) cm |= 1ull << p;
             }
-            if (lane > 0 && !why && tie_rel && !cons_ok) pend = true;  // admitted on the guess: k_bapply verifies
-            const unsigned long long badm = __ballot(why != 0);
-            k = badm ? (uint32_t)__ffsll(badm) - 1 : 64;  // lane 0 always qualifies
-            if (retry && retry < k) k = retry;  // the last batch failed there (nothing changed since)
-            const unsigned long long pm = __ballot(pend && lane < k);
-            const uint32_t endwhy = __shfl(why, (int)(k < 64 ? k : 0));
+            // Members, entry by entry.  An entry that commutes with every earlier
+            // MEMBER joins (its occurrences are the pre-batch ones).  One that
+            // does not is SKIPPED: the sequential passes lower its count when
+            // those members merge (their occurrences consume its tokens), so
+            // it is not the argmax at its turn provided its lowered count falls
+            // below the next member's -- k_bscan counts the decrements, k_bapply
+            // checks every member against the skipped keys before it.  It
+            // merges in a later batch.  (Ids below DENSE: the scan's LDS
+            // vectors hold the decrements; a tie order of its own is moot.)
+            const bool skok = E->skip_on && u < DENSE && v < DENSE && (why == 0 || why == 4);
+            unsigned long long M = 0, S = 0;
+            uint32_t kend = 64, endwhy = 8;
+            {
+                const uint32_t cmlo = (uint32_t)cm, cmhi = (uint32_t)(cm >> 32);
+                for (uint32_t p = 0; p < 64; p++) {  // (uniform: every operand is a readlane)
+                    const unsigned long long cp = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)cmhi, (int)p) << 32) |
+                                                  (uint32_t)__builtin_amdgcn_readlane((int)cmlo, (int)p);
+                    const uint32_t wp = (uint32_t)__builtin_amdgcn_readlane((int)why, (int)p);
+                    if (cp & M) {
+                        if (__builtin_amdgcn_readlane((int)skok, (int)p)) {
+                            S |= 1ull << p;
+                            continue;
+                        }
+                        kend = p;
+                        endwhy = 5;
+                        break;
+                    }
+                    if (wp) {
+                        kend = p;
+                        endwhy = wp;
+                        break;
+                    }
+                    M |= 1ull << p;
+                }
+            }
+            if (retry && retry < (uint32_t)__popcll(M)) {  // the last batch failed at member `retry` (nothing changed since)
+                unsigned long long x = M;
+                for (uint32_t q = 0; q < retry; q++) x &= x - 1;
+                kend = (uint32_t)__builtin_ctzll(x);
+                M &= (1ull << kend) - 1;
+            }
+            S &= M ? (2ull << (63 - __builtin_clzll(M))) - 1 : 0ull;  // (skipped keys a later member must beat)
+            k = (uint32_t)__popcll(M);  // lane 0 always qualifies
+            const unsigned long long below = (1ull << lane) - 1;
+            const bool isM = (M >> lane) & 1;
+            const uint32_t midx = (uint32_t)__popcll(M & below);
+            // skipped keys, in list order: key, count, the members (by index)
+            // that lower it
+            const uint32_t nsk = (uint32_t)__popcll(S);
+            if ((S >> lane) & 1) {
+                const uint32_t si = (uint32_t)__popcll(S & below);
+                unsigned long long cmm = 0;
+                for (unsigned long long x = cm & M; x; x &= x - 1) cmm |= 1ull << __popcll(M & ((1ull << __builtin_ctzll(x)) - 1));
+                Bg->sk_a[si] = u;
+                Bg->sk_b[si] = v;
+                Bg->sk_c[si] = c;
+                Bg->sk_cm[si] = cmm;
+                Bg->sdec[si] = 0;
+            }
+            const bool pend = isM && lane > 0 && tie_rel && !cons_ok;  // admitted on the guess: k_bapply verifies
+            const unsigned long long pmk = __ballot(pend);
+            const uint32_t tpend = pmk ? (uint32_t)__popcll(M & ((1ull << __builtin_ctzll(pmk)) - 1)) : BK;
+            // the members' entries into lanes 0..k-1 (forward permute: members
+            // first, in list order, then the rest)
+            const uint32_t dst = isM ? midx : k + (uint32_t)__popcll(~M & below);
+            auto fwd = [&](uint32_t x) { return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4), (int)x); };
+            const uint32_t nskb = (uint32_t)__popcll(S & below);
+            const uint32_t mu = fwd(u), mv = fwd(v), mc = fwd(c), mtmask = fwd(tmask), mnskb = fwd(nskb);
+            const unsigned long long mspan =
+                ((unsigned long long)fwd((uint32_t)(span >> 32)) << 32) | (unsigned long long)fwd((uint32_t)span);
             // candidate lists and token lengths, one lane per member
             uint32_t mode = 1, off = 0, len = 0, tl = 0;
             if (lane < k) {
-                cand_of(E, u, v, true, srank, E->poff, &mode, &off, &len);
-                tl = E->tlen[u] + E->tlen[v];
+                cand_of(E, mu, mv, true, srank, E->poff, &mode, &off, &len);
+                tl = E->tlen[mu] + E->tlen[mv];
+                Bg->nskb[lane] = (uint8_t)mnskb;
             }
             // the members' candidates fit the occurrence staging (ids_out, n0
             // positions; sharded: + one slot per member for the occurrence
@@ -372,9 +439,9 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             const uint32_t bigm = 255u - (uint32_t)(big & 255u);
             const uint32_t extra = BSB - used;
             if (lane < k) {
-                B->a[lane] = u;
-                B->b[lane] = v;
-                B->cnt[lane] = c;
+                B->a[lane] = mu;
+                B->b[lane] = mv;
+                B->cnt[lane] = mc;
                 B->mode[lane] = mode;
                 B->off[lane] = off;
                 B->len[lane] = len;
@@ -382,26 +449,28 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->R[lane] = 0;
                 B->bound[lane] = 0;
                 B->blk0[lane] = bpre - nb + (lane > bigm ? extra : 0);
-                B->tmask[lane] = (uint8_t)tmask;
-                B->tspan[lane] = (uint32_t)min(span, 0xFFFFFFFFull);
+                B->tmask[lane] = (uint8_t)mtmask;
+                B->tspan[lane] = (uint32_t)min(mspan, 0xFFFFFFFFull);
                 ctl[lane] = tl;
             }
             if (E->dbg_form && md + 1 >= E->dbg_form) {  // (diagnostics: the formation's state where the batch ended; from merge BPE_DEBUG_FORM - 1)
-                const unsigned long long spk = __shfl(span, (int)(k < 64 ? k : 63));
-                const uint32_t ck = __shfl(c, (int)(k < 64 ? k : 63)), cn = __shfl(cnext, (int)(k < 64 ? k : 63));
-                const uint32_t ok = __shfl(tmask, (int)(k < 64 ? k : 63));
+                const uint32_t ke = kend < 64 ? kend : 63;  // (the list entry that ended it)
+                const unsigned long long spk = __shfl(span, (int)ke);
+                const uint32_t ck = __shfl(c, (int)ke), cn = __shfl(cnext, (int)ke);
+                const uint32_t ok = __shfl(tmask, (int)ke);
                 if (lane == 0)
-                    printf("form shard %u md %u k %u why %u D %llu span %llu B %llu lo %llu hi %llu trunc %d c %u next %u last %u "
-                           "mask %x pend %llx zrate %u\n", E->shard, md, k, endwhy, D, spk, (unsigned long long)Bsz,
-                           (unsigned long long)summary_B(D > spk ? D - spk : 0), (unsigned long long)summary_B(D + spk),
-                           (int)truncated, ck, cn, clast, ok, pm, B->zrate);
+                    printf("form shard %u md %u k %u end %u why %u skipped %u D %llu span %llu B %llu lo %llu hi %llu trunc %d c %u "
+                           "next %u last %u mask %x pend %u zrate %u\n", E->shard, md, k, kend, endwhy, nsk, D, spk,
+                           (unsigned long long)Bsz, (unsigned long long)summary_B(D > spk ? D - spk : 0),
+                           (unsigned long long)summary_B(D + spk), (int)truncated, ck, cn, clast, ok, tpend, B->zrate);
             }
             if (lane == 0) {
                 B->sbase[k] = (uint32_t)stage_end;
                 B->blk0[k] = BSB;
                 B->sumlen = (uint32_t)sumlen;
                 B->over = ovm < k ? ovm : BK;
-                B->tpend = pm ? (uint32_t)__ffsll(pm) - 1 : BK;
+                B->tpend = tpend < k ? tpend : BK;
+                Bg->nsk = nsk;
                 B->ztot = 0;
                 B->tbar = 0;
                 B->tlog_n = 0;
@@ -437,6 +506,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                     B->ndrop += kpr - retry;
                 } else {
                     B->nbatch++;
+                    Bg->nskip += oldnsk;
                 }
                 B->retry = 0;
                 B->applied = 0;
@@ -473,8 +543,8 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
     for (uint32_t q = tid; q < BAT_HEAD_WORDS; q += blockDim.x) reinterpret_cast<uint32_t *>(Bg)[q] = sbw[q];
     for (uint32_t q = tid; q < clear_k * 4; q += blockDim.x) E->bvnl[q] = 0;
     if (xclr_k) {  // sharded: the words every k_bapply block's prologue read
-        if (tid < BK) E->xbat[tid] = 0;
-        if (tid < 2 * xclr_k) E->xbat[BK + (uint64_t)(tid >> 1) * xbat_member_words(xclr_w) + (tid & 1)] = 0;
+        if (tid < XBH) E->xbat[tid] = 0;
+        if (tid < 2 * xclr_k) E->xbat[XBH + (uint64_t)(tid >> 1) * xbat_member_words(xclr_w) + (tid & 1)] = 0;
     }
     if (tid == 0 && sc.stop != STOP_NONE && E->hprobe) {
         __hip_atomic_store(E->hprobe, sc.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1085,8 +1155,20 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     }
     __syncthreads();
     ts_mark(E, bi, BT_SCAN_CAND, false, true);
+    // the skipped keys my member lowers (Bat::sk_*): a key (x, y) loses the
+    // pairs whose x is my b (my right neighbours y) and whose y is my a (my
+    // left neighbours x) -- from this block's LDS vectors.  Pairs a covered
+    // left neighbour or the edge step accounts elsewhere are left out: the
+    // sum is a lower bound on the decrements, so k_bapply's check errs safe
+    if (tid < BK && tid < B->nsk && ((B->sk_cm[tid] >> m) & 1ull)) {
+        const uint32_t xs = B->sk_a[tid], ys = B->sk_b[tid];
+        uint32_t d = 0;
+        if (xs == b && ys < lim) d += s[V_DR][ys];
+        if (ys == a && xs < lim) d += s[V_DL][xs];
+        if (d) atomicAdd(SH ? &E->xbat[BK + tid] : &B->sdec[tid], d);
+    }
     const uint32_t Wx = xbat_vw(z0 + k);  // SH: ids per dense delta vector in the exchange
-    uint32_t *xm = SH ? E->xbat + BK + (uint64_t)m * xbat_member_words(Wx) : nullptr;
+    uint32_t *xm = SH ? E->xbat + XBH + (uint64_t)m * xbat_member_words(Wx) : nullptr;
     if (SH && blockIdx.x == 0 && tid == 0) {
         // Shard edges (thread 0 of block 0, beside the other blocks' flushes).
         // Left: my first token is the b of an occurrence the left shard owns
@@ -1104,7 +1186,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 }
             for (uint32_t mm = 0; mm < k && mm < over; mm++) {
                 if (!(tl1 == sa[mm] && H.HR[0] == sb[mm] && (sa[mm] != sb[mm] || !(H.myi[mm] & 1)))) continue;
-                uint32_t *xo = E->xbat + BK + (uint64_t)mm * xbat_member_words(Wx);
+                uint32_t *xo = E->xbat + XBH + (uint64_t)mm * xbat_member_words(Wx);
                 const uint32_t zz = z0 + mm;
                 const int64_t ps = v_left<SH>(tok, L1);
                 const uint32_t p = tok_at(ps);
@@ -1312,7 +1394,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         unsigned long long ovm = 0;  // SH: members some shard could not stage
         uint32_t Rg = R;             // occurrences over all shards (the live-token count is global)
         if (SH) {
-            uint32_t *xm = E->xbat + BK + (uint64_t)lane * xbat_member_words(z0 + k);
+            uint32_t *xm = E->xbat + XBH + (uint64_t)lane * xbat_member_words(z0 + k);
             // (every block's prologue reads these words: the next select clears them)
             if (in) {
                 const uint32_t rg = xm[0];
@@ -1356,13 +1438,34 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             rexg = g - Rg;
         }
         const uint32_t pm = __shfl_up(bpre, 1);                              // max bound of the members before me
+        // the keys the formation skipped (lane s = skipped key s): their count
+        // after the decrements of the members that conflict with them (summed
+        // over the shards), as a running max in list order; member q must be
+        // strictly ahead of every skipped key listed before it
+        const uint32_t nsk = B->nsk;
+        uint32_t skub = 0;
+        if (lane < nsk) {
+            const uint32_t dec = SH ? E->xbat[BK + lane] : B->sdec[lane], cs = B->sk_c[lane];
+            skub = cs > dec ? cs - dec : 0u;
+        }
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(skub, o);
+            if ((int)lane >= o) skub = max(skub, y);
+        }
+        const uint32_t nsb = in && nsk ? B->nskb[lane] : 0u;
+        const uint32_t skmax = __shfl(skub, (int)(nsb ? nsb - 1 : 0));
+        const bool skfail = nsb && !(skmax < cnt);
         // member q is the argmax after the members before it: its count beats
-        // every key they can create, and the run is still untracked then
+        // every key they can create and every key they lowered past it, and
+        // the run is still untracked then
         const bool fail = in && lane > 0 &&
-                          (!(pm < cnt) || (dt && (z0 + lane) % dt == 0) || (!E->fast && live0 - rexg < TRACK_LIMIT) ||
-                           (ovm & ((2ull << lane) - 1ull)) != 0);
+                          (!(pm < cnt) || skfail || (dt && (z0 + lane) % dt == 0) ||
+                           (!E->fast && live0 - rexg < TRACK_LIMIT) || (ovm & ((2ull << lane) - 1ull)) != 0);
         const unsigned long long fm = __ballot(fail);
         uint32_t js = fm ? (uint32_t)__ffsll(fm) - 1 : k;
+        if (fm && blockIdx.x == 0 && __ballot(skfail) & fm & (0ull - fm)) {  // (the first failure was a skipped key's)
+            if (lane == 0) atomicAdd(&B->nskfail, 1ull);
+        }
         if (E->dbg_form && C->merges_done + 1 >= E->dbg_form && blockIdx.x == 0 && lane == 0)
             printf("verify shard %u z0 %u k %u js %u ovm %llx R0 %u Rg0 %u\n", E->shard, z0, k, js, ovm, R, Rg);
         if (js < k) {  // re-form the batch with the verified prefix; apply nothing
@@ -1464,7 +1567,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             } else if (r >= 2) {
                 cat = (r - 2) / Wd;
                 x = (r - 2) % Wd;
-                uint32_t *pw = E->xbat + BK + (uint64_t)m * per + r;
+                uint32_t *pw = E->xbat + XBH + (uint64_t)m * per + r;
                 val = *pw;
                 if (val) *pw = 0;
             }
@@ -1576,7 +1679,9 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                                                      : __hip_atomic_load(&B->ztot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long D0 = C->D;
                 const uint64_t Bsz = C->B, lo = summary_B(D0 > Z ? D0 - Z : 0);
-                const bool f = lane >= 1 && lane < jsB &&
+                // (members before tpend were admitted on the conservative span
+                // bound, which holds whatever the batch zeroes: not re-checked)
+                const bool f = lane >= 1 && lane >= B->tpend && lane < jsB &&
                                !tie_levels_ok(lo, summary_B(D0 + B->tspan[lane]), Bsz, B->tmask[lane]);
                 const unsigned long long fm = __ballot(f);
                 if (lane == 0) sjf = fm ? (uint32_t)__ffsll(fm) - 1 : jsB;
@@ -1591,10 +1696,15 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                     rd += (long long)(old - d != 0) - (long long)(old != 0);
                 }
                 dD += rd;  // (this block's sum below carries the whole revert's D change)
-                nzero = 0;
                 jf = 0;
+            } else if (tid == 0) {
+                // the batch stands: its zeroed keys count towards the zrate
+                // guess (every block's share is in ztot; reverted batches add none)
+                const uint32_t zt = __hip_atomic_load(&B->ztot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (zt) atomicAdd(&B->nzero, (unsigned long long)zt);
             }
         }
+        nzero = 0;  // (counted through ztot above)
     }
     if (keep) {
         // bookkeeping and the role-A descriptor for k_bsel's rewrite blocks

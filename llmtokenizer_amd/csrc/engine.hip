@@ -423,7 +423,11 @@ int getenv_int(const char *k, int dflt);
 // batch's first member, which the verification never drops, always fits)
 void xsp_layout(uint64_t vcap, uint32_t *cap, uint32_t *stride) {
     const uint64_t one = vcap > DENSE ? 4 * (vcap - DENSE) : 1;
-    *cap = (uint32_t)std::max<uint64_t>(one, (uint64_t)std::min(1 << 22, std::max(1, getenv_int("BPE_XSP_CAP", 1 << 20))));
+    // one batch lists at most BK members x 4 vectors x (vcap - DENSE) ids:
+    // never more room than that (the mailbox and the RCCL gather carry it)
+    const uint64_t most = (uint64_t)BK * one;
+    const uint64_t want = (uint64_t)std::min(1 << 22, std::max(1, getenv_int("BPE_XSP_CAP", 1 << 20)));
+    *cap = (uint32_t)std::max<uint64_t>(one, std::min(want, most));
     *stride = (2 + 2 * *cap + 3) / 4 * 4;
 }
 
@@ -539,6 +543,9 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
                       (c->sharded || c->fast || n0 >= TRACK_LIMIT)  // (batches: untracked iterations only)
                   ? 1
                   : 0;
+    // batches skip list entries that do not commute with an earlier member
+    // (BPE_SKIP=0: the formation ends there, as before round 5)
+    h.skip_on = (uint32_t)(getenv_int("BPE_SKIP", 0) != 0);
     h.xbat = nullptr;
     h.xsp_out = h.xsp_in = nullptr;
     h.xsp_cap = 0;
@@ -1525,6 +1532,12 @@ int batch_stats(bpe_gpu_ctx *c) {
     c->stats.tie_failed = hb.ntfail;
     c->stats.keys_zeroed = hb.nzero;
     {
+        unsigned long long t[2] = {0, 0};  // (nskip, nskfail: outside the head)
+        HIPCHK(hipMemcpy(t, &c->h.bat->nskip, 16, hipMemcpyDeviceToHost));
+        c->stats.keys_skipped = t[0];
+        c->stats.skip_failed = t[1];
+    }
+    {
         unsigned long long t[2] = {0, 0};  // (sl_ticks, nsl: outside the head copied above)
         HIPCHK(hipMemcpy(t, &c->h.bat->sl_ticks, 16, hipMemcpyDeviceToHost));
         int khz = 0;
@@ -1544,9 +1557,9 @@ int batch_stats(bpe_gpu_ctx *c) {
     if (getenv("BPE_DEBUG"))
         fprintf(stderr, "batches %llu, dropped %llu, re-formed %llu; formation ended by: list %llu, cap/count/hot_T %llu, a==b %llu, "
                 "duplicate %llu, tie %llu, conflict %llu, table margin %llu, staging %llu; tie-verified %llu (re-formed %llu); "
-                "keys zeroed %llu\n", hb.nbatch, hb.ndrop, hb.nretry,
+                "keys zeroed %llu; keys skipped %llu (re-formed %llu)\n", hb.nbatch, hb.ndrop, hb.nretry,
                 hb.why[0], hb.why[1], hb.why[2], hb.why[3], hb.why[4], hb.why[5], hb.why[6], hb.why[7], hb.ntie, hb.ntfail,
-                hb.nzero);
+                hb.nzero, (unsigned long long)c->stats.keys_skipped, (unsigned long long)c->stats.skip_failed);
     return 0;
 }
 

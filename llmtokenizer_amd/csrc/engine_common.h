@@ -167,17 +167,30 @@ struct Bat {
     // block exit), folded by the next k_bapply (outside the select's staged
     // head, which it writes back whole); launches folded
     unsigned long long sl_in, sl_out, sl_ticks, nsl;
+    // keys the formation skipped (batch.hip): a listed key that shares an id,
+    // on the opposite side, with an earlier member is no member -- the
+    // sequential passes lower its count when that member merges -- and every
+    // member after it must beat its lowered count (k_bapply).  Written by the
+    // selection directly (outside its staged head).
+    uint32_t nsk, skpad;
+    uint32_t sk_a[BK], sk_b[BK], sk_c[BK];
+    uint32_t sdec[BK];                  // one GPU: the decrements its conflicting members made (k_bscan, atomic)
+    unsigned long long sk_cm[BK];       // those members (bit = member index)
+    uint8_t nskb[64];                   // per member: keys skipped before it in the list
+    unsigned long long nskip, nskfail;  // keys skipped in applied batches; batches re-formed by that check
 };
 
 // Sharded batches: the words one batch exchanges (summed over the shards):
-// [BK] staging-overflow flags, then per member [R, bound, DL, DR, IL, IR] with
-// the four delta vectors dense over the ids < z0 + k (the batch's W)
+// [BK] staging-overflow flags, [BK] the skipped keys' decrements (Bat::sdec),
+// then per member [R, bound, DL, DR, IL, IR] with the four delta vectors dense
+// over the ids < z0 + k (the batch's W)
 // sharded batches: a member's exchange words are R, bound and its four delta
 // vectors dense over the ids below min(W, DENSE); larger ids travel as (id,
 // delta) lists (xsp_*, k_bpack)
 __host__ __device__ inline uint32_t xbat_vw(uint32_t W) { return W < DENSE ? W : DENSE; }
 __host__ __device__ inline uint32_t xbat_member_words(uint32_t W) { return 2 + 4 * xbat_vw(W); }
-__host__ __device__ inline uint32_t xbat_words(uint32_t k, uint32_t W) { return BK + k * xbat_member_words(W); }
+constexpr uint32_t XBH = 2 * BK;  // head words of the exchange: overflow flags, skipped keys' decrements
+__host__ __device__ inline uint32_t xbat_words(uint32_t k, uint32_t W) { return XBH + k * xbat_member_words(W); }
 
 // Device-resident descriptor: every kernel takes a pointer to it, so tables can
 // be regrown without re-capturing the iteration graph.
@@ -265,6 +278,7 @@ struct Eng {
     uint32_t *hotp_tie;
     // batched training (batch.hip; occurrence positions staged in ids_out)
     uint32_t batch;       // 1: the batch kernels drive the run
+    uint32_t skip_on;     // batches: skip non-commuting list entries instead of ending there (BPE_SKIP, default 1)
     uint32_t bvs;         // ids >= DENSE per (member, vector) in bvec / bvlist
     Bat *bat;
     uint16_t *btag;       // [n0] neighbour tags of the staged occurrences

@@ -581,7 +581,10 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         // and a P2P mailbox with the list channel)
         uint32_t xcap, xstride;
         xsp_layout(vc, &xcap, &xstride);
-        c->sbatch = getenv_int("BPE_BATCH", 1) && (!g->p2p || xbat_words(BK, (uint32_t)vc) <= g->hp.c0) &&
+        // (vc <= BATCH_VCAP_MAX as setup_run requires for h.batch: a run that
+        // set h.hot for batches but could not batch would have no argmax)
+        c->sbatch = getenv_int("BPE_BATCH", 1) && vc <= BATCH_VCAP_MAX &&
+                    (!g->p2p || xbat_words(BK, (uint32_t)vc) <= g->hp.c0) &&
                     (vc <= DENSE || (g->nshards <= P2P_MAXR_B && (!g->p2p || g->hp.stride2 >= xstride)));
         c->xfused = g->p2p && K == 1 && FUSED_SH && !c->sbatch;
         c->xtimeout = g->hp.timeout;
@@ -685,6 +688,8 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     g->stats.tie_verified = s0.tie_verified;
     g->stats.tie_failed = s0.tie_failed;
     g->stats.keys_zeroed = s0.keys_zeroed;
+    g->stats.keys_skipped = s0.keys_skipped;
+    g->stats.skip_failed = s0.skip_failed;
     g->stats.ms_scan_span = s0.ms_scan_span;
     g->stats.ms_apply_span = s0.ms_apply_span;
     g->stats.hot_rebuilds = g->cs[0]->hC->hot_rebuilds;

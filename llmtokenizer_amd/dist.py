@@ -114,15 +114,24 @@ def first_job(g, device, job, make_rccl=None):
     shard into it and runs the job again.  A failure on an RCCL group is
     raised (nothing to fall back to)."""
     import torch.distributed as dist
-    err, dig = None, None
+    err, dig, other = None, None, None
     try:
         dig = job(g)
     except api.BpeError as e:
         err = str(e)
+    except Exception as e:  # (any failure: the other ranks must not block in the gather)
+        err, other = f"{type(e).__name__}: {e}", e
     outs = [None] * dist.get_world_size()
-    dist.all_gather_object(outs, (err, dig))
-    errs = [e for e, _ in outs if e]
-    if not errs and len({d for _, d in outs}) > 1:
+    dist.all_gather_object(outs, (err, dig, other is not None))
+    # not a transport failure somewhere: every rank raises (no fallback
+    # group, whose set-up would wait for the failed rank)
+    if other is not None:
+        raise other
+    fatal = [e for e, _, f in outs if f]
+    if fatal:
+        raise api.BpeError("sharded job failed on another rank: " + fatal[0])
+    errs = [e for e, _, _ in outs if e]
+    if not errs and len({d for _, d, _ in outs}) > 1:
         errs = ["the ranks' results differ"]
     if not errs:
         return g, True

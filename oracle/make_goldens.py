@@ -73,7 +73,12 @@ def cases(big: bool):
         c.append(dict(name=f"synth_s{seed}_{n}", seed=seed, n=n, max_merges=m))
     c.append(dict(name="synth_s7_64k", seed=7, n=65536, max_merges=512))
     c.append(dict(name="synth_s3_300k", seed=3, n=300000, max_merges=256))
+    # the reference's own corpora, committed as data fixtures
+    # under tests/golden/: testing.txt to the stop rule (config 0's input) and
+    # random_text.txt x 1024 merges (config 1's input; ~2 min of reference time)
+    c.append(dict(name="ref_testing", file="testing.txt", max_merges=-1))
     if big:
+        c.append(dict(name="ref_random_text", file="random_text.txt", max_merges=1024))
         # config 2 analog: 1 MiB (n == 2^20: iteration 0 is dynamic), 1024 merges
         c.append(dict(name="synth_s1_1m", seed=1, n=1 << 20, max_merges=1024))
         # dynamic but tracked (2^20 <= n < 2^21)
@@ -86,7 +91,7 @@ def cases(big: bool):
 
 # fixtures that also keep the reference's own dump_pairs file (bpe.c:243-278)
 # and main.c's stdout (print_text of the encoding, bpe.c:182-196)
-WITH_IO = ("prose", "synth_s1_4k", "aab_runs", "binary_5k", "nul_truncates")
+WITH_IO = ("prose", "synth_s1_4k", "aab_runs", "binary_5k", "nul_truncates", "ref_testing", "ref_random_text")
 
 
 def run_ref(data: bytes, max_merges: int, with_io=False):
@@ -127,12 +132,18 @@ def main():
         if args.only and c["name"] not in args.only:
             continue
         data = c.get("data")
-        if data is None:
+        if "file" in c:
+            with open(os.path.join(GOLD, c["file"]), "rb") as f:
+                data = f.read()
+        elif data is None:
             data = synth_bytes(c["seed"], c["n"])
         r = run_ref(data, c["max_merges"], with_io=c["name"] in WITH_IO)
         fx = dict(name=c["name"], max_merges=c["max_merges"], generator="oracle/make_goldens.py",
                   ref_seconds=round(r["seconds"], 3))
-        if "data" in c:
+        if "file" in c:
+            fx["input_file"] = c["file"]
+            fx["input_sha256"] = hashlib.sha256(data).hexdigest()
+        elif "data" in c:
             fx["input_b64"] = base64.b64encode(c["data"]).decode()
         else:
             fx["synth"] = dict(seed=c["seed"], n=c["n"])

@@ -29,6 +29,9 @@ def load(name):
 
 
 def input_bytes(fx) -> bytes:
+    if "input_file" in fx:  # a data fixture beside the json (the reference's own corpora)
+        with open(os.path.join(GOLD, fx["input_file"]), "rb") as f:
+            return f.read()
     if "input_b64" in fx:
         return base64.b64decode(fx["input_b64"])
     from llmtokenizer_amd.synth import synth_bytes
@@ -36,6 +39,8 @@ def input_bytes(fx) -> bytes:
 
 
 def input_size(fx) -> int:
+    if "input_file" in fx:
+        return os.path.getsize(os.path.join(GOLD, fx["input_file"]))
     if "input_b64" in fx:
         return len(base64.b64decode(fx["input_b64"]))
     return fx["synth"]["n"]

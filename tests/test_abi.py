@@ -73,7 +73,7 @@ def test_dump_read_pairs_format(tmp_path):
     assert back.tolist() == merges[:3].tolist()
 
 
-IO_FIXTURES = ["prose", "synth_s1_4k", "aab_runs", "binary_5k", "nul_truncates"]
+IO_FIXTURES = ["prose", "synth_s1_4k", "aab_runs", "binary_5k", "nul_truncates", "ref_testing", "ref_random_text"]
 
 
 @pytest.mark.parametrize("name", IO_FIXTURES)

@@ -216,3 +216,33 @@ def test_streaming_file_load(tmp_path):
     ref.load(bytes(data[:cut]))
     ref.train(4)
     assert (merges == ref.merges()).all() and (ids == ref.ids()).all()
+
+
+# the reference's own corpora, committed as data fixtures (tests/golden/*.txt);
+# merges md5 of "id a b\n" lines and ids md5 (u32 LE) of the reference's run
+# on them (regenerated by oracle/make_goldens.py: ref_*.json)
+REF_CORPORA = {
+    "testing.txt": ("2cbb056a34a294df9ff8e80c9326c19b", "327cc96dfd8cfbbb5c69c83324c87b9f", None, "ref_testing"),
+    "random_text.txt": ("45c9290b9dc2554bb90bca1a0dc4be9a", "9c5f6099bc1adcbd06d2afbee767f8dd", 1024,
+                        "ref_random_text"),
+}
+
+
+@pytest.mark.parametrize("fname", sorted(REF_CORPORA))
+def test_reference_corpora_literal_inputs(fname):
+    """configs[0] / configs[1] on their literal inputs on the GPU: compress(path)
+    through the C-ABI, and the reference-compatible CLI (tools/bpe_main,
+    main.c's contract) with BPE_MAX_MERGES, against the reference's hashes"""
+    import subprocess
+    m_md5, i_md5, cap, gname = REF_CORPORA[fname]
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", fname)
+    merges, ids = api.compress(path, max_merges=cap)
+    txt = "".join(f"{256 + r} {a} {b}\n" for r, (a, b) in enumerate(merges.tolist()))
+    assert hashlib.md5(txt.encode()).hexdigest() == m_md5
+    assert G.ids_md5(ids) == i_md5
+    fx = G.load(gname)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, BPE_MAX_MERGES=str(cap if cap is not None else -1))
+    out = subprocess.run([os.path.join(root, "tools", "bpe_main"), path], capture_output=True, check=True,
+                         timeout=120, env=env).stdout
+    assert len(out) == fx["print_text_len"] and hashlib.md5(out).hexdigest() == fx["print_text_md5"]

@@ -193,3 +193,22 @@ def test_batches_beyond_dense_ids_equal_single_engine(cap, engine_mode, monkeypa
     if engine_mode == "batch":
         assert st["batches"] > 0
         print("beyond DENSE", cap, {k: st[k] for k in ("batches", "batch_retries", "batch_dropped")})
+
+
+def test_unlimited_merges_above_batch_vocabulary_equal_single_engine():
+    """max_merges = -1 on a group of more than 2^18 tokens: the merge cap (and
+    the vocabulary) is then above what batches take, so the sharded run must
+    not enable the hot set for batches it cannot form (it takes the one-merge
+    exchange); trained to the stop rule, == the single engine"""
+    rng = np.random.default_rng(11)
+    block = bytes(rng.integers(32, 127, 3000, dtype=np.uint8))
+    data = block * 100  # 300 000 tokens; every pair of the block repeats
+    e = api.Engine(0)
+    e.load(data)
+    e.train(-1, fast=True)
+    em, ei = e.merges(), e.ids()
+    e.close()
+    gm, gi, g = _group_train(data, [0, 100003, 200001, len(data)], -1)
+    g.close()
+    _assert_same(gm, gi, em, ei, "unlimited merges")
+    assert em.shape[0] > 2000
