@@ -203,6 +203,46 @@ def timed_jobs(cx, run, k):
     return cx.allreduce(t1 - t0, "max")
 
 
+GATHER_CEILING = os.path.join(ROOT, "profiles", "r5_gather_ceiling.jsonl")  # tools/gather_bench on the MI355X
+
+
+def gather_ceiling(mode, waves=None):
+    """the measured random-access ceiling (tools/gather_bench.hip, committed
+    summary): best gathers/s of `mode` over in-flight depth U (and over the
+    waves per CU unless `waves` is given), with the configuration it took"""
+    if not os.path.exists(GATHER_CEILING):
+        return None
+    best = None
+    with open(GATHER_CEILING) as f:
+        for line in f:
+            try:
+                r = json.loads(line)
+            except ValueError:
+                continue
+            if r.get("mode") != mode or (waves is not None and r.get("waves_per_cu") != waves):
+                continue
+            if best is None or r["gathers_per_s"] > best["gathers_per_s"]:
+                best = r
+    return best
+
+
+def line_rate(achieved, mode, waves, note):
+    """roofline.line_rate: random accesses per second of a loop kernel against
+    the part's measured ceiling for that access shape"""
+    at = gather_ceiling(mode, waves)
+    top = gather_ceiling(mode)
+    if not at or not top:
+        return None
+    return {"unit": "random accesses/s", "achieved": float("%.4g" % achieved), "shape": mode,
+            "ceiling_at_kernel_occupancy": float("%.4g" % at["gathers_per_s"]),
+            "ceiling_config": {"waves_per_cu": at["waves_per_cu"], "in_flight_per_thread": at["U"]},
+            "frac": round(achieved / at["gathers_per_s"], 4),
+            "ceiling_best": float("%.4g" % top["gathers_per_s"]),
+            "ceiling_best_config": {"waves_per_cu": top["waves_per_cu"], "in_flight_per_thread": top["U"]},
+            "frac_of_best": round(achieved / top["gathers_per_s"], 4),
+            "source": os.path.relpath(GATHER_CEILING, ROOT), "note": note}
+
+
 def committed_profile(name, sharded=False):
     """rocprof average (ms) of kernel `name` and PMC traffic per launch from
     the committed summaries of this same command (profiles/<tag>_*): the
@@ -591,6 +631,14 @@ def main():
         out["roofline"]["traffic"] = cp["traffic"]
     if "avg_ms_rocprof" in cp:
         out["roofline"]["frac_at_rocprof_avg"] = round(kbytes / (cp["avg_ms_rocprof"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    # the scan's real limit: one random 32-byte token window per candidate
+    # (tok_window), 16 waves per CU (one 1024-thread block), against what the
+    # part delivers for that access shape
+    if launches and kms > 0 and st.get("candidates"):
+        lr = line_rate(st["candidates"] / launches / (kms * 1e-3), "window32", 16,
+                       "candidates per launch / k_bscan's span: each gathers one random 32-B window of a 4 GiB tok[]")
+        if lr:
+            out["roofline"]["line_rate"] = lr
     # the batch apply (the pair-table updates): 16 B per update (the key probed,
     # the count read and written), span from the device wall clock like the scan
     nl = st["batches"] + st["batch_retries"]
@@ -603,6 +651,10 @@ def main():
                                  "bytes_per_launch": round(ab), "avg_ms": round(st["ms_apply_span"], 5), "launches": nl,
                                  "avg_ms_rocprof": ap.get("avg_ms_rocprof"), "rocprof_summary": ap.get("rocprof_summary"),
                                  "note": "16 B per pair-table update (random key probe + count); random-line bound"}
+        lr = line_rate(st["table_updates"] / nl / (st["ms_apply_span"] * 1e-3), "atomic_ret", 16,
+                       "table updates / k_bapply's span: each a random key probe, then a returning u32 atomic")
+        if lr:
+            out["roofline_apply"]["line_rate"] = lr
     # the batch select k_bsel: the hot set reduced (16 B per listed key: slot,
     # count, key) beside the previous batch's token rewrite (12 B per
     # occurrence: the id, the end code, the pool entry)

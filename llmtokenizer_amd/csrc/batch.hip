@@ -47,6 +47,10 @@ static_assert(BK < 64, "member masks are 64-bit");
 #ifndef BPE_RU
 #define BPE_RU 4
 #endif
+#ifndef BPE_AU
+#define BPE_AU 4
+#endif
+constexpr uint32_t AU = BPE_AU;  // k_bapply role B: table updates per thread in flight together
 constexpr uint32_t SU = BPE_SU;  // k_bscan candidates per thread per round (1: measured fastest, 85 vs 91 ms at 4)
 #ifndef BPE_FR
 #define BPE_FR 4
@@ -196,6 +200,46 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
     if (tid == 0) clear_k = nmem = xclr_k = 0;
     __syncthreads();
     block_list_tree(part, blockDim.x >> 6);
+    // The list's next TOPK keys (E->list2): the same tree over the partial
+    // lists with the entries the first list took removed (a partial list's
+    // entries in it are a prefix: both are in argmax order).  A FULL partial
+    // list may hold further keys behind its last entry, so the second list is
+    // exact only down to the most advanced such last entry (the horizon) --
+    // with ~500 keys per partial list and ~4 of them in the first 128, it
+    // hardly ever binds.
+    KV e1 = kv_empty(), e2 = kv_empty();
+    uint32_t nl2 = 0;
+    bool trunc2 = false;
+    const KV l1last = part[0][TOPK - 1];
+    if (tid < 64) e1 = part[0][lane];
+    if (E->list2 && l1last.v != 0) {  // (block-uniform)
+        __shared__ KV hzs[16];
+        __syncthreads();  // (every wave has read the first list)
+        auto shift = [&](const KV &z) {
+            const uint32_t n1 = (uint32_t)__popcll(__ballot(z.v != 0 && !kv_ahead(l1last, z)));
+            const uint32_t src = lane + n1;
+            const KV r = kv_shfl(z, (int)(src < 64 ? src : 63));
+            return src < 64 ? r : kv_empty();
+        };
+        const KV xl = kv_shfl(x, 63), yl = kv_shfl(y, 63);
+        KV hz = kv_empty();
+        if (xl.v != 0) hz = xl;
+        if (yl.v != 0 && (hz.v == 0 || kv_ahead(yl, hz))) hz = yl;
+        part[w][lane] = wave_top(shift(x), shift(y));
+        if (lane == 0) hzs[w] = hz;
+        __syncthreads();
+        block_list_tree(part, blockDim.x >> 6);
+        if (tid < 64) {
+            e2 = part[0][lane];
+            KV H = kv_empty();
+            for (uint32_t q = 0; q < (blockDim.x >> 6); q++)
+                if (hzs[q].v != 0 && (H.v == 0 || kv_ahead(hzs[q], H))) H = hzs[q];
+            const bool ok = e2.v != 0 && (H.v == 0 || !kv_ahead(H, e2));  // (ahead of or at the horizon)
+            nl2 = (uint32_t)__popcll(__ballot(ok));
+            trunc2 = nl2 == TOPK || nl2 < (uint32_t)__popcll(__ballot(e2.v != 0));
+            if (!ok) e2 = kv_empty();
+        }
+    }
     ts_mark(E, bi, BT_SEL_LIST, false);
     Bat *B = reinterpret_cast<Bat *>(&sbh);  // (head fields only)
     // Wave 0 decides, one list entry per lane; every lane reads the staged
@@ -223,7 +267,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         const uint32_t md = C->merges_done + jst;
         const unsigned long long n_live = C->n_live - rg;
         // ---- the list, one entry per lane
-        const KV e = lane < TOPK ? part[0][lane] : kv_empty();
+        const KV e = e1;  // (part[0] may hold the second list now)
         const unsigned long long kprev = __shfl(e.k, (int)(lane ? lane - 1 : 0));
         const uint32_t nl = (uint32_t)__popcll(__ballot(lane < TOPK && e.v != 0));  // non-empty (sorted first)
         const bool truncated = nl == TOPK;  // more keys may follow the list
@@ -250,146 +294,205 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         else if (relist_due) stop = STOP_RELIST;
         else if (v0 == 0 || cnt0 <= 1) stop = STOP_DONE;
         else if (C->nkeys + 4ull * (256ull + md + 2) >= E->hcap / 2) stop = STOP_GROW;
-        // ---- the batch: the longest prefix of the list whose entries qualify
+        // ---- the batch: members from the list in order, skipping the entries
+        // that do not commute with an earlier member, up to the first entry
+        // that qualifies as neither; over the second list too when the first
+        // one is used up (two passes of the same rules)
         uint32_t k = 0;
         if (stop == STOP_NONE) {
-            const uint32_t u = (uint32_t)(e.k >> 32), v = (uint32_t)e.k, c = (uint32_t)(e.v >> 32);
-            // ties with the next key keep their pre-batch order when the members
-            // before it cannot move B_final: a member adds or zeroes at most
-            // 2 min(ids, count) + 1 keys (its neighbours' pairs and its own),
-            // where the ids a neighbour can be are the A byte values present and
-            // the merged ids up to this batch's last (not all 256 byte values:
-            // text has ~95, which early in a run is most of the bound)
-            const uint32_t cprev = (uint32_t)(__shfl(e.v, (int)(lane ? lane - 1 : 0)) >> 32);
-            unsigned long long span =
-                lane > 0 && lane <= nl ? min(2ull * ((unsigned long long)E->A + md + BK), 2ull * cprev) + 1 : 0ull;
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned long long y = __shfl_up(span, o);
-                if ((int)lane >= o) span += y;
-            }
-            const uint64_t Blo = summary_B(D > span ? D - span : 0), Bhi = summary_B(D + span);
-            const bool stable = Blo == Bsz && Bhi == Bsz;
-            // D only falls by the keys the members zero (their own and a few
-            // neighbour pairs): with a guess of those from the batches so far,
-            // the lower end of the reachable B is usually B_sz; k_bapply counts
-            // the keys really zeroed and checks that guess (verified members)
-            const unsigned long long zg = 16ull + (unsigned long long)B->zrate * lane;
-            const uint64_t Blo_o = summary_B(D > zg ? D - zg : 0);
-            const uint32_t cnext = __shfl(c, (int)(lane < 63 ? lane + 1 : 63));
-            // otherwise keys of one count keep my order against them under every
-            // B the members before me can reach (bucket = murmur & (B - 1), then
-            // the key): checked against the listed keys of my count after me, as
-            // a mask of the levels B = B_sz 2^e (bit e + 5) where it holds
-            const uint32_t hsh = murmur_pair(u, v);
-            const uint32_t clast = __shfl(c, (int)(nl ? nl - 1 : 0));
             const int zsz = __builtin_ctzll(Bsz);
-            uint32_t tmask = 0xFFu;
-            const bool tie_next = lane < nl && !(c > (lane + 1 < nl ? cnext : 0u));
-            const bool check = __ballot(!stable && lane > 0 && lane < BK && tie_next) != 0;  // (wave-uniform)
-            for (uint32_t p = 1; check && p < TOPK; p++) {  // (uniform loop; readlane needs every lane)
-                const uint32_t cp = __builtin_amdgcn_readlane((int)c, (int)p);
-                const uint32_t hp = __builtin_amdgcn_readlane((int)hsh, (int)p);
-                const unsigned long long kp =
-                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)u, (int)p) << 32) |
-                    (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p);
-                if (p > lane && p < nl && cp == c)
-                    for (uint64_t Bx = Blo; Bx <= Bhi; Bx <<= 1) {
-                        const uint64_t bj = hsh & (Bx - 1), bp = hp & (Bx - 1);
-                        const int lv = __builtin_ctzll(Bx) - zsz + 5;
-                        if (!(bj < bp || (bj == bp && e.k < kp)) && lv >= 0 && lv < 8) tmask &= ~(1u << lv);
-                    }
-            }
-            if (truncated && c == clast) tmask &= 1u << 5;  // (keys past the list keep their order under B_sz only)
-            const bool tie_rel = !stable && ((truncated && c == clast) || tie_next);
-            const bool cons_ok = tie_levels_ok(Blo, Bhi, Bsz, tmask);
-            const bool opt_ok = tie_levels_ok(Blo_o, Bhi, Bsz, tmask);
-            uint32_t why = 0;  // 0: qualifies
-            if (lane >= nl || lane >= BK) why = 8;  // past the list (reported as "list")
-            else if (lane > 0) {
-                if (e.k == kprev) why = 3;  // the same key listed twice (the one-merge engine's undo): end here
-                else if (md + lane >= E->mcap || c <= 1 || (hotT > 2 && c < hotT)) why = 1;
-                else if (tie_rel && !cons_ok && !(opt_ok && E->tie_verify))
-                    why = 4;  // (a tie whose order the batch could change, or one running past the list)
-                else if (C->nkeys + 4ull * (256ull + md + lane + 2) * (lane + 1) >= E->hcap / 2) why = 6;
-            }
-            // the earlier entries that do not commute with me: one uses my left
-            // id on its right or my right id on its left
-            unsigned long long cm = 0;
+            uint32_t kk = 0, nskt = 0, tpend = BK, endwhy = 8, kend = 64;
+            unsigned long long spanbase = 0;
+            // the members so far, lane q = member q (list order)
+            uint32_t mu = 0, mv = 0, mc = 0, mtmask = 0, mnskb = 0;
+            unsigned long long mspan = 0;
+            bool more = true;
+            uint32_t npass = 0;
 #pragma unroll
-            for (uint32_t p = 0; p < BK; p++) {
-                const uint32_t up = __builtin_amdgcn_readlane((int)u, (int)p), vp = __builtin_amdgcn_readlane((int)v, (int)p);
-                if (p < lane && (u == vp || v == up)) cm |= 1ull << p;
-            }
-            // Members, entry by entry.  An entry that commutes with every earlier
-            // MEMBER joins (its occurrences are the pre-batch ones).  One that
-            // does not is SKIPPED: the sequential passes lower its count when
-            // those members merge (their occurrences consume its tokens), so
-            // it is not the argmax at its turn provided its lowered count falls
-            // below the next member's -- k_bscan counts the decrements, k_bapply
-            // checks every member against the skipped keys before it.  It
-            // merges in a later batch.  (Ids below DENSE: the scan's LDS
-            // vectors hold the decrements; a tie order of its own is moot.)
-            const bool skok = E->skip_on && u < DENSE && v < DENSE && (why == 0 || why == 4);
-            unsigned long long M = 0, S = 0;
-            uint32_t kend = 64, endwhy = 8;
-            {
-                const uint32_t cmlo = (uint32_t)cm, cmhi = (uint32_t)(cm >> 32);
-                for (uint32_t p = 0; p < 64; p++) {  // (uniform: every operand is a readlane)
-                    const unsigned long long cp = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)cmhi, (int)p) << 32) |
-                                                  (uint32_t)__builtin_amdgcn_readlane((int)cmlo, (int)p);
-                    const uint32_t wp = (uint32_t)__builtin_amdgcn_readlane((int)why, (int)p);
-                    if (cp & M) {
-                        if (__builtin_amdgcn_readlane((int)skok, (int)p)) {
-                            S |= 1ull << p;
-                            continue;
-                        }
-                        kend = p;
-                        endwhy = 5;
-                        break;
-                    }
-                    if (wp) {
-                        kend = p;
-                        endwhy = wp;
-                        break;
-                    }
-                    M |= 1ull << p;
+            for (uint32_t pass = 0; pass < 2; pass++) {  // (uniform)
+                if (!more) break;
+                more = false;
+                const KV ep = pass ? e2 : e;
+                const uint32_t nlp = pass ? nl2 : nl;
+                const bool trunc = pass ? trunc2 : truncated;
+                const uint32_t u = (uint32_t)(ep.k >> 32), v = (uint32_t)ep.k, c = (uint32_t)(ep.v >> 32);
+                // the entry before me (the first list's last one for the second's first)
+                const unsigned long long vprev0 = __shfl(ep.v, (int)(lane ? lane - 1 : 0));
+                const unsigned long long kprevp = lane ? __shfl(ep.k, (int)(lane - 1)) : (pass ? l1last.k : ep.k);
+                const uint32_t cprev = (uint32_t)((lane ? vprev0 : (pass ? l1last.v : 0ull)) >> 32);
+                const bool first = pass == 0 && lane == 0;  // the argmax itself
+                // ties with the next key keep their pre-batch order when the members
+                // before it cannot move B_final: a member adds or zeroes at most
+                // 2 min(ids, count) + 1 keys (its neighbours' pairs and its own),
+                // where the ids a neighbour can be are the A byte values present and
+                // the merged ids up to this batch's last (not all 256 byte values:
+                // text has ~95, which early in a run is most of the bound)
+                unsigned long long span =
+                    !first && lane < nlp ? min(2ull * ((unsigned long long)E->A + md + BK), 2ull * cprev) + 1 : 0ull;
+                for (int o = 1; o < 64; o <<= 1) {
+                    const unsigned long long y = __shfl_up(span, o);
+                    if ((int)lane >= o) span += y;
                 }
+                span += spanbase;
+                const uint64_t Blo = summary_B(D > span ? D - span : 0), Bhi = summary_B(D + span);
+                const bool stable = Blo == Bsz && Bhi == Bsz;
+                // D only falls by the keys the members zero (their own and a few
+                // neighbour pairs): with a guess of those from the batches so far,
+                // the lower end of the reachable B is usually B_sz; k_bapply counts
+                // the keys really zeroed and checks that guess (verified members)
+                const unsigned long long zg = 16ull + (unsigned long long)B->zrate * (kk + lane);
+                const uint64_t Blo_o = summary_B(D > zg ? D - zg : 0);
+                const uint32_t cnext = __shfl(c, (int)(lane < 63 ? lane + 1 : 63));
+                // otherwise keys of one count keep my order against them under every
+                // B the members before me can reach (bucket = murmur & (B - 1), then
+                // the key): checked against the listed keys of my count after me, as
+                // a mask of the levels B = B_sz 2^e (bit e + 5) where it holds
+                const uint32_t hsh = murmur_pair(u, v);
+                const uint32_t clast = __shfl(c, (int)(nlp ? nlp - 1 : 0));
+                uint32_t tmask = 0xFFu;
+                const bool tie_next = lane < nlp && !(c > (lane + 1 < nlp ? cnext : 0u));
+                const bool check = __ballot(!stable && !first && tie_next) != 0;  // (wave-uniform)
+                for (uint32_t p = 1; check && p < TOPK; p++) {  // (uniform loop; readlane needs every lane)
+                    const uint32_t cp = __builtin_amdgcn_readlane((int)c, (int)p);
+                    const uint32_t hp = __builtin_amdgcn_readlane((int)hsh, (int)p);
+                    const unsigned long long kp =
+                        ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)u, (int)p) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p);
+                    if (p > lane && p < nlp && cp == c)
+                        for (uint64_t Bx = Blo; Bx <= Bhi; Bx <<= 1) {
+                            const uint64_t bj = hsh & (Bx - 1), bp = hp & (Bx - 1);
+                            const int lv = __builtin_ctzll(Bx) - zsz + 5;
+                            if (!(bj < bp || (bj == bp && ep.k < kp)) && lv >= 0 && lv < 8) tmask &= ~(1u << lv);
+                        }
+                }
+                // (keys past this list -- the second list's, or unknown -- keep
+                // their order under B_sz only)
+                const bool past = trunc || (pass == 0 && E->list2);
+                if (past && c == clast) tmask &= 1u << 5;
+                const bool tie_rel = !stable && ((past && c == clast) || tie_next);
+                const bool cons_ok = tie_levels_ok(Blo, Bhi, Bsz, tmask);
+                const bool opt_ok = tie_levels_ok(Blo_o, Bhi, Bsz, tmask);
+                const uint32_t mi = kk + lane;  // (at least my member index)
+                uint32_t why = 0;               // 0: qualifies
+                if (lane >= nlp) why = 8;       // past the list (reported as "list")
+                else if (!first) {
+                    if (ep.k == kprevp) why = 3;  // the same key listed twice (the one-merge engine's undo): end here
+                    else if (md + mi >= E->mcap || c <= 1 || (hotT > 2 && c < hotT)) why = 1;
+                    else if (tie_rel && !cons_ok && !(opt_ok && E->tie_verify))
+                        why = 4;  // (a tie whose order the batch could change, or one running past the list)
+                    else if (C->nkeys + 4ull * (256ull + md + mi + 2) * (mi + 1) >= E->hcap / 2) why = 6;
+                }
+                // the earlier entries of this list that do not commute with me
+                // (one uses my left id on its right or my right id on its left),
+                // and the earlier passes' members that do not (by member index)
+                unsigned long long cm = 0, cmk = 0;
+#pragma unroll
+                for (uint32_t p = 0; p < BK; p++) {
+                    const uint32_t up = __builtin_amdgcn_readlane((int)u, (int)p), vp = __builtin_amdgcn_readlane((int)v, (int)p);
+                    if (p < lane && (u == vp || v == up)) cm |= 1ull << p;
+                }
+                for (uint32_t q = 0; q < kk; q++) {  // (uniform)
+                    const uint32_t uq = __builtin_amdgcn_readlane((int)mu, (int)q), vq = __builtin_amdgcn_readlane((int)mv, (int)q);
+                    if (u == vq || v == uq) cmk |= 1ull << q;
+                }
+                // Members, entry by entry.  An entry that commutes with every earlier
+                // MEMBER joins (its occurrences are the pre-batch ones).  One that
+                // does not is SKIPPED: the sequential passes lower its count when
+                // those members merge (their occurrences consume its tokens), so
+                // it is not the argmax at its turn provided its lowered count falls
+                // below the next member's -- k_bscan counts the decrements, k_bapply
+                // checks every member against the skipped keys before it.  It
+                // merges in a later batch.  (Ids below DENSE: the scan's LDS
+                // vectors hold the decrements; a tie order of its own is moot.)
+                const bool skok = E->skip_on && u < DENSE && v < DENSE && (why == 0 || why == 4);
+                unsigned long long M = 0, S = 0;
+                kend = 64;
+                {
+                    const uint32_t cmlo = (uint32_t)cm, cmhi = (uint32_t)(cm >> 32);
+                    const uint32_t cklo = (uint32_t)cmk, ckhi = (uint32_t)(cmk >> 32);
+                    for (uint32_t p = 0; p < 64; p++) {  // (uniform: every operand is a readlane)
+                        const unsigned long long cp = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)cmhi, (int)p) << 32) |
+                                                      (uint32_t)__builtin_amdgcn_readlane((int)cmlo, (int)p);
+                        const bool ck = (__builtin_amdgcn_readlane((int)cklo, (int)p) | __builtin_amdgcn_readlane((int)ckhi, (int)p)) != 0;
+                        const uint32_t wp = (uint32_t)__builtin_amdgcn_readlane((int)why, (int)p);
+                        if (ck || (cp & M)) {
+                            if (__builtin_amdgcn_readlane((int)skok, (int)p) && nskt + (uint32_t)__popcll(S) < BK) {
+                                S |= 1ull << p;
+                                continue;
+                            }
+                            kend = p;
+                            endwhy = 5;
+                            break;
+                        }
+                        if (wp) {
+                            kend = p;
+                            endwhy = wp;
+                            break;
+                        }
+                        if (kk + (uint32_t)__popcll(M) >= BK) {  // (the member cap: reported as "list")
+                            kend = p;
+                            endwhy = 8;
+                            break;
+                        }
+                        M |= 1ull << p;
+                    }
+                }
+                if (retry && retry < kk + (uint32_t)__popcll(M)) {  // the last batch failed at member `retry` (nothing changed since)
+                    unsigned long long xm = M;
+                    for (uint32_t q = kk; q < retry; q++) xm &= xm - 1;
+                    kend = (uint32_t)__builtin_ctzll(xm);
+                    M &= (1ull << kend) - 1;
+                    S &= (1ull << kend) - 1;
+                    endwhy = 8;
+                }
+                const uint32_t km = (uint32_t)__popcll(M);
+                const unsigned long long below = (1ull << lane) - 1;
+                const bool isM = (M >> lane) & 1;
+                // skipped keys, in list order: key, count, the members (by index)
+                // that lower it
+                if ((S >> lane) & 1) {
+                    const uint32_t si = nskt + (uint32_t)__popcll(S & below);
+                    unsigned long long cmm = cmk;
+                    for (unsigned long long xq = cm & M; xq; xq &= xq - 1)
+                        cmm |= 1ull << (kk + __popcll(M & ((1ull << __builtin_ctzll(xq)) - 1)));
+                    Bg->sk_a[si] = u;
+                    Bg->sk_b[si] = v;
+                    Bg->sk_c[si] = c;
+                    Bg->sk_cm[si] = cmm;
+                    Bg->sdec[si] = 0;
+                }
+                const bool pend = isM && !first && tie_rel && !cons_ok;  // admitted on the guess: k_bapply verifies
+                const unsigned long long pmk = __ballot(pend);
+                if (tpend == BK && pmk) tpend = kk + (uint32_t)__popcll(M & ((1ull << __builtin_ctzll(pmk)) - 1));
+                // this pass's members into lanes kk..kk+km-1 (forward permute:
+                // a full permutation, the rest into the other lanes in order)
+                const uint32_t j = (uint32_t)__popcll(~M & below);
+                const uint32_t dst = isM ? kk + (uint32_t)__popcll(M & below) : (j < kk ? j : j + km);
+                auto fwd = [&](uint32_t xv) { return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4), (int)xv); };
+                const uint32_t nskb = nskt + (uint32_t)__popcll(S & below);
+                const uint32_t pu = fwd(u), pv = fwd(v), pc = fwd(c), ptm = fwd(tmask), pnb = fwd(nskb);
+                const unsigned long long psp =
+                    ((unsigned long long)fwd((uint32_t)(span >> 32)) << 32) | (unsigned long long)fwd((uint32_t)span);
+                if (lane >= kk && lane < kk + km) {
+                    mu = pu;
+                    mv = pv;
+                    mc = pc;
+                    mtmask = ptm;
+                    mnskb = pnb;
+                    mspan = psp;
+                }
+                spanbase = __shfl(span, 63);
+                kk += km;
+                nskt += (uint32_t)__popcll(S);
+                npass = pass + 1;
+                // the first list used up (every entry a member or skipped): the second
+                more = pass == 0 && kend == 64 && endwhy == 8 && nl == TOPK && nl2 > 0 && kk < BK &&
+                       !(retry && retry <= kk);
             }
-            if (retry && retry < (uint32_t)__popcll(M)) {  // the last batch failed at member `retry` (nothing changed since)
-                unsigned long long x = M;
-                for (uint32_t q = 0; q < retry; q++) x &= x - 1;
-                kend = (uint32_t)__builtin_ctzll(x);
-                M &= (1ull << kend) - 1;
-            }
-            S &= M ? (2ull << (63 - __builtin_clzll(M))) - 1 : 0ull;  // (skipped keys a later member must beat)
-            k = (uint32_t)__popcll(M);  // lane 0 always qualifies
-            const unsigned long long below = (1ull << lane) - 1;
-            const bool isM = (M >> lane) & 1;
-            const uint32_t midx = (uint32_t)__popcll(M & below);
-            // skipped keys, in list order: key, count, the members (by index)
-            // that lower it
-            const uint32_t nsk = (uint32_t)__popcll(S);
-            if ((S >> lane) & 1) {
-                const uint32_t si = (uint32_t)__popcll(S & below);
-                unsigned long long cmm = 0;
-                for (unsigned long long x = cm & M; x; x &= x - 1) cmm |= 1ull << __popcll(M & ((1ull << __builtin_ctzll(x)) - 1));
-                Bg->sk_a[si] = u;
-                Bg->sk_b[si] = v;
-                Bg->sk_c[si] = c;
-                Bg->sk_cm[si] = cmm;
-                Bg->sdec[si] = 0;
-            }
-            const bool pend = isM && lane > 0 && tie_rel && !cons_ok;  // admitted on the guess: k_bapply verifies
-            const unsigned long long pmk = __ballot(pend);
-            const uint32_t tpend = pmk ? (uint32_t)__popcll(M & ((1ull << __builtin_ctzll(pmk)) - 1)) : BK;
-            // the members' entries into lanes 0..k-1 (forward permute: members
-            // first, in list order, then the rest)
-            const uint32_t dst = isM ? midx : k + (uint32_t)__popcll(~M & below);
-            auto fwd = [&](uint32_t x) { return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4), (int)x); };
-            const uint32_t nskb = (uint32_t)__popcll(S & below);
-            const uint32_t mu = fwd(u), mv = fwd(v), mc = fwd(c), mtmask = fwd(tmask), mnskb = fwd(nskb);
-            const unsigned long long mspan =
-                ((unsigned long long)fwd((uint32_t)(span >> 32)) << 32) | (unsigned long long)fwd((uint32_t)span);
+            k = kk;
+            if (E->dbg_form && md + 1 >= E->dbg_form && lane == 0)  // (diagnostics: where the formation ended; from merge BPE_DEBUG_FORM - 1)
+                printf("form shard %u md %u passes %u k %u end %u why %u skipped %u D %llu B %llu pend %u zrate %u\n", E->shard,
+                       md, npass, kk, kend, endwhy, nskt, D, (unsigned long long)Bsz, tpend, B->zrate);
             // candidate lists and token lengths, one lane per member
             uint32_t mode = 1, off = 0, len = 0, tl = 0;
             if (lane < k) {
@@ -453,17 +556,8 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->tspan[lane] = (uint32_t)min(mspan, 0xFFFFFFFFull);
                 ctl[lane] = tl;
             }
-            if (E->dbg_form && md + 1 >= E->dbg_form) {  // (diagnostics: the formation's state where the batch ended; from merge BPE_DEBUG_FORM - 1)
-                const uint32_t ke = kend < 64 ? kend : 63;  // (the list entry that ended it)
-                const unsigned long long spk = __shfl(span, (int)ke);
-                const uint32_t ck = __shfl(c, (int)ke), cn = __shfl(cnext, (int)ke);
-                const uint32_t ok = __shfl(tmask, (int)ke);
-                if (lane == 0)
-                    printf("form shard %u md %u k %u end %u why %u skipped %u D %llu span %llu B %llu lo %llu hi %llu trunc %d c %u "
-                           "next %u last %u mask %x pend %u zrate %u\n", E->shard, md, k, kend, endwhy, nsk, D, spk,
-                           (unsigned long long)Bsz, (unsigned long long)summary_B(D > spk ? D - spk : 0),
-                           (unsigned long long)summary_B(D + spk), (int)truncated, ck, cn, clast, ok, tpend, B->zrate);
-            }
+            // the skipped keys a member must beat: those before the last member
+            const uint32_t nsk = k ? (uint32_t)__builtin_amdgcn_readlane((int)mnskb, (int)(k - 1)) : 0u;
             if (lane == 0) {
                 B->sbase[k] = (uint32_t)stage_end;
                 B->blk0[k] = BSB;
@@ -1554,9 +1648,11 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     const bool hot = E->hot != 0;
     long long dD = 0;
     uint32_t nins = 0, nupd = 0, nzero = 0;
-    for (uint32_t t0 = bidB * blockDim.x; t0 < total; t0 += nB * blockDim.x) {  // uniform per block
-        const uint32_t t = t0 + tid;
-        uint32_t m = BK, cat = 0, x = 0, val = 0;
+    // one entry: (member, vector or 4 = the member's own key, id, delta),
+    // read and cleared
+    auto decode = [&](uint32_t t, uint32_t &m, uint32_t &cat, uint32_t &x, uint32_t &val) {
+        m = BK;
+        cat = x = val = 0;
         if (SH && t < dense_total) {
             // [R, bound, DL, DR, IL, IR] per member (R and bound were read by the prologue)
             m = t / per;
@@ -1611,44 +1707,95 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             val = E->bvec[base + (x - DENSE)];
             E->bvec[base + (x - DENSE)] = 0;
         }
-        bool hot_in = false, logged = false;
-        uint32_t hslot = 0, dlog = 0;
-        if (m < jsB && val != 0) {
-            const uint32_t a = sa[m], b = sb[m], z = z0 + m;
-            uint32_t u, v;
-            long long d;
-            if (cat == 4) { u = a; v = b; d = -(long long)val; }
-            else if (cat == V_DL) { u = x; v = a; d = -(long long)val; }
-            else if (cat == V_DR) { u = b; v = x; d = -(long long)val; }
-            else if (cat == V_IL) { u = x; v = z; d = val; }
-            else { u = z; v = x; d = val; }
-            const uint64_t slot = d > 0 ? hinsert_c(E, u, v, &nins) : hfind(E, u, v);
-            if (slot == ~0ull) {
-                C->err = d > 0 ? 2 : 1;
-                if (E->dbg_form)
-                    printf("apply shard %u z0 %u k %u js %u: no key (%u, %u) for member %u cat %u delta %lld (x %u t %u)\n",
-                           E->shard, z0, k, jsB, u, v, m, cat, d, x, t);
-            } else {
-                const uint32_t old = atomicAdd(&E->hcnt[(uint64_t)(slot) * E->hcs], (uint32_t)d);
-                const uint32_t nw = old + (uint32_t)d;
-                dD += (long long)(nw != 0) - (long long)(old != 0);
-                if (d < 0 && nw == 0 && old != 0) nzero++;
-                hot_in = hot && d > 0 && nw >= hotT && old < hotT;
-                hslot = (uint32_t)slot;
-                logged = tie;
-                dlog = (uint32_t)d;
-                nupd++;
+    };
+    // AU entries per thread per round, each step over all of them before the
+    // next (the entries, then every update's first-slot probe, then the count
+    // atomics): three dependent round trips per round instead of per entry
+    const uint64_t hmsk = E->hcap - 1;
+    const uint32_t step = nB * blockDim.x;
+    for (uint32_t t0 = bidB * blockDim.x; t0 < total; t0 += step * AU) {  // uniform per block
+        uint32_t m[AU], cat[AU], x[AU], val[AU];
+#pragma unroll
+        for (uint32_t q = 0; q < AU; q++) decode(t0 + q * step + tid, m[q], cat[q], x[q], val[q]);
+        bool act[AU];
+        int dneg[AU];
+        unsigned long long key[AU], prev[AU];
+        uint64_t slot[AU];
+#pragma unroll
+        for (uint32_t q = 0; q < AU; q++) {
+            act[q] = m[q] < jsB && val[q] != 0;
+            slot[q] = ~0ull;
+            key[q] = prev[q] = 0;
+            dneg[q] = 0;
+            if (act[q]) {
+                const uint32_t a = sa[m[q]], b = sb[m[q]], z = z0 + m[q];
+                uint32_t u, v;
+                if (cat[q] == 4) { u = a; v = b; dneg[q] = 1; }
+                else if (cat[q] == V_DL) { u = x[q]; v = a; dneg[q] = 1; }
+                else if (cat[q] == V_DR) { u = b; v = x[q]; dneg[q] = 1; }
+                else if (cat[q] == V_IL) { u = x[q]; v = z; }
+                else { u = z; v = x[q]; }
+                key[q] = (((unsigned long long)u << 32) | v) + 1ull;
+                slot[q] = mix64(key[q]) & hmsk;
+                unsigned long long *hk = &E->hkey[slot[q] * E->hks];
+                prev[q] = dneg[q] ? *hk : atomicCAS(hk, 0ull, key[q]);
             }
         }
-        if (hot) {
-            const uint32_t hp = wave_append(hot_in, &C->hot_n);
-            if (hot_in && hp < HOT_CAP) E->hot_slot[hp] = hslot;
+#pragma unroll
+        for (uint32_t q = 0; q < AU; q++) {
+            if (!act[q]) continue;
+            if (prev[q] == key[q]) continue;               // found at the first slot
+            if (!dneg[q] && prev[q] == 0) { nins++; continue; }  // inserted there
+            // (rare: the key sits further along its probe run)
+            uint64_t sq = (slot[q] + 1) & hmsk, res = ~0ull;
+            for (uint64_t p = 1; p <= hmsk; p++) {
+                unsigned long long *hk = &E->hkey[sq * E->hks];
+                const unsigned long long pk = dneg[q] ? *hk : atomicCAS(hk, 0ull, key[q]);
+                if (pk == key[q]) { res = sq; break; }
+                if (pk == 0) {
+                    if (!dneg[q]) { nins++; res = sq; }
+                    break;
+                }
+                sq = (sq + 1) & hmsk;
+            }
+            slot[q] = res;
         }
-        if (tie) {  // (uniform) the undo log: (slot, delta)
-            const uint32_t lp = wave_append(logged, &B->tlog_n);
-            if (logged) {
-                E->tlog[2 * (uint64_t)lp] = hslot;
-                E->tlog[2 * (uint64_t)lp + 1] = dlog;
+        uint32_t old[AU];
+#pragma unroll
+        for (uint32_t q = 0; q < AU; q++) {
+            old[q] = 0;
+            if (act[q] && slot[q] != ~0ull)
+                old[q] = atomicAdd(&E->hcnt[slot[q] * E->hcs], dneg[q] ? 0u - val[q] : val[q]);
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < AU; q++) {  // (uniform: the appends are wave-collective)
+            bool hot_in = false, logged = false;
+            const uint32_t d = dneg[q] ? 0u - val[q] : val[q];
+            if (act[q]) {
+                if (slot[q] == ~0ull) {
+                    C->err = dneg[q] ? 1 : 2;
+                    if (E->dbg_form)
+                        printf("apply shard %u z0 %u k %u js %u: no key %llx for member %u cat %u delta %s%u (x %u)\n",
+                               E->shard, z0, k, jsB, key[q] - 1, m[q], cat[q], dneg[q] ? "-" : "", val[q], x[q]);
+                } else {
+                    const uint32_t nw = old[q] + d;
+                    dD += (long long)(nw != 0) - (long long)(old[q] != 0);
+                    if (dneg[q] && nw == 0 && old[q] != 0) nzero++;
+                    hot_in = hot && !dneg[q] && nw >= hotT && old[q] < hotT;
+                    logged = tie;
+                    nupd++;
+                }
+            }
+            if (hot) {
+                const uint32_t hp = wave_append(hot_in, &C->hot_n);
+                if (hot_in && hp < HOT_CAP) E->hot_slot[hp] = (uint32_t)slot[q];
+            }
+            if (tie) {  // (uniform) the undo log: (slot, delta)
+                const uint32_t lp = wave_append(logged, &B->tlog_n);
+                if (logged) {
+                    E->tlog[2 * (uint64_t)lp] = (uint32_t)slot[q];
+                    E->tlog[2 * (uint64_t)lp + 1] = d;
+                }
             }
         }
     }

@@ -279,6 +279,7 @@ struct Eng {
     // batched training (batch.hip; occurrence positions staged in ids_out)
     uint32_t batch;       // 1: the batch kernels drive the run
     uint32_t skip_on;     // batches: skip non-commuting list entries instead of ending there (BPE_SKIP, default 1)
+    uint32_t list2;       // batches: the selection lists the next TOPK keys too (BPE_LIST2, default 1)
     uint32_t bvs;         // ids >= DENSE per (member, vector) in bvec / bvlist
     Bat *bat;
     uint16_t *btag;       // [n0] neighbour tags of the staged occurrences
