@@ -48,7 +48,7 @@ static_assert(BK < 64, "member masks are 64-bit");
 #define BPE_RU 4
 #endif
 #ifndef BPE_AU
-#define BPE_AU 4
+#define BPE_AU 1  // (4: apply 46.5 vs 43.2 us per batch on configs[2] -- the updates are random-atomic bound, not a chain)
 #endif
 constexpr uint32_t AU = BPE_AU;  // k_bapply role B: table updates per thread in flight together
 constexpr uint32_t SU = BPE_SU;  // k_bscan candidates per thread per round (1: measured fastest, 85 vs 91 ms at 4)
@@ -58,6 +58,9 @@ constexpr uint32_t SU = BPE_SU;  // k_bscan candidates per thread per round (1: 
 // k_bscan rounds staged in LDS per flush (one block barrier pair per flush;
 // 1 GiB x 8192: 1 -> 75.6 ms, 2 -> 72.5, 4 -> 71.8)
 constexpr uint32_t FR = BPE_FR;
+#ifndef BPE_WFLUSH
+#define BPE_WFLUSH 0  // k_bscan: each wave flushes its own staged occurrences (no block barriers in the candidate loop)
+#endif
 #ifndef BPE_SCAN_PF
 #define BPE_SCAN_PF 1
 #endif
@@ -1049,6 +1052,11 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         };
         fetch(bid * SCAN_T * SU);
         uint32_t round = 0;
+#if BPE_WFLUSH
+        const uint32_t lane = tid & 63, wbase = (tid >> 6) * 64 * SU * FR;
+        uint32_t wcnt = 0, wocc = 0;  // (wave-uniform)
+        (void)round;
+#endif
         for (uint32_t e0 = bid * SCAN_T * SU; e0 < len; e0 += stride) {  // uniform trip count
             uint32_t ent[SU];
             uint16_t etg[SU];
@@ -1145,12 +1153,41 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                         vadd_b(s, E, m, V_IR, rfin, gcnt);
                     }
                 }
+#if BPE_WFLUSH
+                // the wave's own slice of the staging list (no block barrier)
+                const unsigned long long om = __ballot(ok[u]);
+                if (ok[u]) {
+                    const uint32_t slot = wbase + wcnt + (uint32_t)__popcll(om & ((1ull << lane) - 1ull));
+                    list[slot] = (uint32_t)i;
+                    ltag[slot] = nb_tag(lfin, rfin);
+                }
+                wcnt += (uint32_t)__popcll(om);
+#else
                 const uint32_t slot = wave_append(ok[u], &lcount);
                 if (ok[u]) {
                     list[slot] = (uint32_t)i;
                     ltag[slot] = nb_tag(lfin, rfin);
                 }
+#endif
             }
+#if BPE_WFLUSH
+            // flush the wave's slice once another round may not fit, and at the
+            // end: one global atomic per wave, no block barrier
+            if (wcnt + 64 * SU > 64 * SU * FR || e0 + stride >= len) {  // (wave-uniform)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the slice's LDS stores before the reads)
+                __builtin_amdgcn_wave_barrier();
+                uint32_t g = 0;
+                if (lane == 0 && wcnt) g = atomicAdd(Rm, wcnt);
+                g = __shfl(g, 0);
+                for (uint32_t q = lane; q < wcnt; q += 64) {
+                    occz[g + q] = list[wbase + q];
+                    tagz[g + q] = ltag[wbase + q];
+                }
+                wocc += wcnt;
+                wcnt = 0;
+                __builtin_amdgcn_wave_barrier();
+            }
+#else
             // flush the staged rounds' list: one global atomic per block
             if (++round % FR == 0 || e0 + stride >= len) {  // (uniform)
                 __syncthreads();
@@ -1168,7 +1205,11 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 }
                 __syncthreads();
             }
+#endif
         }
+#if BPE_WFLUSH
+        if (lane == 0 && wocc) atomicAdd(&bRs, wocc);  // (the block's occurrences: read after the barrier below)
+#endif
     } else {
         // a == b (a batch of its own): the thread holding a run's first token
         // walks it, pairing tokens 0-1, 2-3, ... (greedy left-to-right); a run
@@ -1539,7 +1580,9 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         const uint32_t nsk = B->nsk;
         uint32_t skub = 0;
         if (lane < nsk) {
-            const uint32_t dec = SH ? E->xbat[BK + lane] : B->sdec[lane], cs = B->sk_c[lane];
+            // (BPE_SKIP_TEST: tests pretend no member lowered it, so every member
+            // after a skipped key fails and the batch is re-formed before it)
+            const uint32_t dec = E->skip_on > 1 ? 0u : SH ? E->xbat[BK + lane] : B->sdec[lane], cs = B->sk_c[lane];
             skub = cs > dec ? cs - dec : 0u;
         }
         for (int o = 1; o < 64; o <<= 1) {

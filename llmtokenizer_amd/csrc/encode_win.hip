@@ -162,24 +162,6 @@ __device__ inline uint32_t ew_in(const uint4 &a, const uint4 &c, uint32_t r0, ui
     return m;
 }
 
-#ifndef EW_SKIPB
-#define EW_SKIPB 1  // jump over the batches without work in a window (EW_SKIPB=0: walk every batch)
-#endif
-
-// smallest of the 16 ranks (two uint4 of u16) that is >= r0 (0xFFFF if none;
-// EW_PEND / EW_NONE never count)
-__device__ inline uint32_t ew_min_from(const uint4 &a, const uint4 &c, uint32_t r0) {
-    const uint32_t w[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-    uint32_t m = 0xFFFFu;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; j++) {
-        const uint32_t lo = w[j] & 0xFFFFu, hi = w[j] >> 16;
-        m = min(m, lo >= r0 && lo < EW_PEND ? lo : 0xFFFFu);
-        m = min(m, hi >= r0 && hi < EW_PEND ? hi : 0xFFFFu);
-    }
-    return m;
-}
-
 // mark p's pair for a rank lookup after the batch
 __device__ inline void ew_pend(uint16_t *rk, uint16_t *pend, uint32_t *npend, uint32_t p) {
     rk[p] = EW_PEND;
@@ -206,17 +188,10 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
     __shared__ uint32_t s_win, s_Lu, s_Ru, s_runend, s_npend;
     __shared__ uint32_t s_lid, s_rid, s_lm[8], s_rm[8], s_lact, s_ract, s_tpos;  // edge tokens and their batch masks
     __shared__ uint32_t s_wcnt[EW_T / 64];
-#if EW_SKIPB
-    __shared__ uint32_t s_bst[EW_MAX_BATCHES + 1], s_min[2];  // batch starts (ranks); the window's smallest rank
-#endif
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t p0 = tid * EW_PER;
     uint16_t *myrk = rk + p0;
     uint32_t *tok32 = (uint32_t *)tok;
-#if EW_SKIPB
-    for (uint32_t q = tid; q <= A.nb; q += EW_T) s_bst[q] = A.bstart[q];  // (ordered by the window loop's barrier)
-    if (tid < 2) s_min[tid] = 0xFFFFu;
-#endif
     for (;;) {
         if (tid == 0) s_win = atomicAdd(A.ticket, 1u);
         __syncthreads();
@@ -297,64 +272,6 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
         };
         if (tid == EW_EDGE_T) snapshot(0, W);  // (tok is complete: the init barrier)
         unsigned long long tp1 = EW_PROF_ON ? wall_clock64() : 0;
-#if EW_SKIPB
-        uint32_t par = 0;
-        for (uint32_t b = 0;; b++) {
-            // The next batch with work, found in one step: a batch is a rank
-            // range and the cached ranks only grow (a pair a merge creates
-            // belongs to a later batch), so it is the batch of the window's
-            // smallest cached rank >= bstart[b] -- batches before it have no
-            // work here, only edge bookkeeping (the edge thread, below)
-            uint32_t mr;
-            {
-                const uint4 xa = ((const uint4 *)myrk)[0], xc = ((const uint4 *)myrk)[1];
-                mr = ew_min_from(xa, xc, s_bst[b]);
-            }
-            for (int o = 32; o > 0; o >>= 1) mr = min(mr, (uint32_t)__shfl_xor(mr, o));
-            if (lane == 0) atomicMin(&s_min[par], mr);
-            __syncthreads();
-            const uint32_t mn = s_min[par];
-            if (tid == 0) s_min[par ^ 1] = 0xFFFFu;  // (its last readers passed a barrier since)
-            par ^= 1;
-            uint32_t bt = A.nb;
-            for (uint32_t q0 = b; q0 < A.nb; q0 += 64) {  // (uniform) first batch whose end lies past mn
-                const uint32_t q = q0 + lane;
-                const unsigned long long past = __ballot(q < A.nb && s_bst[q + 1] > mn);
-                if (past) {
-                    bt = q0 + (uint32_t)__builtin_ctzll(past);
-                    break;
-                }
-            }
-            if (bt > b) {  // (uniform) batches without work: their edge rules only
-                if (tid == EW_EDGE_T) {  // (no thread writes tok / sb until the barrier)
-                    uint32_t Lu = s_Lu, Ru = s_Ru;
-                    for (uint32_t bb = b; bb < bt; bb++) {
-                        const bool lm = s_lact && ((s_lm[bb >> 5] >> (bb & 31)) & 1u);
-                        const bool rm = s_ract && ((s_rm[bb >> 5] >> (bb & 31)) & 1u);
-                        if (lm || rm) {
-                            Lu = lm ? ew_next(sb, Lu) : Lu;
-                            Ru = rm ? s_tpos : Ru;
-                            s_Lu = Lu;
-                            s_Ru = Ru;
-                            snapshot(Lu, Ru);
-                        }
-                    }
-                }
-                __syncthreads();
-            }
-            if (bt >= A.nb) break;
-            b = bt;
-            const uint32_t r0 = s_bst[b], r1 = s_bst[b + 1];
-            // (no thread wrote rk since the loads above: reloaded, not kept live)
-            uint4 va = ((const uint4 *)myrk)[0], vc = ((const uint4 *)myrk)[1];
-            uint32_t mine = ew_in(va, vc, r0, r1);  // (some thread's is nonzero)
-            const uint32_t Lu = s_Lu, Ru = s_Ru;
-            bool lmove = false, rmove = false;
-            if (tid == EW_EDGE_T) {
-                lmove = s_lact && ((s_lm[b >> 5] >> (b & 31)) & 1u);
-                rmove = s_ract && ((s_rm[b >> 5] >> (b & 31)) & 1u);
-            }
-#else
         for (uint32_t b = 0; b < A.nb; b++) {
             const uint32_t r0 = A.bstart[b], r1 = A.bstart[b + 1];
             // this thread's 16 ranks (no other thread writes them before phase A)
@@ -378,7 +295,6 @@ __global__ __launch_bounds__(EW_T) __attribute__((amdgpu_waves_per_eu(EW_WAVES, 
                 }
                 continue;  // the next batch's barrier orders these stores
             }
-#endif
             nhas++;
             if (EW_PROF_ON) tq = wall_clock64();
             if (A.beq[b]) {

@@ -545,7 +545,8 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
                   : 0;
     // batches skip list entries that do not commute with an earlier member
     // (BPE_SKIP=0: the formation ends there, as before round 5)
-    h.skip_on = (uint32_t)(getenv_int("BPE_SKIP", 0) != 0);
+    h.skip_on = (uint32_t)(getenv_int("BPE_SKIP", 1) != 0);
+    if (h.skip_on && getenv_int("BPE_SKIP_TEST", 0)) h.skip_on = 2;  // (tests: every skipped key's check fails)
     // and take members from the next TOPK keys once the first list is used up
     // (BPE_LIST2=0: one list)
     h.list2 = (uint32_t)(getenv_int("BPE_LIST2", 0) != 0);

@@ -27,8 +27,9 @@
         }                                                                          \
     } while (0)
 
-enum { M_A4 = 0, M_V16 = 1, M_W32 = 2, M_ATOM = 3, M_ATOMRET = 4, M_STREAM = 5 };
-static const char *mode_name[] = {"load4", "load16", "window32", "atomic_noret", "atomic_ret", "stream16"};
+enum { M_A4 = 0, M_V16 = 1, M_W32 = 2, M_ATOM = 3, M_ATOMRET = 4, M_STREAM = 5, M_ST4 = 6, M_ST8 = 7 };
+static const char *mode_name[] = {"load4", "load16", "window32", "atomic_noret", "atomic_ret", "stream16", "store4",
+                                  "store_pair"};
 
 __device__ inline uint64_t mix64(uint64_t x) {
     x ^= x >> 33;
@@ -67,6 +68,14 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t *__restrict__ idx
         if (MODE == M_ATOM) {
 #pragma unroll
             for (int u = 0; u < U; u++) __hip_atomic_fetch_add(&buf[p[u]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        if (MODE == M_ST4 || MODE == M_ST8) {  // the rewrite's shape: the new id, and the end code one slot on
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                buf[p[u]] = (uint32_t)e0;
+                if (MODE == M_ST8) buf[p[u] + 1] = 0x80000001u;
+            }
             continue;
         }
         uint32_t v[U];
@@ -116,7 +125,7 @@ static float run(const uint32_t *idx, uint64_t n_idx, uint32_t *buf, uint32_t *o
 static double lines_per_gather(int mode) {
     switch (mode) {
     case M_W32: return 1.0 + 16.0 / 128.0;  // 32 B at a 16-B aligned base: crosses a line when base % 128 == 112
-    case M_STREAM: return 16.0 / 128.0;
+    case M_ST8: return 1.0 + 4.0 / 128.0;  // 8 B at a 4-B aligned base: crosses a line when base % 128 == 124
     default: return 1.0;
     }
 }
@@ -161,7 +170,8 @@ int main(int argc, char **argv) {
     sweep<M_W32>(idx, n_idx, buf, out, buf_mib, ncu);
     sweep<M_ATOM>(idx, n_idx, buf, out, buf_mib, ncu);
     sweep<M_ATOMRET>(idx, n_idx, buf, out, buf_mib, ncu);
-    if (n_idx * 16 <= nbuf * 4) sweep<M_STREAM>(idx, n_idx, buf, out, buf_mib, ncu);
+    sweep<M_ST4>(idx, n_idx, buf, out, buf_mib, ncu);
+    sweep<M_ST8>(idx, n_idx, buf, out, buf_mib, ncu);
     CHK(hipFree(buf));
     CHK(hipFree(idx));
     CHK(hipFree(out));
