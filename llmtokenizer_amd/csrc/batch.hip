@@ -59,7 +59,7 @@ constexpr uint32_t SU = BPE_SU;  // k_bscan candidates per thread per round (1: 
 // 1 GiB x 8192: 1 -> 75.6 ms, 2 -> 72.5, 4 -> 71.8)
 constexpr uint32_t FR = BPE_FR;
 #ifndef BPE_WFLUSH
-#define BPE_WFLUSH 0  // k_bscan: each wave flushes its own staged occurrences (no block barriers in the candidate loop)
+#define BPE_WFLUSH 1  // k_bscan: each wave flushes its own staged occurrences (no block barriers in the candidate loop)
 #endif
 #ifndef BPE_SCAN_PF
 #define BPE_SCAN_PF 1
@@ -258,6 +258,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         const uint32_t olda = jst ? B->a[jst - 1] : 0, oldb = jst ? B->b[jst - 1] : 0, oldz0 = B->z0;
         const uint32_t oldsum = B->sumlen;
         const uint32_t oldnsk = Bg->nsk;  // (outside the staged head; the formation below rewrites it)
+        const uint32_t crate = Bg->crate;
         const uint32_t raerr = aload(&Bg->ra_err);  // a token too long for an end code (rewrite blocks)
         const bool sh = E->sharded != 0;
         unsigned long long rs = lane < jst ? B->R[lane] : 0ull;   // this shard's occurrences
@@ -345,6 +346,11 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 // the keys really zeroed and checks that guess (verified members)
                 const unsigned long long zg = 16ull + (unsigned long long)B->zrate * (kk + lane);
                 const uint64_t Blo_o = summary_B(D > zg ? D - zg : 0);
+                // and D only rises by the keys they create, fewer than the span
+                // bound allows: a guess from the run's creations so far, checked
+                // by k_bapply against the keys really created (round 5)
+                const unsigned long long cg = E->tie_up ? min(span, 16ull + (unsigned long long)crate * (kk + lane)) : span;
+                const uint64_t Bhi_o = summary_B(D + cg);
                 const uint32_t cnext = __shfl(c, (int)(lane < 63 ? lane + 1 : 63));
                 // otherwise keys of one count keep my order against them under every
                 // B the members before me can reach (bucket = murmur & (B - 1), then
@@ -374,7 +380,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 if (past && c == clast) tmask &= 1u << 5;
                 const bool tie_rel = !stable && ((past && c == clast) || tie_next);
                 const bool cons_ok = tie_levels_ok(Blo, Bhi, Bsz, tmask);
-                const bool opt_ok = tie_levels_ok(Blo_o, Bhi, Bsz, tmask);
+                const bool opt_ok = tie_levels_ok(Blo_o, Bhi_o, Bsz, tmask);
                 const uint32_t mi = kk + lane;  // (at least my member index)
                 uint32_t why = 0;               // 0: qualifies
                 if (lane >= nlp) why = 8;       // past the list (reported as "list")
@@ -494,14 +500,16 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             }
             k = kk;
             if (E->dbg_form && md + 1 >= E->dbg_form && lane == 0)  // (diagnostics: where the formation ended; from merge BPE_DEBUG_FORM - 1)
-                printf("form shard %u md %u passes %u k %u end %u why %u skipped %u D %llu B %llu pend %u zrate %u\n", E->shard,
-                       md, npass, kk, kend, endwhy, nskt, D, (unsigned long long)Bsz, tpend, B->zrate);
+                printf("form shard %u md %u passes %u k %u end %u why %u skipped %u D %llu B %llu pend %u zrate %u applied %u retry %u\n",
+                       E->shard, md, npass, kk, kend, endwhy, nskt, D, (unsigned long long)Bsz, tpend, B->zrate,
+                       (uint32_t)applied, retry);
             // candidate lists and token lengths, one lane per member
             uint32_t mode = 1, off = 0, len = 0, tl = 0;
             if (lane < k) {
                 cand_of(E, mu, mv, true, srank, E->poff, &mode, &off, &len);
                 tl = E->tlen[mu] + E->tlen[mv];
                 Bg->nskb[lane] = (uint8_t)mnskb;
+                Bg->cnew[lane] = 0;
             }
             // the members' candidates fit the occurrence staging (ids_out, n0
             // positions; sharded: + one slot per member for the occurrence
@@ -586,6 +594,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 // the formation's guess of the keys a member zeroes: twice the
                 // run's average so far, + 2
                 B->zrate = (uint32_t)min(2ull * B->nzero / (md ? md : 1u) + 2ull, 1ull << 20);
+                Bg->crate = (uint32_t)min(2ull * Bg->ncre / (md ? md : 1u) + 16ull, 1ull << 20);
                 C->merges_done = md;
                 C->occ_top += (uint32_t)rs;
                 C->n_live = n_live;
@@ -1505,9 +1514,11 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     if (threadIdx.x == 0) atomicMax(&B->ap_in, ~wall_clock64());
     __shared__ uint32_t sa[BK], sb[BK], sla[BK], slb[BK], sR[BK], ssb[BK], spre[BK + 1], snl[BK * 4 + 1], sRg[BK];
     __shared__ uint32_t scut[BK], ablk[BK + 1];
+    __shared__ uint32_t s_cnew[BK];  // keys this block's updates created, per member (logged batches)
     __shared__ uint32_t sk, sj, sz0;
     __shared__ uint32_t ssp[P2P_MAXR_B + 1];  // SH: prefix of the shards' list lengths
     const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (tid >= 64 && tid < 64 + BK) s_cnew[tid - 64] = 0;  // (ordered by the prologue's barrier)
     // prologue, wave 0, lane q = member q: the verified prefix, prefix sums of
     // the occurrences and of the listed-id counts, role A's blocks per member
     if (tid < 64) {
@@ -1690,7 +1701,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     const uint32_t hotT = C->hot_T;
     const bool hot = E->hot != 0;
     long long dD = 0;
-    uint32_t nins = 0, nupd = 0, nzero = 0;
+    uint32_t nins = 0, nupd = 0, nzero = 0, ncre = 0;
     // one entry: (member, vector or 4 = the member's own key, id, delta),
     // read and cleared
     auto decode = [&](uint32_t t, uint32_t &m, uint32_t &cat, uint32_t &x, uint32_t &val) {
@@ -1823,6 +1834,10 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                 } else {
                     const uint32_t nw = old[q] + d;
                     dD += (long long)(nw != 0) - (long long)(old[q] != 0);
+                    if (!dneg[q] && old[q] == 0 && nw != 0) {  // a key created (new keys only rise)
+                        ncre++;
+                        if (tie) atomicAdd(&s_cnew[m[q]], 1u);
+                    }
                     if (dneg[q] && nw == 0 && old[q] != 0) nzero++;
                     hot_in = hot && !dneg[q] && nw >= hotT && old[q] < hotT;
                     logged = tie;
@@ -1851,6 +1866,9 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         if ((tid & 63) == 0) szb[tid >> 6] = zb;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (tid < sj && s_cnew[tid]) atomicAdd(&B->cnew[tid], s_cnew[tid]);  // (before the ticket's release)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         if (tid == 0) {
             uint32_t zt = 0;
             for (uint32_t w = 0; w < blockDim.x / 64; w++) zt += szb[w];
@@ -1869,10 +1887,20 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                                                      : __hip_atomic_load(&B->ztot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned long long D0 = C->D;
                 const uint64_t Bsz = C->B, lo = summary_B(D0 > Z ? D0 - Z : 0);
-                // (members before tpend were admitted on the conservative span
-                // bound, which holds whatever the batch zeroes: not re-checked)
+                // D before member j's turn: at least D0 - Z (old keys only fall),
+                // at most D0 + the keys the members before it created (new
+                // keys only rise); members before tpend were admitted on the
+                // conservative bounds: not re-checked
+                uint32_t cb = lane < jsB ? __hip_atomic_load(&B->cnew[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(cb, o);
+                    if ((int)lane >= o) cb += y;
+                }
+                cb = __shfl_up(cb, 1);
+                if (lane == 0) cb = 0;
+                const unsigned long long hiD = D0 + min((unsigned long long)cb, (unsigned long long)B->tspan[lane < BK ? lane : 0]);
                 const bool f = lane >= 1 && lane >= B->tpend && lane < jsB &&
-                               !tie_levels_ok(lo, summary_B(D0 + B->tspan[lane]), Bsz, B->tmask[lane]);
+                               !tie_levels_ok(lo, summary_B(hiD), Bsz, B->tmask[lane]);
                 const unsigned long long fm = __ballot(f);
                 if (lane == 0) sjf = fm ? (uint32_t)__ffsll(fm) - 1 : jsB;
             }
@@ -1939,6 +1967,9 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                 }
             }
             if (lfull) B->retry = B->tpend;
+            if (E->dbg_form && C->merges_done + 1 >= E->dbg_form)
+                printf("keep shard %u jf %u jsB %u tie %u lfull %u retry %u\n", E->shard, jf, jsB, (uint32_t)tie,
+                       (uint32_t)lfull, B->retry);
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -1946,30 +1977,34 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         nins += __shfl_xor(nins, o);
         nupd += __shfl_xor(nupd, o);
         nzero += __shfl_xor(nzero, o);
+        ncre += __shfl_xor(ncre, o);
     }
     __shared__ long long sd[16];
-    __shared__ uint32_t si[16], su[16], sz[16];
+    __shared__ uint32_t si[16], su[16], sz[16], scr[16];
     if ((tid & 63) == 0) {
         sd[tid >> 6] = dD;
         si[tid >> 6] = nins;
         su[tid >> 6] = nupd;
         sz[tid >> 6] = nzero;
+        scr[tid >> 6] = ncre;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         long long t = 0;
-        unsigned long long ni = 0, nu = 0, nz = 0;
+        unsigned long long ni = 0, nu = 0, nz = 0, nc = 0;
         for (uint32_t w = 0; w < blockDim.x / 64; w++) {
             t += sd[w];
             ni += si[w];
             nu += su[w];
             nz += sz[w];
+            nc += scr[w];
         }
         if (t != 0) atomicAdd(&B->dD, (unsigned long long)t);
         if (ni != 0) atomicAdd(&C->nkeys, ni);
         if (nu != 0) atomicAdd(&B->nupd, nu);
         if (nz != 0) atomicAdd(&B->nzero, nz);
+        if (nc != 0) atomicAdd(&B->ncre, nc);
         atomicMax(&B->ap_out, wall_clock64());
     }
     ts_mark(E, bi, BT_APPLY_B, false, true);

@@ -550,6 +550,9 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     // and take members from the next TOPK keys once the first list is used up
     // (BPE_LIST2=0: one list)
     h.list2 = (uint32_t)(getenv_int("BPE_LIST2", 0) != 0);
+    // tied members admitted on a guess of the keys the members before them
+    // create (D's upper side), checked by k_bapply like the lower side
+    h.tie_up = (uint32_t)(getenv_int("BPE_TIE_UP", 0) != 0);
     h.xbat = nullptr;
     h.xsp_out = h.xsp_in = nullptr;
     h.xsp_cap = 0;

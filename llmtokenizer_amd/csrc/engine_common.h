@@ -178,6 +178,12 @@ struct Bat {
     unsigned long long sk_cm[BK];       // those members (bit = member index)
     uint8_t nskb[64];                   // per member: keys skipped before it in the list
     unsigned long long nskip, nskfail;  // keys skipped in applied batches; batches re-formed by that check
+    // verified tie order, upper side (round 5): the keys each member of a
+    // logged batch created (role B, in member order), the run's creations so
+    // far (the formation's guess per member), and the guess itself
+    uint32_t cnew[BK];
+    uint32_t crate, pad7;
+    unsigned long long ncre;
 };
 
 // Sharded batches: the words one batch exchanges (summed over the shards):
@@ -279,7 +285,8 @@ struct Eng {
     // batched training (batch.hip; occurrence positions staged in ids_out)
     uint32_t batch;       // 1: the batch kernels drive the run
     uint32_t skip_on;     // batches: skip non-commuting list entries instead of ending there (BPE_SKIP, default 1)
-    uint32_t list2;       // batches: the selection lists the next TOPK keys too (BPE_LIST2, default 1)
+    uint32_t list2;       // batches: the selection lists the next TOPK keys too (BPE_LIST2, default 0)
+    uint32_t tie_up;      // batches: the tie order's upper side on a guess of the keys created, verified (BPE_TIE_UP, default 0)
     uint32_t bvs;         // ids >= DENSE per (member, vector) in bvec / bvlist
     Bat *bat;
     uint16_t *btag;       // [n0] neighbour tags of the staged occurrences
