@@ -132,7 +132,8 @@ __device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bs
     __shared__ KV part[16][TOPK];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     KV run = kv_empty();
-    const uint32_t stride = gridDim.x * blockDim.x;
+    // (the BRB reduce blocks share the list: the launch's other blocks rewrite)
+    const uint32_t stride = BRB * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x + w * 64; base < n; base += stride) {  // uniform per wave
         const uint32_t i = base + lane;
         KV x = kv_empty();
@@ -253,7 +254,11 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         // ---- the batch applied last, folded
         const bool applied = B->applied != 0;
         const uint32_t jst = applied ? B->jstar : 0, kpr = applied ? B->k : 0;
-        const uint32_t retry = applied ? B->retry : 0;  // the last batch failed at member `retry`
+        // the last batch failed at member `retry` (or did before a host-side
+        // stop: a selection that stops folds the batch but holds its retry for
+        // the formation after the host's work -- a byte-pair list rebuild, a
+        // hot-set rebuild or table growth leaves the counts as they were)
+        const uint32_t retry = applied ? B->retry : B->rhold;
         // (read before the lanes overwrite the member fields)
         const uint32_t olda = jst ? B->a[jst - 1] : 0, oldb = jst ? B->b[jst - 1] : 0, oldz0 = B->z0;
         const uint32_t oldsum = B->sumlen;
@@ -285,8 +290,8 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         const uint32_t hotT = C->hot_T;
         // byte-pair lists gone stale (opt-in, BPE_RELIST): the host rebuilds them
         bool relist_due = false;
-        if (E->relist_stale) {
-            const uint32_t cs = (uint32_t)(C->counters[4] + (applied ? oldsum : 0u)) - C->relist_c0;
+        if (E->relist_stale) {  // (a re-formed batch's candidates are scanned again: not stale ones)
+            const uint32_t cs = (uint32_t)(C->counters[4] + (applied && !retry ? oldsum : 0u)) - C->relist_c0;
             const uint32_t os = (uint32_t)(C->counters[5] + rs) - C->relist_o0;
             relist_due = cs > os && cs - os >= E->relist_stale;
         }
@@ -298,6 +303,9 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         else if (relist_due) stop = STOP_RELIST;
         else if (v0 == 0 || cnt0 <= 1) stop = STOP_DONE;
         else if (C->nkeys + 4ull * (256ull + md + 2) >= E->hcap / 2) stop = STOP_GROW;
+        if (stop != STOP_NONE && E->dbg_form && md + 1 >= E->dbg_form && lane == 0)
+            printf("stop shard %u md %u stop %u cnt0 %u hotT %u hot_n %u applied %u retry %u\n", E->shard, md, stop, cnt0,
+                   hotT, (uint32_t)C->hot_n, (uint32_t)applied, retry);
         // ---- the batch: members from the list in order, skipping the entries
         // that do not commute with an earlier member, up to the first entry
         // that qualifies as neither; over the second list too when the first
@@ -503,6 +511,24 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 printf("form shard %u md %u passes %u k %u end %u why %u skipped %u D %llu B %llu pend %u zrate %u applied %u retry %u\n",
                        E->shard, md, npass, kk, kend, endwhy, nskt, D, (unsigned long long)Bsz, tpend, B->zrate,
                        (uint32_t)applied, retry);
+            if (E->dbg_ku && md + 1 >= E->dbg_form) {  // (diagnostics: one key's table slots and hot-set entries)
+                const unsigned long long want = (((unsigned long long)E->dbg_ku << 32) | E->dbg_kv) + 1ull;
+                for (uint64_t s0 = 0; s0 < E->hcap; s0 += 64) {
+                    const uint64_t sl = s0 + lane;
+                    if (sl < E->hcap && E->hkey[sl * E->hks] == want)
+                        printf("  key %u %u at slot %llu count %u (home %llu)\n", E->dbg_ku, E->dbg_kv,
+                               (unsigned long long)sl, E->hcnt[sl * E->hcs], (unsigned long long)(mix64(want) & (E->hcap - 1)));
+                }
+                const uint32_t nh = min(C->hot_n, HOT_CAP);
+                for (uint32_t i = lane; i < nh; i += 64) {
+                    const uint32_t sl = E->hot_slot[i];
+                    if (E->hkey[(uint64_t)sl * E->hks] == want) printf("  key %u %u hot entry %u slot %u\n", E->dbg_ku, E->dbg_kv, i, sl);
+                }
+                if (lane == 0) printf("  hot_n %u hotT %u\n", nh, hotT);
+            }
+            if (E->dbg_form > 1 && md + 1 >= E->dbg_form && lane < 8)  // (the list head: key, count)
+                printf("  list %u: %u %u c %u member %u\n", lane, (uint32_t)(e.k >> 32), (uint32_t)e.k,
+                       (uint32_t)(e.v >> 32), lane < kk ? mu : 0u);
             // candidate lists and token lengths, one lane per member
             uint32_t mode = 1, off = 0, len = 0, tl = 0;
             if (lane < k) {
@@ -590,6 +616,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->nspan++;
             }
             B->sc_in = B->sc_out = B->ap_in = B->ap_out = 0;
+            B->rhold = stop != STOP_NONE ? retry : 0u;
             if (applied) {
                 // the formation's guess of the keys a member zeroes: twice the
                 // run's average so far, + 2
@@ -601,6 +628,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 C->D = D;
                 C->counters[0] += jst;
                 C->counters[4] += oldsum;
+                if (retry) C->relist_c0 += oldsum;  // (scanned again: not stale candidates)
                 C->counters[5] += rs;
                 if (jst) {
                     C->a = olda;

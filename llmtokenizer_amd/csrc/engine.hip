@@ -493,6 +493,14 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.scan_tend, STAMPS))) return r;
     h.dbgts = nullptr;
     h.dbg_form = (uint32_t)getenv_int("BPE_DEBUG_FORM", 0);
+    h.dbg_ku = h.dbg_kv = 0;
+    if (const char *t = getenv("BPE_DEBUG_KEY")) {
+        unsigned ku = 0, kv = 0;
+        if (sscanf(t, "%u,%u", &ku, &kv) == 2) {
+            h.dbg_ku = ku;
+            h.dbg_kv = kv;
+        }
+    }
     h.tie_verify = (uint32_t)getenv_int("BPE_TIE_VERIFY", 1);
     if (h.tie_verify && getenv_int("BPE_TIE_TEST", 0)) h.tie_verify = 2;  // (tests: every verification fails)
     if (getenv("BPE_DEBUG_TS") && !encode && (r = dalloc(c, &h.dbgts, (size_t)TS_SLOTS * TS_N))) return r;

@@ -123,7 +123,8 @@ constexpr uint32_t P2P_MAXR_B = 16;  // shards of a sharded batch run (BPE_GPU_P
 
 struct Bat {
     uint32_t k, z0, applied, jstar;   // members; id of member 0; an apply ran (the select folds it); applied prefix
-    uint32_t ticket, retry, sumlen, pad0;  // reduce blocks done; > 0: re-form the batch with this many members; candidates
+    uint32_t ticket, retry, sumlen, rhold;  // reduce blocks done; > 0: re-form the batch with this many members; candidates;
+                                          // a retry a stopping select kept for the next formation
     unsigned long long dD;            // distinct-pair delta of the applied batch
     unsigned long long nbatch, ndrop, nretry;  // batches applied; members dropped by the verification; batches re-formed
     unsigned long long why[8];        // what ended each batch's formation (BPE_DEBUG report)
@@ -250,6 +251,7 @@ struct Eng {
     unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
     unsigned long long *dbgts;      // [TS_SLOTS][TS_N] per-merge block timeline (BPE_DEBUG_TS) or null
     uint32_t dbg_form;
+    uint32_t dbg_ku, dbg_kv;  // BPE_DEBUG_KEY=u,v: k_bsel reports that key's table slot, count and hot-set entries
     uint32_t *tlog;       // batches: undo log of a verified-tie batch's table updates (slot, delta)
     uint32_t tlog_cap;    // ... records
     uint32_t tie_verify;  // batches: admit members on the tie-order guess k_bapply verifies (BPE_TIE_VERIFY,

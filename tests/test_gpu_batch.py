@@ -193,3 +193,51 @@ def test_formation_variants_match_oracle(skip, list2, test, monkeypatch):
         assert skipped > 0
     if test == "1":
         assert failed > 0 and retries >= failed
+
+
+ENGLISH_WORKER = r"""
+import hashlib, sys
+sys.path.insert(0, %r)
+from llmtokenizer_amd import api
+from llmtokenizer_amd.synth import english_like
+e = api.Engine(0)
+e.load(english_like(int(sys.argv[1])))
+e.train(int(sys.argv[2]))
+st = e.stats()
+print(hashlib.md5(e.merges().tobytes()).hexdigest(), "%%016x" %% e.ids_checksum(), st["merges"], st["batches"],
+      st["batch_retries"], st["relists"])
+""" % ROOT
+
+
+@pytest.mark.parametrize("extra", [{}, {"BPE_SKIP_TEST": "1", "BPE_RELIST_STALE": "1"}])
+def test_english_like_retries_across_relists(extra):
+    """16 MiB of Zipf pseudo-words (skewed pairs, the batch verification fails
+    often): batch engine == one-merge engine, merges and ids.  Regression:
+    a batch re-formed after a failed verification must keep its cut across a
+    host-side stop (here the byte-pair list rebuild, on by default at 2^24
+    tokens) -- the selection that stops folds the failed batch, the one after
+    the rebuild forms it again, and formerly did so uncut, forever.  The
+    second case re-forms every batch with a skipped key (BPE_SKIP_TEST) and
+    rebuilds the lists whenever a stale candidate was scanned."""
+    outs = []
+    for flag in ("1", "0"):
+        env = dict(os.environ, BPE_BATCH=flag, **extra)
+        p = subprocess.run([sys.executable, "-c", ENGLISH_WORKER, str(16 << 20), "600"], env=env,
+                           capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr[-2000:]
+        md5, cs, nm, nb, nr, nrl = p.stdout.split()
+        outs.append((md5, cs, int(nm), int(nb), int(nr), int(nrl)))
+    print(outs)
+    assert outs[0][:3] == outs[1][:3], outs
+    assert outs[0][2] == 600 and outs[0][3] > 0 and outs[0][4] > 0 and outs[0][5] > 0, outs
+
+
+def test_hot_set_past_the_reduce_blocks(monkeypatch):
+    """a hot set longer than the select's reduce blocks cover in one sweep
+    (32 blocks x 1024 keys): every entry is listed (regression: entries past
+    32768 went to the launch's rewrite blocks, which never list, and a new
+    key there was passed over)"""
+    monkeypatch.setenv("BPE_HOT_TARGET", "60000")
+    data = synth_bytes(510, 3 << 20)
+    st = _check(data, 1500)
+    assert st["batches"] > 0

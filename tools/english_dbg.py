@@ -8,9 +8,8 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from llmtokenizer_amd import api  # noqa: E402
+from llmtokenizer_amd.synth import english_like  # noqa: E402
 
-src = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "init_skew.py")).read()
-exec(src[src.index("def english_like"):src.index("def corpus")])
 mib = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 caps = [int(x) for x in sys.argv[2:]] or [2, 64, 256, 1024]
 t = time.time()

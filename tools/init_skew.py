@@ -15,36 +15,10 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from llmtokenizer_amd import api  # noqa: E402
+from llmtokenizer_amd.synth import english_like  # noqa: E402
 
 size = (int(sys.argv[1]) if len(sys.argv) > 1 else 16) << 20
 names = sys.argv[2:] or ["uniform", "one_byte", "alternating", "mostly_space", "english_like"]
-
-
-def english_like(n, seed=7):
-    """Zipf-distributed pseudo-words over English letter frequencies, with
-    spaces, commas, periods and newlines (no network, no real text here)"""
-    rng = np.random.default_rng(seed)
-    letters = np.frombuffer(b"etaoinshrdlcumwfgypbvkjxqz", np.uint8)
-    freq = np.array([12.7, 9.1, 8.2, 7.5, 7.0, 6.7, 6.3, 6.1, 6.0, 4.3, 4.0, 2.8, 2.8, 2.4, 2.4, 2.2, 2.0,
-                     2.0, 1.9, 1.5, 1.0, 0.8, 0.15, 0.15, 0.1, 0.07])
-    freq /= freq.sum()
-    nw = 20000
-    lens = np.clip(rng.geometric(0.22, nw), 1, 14)
-    words = [bytes(rng.choice(letters, L, p=freq)) for L in lens]
-    ranks = np.minimum(rng.zipf(1.15, n // 5 + 16) - 1, nw - 1)
-    seps = rng.choice(np.frombuffer(b"    ,.\n", np.uint8), ranks.size, p=[0.8 / 4] * 4 + [0.1, 0.07, 0.03])
-    bank = np.frombuffer(b"".join(words), np.uint8)
-    woff = np.concatenate([[0], np.cumsum(lens)[:-1]])
-    wl = lens[ranks] + 1  # the word and its separator
-    ends = np.cumsum(wl)
-    k = int(np.searchsorted(ends, n)) + 1
-    ranks, seps, wl, ends = ranks[:k], seps[:k], wl[:k], ends[:k]
-    starts = ends - wl
-    # position j of the output: word t = the one whose span holds j, offset j - starts[t]
-    t = np.repeat(np.arange(k), wl)
-    off = np.arange(t.size) - starts[t]
-    out = np.where(off < lens[ranks][t], bank[np.minimum(woff[ranks][t] + off, bank.size - 1)], seps[t]).astype(np.uint8)
-    return out[:n].tobytes()
 
 
 def corpus(name):
