@@ -262,7 +262,39 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         // (read before the lanes overwrite the member fields)
         const uint32_t olda = jst ? B->a[jst - 1] : 0, oldb = jst ? B->b[jst - 1] : 0, oldz0 = B->z0;
         const uint32_t oldsum = B->sumlen;
+        // candidates scanned for nothing (a re-formed batch's, a dropped
+        // member's): they scan again, so they do not count as stale list entries
+        uint32_t rescan = applied && !retry && lane >= jst && lane < kpr ? B->len[lane] : 0u;
+        // and the applied members' candidates and occurrences from occurrence
+        // lists: a byte-pair list rebuild leaves those lists as they are, so
+        // only byte-pair lists' stale entries count towards one
+        const bool occm = lane < jst && B->mode[lane] != 0;
+        uint32_t ocand = occm ? B->len[lane] : 0u, oocc = occm ? B->R[lane] : 0u;
+        for (int o = 32; o > 0; o >>= 1) {
+            rescan += __shfl_xor(rescan, o);
+            ocand += __shfl_xor(ocand, o);
+            oocc += __shfl_xor(oocc, o);
+        }
+        if (applied && retry) rescan = oldsum;
         const uint32_t oldnsk = Bg->nsk;  // (outside the staged head; the formation below rewrites it)
+        // skipped keys back off where batches holding them keep failing
+        // (skewed text: the members past a skipped key rarely verify, and
+        // every failure costs a batch): each failure of a batch with skipped
+        // keys raises an exponent, each such batch that verifies lowers it;
+        // at 2 and above a failure has the next 2^e fresh formations skip
+        // nothing (4 ... 128).  Isolated failures (uniform corpora) never
+        // gate.  A re-formation keeps them (its verified prefix may hold
+        // skipped keys).
+        uint32_t skg = B->skgate & 0xFFFFu, ske = B->skgate >> 16;
+        if (applied && oldnsk) {
+            if (retry || jst < kpr) {
+                ske = min(ske + 1u, 7u);
+                if (ske >= 2) skg = 1u << ske;
+            } else if (ske) {
+                ske--;
+            }
+        }
+        const bool skip_now = E->skip_on && (skg == 0 || retry != 0);
         const uint32_t crate = Bg->crate;
         const uint32_t raerr = aload(&Bg->ra_err);  // a token too long for an end code (rewrite blocks)
         const bool sh = E->sharded != 0;
@@ -290,9 +322,9 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         const uint32_t hotT = C->hot_T;
         // byte-pair lists gone stale (opt-in, BPE_RELIST): the host rebuilds them
         bool relist_due = false;
-        if (E->relist_stale) {  // (a re-formed batch's candidates are scanned again: not stale ones)
-            const uint32_t cs = (uint32_t)(C->counters[4] + (applied && !retry ? oldsum : 0u)) - C->relist_c0;
-            const uint32_t os = (uint32_t)(C->counters[5] + rs) - C->relist_o0;
+        if (E->relist_stale) {
+            const uint32_t cs = (uint32_t)(C->counters[4] + (applied ? oldsum - rescan - ocand : 0u)) - C->relist_c0;
+            const uint32_t os = (uint32_t)(C->counters[5] + rs - oocc) - C->relist_o0;
             relist_due = cs > os && cs - os >= E->relist_stale;
         }
         uint32_t stop = STOP_NONE;
@@ -421,7 +453,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 // checks every member against the skipped keys before it.  It
                 // merges in a later batch.  (Ids below DENSE: the scan's LDS
                 // vectors hold the decrements; a tie order of its own is moot.)
-                const bool skok = E->skip_on && u < DENSE && v < DENSE && (why == 0 || why == 4);
+                const bool skok = skip_now && u < DENSE && v < DENSE && (why == 0 || why == 4);
                 unsigned long long M = 0, S = 0;
                 kend = 64;
                 {
@@ -536,6 +568,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 tl = E->tlen[mu] + E->tlen[mv];
                 Bg->nskb[lane] = (uint8_t)mnskb;
                 Bg->cnew[lane] = 0;
+                Bg->adj[lane] = 0;
             }
             // the members' candidates fit the occurrence staging (ids_out, n0
             // positions; sharded: + one slot per member for the occurrence
@@ -617,6 +650,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             }
             B->sc_in = B->sc_out = B->ap_in = B->ap_out = 0;
             B->rhold = stop != STOP_NONE ? retry : 0u;
+            B->skgate = (stop == STOP_NONE && !retry && skg ? skg - 1u : skg) | (ske << 16);
             if (applied) {
                 // the formation's guess of the keys a member zeroes: twice the
                 // run's average so far, + 2
@@ -628,7 +662,8 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 C->D = D;
                 C->counters[0] += jst;
                 C->counters[4] += oldsum;
-                if (retry) C->relist_c0 += oldsum;  // (scanned again: not stale candidates)
+                C->relist_c0 += rescan + ocand;
+                C->relist_o0 += oocc;
                 C->counters[5] += rs;
                 if (jst) {
                     C->a = olda;
@@ -640,6 +675,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                     B->ndrop += kpr - retry;
                 } else {
                     B->nbatch++;
+                    B->ndrop += kpr - jst;  // (a verified prefix applied alone)
                     Bg->nskip += oldnsk;
                 }
                 B->retry = 0;
@@ -1003,6 +1039,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     __shared__ uint32_t list[SCAN_T * SU * FR];  // the rounds' occurrences (position, tag), flushed every FR rounds
     __shared__ uint16_t ltag[SCAN_T * SU * FR];
     __shared__ uint32_t lcount, gbase, list_n, covc, sm, sk, sz0, bRs;
+    __shared__ unsigned long long badj;  // the members whose occurrences abut my member's (Bat::adj)
     __shared__ uint32_t gcnt[2];
     __shared__ uint32_t sa[BK], sb[BK], sla[BK];
     __shared__ RoleTab rt;
@@ -1012,6 +1049,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     if (tid == 0) {
         sm = BK;
         covc = lcount = bRs = 0;
+        badj = 0;
         gcnt[0] = gcnt[1] = 0;
         sk = B->k;
         sz0 = B->z0;
@@ -1034,6 +1072,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         if (tid == 0) atomicMax(&B->sc_out, wall_clock64());
         return;
     }
+    unsigned long long tadj = 0;  // members whose occurrences abut the ones this thread found
     if (tid < k) {
         rt.put(sa[tid], false, tid);
         rt.put(sb[tid], true, tid);
@@ -1173,6 +1212,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                         const uint32_t cv = cover_of<SH>(tok, rt, sa, sb, H, p, ps[u], n);
                         if (cv < BK) {
                             lfin = z0 + cv;
+                            tadj |= 1ull << cv;
                             atomicAdd(&covc, 1u);
                         } else {
                             vadd_b(s, E, m, V_DL, p, gcnt);
@@ -1185,7 +1225,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     rfin = q;
                     if (q != HOLE) {
                         const uint32_t st = starts_of<SH>(tok, rt, sb, sla, H, q, kq, n);
-                        if (st < BK) rfin = z0 + st;
+                        if (st < BK) {
+                            rfin = z0 + st;
+                            tadj |= 1ull << st;
+                        }
                         vadd_b(s, E, m, V_DR, q, gcnt);
                         vadd_b(s, E, m, V_IR, rfin, gcnt);
                     }
@@ -1271,7 +1314,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
             const uint32_t p = ok ? tok_at(ps) : HOLE;
             // the run's left neighbour, unless another member's occurrence covers it
             const uint32_t cv = (ok && p != HOLE && p != a) ? cover_of<SH>(tok, rt, sa, sb, H, p, ps, n) : BK;
-            if (cv < BK) atomicAdd(&covc, 1u);
+            if (cv < BK) {
+                atomicAdd(&covc, 1u);
+                tadj |= 1ull << cv;
+            }
             const bool left = p != HOLE && p != a && cv == BK;
             // my first token continues a run of the left shard: pairs with its
             // last token (the left shard's occurrence) when an odd number precede
@@ -1287,6 +1333,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 // a right neighbour that starts another member's occurrence becomes its id
                 const uint32_t st = (!knext && q != HOLE) ? starts_of<SH>(tok, rt, sb, sla, H, q, kq, n) : BK;
                 const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
+                if (st < BK) tadj |= 1ull << st;
                 const uint32_t pfin = (mi > 0 || cont) ? z : (left ? p : cv < BK ? z0 + cv : HOLE);
                 const uint32_t slot = atomicAdd(&lcount, 1u);
                 if (slot < SCAN_T * SU) {
@@ -1392,6 +1439,14 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         }
         B->xl_m = xlm;
         if (over < k) atomicAdd(&E->xbat[over], 1u);  // my staging overflowed there
+    }
+    // which members' occurrences abut my member's: k_bapply may apply a
+    // verified prefix only when none of them abuts a dropped member
+    if (k > 1) {
+        for (int o = 32; o > 0; o >>= 1) tadj |= __shfl_xor(tadj, o);
+        if ((tid & 63) == 0 && tadj) atomicOr(&badj, tadj);
+        __syncthreads();
+        if (tid == 0 && badj) atomicOr(&B->adj[m], badj);
     }
     // deltas into replica (block % BREPL) of the member's accumulators (SH:
     // the exchange buffer), and the member's new-key bound: per block max over
@@ -1644,9 +1699,20 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         }
         if (E->dbg_form && C->merges_done + 1 >= E->dbg_form && blockIdx.x == 0 && lane == 0)
             printf("verify shard %u z0 %u k %u js %u ovm %llx R0 %u Rg0 %u\n", E->shard, z0, k, js, ovm, R, Rg);
-        if (js < k) {  // re-form the batch with the verified prefix; apply nothing
-            if (lane == 0) B->retry = js;
-            js = 0;
+        // A member failed: the verified prefix is applied as it stands when no
+        // occurrence of its members abuts one of a dropped member (the pair
+        // between two abutting occurrences is counted once, by the left one,
+        // with the right one's new id: those deltas assume both merge).
+        // Otherwise nothing is applied and the batch is formed again with the
+        // prefix (nothing changed in between, so the selection repeats).
+        // (Sharded runs re-form always: the adjacency is per shard.)
+        if (js < k) {
+            const unsigned long long am = in ? B->adj[lane] : 0ull, pre = (1ull << js) - 1ull;
+            const bool abut = lane < js ? (am & ~pre) != 0 : (am & pre) != 0;
+            if (SH || E->prefix_apply == 0 || __ballot(in && abut)) {
+                if (lane == 0) B->retry = js;
+                js = 0;
+            }
         }
         const uint32_t rall = (uint32_t)__shfl(rpre, (int)(k ? k - 1 : 0));
         // the first part of each verified member's rewrite runs here, in

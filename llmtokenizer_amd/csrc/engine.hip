@@ -493,6 +493,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     if ((r = dalloc(c, &h.scan_tend, STAMPS))) return r;
     h.dbgts = nullptr;
     h.dbg_form = (uint32_t)getenv_int("BPE_DEBUG_FORM", 0);
+    h.prefix_apply = (uint32_t)(getenv_int("BPE_PREFIX", 1) != 0);
     h.dbg_ku = h.dbg_kv = 0;
     if (const char *t = getenv("BPE_DEBUG_KEY")) {
         unsigned ku = 0, kv = 0;

@@ -128,7 +128,9 @@ struct Bat {
     unsigned long long dD;            // distinct-pair delta of the applied batch
     unsigned long long nbatch, ndrop, nretry;  // batches applied; members dropped by the verification; batches re-formed
     unsigned long long why[8];        // what ended each batch's formation (BPE_DEBUG report)
-    uint32_t drop_test, pad1;              // > 0: members j >= 1 with (z0 + j) % drop_test == 0 fail (tests)
+    uint32_t drop_test;               // > 0: members j >= 1 with (z0 + j) % drop_test == 0 fail (tests)
+    uint32_t skgate;                  // skipped keys: fresh formations left without them (low 16 bits) after
+                                      // batches with skipped keys failed; the back-off exponent (high 16)
     unsigned long long stage_cap;          // occurrence staging positions (n0; BPE_BATCH_STAGE lowers it: tests)
     // device wall-clock spans (first block entry, complemented, and last block
     // exit of this batch's k_bscan / k_bapply; folded by the select) and
@@ -168,6 +170,8 @@ struct Bat {
     // block exit), folded by the next k_bapply (outside the select's staged
     // head, which it writes back whole); launches folded
     unsigned long long sl_in, sl_out, sl_ticks, nsl;
+    unsigned long long adj[BK];       // per member: the members whose occurrences abut its own (k_bscan; cleared by
+                                      // the select that forms the batch)
     // keys the formation skipped (batch.hip): a listed key that shares an id,
     // on the opposite side, with an earlier member is no member -- the
     // sequential passes lower its count when that member merges -- and every
@@ -251,6 +255,7 @@ struct Eng {
     unsigned long long *scan_tend;  // [SCAN_BLOCKS] exit wall-clock stamp of each k_scan block
     unsigned long long *dbgts;      // [TS_SLOTS][TS_N] per-merge block timeline (BPE_DEBUG_TS) or null
     uint32_t dbg_form;
+    uint32_t prefix_apply;  // batches: apply a verified prefix that abuts no dropped member (BPE_PREFIX, default 1)
     uint32_t dbg_ku, dbg_kv;  // BPE_DEBUG_KEY=u,v: k_bsel reports that key's table slot, count and hot-set entries
     uint32_t *tlog;       // batches: undo log of a verified-tie batch's table updates (slot, delta)
     uint32_t tlog_cap;    // ... records

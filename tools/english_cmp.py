@@ -18,13 +18,13 @@ e.train(int(sys.argv[2]))
 st = e.stats()
 np.save(sys.argv[3], e.merges())
 print(st["merges"], st["batches"], st["batch_retries"], st["relists"], st["keys_skipped"], st["skip_failed"],
-      "%%016x" %% e.ids_checksum(), flush=True)
+      "%%016x" %% e.ids_checksum(), "dropped", st["batch_dropped"], "loop_ms", round(st["ms_train"], 2), flush=True)
 """ % ROOT
 mib = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 mm = int(sys.argv[2]) if len(sys.argv) > 2 else 600
 variants = [("one", {"BPE_BATCH": "0"}), ("batch", {}), ("norelist", {"BPE_RELIST": "0"}),
             ("noskip", {"BPE_SKIP": "0"}), ("noskip_norelist", {"BPE_SKIP": "0", "BPE_RELIST": "0"}),
-            ("notie", {"BPE_TIE_VERIFY": "0"})]
+            ("notie", {"BPE_TIE_VERIFY": "0"}), ("noprefix", {"BPE_PREFIX": "0"})]
 import numpy as np  # noqa: E402
 
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
