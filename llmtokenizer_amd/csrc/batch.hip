@@ -44,6 +44,9 @@ static_assert(BK < 64, "member masks are 64-bit");
 #ifndef BPE_SU
 #define BPE_SU 1
 #endif
+#ifndef BPE_FORM_PRINT
+#define BPE_FORM_PRINT 0  // 1: BPE_DEBUG_FORM also prints each formation's end (k_bsel)
+#endif
 #ifndef BPE_RU
 #define BPE_RU 4
 #endif
@@ -335,9 +338,6 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         else if (relist_due) stop = STOP_RELIST;
         else if (v0 == 0 || cnt0 <= 1) stop = STOP_DONE;
         else if (C->nkeys + 4ull * (256ull + md + 2) >= E->hcap / 2) stop = STOP_GROW;
-        if (stop != STOP_NONE && E->dbg_form && md + 1 >= E->dbg_form && lane == 0)
-            printf("stop shard %u md %u stop %u cnt0 %u hotT %u hot_n %u applied %u retry %u\n", E->shard, md, stop, cnt0,
-                   hotT, (uint32_t)C->hot_n, (uint32_t)applied, retry);
         // ---- the batch: members from the list in order, skipping the entries
         // that do not commute with an earlier member, up to the first entry
         // that qualifies as neither; over the second list too when the first
@@ -539,28 +539,11 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                        !(retry && retry <= kk);
             }
             k = kk;
+#if BPE_FORM_PRINT  // (a build option: the printf costs k_bsel 180 B of scratch per lane)
             if (E->dbg_form && md + 1 >= E->dbg_form && lane == 0)  // (diagnostics: where the formation ended; from merge BPE_DEBUG_FORM - 1)
-                printf("form shard %u md %u passes %u k %u end %u why %u skipped %u D %llu B %llu pend %u zrate %u applied %u retry %u\n",
-                       E->shard, md, npass, kk, kend, endwhy, nskt, D, (unsigned long long)Bsz, tpend, B->zrate,
-                       (uint32_t)applied, retry);
-            if (E->dbg_ku && md + 1 >= E->dbg_form) {  // (diagnostics: one key's table slots and hot-set entries)
-                const unsigned long long want = (((unsigned long long)E->dbg_ku << 32) | E->dbg_kv) + 1ull;
-                for (uint64_t s0 = 0; s0 < E->hcap; s0 += 64) {
-                    const uint64_t sl = s0 + lane;
-                    if (sl < E->hcap && E->hkey[sl * E->hks] == want)
-                        printf("  key %u %u at slot %llu count %u (home %llu)\n", E->dbg_ku, E->dbg_kv,
-                               (unsigned long long)sl, E->hcnt[sl * E->hcs], (unsigned long long)(mix64(want) & (E->hcap - 1)));
-                }
-                const uint32_t nh = min(C->hot_n, HOT_CAP);
-                for (uint32_t i = lane; i < nh; i += 64) {
-                    const uint32_t sl = E->hot_slot[i];
-                    if (E->hkey[(uint64_t)sl * E->hks] == want) printf("  key %u %u hot entry %u slot %u\n", E->dbg_ku, E->dbg_kv, i, sl);
-                }
-                if (lane == 0) printf("  hot_n %u hotT %u\n", nh, hotT);
-            }
-            if (E->dbg_form > 1 && md + 1 >= E->dbg_form && lane < 8)  // (the list head: key, count)
-                printf("  list %u: %u %u c %u member %u\n", lane, (uint32_t)(e.k >> 32), (uint32_t)e.k,
-                       (uint32_t)(e.v >> 32), lane < kk ? mu : 0u);
+                printf("form shard %u md %u passes %u k %u end %u why %u skipped %u D %llu B %llu pend %u zrate %u\n", E->shard,
+                       md, npass, kk, kend, endwhy, nskt, D, (unsigned long long)Bsz, tpend, B->zrate);
+#endif
             // candidate lists and token lengths, one lane per member
             uint32_t mode = 1, off = 0, len = 0, tl = 0;
             if (lane < k) {

@@ -319,7 +319,7 @@ struct bpe_gpu_ctx {
     hipEvent_t stage_ev[2] = {};
     size_t bytes_cap = 0;        // capacity of h.bytes (kept across loads of the same or smaller size)
     uint32_t *d_skew = nullptr;  // k_pair_skew_sample's {largest pair count, pairs sampled} (device)
-    uint32_t skew[2] = {0, 0};   // ... on the host once skew_valid
+    uint32_t skew[3] = {0, 0, 0};   // ... on the host once skew_valid
     bool skew_valid = false;
     uint32_t *d_pres = nullptr;  // [256] byte presence gathered while bpe_gpu_load_fd streamed the corpus
     bool pres_valid = false;     // d_pres describes the bytes loaded now
@@ -494,14 +494,6 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.dbgts = nullptr;
     h.dbg_form = (uint32_t)getenv_int("BPE_DEBUG_FORM", 0);
     h.prefix_apply = (uint32_t)(getenv_int("BPE_PREFIX", 1) != 0);
-    h.dbg_ku = h.dbg_kv = 0;
-    if (const char *t = getenv("BPE_DEBUG_KEY")) {
-        unsigned ku = 0, kv = 0;
-        if (sscanf(t, "%u,%u", &ku, &kv) == 2) {
-            h.dbg_ku = ku;
-            h.dbg_kv = kv;
-        }
-    }
     h.tie_verify = (uint32_t)getenv_int("BPE_TIE_VERIFY", 1);
     if (h.tie_verify && getenv_int("BPE_TIE_TEST", 0)) h.tie_verify = 2;  // (tests: every verification fails)
     if (getenv("BPE_DEBUG_TS") && !encode && (r = dalloc(c, &h.dbgts, (size_t)TS_SLOTS * TS_N))) return r;
@@ -1613,7 +1605,7 @@ int compact_ids(bpe_gpu_ctx *c) {
 // (+ the skew probe of the count pass into words 256-257 of the same buffer)
 int init_presence(bpe_gpu_ctx *c, uint32_t **d_bh) {
     int r;
-    if ((r = dalloc(c, d_bh, 256 + 2))) return r;
+    if ((r = dalloc(c, d_bh, 256 + 3))) return r;
     c->d_skew = *d_bh + 256;
     c->skew_valid = false;
     if (c->n0 >= 2) k_pair_skew_sample<<<1, 1024, 0, c->st>>>(c->h.bytes, c->n0, c->d_skew);
@@ -1658,9 +1650,9 @@ void launch_hist_pk(bpe_gpu_ctx *c, size_t lds, uint32_t ntl, uint32_t *d_hist, 
 uint32_t launch_count_pass(bpe_gpu_ctx *c, uint32_t ntl, uint32_t *d_hist, uint64_t tile, uint32_t lo, uint32_t S) {
     int r;
     if (!c->skew_valid && c->d_skew) {
-        if ((r = hipMemcpyAsync(c->skew, c->d_skew, 8, hipMemcpyDeviceToHost, c->st)) == hipSuccess)
+        if ((r = hipMemcpyAsync(c->skew, c->d_skew, 12, hipMemcpyDeviceToHost, c->st)) == hipSuccess)
             r = hipStreamSynchronize(c->st);
-        if (r != hipSuccess) c->skew[0] = c->skew[1] = 0;
+        if (r != hipSuccess) c->skew[0] = c->skew[1] = c->skew[2] = 0;
         c->skew_valid = true;
     }
     bool skew = c->skew[1] > 0 && (uint64_t)c->skew[0] * 16 > c->skew[1];
@@ -1789,6 +1781,15 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
         // relative to the group: G * tile <= 2^24); BPE_SORT_G caps G (tuning)
         uint32_t G = (uint32_t)std::max<uint64_t>(1, (1ull << SORT_LOCAL_BITS) / tile);
         G = std::min<uint32_t>(G, (uint32_t)std::max(1, getenv_int("BPE_SORT_G", 16)));
+        // a unit (group, first byte) is one block's work: on skewed input
+        // (one first byte in most pairs) fewer tiles per group keep units at
+        // <= SORT_UNIT_MAX entries, so the blocks share the work (one-byte
+        // corpus, 1 GiB: 64 units of 16 M -> 1024 of 1 M; sort_b 11 -> 3 ms)
+        if (c->skew_valid && c->skew[1] && c->skew[2]) {
+            constexpr uint64_t SORT_UNIT_MAX = 1u << 18;
+            const uint64_t gs = SORT_UNIT_MAX * c->skew[1] / ((uint64_t)tile * c->skew[2]);
+            G = std::min<uint32_t>(G, (uint32_t)std::max<uint64_t>(1, gs));
+        }
         k_sort_a<<<ntl, SORT_T, 0, c->st>>>(c->dE, d_hist, tile, G, d_tmp);
         k_sort_b<<<1024 * (1024 / SORT_T), SORT_T, 0, c->st>>>(c->dE, d_hist, d_tot, ntl, tile, G, d_tmp);
         HIPCHK(hipGetLastError());
@@ -1806,11 +1807,12 @@ int init_tokens(bpe_gpu_ctx *c, std::vector<uint32_t> *unrank_out, uint32_t **d_
     uint32_t *d_bh;
     int r;
     if ((r = init_presence(c, &d_bh))) return r;
-    std::vector<uint32_t> bh(256 + 2);
+    std::vector<uint32_t> bh(256 + 3);
     HIPCHK(hipMemcpyAsync(bh.data(), d_bh, bh.size() * 4, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     c->skew[0] = bh[256];
     c->skew[1] = bh[257];
+    c->skew[2] = bh[258];
     c->skew_valid = true;
     bh.resize(256);
     return init_sort(c, bh, unrank_out, d_tot_out);

@@ -2389,14 +2389,16 @@ template __global__ void k_pair_hist_v<4, true>(const Eng *, uint32_t *, uint64_
 
 // Skew probe of the corpus (one block, before the count pass): the byte pairs
 // inside SKEW_SAMPLES dwords spread evenly over it, counted in 16-bit LDS bins
-// (two to a word); out[0] = the largest count, out[1] = pairs sampled.
+// (two to a word); out[0] = the largest count, out[1] = pairs sampled,
+// out[2] = the largest count of one first byte (the init sort's unit sizes).
 constexpr uint32_t SKEW_SAMPLES = 16384;
 __global__ __launch_bounds__(1024) void k_pair_skew_sample(const uint8_t *__restrict__ bytes, uint64_t n0,
                                                            uint32_t *__restrict__ out) {
-    __shared__ uint32_t h[32768];
-    __shared__ uint32_t smax, stot;
+    __shared__ uint32_t h[32768], hb[256];
+    __shared__ uint32_t smax, stot, sbmax;
     for (uint32_t i = threadIdx.x; i < 32768; i += blockDim.x) h[i] = 0;
-    if (threadIdx.x == 0) smax = stot = 0;
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) hb[i] = 0;
+    if (threadIdx.x == 0) smax = stot = sbmax = 0;
     __syncthreads();
     const uint64_t nwords = n0 / 4;  // whole dwords only
     const uint32_t ns = (uint32_t)min<uint64_t>(SKEW_SAMPLES, nwords);
@@ -2408,6 +2410,7 @@ __global__ __launch_bounds__(1024) void k_pair_skew_sample(const uint8_t *__rest
         for (uint32_t k = 0; k < 3; k++) {
             const uint32_t key = (w >> (8 * k)) & 0xFFFF;
             atomicAdd(&h[key >> 1], 1u << ((key & 1) << 4));
+            atomicAdd(&hb[key & 0xFF], 1u);
         }
         mine += 3;
     }
@@ -2416,10 +2419,12 @@ __global__ __launch_bounds__(1024) void k_pair_skew_sample(const uint8_t *__rest
     uint32_t m = 0;
     for (uint32_t i = threadIdx.x; i < 32768; i += blockDim.x) m = max(m, max(h[i] & 0xFFFF, h[i] >> 16));
     atomicMax(&smax, m);
+    if (threadIdx.x < 256) atomicMax(&sbmax, hb[threadIdx.x]);
     __syncthreads();
     if (threadIdx.x == 0) {
         out[0] = smax;
         out[1] = stot;
+        out[2] = sbmax;
     }
 }
 
@@ -2772,12 +2777,44 @@ __device__ inline void lds_sort_emit(SortLds &L, const uint32_t *bins, const uin
     for (uint32_t x = threadIdx.x; x < nb; x += SORT_T) L.cnt[x] = 0;
     __syncthreads();
     uint32_t rank[SORT_PER];
+    // Skewed input (one byte value, two alternating, 97 % spaces) puts most
+    // of a wave's entries in one bin, and same-address LDS atomics serialise
+    // lane by lane (init 4x slower).  A wave whose first entries mostly share
+    // a bin ranks each entry's largest group (up to two) with one atomic by
+    // its first lane, the rest one by one; uniform input pays one ballot.
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t b00 = (uint32_t)__builtin_amdgcn_readfirstlane((int)bins[0]);
+    const bool skewed = __popcll(__ballot(bins[0] == b00)) >= 16;  // (wave-uniform)
+    if (skewed) {
+        const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
-    for (uint32_t k = 0; k < SORT_PER; k++) rank[k] = bins[k] < nb ? atomicAdd(&L.cnt[bins[k]], 1u) : 0;
+        for (uint32_t k = 0; k < SORT_PER; k++) {
+            bool done = !(bins[k] < nb);
+            unsigned long long rem = __ballot(!done);
+            rank[k] = 0;
+            for (int it = 0; it < 2 && rem; it++) {  // (uniform)
+                const uint32_t lead = (uint32_t)__builtin_ctzll(rem);
+                const uint32_t b = (uint32_t)__shfl((int)bins[k], (int)lead);
+                const unsigned long long m = __ballot(!done && bins[k] == b);
+                if (__popcll(m) < 8) break;
+                uint32_t base = 0;
+                if (lane == lead) base = atomicAdd(&L.cnt[b], (uint32_t)__popcll(m));
+                base = (uint32_t)__shfl((int)base, (int)lead);
+                if (!done && bins[k] == b) {
+                    rank[k] = base + (uint32_t)__popcll(m & lt);
+                    done = true;
+                }
+                rem &= ~m;
+            }
+            if (!done) rank[k] = atomicAdd(&L.cnt[bins[k]], 1u);
+        }
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < SORT_PER; k++) rank[k] = bins[k] < nb ? atomicAdd(&L.cnt[bins[k]], 1u) : 0;
+    }
     __syncthreads();
     if (threadIdx.x < 64) {
         // wave-parallel exclusive scan over the (<= 256) bins, 4 per lane
-        const uint32_t lane = threadIdx.x;
         uint32_t c[4], sum = 0;
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {

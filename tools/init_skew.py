@@ -1,9 +1,10 @@
 """Init time (stats.ms_init: count pass, counting sort, table and hot-set
 build) on skewed corpora against the uniform corpus of the same size, and
 an english-like corpus timed end to end.  Each input is
-SIZE_MIB (default 16: a corpus of one repeated byte is one a == a run, which
-the scan pairs with one thread per run), trained for 2 merges three times
-(init) and, for the english-like corpus, for 1024 merges (end to end).
+SIZE_MIB (default 1024), "trained" for 0 merges three times (the whole init
+and one selection, which stops at the cap: a corpus of one repeated byte is
+one a == a run, whose first merge the batch scan walks with one thread) and,
+for the english-like corpus, for 1024 merges (end to end).
 
 usage: python tools/init_skew.py [SIZE_MIB] [NAMES...]"""
 import hashlib
@@ -17,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from llmtokenizer_amd import api  # noqa: E402
 from llmtokenizer_amd.synth import english_like  # noqa: E402
 
-size = (int(sys.argv[1]) if len(sys.argv) > 1 else 16) << 20
+size = (int(sys.argv[1]) if len(sys.argv) > 1 else 1024) << 20
 names = sys.argv[2:] or ["uniform", "one_byte", "alternating", "mostly_space", "english_like"]
 
 
@@ -44,12 +45,12 @@ for name in names:
         e.load(data)
     init, cp = [], []
     for _ in range(3):
-        e.train(2)
+        e.train(0)
         st = e.stats()
         init.append(round(st["ms_init"], 3))
         cp.append(round(st["ms_count_pass"], 4))
     r = {"input": name, "mib": size >> 20, "init_ms": init, "count_ms": cp, "form": int(st["count_pass_span"]),
-         "md5_2": hashlib.md5(e.merges().tobytes()).hexdigest(), "ids_2": "%016x" % e.ids_checksum()}
+         "ids_0": "%016x" % e.ids_checksum()}
     if name == "english_like":
         e.train(1024)
         st = e.stats()
