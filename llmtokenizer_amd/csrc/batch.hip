@@ -71,7 +71,8 @@ constexpr uint32_t RU = BPE_RU;  // rewrite occurrences per thread per round
 
 // debug timeline of a batch (BPE_DEBUG_TS; E->dbgts rows indexed by batch)
 enum { BT_SCAN_IN = 0, BT_SCAN_CAND, BT_SCAN_OUT, BT_APPLY_IN, BT_APPLY_PRO, BT_APPLY_A, BT_APPLY_B, BT_SEL_IN,
-       BT_SEL_RED, BT_SEL_LIST, BT_SEL_OUT, BT_N };
+       BT_SEL_RED, BT_SEL_LIST, BT_SEL_OUT, BT_SEL_FORMED, BT_SEL_CAND, BT_SEL_FOLD, BT_SEL_WB,
+       BT_F_TIE, BT_F_CM, BT_F_MEMB, BT_F_FOLD, BT_F_PRE, BT_F_CHK, BT_N };
 static_assert(BT_N <= TS_N, "batch stamps fit a timeline row");
 __device__ inline uint32_t bat_idx(const Eng *E) {
     return E->dbgts ? (uint32_t)(E->bat->nbatch + E->bat->nretry) : 0u;
@@ -307,6 +308,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             rs += __shfl_xor(rs, o);
             rg += __shfl_xor(rg, o);
         }
+        ts_mark(E, bi, BT_F_FOLD, false);
         const unsigned long long D = C->D + (applied ? B->dD : 0ull);
         const uint32_t md = C->merges_done + jst;
         const unsigned long long n_live = C->n_live - rg;
@@ -343,6 +345,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         // that qualifies as neither; over the second list too when the first
         // one is used up (two passes of the same rules)
         uint32_t k = 0;
+        ts_mark(E, bi, BT_F_PRE, false);
         if (stop == STOP_NONE) {
             const int zsz = __builtin_ctzll(Bsz);
             uint32_t kk = 0, nskt = 0, tpend = BK, endwhy = 8, kend = 64;
@@ -401,19 +404,40 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 uint32_t tmask = 0xFFu;
                 const bool tie_next = lane < nlp && !(c > (lane + 1 < nlp ? cnext : 0u));
                 const bool check = __ballot(!stable && !first && tie_next) != 0;  // (wave-uniform)
-                for (uint32_t p = 1; check && p < TOPK; p++) {  // (uniform loop; readlane needs every lane)
-                    const uint32_t cp = __builtin_amdgcn_readlane((int)c, (int)p);
-                    const uint32_t hp = __builtin_amdgcn_readlane((int)hsh, (int)p);
-                    const unsigned long long kp =
-                        ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)u, (int)p) << 32) |
-                        (uint32_t)__builtin_amdgcn_readlane((int)v, (int)p);
-                    if (p > lane && p < nlp && cp == c)
-                        for (uint64_t Bx = Blo; Bx <= Bhi; Bx <<= 1) {
-                            const uint64_t bj = hsh & (Bx - 1), bp = hp & (Bx - 1);
-                            const int lv = __builtin_ctzll(Bx) - zsz + 5;
-                            if (!(bj < bp || (bj == bp && ep.k < kp)) && lv >= 0 && lv < 8) tmask &= ~(1u << lv);
+                if (pass == 0) ts_mark(E, bi, BT_F_CHK, false);
+                if (check) {
+                    // per level B = B_sz 2^(e - 5) (e in [0, 8), where my range
+                    // [Blo, Bhi] reaches it): the smallest (bucket, key) among the
+                    // listed keys of my count after me must be above mine -- a
+                    // segmented suffix minimum over the lanes (equal counts are
+                    // contiguous in the list), ~20 shuffles per level instead of a
+                    // 63-step readlane loop (9 of the formation's ~25 us)
+                    const uint32_t khi = (uint32_t)(ep.k >> 32), klo = (uint32_t)ep.k;
+                    const bool inl = lane < nlp;
+                    const bool has = lane + 1 < nlp && cnext == c;  // a key of my count after me
+#pragma unroll 1
+                    for (uint32_t ee = 0; ee < 8; ee++) {  // (uniform)
+                        const uint64_t Bx = ee >= 5 ? (Bsz << (ee - 5)) : (Bsz >> (5 - ee));
+                        if (Bx == 0 || (Bx << (ee >= 5 ? 0 : 5 - ee)) != (ee >= 5 ? Bx : Bsz)) continue;  // (B_sz < 2^(5 - e))
+                        const bool need = inl && has && Bx >= Blo && Bx <= Bhi;
+                        if (!__ballot(need)) continue;
+                        const uint32_t bk = hsh & (uint32_t)(Bx - 1);
+                        uint32_t m0 = inl ? bk : ~0u, m1 = inl ? khi : ~0u, m2 = inl ? klo : ~0u;
+                        for (uint32_t d = 1; d < 64; d <<= 1) {  // inclusive suffix minimum within my count
+                            const uint32_t o0 = __shfl_down(m0, d), o1 = __shfl_down(m1, d), o2 = __shfl_down(m2, d);
+                            const uint32_t cd = __shfl_down(c, d);
+                            if (lane + d < nlp && cd == c && (o0 < m0 || (o0 == m0 && (o1 < m1 || (o1 == m1 && o2 < m2))))) {
+                                m0 = o0;
+                                m1 = o1;
+                                m2 = o2;
+                            }
                         }
+                        const uint32_t x0 = __shfl_down(m0, 1), x1 = __shfl_down(m1, 1), x2 = __shfl_down(m2, 1);
+                        const bool ahead = bk < x0 || (bk == x0 && (khi < x1 || (khi == x1 && klo < x2)));
+                        if (need && !ahead) tmask &= ~(1u << ee);
+                    }
                 }
+                if (pass == 0) ts_mark(E, bi, BT_F_TIE, false);
                 // (keys past this list -- the second list's, or unknown -- keep
                 // their order under B_sz only)
                 const bool past = trunc || (pass == 0 && E->list2);
@@ -453,39 +477,51 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 // checks every member against the skipped keys before it.  It
                 // merges in a later batch.  (Ids below DENSE: the scan's LDS
                 // vectors hold the decrements; a tie order of its own is moot.)
+                if (pass == 0) ts_mark(E, bi, BT_F_CM, false);
                 const bool skok = skip_now && u < DENSE && v < DENSE && (why == 0 || why == 4);
                 unsigned long long M = 0, S = 0;
                 kend = 64;
                 {
-                    const uint32_t cmlo = (uint32_t)cm, cmhi = (uint32_t)(cm >> 32);
-                    const uint32_t cklo = (uint32_t)cmk, ckhi = (uint32_t)(cmk >> 32);
-                    for (uint32_t p = 0; p < 64; p++) {  // (uniform: every operand is a readlane)
-                        const unsigned long long cp = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)cmhi, (int)p) << 32) |
-                                                      (uint32_t)__builtin_amdgcn_readlane((int)cmlo, (int)p);
-                        const bool ck = (__builtin_amdgcn_readlane((int)cklo, (int)p) | __builtin_amdgcn_readlane((int)ckhi, (int)p)) != 0;
-                        const uint32_t wp = (uint32_t)__builtin_amdgcn_readlane((int)why, (int)p);
-                        if (ck || (cp & M)) {
-                            if (__builtin_amdgcn_readlane((int)skok, (int)p) && nskt + (uint32_t)__popcll(S) < BK) {
-                                S |= 1ull << p;
-                                continue;
-                            }
-                            kend = p;
-                            endwhy = 5;
-                            break;
-                        }
-                        if (wp) {
-                            kend = p;
-                            endwhy = wp;
-                            break;
-                        }
-                        if (kk + (uint32_t)__popcll(M) >= BK) {  // (the member cap: reported as "list")
-                            kend = p;
-                            endwhy = 8;
-                            break;
-                        }
-                        M |= 1ull << p;
+                    // The rules above applied entry by entry in list order, computed
+                    // lane-parallel: which entries are members is a greedy
+                    // independent set of the conflict graph in list order (an entry
+                    // joins iff none of the earlier entries it conflicts with did),
+                    // settled in rounds -- an entry is decided once every earlier
+                    // entry it conflicts with is (a few rounds; the 64-step readlane
+                    // loop took 6 us).  The batch then ends at the first entry whose
+                    // end condition holds given the members and skips before it.
+                    const bool myck = cmk != 0;
+                    unsigned long long X = 0;  // entries that conflict with an earlier member
+                    for (;;) {  // (uniform; <= 64 rounds: the first undecided entry is always ready)
+                        const unsigned long long dec = M | X;
+                        if (dec == ~0ull) break;
+                        const bool ready = !((dec >> lane) & 1ull) && (cm & ~dec) == 0;
+                        const bool isx = ready && (myck || (cm & M) != 0);
+                        const unsigned long long nm = __ballot(ready && !isx), nx = __ballot(isx);
+                        M |= nm;
+                        X |= nx;
+                    }
+                    const unsigned long long skm = __ballot(skok), below_l = (1ull << lane) - 1ull;
+                    const unsigned long long Sc = X & skm;  // skipped, unless the skip cap ends the batch first
+                    uint32_t ew = 0;
+                    if ((X >> lane) & 1ull) {
+                        if (!skok || nskt + (uint32_t)__popcll(Sc & below_l) >= BK) ew = 5;
+                    } else if (why) {
+                        ew = why;
+                    } else if (kk + (uint32_t)__popcll(M & below_l) >= BK) {  // (the member cap: reported as "list")
+                        ew = 8;
+                    }
+                    const unsigned long long ends = __ballot(ew != 0);
+                    if (ends) {
+                        kend = (uint32_t)__builtin_ctzll(ends);
+                        endwhy = (uint32_t)__builtin_amdgcn_readlane((int)ew, (int)kend);
+                        M &= (1ull << kend) - 1ull;
+                        S = Sc & ((1ull << kend) - 1ull);
+                    } else {
+                        S = Sc;
                     }
                 }
+                if (pass == 0) ts_mark(E, bi, BT_F_MEMB, false);
                 if (retry && retry < kk + (uint32_t)__popcll(M)) {  // the last batch failed at member `retry` (nothing changed since)
                     unsigned long long xm = M;
                     for (uint32_t q = kk; q < retry; q++) xm &= xm - 1;
@@ -539,6 +575,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                        !(retry && retry <= kk);
             }
             k = kk;
+            ts_mark(E, bi, BT_SEL_FORMED, false);
 #if BPE_FORM_PRINT  // (a build option: the printf costs k_bsel 180 B of scratch per lane)
             if (E->dbg_form && md + 1 >= E->dbg_form && lane == 0)  // (diagnostics: where the formation ended; from merge BPE_DEBUG_FORM - 1)
                 printf("form shard %u md %u passes %u k %u end %u why %u skipped %u D %llu B %llu pend %u zrate %u\n", E->shard,
@@ -624,6 +661,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 B->why[why_end]++;
                 if (ties > 1) C->counters[2]++;
             }
+            ts_mark(E, bi, BT_SEL_CAND, false);
         }
         if (lane == 0) {
             if (B->sc_out && B->ap_out) {  // spans of the batch just scanned and applied
@@ -682,6 +720,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             B->z0 = 256 + md;
             nmem = k;
         }
+        ts_mark(E, bi, BT_SEL_FOLD, false);
     }
     __syncthreads();
     if (tid < nmem) E->tlen[256 + sc.merges_done + tid] = ctl[tid];
@@ -703,6 +742,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         __hip_atomic_store(E->hprobe, sc.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     }
+    ts_mark(E, bi, BT_SEL_WB, false);
     ts_mark(E, bi, BT_SEL_OUT, false, true);
 }
 
