@@ -85,6 +85,7 @@ struct KV {
 __device__ inline KV kv_empty() { return KV{0ull, ~0ull}; }
 __device__ inline bool kv_ahead(const KV &x, const KV &y) { return x.v > y.v || (x.v == y.v && x.k < y.k); }
 __device__ inline KV kv_shfl(const KV &x, int src) { return KV{__shfl(x.v, src), __shfl(x.k, src)}; }
+__device__ inline KV kv_xor(const KV &x, int m) { return KV{__shfl_xor(x.v, m), __shfl_xor(x.k, m)}; }
 
 // bitonic sort of the wave's 64 entries (one per lane): lane 0 holds the first
 // in argmax order
@@ -94,7 +95,7 @@ __device__ inline KV wave_sort64(KV x) {
     for (uint32_t k = 2; k <= 64; k <<= 1) {
 #pragma unroll
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            const KV y = kv_shfl(x, (int)(lane ^ j));
+            const KV y = kv_xor(x, (int)j);
             const bool desc = (lane & k) == 0, lower = (lane & j) == 0;
             if (lower == desc ? kv_ahead(y, x) : kv_ahead(x, y)) x = y;
         }
@@ -107,7 +108,7 @@ __device__ inline KV wave_merge64(KV x) {
     const uint32_t lane = lane_id();
 #pragma unroll
     for (uint32_t j = 32; j > 0; j >>= 1) {
-        const KV y = kv_shfl(x, (int)(lane ^ j));
+        const KV y = kv_xor(x, (int)j);
         if ((lane & j) == 0 ? kv_ahead(y, x) : kv_ahead(x, y)) x = y;
     }
     return x;
