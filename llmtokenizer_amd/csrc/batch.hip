@@ -586,7 +586,10 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             uint32_t mode = 1, off = 0, len = 0, tl = 0;
             if (lane < k) {
                 cand_of(E, mu, mv, true, srank, E->poff, &mode, &off, &len);
-                tl = E->tlen[mu] + E->tlen[mv];
+                const uint32_t tlu = E->tlen[mu], tlv = E->tlen[mv];
+                tl = tlu + tlv;
+                Bg->mla[lane] = tlu;
+                Bg->mlb[lane] = tlv;
                 Bg->nskb[lane] = (uint8_t)mnskb;
                 Bg->cnew[lane] = 0;
                 Bg->adj[lane] = 0;
@@ -1615,6 +1618,36 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         B->nsl++;
         B->sl_in = B->sl_out = 0;
     }
+    // wave 0 issues every word its prologue reads together with the stop
+    // flag, lane q member q's (one round trip instead of four dependent ones:
+    // stop, k, the members' words, their token lengths)
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    uint32_t pf_k = 0, pf_z0 = 0, pf_dt = 0, pf_a = 0, pf_b = 0, pf_R = 0, pf_cnt = 0, pf_bnd = 0, pf_sb = 0, pf_la = 0,
+             pf_lb = 0, pf_nsk = 0, pf_skc = 0, pf_sdec = 0, pf_nskb = 0, pf_nl[4] = {0, 0, 0, 0};
+    unsigned long long pf_live = 0, pf_adj = 0;
+    if (tid < 64) {
+        pf_k = B->k;
+        pf_z0 = B->z0;
+        pf_dt = B->drop_test;
+        pf_live = C->n_live;
+        pf_nsk = B->nsk;
+        if (lane < BK) {
+            pf_a = B->a[lane];
+            pf_b = B->b[lane];
+            pf_R = B->R[lane];
+            pf_cnt = B->cnt[lane];
+            pf_bnd = B->bound[lane];
+            pf_sb = B->sbase[lane];
+            pf_la = B->mla[lane];
+            pf_lb = B->mlb[lane];
+            pf_adj = B->adj[lane];
+            pf_skc = B->sk_c[lane];
+            pf_sdec = B->sdec[lane];
+            pf_nskb = B->nskb[lane];
+#pragma unroll
+            for (uint32_t v = 0; v < 4; v++) pf_nl[v] = E->bvnl[4 * lane + v];
+        }
+    }
     if (C->stop) return;
     const uint32_t bi = bat_idx(E);
     ts_mark(E, bi, BT_APPLY_IN, true);
@@ -1624,17 +1657,16 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     __shared__ uint32_t s_cnew[BK];  // keys this block's updates created, per member (logged batches)
     __shared__ uint32_t sk, sj, sz0;
     __shared__ uint32_t ssp[P2P_MAXR_B + 1];  // SH: prefix of the shards' list lengths
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
     if (tid >= 64 && tid < 64 + BK) s_cnew[tid - 64] = 0;  // (ordered by the prologue's barrier)
     // prologue, wave 0, lane q = member q: the verified prefix, prefix sums of
     // the occurrences and of the listed-id counts, role A's blocks per member
     if (tid < 64) {
-        const uint32_t k = B->k, z0 = B->z0, dt = B->drop_test;
-        const unsigned long long live0 = C->n_live;
+        const uint32_t k = pf_k, z0 = pf_z0, dt = pf_dt;
+        const unsigned long long live0 = pf_live;
         const bool in = lane < k;
-        const uint32_t ma = in ? B->a[lane] : 0, mb = in ? B->b[lane] : 0;
-        const uint32_t R = in ? B->R[lane] : 0, cnt = in ? B->cnt[lane] : 0;
-        uint32_t bnd = in && !SH ? B->bound[lane] : 0;
+        const uint32_t ma = in ? pf_a : 0, mb = in ? pf_b : 0;
+        const uint32_t R = in ? pf_R : 0, cnt = in ? pf_cnt : 0;
+        uint32_t bnd = in && !SH ? pf_bnd : 0;
         if (SH && lane == 0) {  // every shard's list of ids >= DENSE (gathered): prefix of their lengths
             uint32_t acc = 0;
             ssp[0] = 0;
@@ -1659,14 +1691,14 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             const uint32_t ov = lane < BK ? E->xbat[lane] : 0;
             ovm = __ballot(lane < k && ov != 0);
         }
-        const uint32_t sbase = in ? B->sbase[lane] : 0;
+        const uint32_t sbase = in ? pf_sb : 0;
         uint32_t nlv[4], nls = 0;  // my member's listed-id counts (ids >= DENSE) per vector
 #pragma unroll
         for (uint32_t v = 0; v < 4; v++) {
-            nlv[v] = in ? E->bvnl[4 * lane + v] : 0u;
+            nlv[v] = in ? pf_nl[v] : 0u;
             nls += nlv[v];
         }
-        const uint32_t tla = in ? E->tlen[ma] : 0, tlb = in ? E->tlen[mb] : 0;
+        const uint32_t tla = in ? pf_la : 0, tlb = in ? pf_lb : 0;
         // exclusive prefix sum of R and max of bound over the members before me
         unsigned long long rpre = R;
         uint32_t bpre = bnd, lpre = nls;
@@ -1695,19 +1727,19 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         // after the decrements of the members that conflict with them (summed
         // over the shards), as a running max in list order; member q must be
         // strictly ahead of every skipped key listed before it
-        const uint32_t nsk = B->nsk;
+        const uint32_t nsk = pf_nsk;
         uint32_t skub = 0;
         if (lane < nsk) {
             // (BPE_SKIP_TEST: tests pretend no member lowered it, so every member
             // after a skipped key fails and the batch is re-formed before it)
-            const uint32_t dec = E->skip_on > 1 ? 0u : SH ? E->xbat[BK + lane] : B->sdec[lane], cs = B->sk_c[lane];
+            const uint32_t dec = E->skip_on > 1 ? 0u : SH ? E->xbat[BK + lane] : pf_sdec, cs = pf_skc;
             skub = cs > dec ? cs - dec : 0u;
         }
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(skub, o);
             if ((int)lane >= o) skub = max(skub, y);
         }
-        const uint32_t nsb = in && nsk ? B->nskb[lane] : 0u;
+        const uint32_t nsb = in && nsk ? pf_nskb : 0u;
         const uint32_t skmax = __shfl(skub, (int)(nsb ? nsb - 1 : 0));
         const bool skfail = nsb && !(skmax < cnt);
         // member q is the argmax after the members before it: its count beats
@@ -1731,7 +1763,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         // prefix (nothing changed in between, so the selection repeats).
         // (Sharded runs re-form always: the adjacency is per shard.)
         if (js < k) {
-            const unsigned long long am = in ? B->adj[lane] : 0ull, pre = (1ull << js) - 1ull;
+            const unsigned long long am = in ? pf_adj : 0ull, pre = (1ull << js) - 1ull;
             const bool abut = lane < js ? (am & ~pre) != 0 : (am & pre) != 0;
             if (SH || E->prefix_apply == 0 || __ballot(in && abut)) {
                 if (lane == 0) B->retry = js;

@@ -172,6 +172,7 @@ struct Bat {
     unsigned long long sl_in, sl_out, sl_ticks, nsl;
     unsigned long long adj[BK];       // per member: the members whose occurrences abut its own (k_bscan; cleared by
                                       // the select that forms the batch)
+    uint32_t mla[BK], mlb[BK];        // per member: the token lengths of its a and b (the select; k_bapply's prologue)
     // keys the formation skipped (batch.hip): a listed key that shares an id,
     // on the opposite side, with an earlier member is no member -- the
     // sequential passes lower its count when that member merges -- and every
