@@ -72,7 +72,7 @@ constexpr uint32_t RU = BPE_RU;  // rewrite occurrences per thread per round
 // debug timeline of a batch (BPE_DEBUG_TS; E->dbgts rows indexed by batch)
 enum { BT_SCAN_IN = 0, BT_SCAN_CAND, BT_SCAN_OUT, BT_APPLY_IN, BT_APPLY_PRO, BT_APPLY_A, BT_APPLY_B, BT_SEL_IN,
        BT_SEL_RED, BT_SEL_LIST, BT_SEL_OUT, BT_SEL_FORMED, BT_SEL_CAND, BT_SEL_FOLD, BT_SEL_WB,
-       BT_F_TIE, BT_F_CM, BT_F_MEMB, BT_F_FOLD, BT_F_PRE, BT_F_CHK, BT_N };
+       BT_F_TIE, BT_F_CM, BT_F_MEMB, BT_F_FOLD, BT_F_PRE, BT_F_CHK, BT_B_DEC, BT_B_UPD, BT_N };
 static_assert(BT_N <= TS_N, "batch stamps fit a timeline row");
 __device__ inline uint32_t bat_idx(const Eng *E) {
     return E->dbgts ? (uint32_t)(E->bat->nbatch + E->bat->nretry) : 0u;
@@ -133,23 +133,25 @@ __device__ inline void block_list_tree(KV (*part)[TOPK], uint32_t nw) {
 // ------------------------------------------------------------------ k_bsel
 // this block's share of the hot set (counts after the batch applied last,
 // buckets under B_final of its D) as a sorted top-TOPK list in out (LDS)
-__device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bsz, KV *out) {
+// slot0: hot_slot of this thread's first entry, loaded by the caller ahead
+__device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bsz, KV *out, uint32_t slot0) {
     __shared__ KV part[16][TOPK];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     KV run = kv_empty();
     // (the BRB reduce blocks share the list: the launch's other blocks rewrite)
     const uint32_t stride = BRB * blockDim.x;
-    for (uint32_t base = blockIdx.x * blockDim.x + w * 64; base < n; base += stride) {  // uniform per wave
+    const uint32_t base0 = blockIdx.x * blockDim.x + w * 64;
+    for (uint32_t base = base0; base < n; base += stride) {  // uniform per wave
         const uint32_t i = base + lane;
         KV x = kv_empty();
         if (i < n) {
-            const uint32_t slot = E->hot_slot[i];
+            const uint32_t slot = base == base0 ? slot0 : E->hot_slot[i];
             const uint32_t c = E->hcnt[(uint64_t)(slot) * E->hcs];
             const unsigned long long key = E->hkey[(uint64_t)(slot) * E->hks] - 1;
             if (c) x = KV{pack_val(c, (uint32_t)(key >> 32), (uint32_t)key, Bsz), key};
         }
         x = wave_sort64(x);
-        run = wave_top(run, x);
+        run = base == base0 ? x : wave_top(run, x);  // (the first round: nothing to merge with)
     }
     part[w][lane] = run;
     __syncthreads();
@@ -893,17 +895,23 @@ __global__ __launch_bounds__(1024) void k_bsel(const Eng *__restrict__ E, Ctl *_
         sel_exit_stamp(B);
         return;
     }
+    // the words the reduce needs first, issued with the stop flag (one round
+    // trip instead of three: stop, D / hot-set size, the first hot slots)
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t slot0 = i0 < HOT_CAP ? E->hot_slot[i0] : 0u;
+    const unsigned long long D0 = C->D, dD0 = B->dD;
+    const uint32_t hn0 = C->hot_n;
     if (C->stop) {
         sel_exit_stamp(B);
         return;
     }
     const uint32_t bi = bat_idx(E);
     ts_mark(E, bi, BT_SEL_IN, true);
-    const uint64_t Bsz = summary_B(C->D + B->dD);  // D after the batch applied last
-    const uint32_t n = min(C->hot_n, HOT_CAP);
+    const uint64_t Bsz = summary_B(D0 + dD0);  // D after the batch applied last
+    const uint32_t n = min(hn0, HOT_CAP);
     __shared__ KV top[TOPK];
     __shared__ uint32_t last;
-    bat_block_top(E, n, Bsz, top);
+    bat_block_top(E, n, Bsz, top, slot0);
     if (threadIdx.x < TOPK) {
         B->pv[blockIdx.x * TOPK + threadIdx.x] = top[threadIdx.x].v;
         B->pk[blockIdx.x * TOPK + threadIdx.x] = top[threadIdx.x].k;
@@ -1921,6 +1929,10 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         uint32_t m[AU], cat[AU], x[AU], val[AU];
 #pragma unroll
         for (uint32_t q = 0; q < AU; q++) decode(t0 + q * step + tid, m[q], cat[q], x[q], val[q]);
+        if (E->dbgts && t0 == bidB * blockDim.x) {  // (timeline: the first round's entries decoded, block by block)
+            __builtin_amdgcn_s_waitcnt(0);
+            if (tid == 0) atomicMax(&E->dbgts[(uint64_t)(bi % TS_SLOTS) * TS_N + BT_B_DEC], wall_clock64());
+        }
         bool act[AU];
         int dneg[AU];
         unsigned long long key[AU], prev[AU];
@@ -1970,6 +1982,10 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             old[q] = 0;
             if (act[q] && slot[q] != ~0ull)
                 old[q] = atomicAdd(&E->hcnt[slot[q] * E->hcs], dneg[q] ? 0u - val[q] : val[q]);
+        }
+        if (E->dbgts && t0 == bidB * blockDim.x) {  // (timeline: the first round's count updates returned)
+            __builtin_amdgcn_s_waitcnt(0);
+            if (tid == 0) atomicMax(&E->dbgts[(uint64_t)(bi % TS_SLOTS) * TS_N + BT_B_UPD], wall_clock64());
         }
 #pragma unroll
         for (uint32_t q = 0; q < AU; q++) {  // (uniform: the appends are wave-collective)
