@@ -1461,7 +1461,8 @@ void print_timeline(bpe_gpu_ctx *c, uint32_t zlast) {
     const double khz = ikhz > 0 ? ikhz : 100000.0;
     double sum[TS_N] = {}, gap = 0;
     uint32_t n = 0, ng = 0;
-    static const char *nm[TS_N] = {"K1 first in", "K1 rescan out", "K1 scan out", "K2 first in",
+    constexpr int NK = TS_SPARE0;  // (the one-merge engine's stamps; the spares are the batch engine's)
+    static const char *nm[NK] = {"K1 first in", "K1 rescan out", "K1 scan out", "K2 first in",
                                    "K2 select out", "K2 applyA out", "K2 applyB out", "K1 last in",
                                    "scan cands done", "scan list flushed", "scan deltas flushed",
                                    "B deltas loaded", "B table updated", "B marks listed",
@@ -1470,10 +1471,10 @@ void print_timeline(bpe_gpu_ctx *c, uint32_t zlast) {
     for (uint32_t z = std::max<uint32_t>(257, zfrom); z < zlast && z < TS_SLOTS; z++) {
         const unsigned long long *r = &t[(size_t)z * TS_N];
         bool ok = true;
-        for (int k = 0; k < TS_N; k++) ok = ok && r[k] != 0;
+        for (int k = 0; k < NK; k++) ok = ok && r[k] != 0;
         if (!ok) continue;
         const double k1 = (double)~r[TS_K1_IN];
-        for (int k = 0; k < TS_N; k++) {
+        for (int k = 0; k < NK; k++) {
             const double v = (k == TS_K1_IN || k == TS_K2_IN) ? (double)~r[k] : (double)r[k];
             sum[k] += (v - k1) * 1000.0 / khz;
         }
@@ -1487,7 +1488,7 @@ void print_timeline(bpe_gpu_ctx *c, uint32_t zlast) {
     }
     if (!n) return;
     fprintf(stderr, "block timeline over %u merges (us from K1's first block entry):", n);
-    for (int k = 1; k < TS_N; k++) fprintf(stderr, " %s %.2f;", nm[k], sum[k] / n);
+    for (int k = 1; k < NK; k++) fprintf(stderr, " %s %.2f;", nm[k], sum[k] / n);
     fprintf(stderr, " K2 end -> next K1 in %.2f\n", ng ? gap / ng : 0.0);
 }
 

@@ -1072,14 +1072,17 @@ __device__ __forceinline__ void rescan1_body(const Eng *__restrict__ E, Ctl *__r
 // keys (counts after the merge applied last, B_final of its D) into
 // hotp_*[bid]; k_select reduces the hot_parts partials.  No apply runs beside
 // it, so hot_n is stable.
+// hn0 / slot0: hot_n and this thread's first hot_slot entry when the caller
+// loaded them ahead (HOLE: load them here)
 __device__ void hot_reduce_body(const Eng *__restrict__ E, Ctl *__restrict__ C, const Snap &S, uint32_t bid,
-                                uint32_t nblk) {
+                                uint32_t nblk, uint32_t hn0 = HOLE, uint32_t slot0 = HOLE) {
     const uint64_t B = summary_B(S.D);
-    const uint32_t n = min(C->hot_n, HOT_CAP);
+    const uint32_t n = min(hn0 != HOLE ? hn0 : C->hot_n, HOT_CAP);
     if (bid == 0 && threadIdx.x == 0) C->hot_scanned += n;
     Top2 mine = top2_one(0, 0, ~0ull);
-    for (uint32_t i = bid * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
-        const uint32_t slot = E->hot_slot[i];
+    const uint32_t i0 = bid * blockDim.x + threadIdx.x;
+    for (uint32_t i = i0; i < n; i += nblk * blockDim.x) {
+        const uint32_t slot = i == i0 && slot0 != HOLE ? slot0 : E->hot_slot[i];
         const uint32_t c = E->hcnt[(uint64_t)(slot) * E->hcs];
         const unsigned long long k = E->hkey[(uint64_t)(slot) * E->hks] - 1;
         if (c) mine = top2_merge(mine, top2_one(pack_val(c, (uint32_t)(k >> 32), (uint32_t)k, B), 1, k));
@@ -1278,6 +1281,14 @@ __device__ inline void spec_descriptor(Ctl *C, const Snap &S) {
 // the exact pass (STOP_STATS) instead of failing the run.
 __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ E, Ctl *__restrict__ C,
                                                          uint32_t rblocks, uint32_t track) {
+    // the rescan blocks' hot-set words issued with the control block (no apply
+    // runs beside K1: hot_n and the list are stable), two round trips less
+    uint32_t hn0 = HOLE, slot0 = HOLE;
+    if (blockIdx.x < rblocks && E->hot) {
+        const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+        hn0 = C->hot_n;
+        slot0 = i0 < HOT_CAP ? E->hot_slot[i0] : HOLE;
+    }
     const Snap S = snap(C);
     if (blockIdx.x == 0 && threadIdx.x == 0) spec_descriptor(C, S);
     if (S.stop) return;
@@ -1320,7 +1331,7 @@ __global__ __launch_bounds__(SCAN_T) void k_rescan_spec(const Eng *__restrict__ 
     if (blockIdx.x < rblocks) {
         rescan1_body(E, C, S, blockIdx.x, rblocks);
         ts_mark(E, S.z, TS_K1_CLEARED, false, true);
-        if (E->hot) hot_reduce_body(E, C, S, blockIdx.x, rblocks);
+        if (E->hot) hot_reduce_body(E, C, S, blockIdx.x, rblocks, hn0, slot0);
         scan_exit_stamp(E, blockIdx.x);
         ts_mark(E, S.z, TS_K1_RESCAN, false, true);
     } else if (S.spec) {
