@@ -2768,9 +2768,12 @@ __device__ inline uint32_t tile_count(const uint32_t *hist, const uint32_t *tot,
 #define BPE_SORT_T 1024
 #endif
 #ifndef BPE_SORT_A_WAVES
-#define BPE_SORT_A_WAVES 1
+#define BPE_SORT_A_WAVES 8
 #endif
-constexpr uint32_t SORT_A_WAVES = BPE_SORT_A_WAVES;  // pass A's waves per SIMD target (8: two blocks per CU)
+// pass A's waves per SIMD target: 8 = two 1024-thread blocks per CU (64 VGPRs,
+// three dwords spilled) -- 1 GiB init 5.95-6.50 -> 5.63-5.89 ms against one
+// block per CU (80 VGPRs; round 5, tools/sort_a_waves_ab.sh, alternated twice)
+constexpr uint32_t SORT_A_WAVES = BPE_SORT_A_WAVES;
 constexpr uint32_t SORT_T = BPE_SORT_T, SORT_PER = 8, SORT_CH = SORT_T * SORT_PER;
 constexpr uint32_t SORT_LOCAL_BITS = 24;
 
@@ -2954,7 +2957,10 @@ __global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_A_W
 // coalesce).  A wave takes 512 consecutive slots of tok[] per round (lane L
 // holds slots 4L.. and 256 + 4L..; the slot after a lane's four comes from
 // the next lane, after the wave's 512 from one extra load).
-__global__ __launch_bounds__(SORT_T) void k_relist_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
+#ifndef BPE_RELIST_A_WAVES
+#define BPE_RELIST_A_WAVES 8
+#endif
+__global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(BPE_RELIST_A_WAVES, 8))) void k_relist_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
                                                      uint64_t tile, uint32_t G, uint32_t *__restrict__ tmp) {
     static_assert(SORT_PER == 8, "two 4-slot groups per lane and round");
     __shared__ SortLds L;

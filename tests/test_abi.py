@@ -207,7 +207,7 @@ def test_per_merge_kernels_have_no_scratch_segment():
     segment delays their wave dispatch.  Round 2 found
     k_fused / k_select / k_fused_sh with a 184-byte call frame from an
     outlined summary reduction; read the gfx950 kernel descriptors of the
-    built library and keep every per-merge kernel at zero."""
+    built library and keep every per-merge (and per-batch) kernel at zero."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("kernel_scratch", os.path.join(ROOT, "tools", "kernel_scratch.py"))
     ks = importlib.util.module_from_spec(spec)
@@ -216,7 +216,9 @@ def test_per_merge_kernels_have_no_scratch_segment():
     kd = ks.scan(lib)
     assert len(kd) > 20, "no gfx950 kernel descriptors found"
     per_merge = ("k_fused", "k_fused_sh", "k_select", "k_rescan_spec", "k_rescan_spec_sh", "k_scan", "k_apply",
-                 "k_undo", "k_rescan1", "k_hot_reduce")
+                 "k_undo", "k_rescan1", "k_hot_reduce",
+                 # the batch engine's per-batch kernels (round 5: a debug printf gave k_bsel 180 B)
+                 "k_bsel", "k_bscan", "k_bapply")
     found = {}
     for name, (lds, scratch) in kd.items():
         for k in per_merge:
