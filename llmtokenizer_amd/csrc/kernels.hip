@@ -2958,7 +2958,7 @@ __global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(SORT_A_W
 // holds slots 4L.. and 256 + 4L..; the slot after a lane's four comes from
 // the next lane, after the wave's 512 from one extra load).
 #ifndef BPE_RELIST_A_WAVES
-#define BPE_RELIST_A_WAVES 8
+#define BPE_RELIST_A_WAVES 1  // (8: two blocks per CU, 7 dwords spilled -- configs[2] within noise, tools/relist_a_waves_ab.sh)
 #endif
 __global__ __launch_bounds__(SORT_T) __attribute__((amdgpu_waves_per_eu(BPE_RELIST_A_WAVES, 8))) void k_relist_a(const Eng *__restrict__ E, const uint32_t *__restrict__ hist,
                                                      uint64_t tile, uint32_t G, uint32_t *__restrict__ tmp) {
