@@ -80,8 +80,10 @@ typedef struct {
     uint64_t enc_windows;     /* encode: windows replayed (window path)           */
     uint64_t relists;         /* training: byte-pair position lists rebuilt       */
     uint64_t batches;         /* training: merge batches (several merges per scan/apply pair) */
-    uint64_t batch_dropped;   /* training: batch members that failed the verification */
-    uint64_t batch_retries;   /* training: batches formed again (shorter) after a failed member */
+    uint64_t batch_dropped;   /* training: batch members that failed the verification (or came after one) */
+    uint64_t batch_retries;   /* training: batches formed again (shorter) after a failed member; a failed
+                                 batch whose verified prefix abuts no dropped member applies that prefix
+                                 instead (counted in batches and batch_dropped, not here) */
     uint64_t table_updates;   /* training, batches: pair-table updates of the applies */
     double ms_scan_span;      /* training, batches: average k_bscan span (device wall clock) */
     double ms_apply_span;     /* training, batches: average k_bapply span (device wall clock) */
@@ -106,7 +108,7 @@ typedef struct {
     uint64_t keys_zeroed;     /* training, batches: pair keys the applied batches took to count 0 */
     uint64_t keys_skipped;    /* training, batches: listed keys the applied batches skipped (they do not
                                  commute with an earlier member; its merge lowers their count) */
-    uint64_t skip_failed;     /* ... batches re-formed because a skipped key stayed ahead of a member */
+    uint64_t skip_failed;     /* ... batches whose first failed member failed on a skipped key */
 } bpe_gpu_stats;
 
 /* Per-merge record (training): the structured per-iteration metrics the
