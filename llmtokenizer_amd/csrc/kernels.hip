@@ -2767,6 +2767,9 @@ __device__ inline uint32_t tile_count(const uint32_t *hist, const uint32_t *tot,
 #ifndef BPE_SORT_T
 #define BPE_SORT_T 1024
 #endif
+#ifndef BPE_SORT_B_PF
+#define BPE_SORT_B_PF 1  // pass B loads the next chunk while it sorts one (64 VGPRs, still two blocks per CU: 1 GiB init -0.2 ms, tools/sort_b_pf_ab.sh)
+#endif
 #ifndef BPE_SORT_A_WAVES
 #define BPE_SORT_A_WAVES 8
 #endif
@@ -3067,6 +3070,29 @@ __global__ __launch_bounds__(SORT_T) void k_sort_b(const Eng *__restrict__ E, co
         __syncthreads();
         const uint32_t lo = range[0], n = range[1];
         prefetch(u + gridDim.x);
+#if BPE_SORT_B_PF
+        // the next chunk's words are loaded while this one sorts
+        uint32_t nw[SORT_PER];
+        auto load = [&](uint32_t q0, uint32_t *w) {
+#pragma unroll
+            for (uint32_t k = 0; k < SORT_PER; k++) {
+                const uint32_t q = q0 + k * SORT_T + threadIdx.x;  // coalesced reads
+                w[k] = q < n ? tmp[lo + q] : 0u;
+            }
+        };
+        if (n) load(0, nw);
+        for (uint32_t q0 = 0; q0 < n; q0 += SORT_CH) {
+            uint32_t bins[SORT_PER], vals[SORT_PER];
+#pragma unroll
+            for (uint32_t k = 0; k < SORT_PER; k++) {
+                const uint32_t q = q0 + k * SORT_T + threadIdx.x;
+                bins[k] = q < n ? nw[k] >> SORT_LOCAL_BITS : 256u;
+                vals[k] = gbase + (nw[k] & LOCAL);
+            }
+            if (q0 + SORT_CH < n) load(q0 + SORT_CH, nw);
+            lds_sort_emit(L, bins, vals, A, E->plist);
+        }
+#else
         for (uint32_t q0 = 0; q0 < n; q0 += SORT_CH) {
             uint32_t bins[SORT_PER], vals[SORT_PER];
 #pragma unroll
@@ -3078,6 +3104,7 @@ __global__ __launch_bounds__(SORT_T) void k_sort_b(const Eng *__restrict__ E, co
             }
             lds_sort_emit(L, bins, vals, A, E->plist);
         }
+#endif
     }
 }
 
