@@ -3239,7 +3239,11 @@ __global__ __launch_bounds__(256) void k_live_write(const Eng *__restrict__ E, c
 // each wave stages a round's live tokens in LDS and stores them as one
 // coalesced run.  Replaces k_live_count + k_live_scan + k_live_write for the
 // final ids (one read of tok instead of two).
-constexpr uint32_t LC_T = 256, LC_R = CTILE / (4 * LC_T);  // 16 rounds of 4 tokens per thread
+#ifndef BPE_LC_T
+#define BPE_LC_T 256
+#endif
+constexpr uint32_t LC_T = BPE_LC_T, LC_W = LC_T / 64, LC_R = CTILE / (4 * LC_T);  // 256: 16 rounds of 4 tokens per thread
+static_assert(LC_R * LC_W == 64, "one wave scans the (round, wave) totals");
 constexpr unsigned long long LC_AGG = 1ull << 32, LC_INC = 2ull << 32;
 
 __device__ inline void lc_publish(unsigned long long *st, unsigned long long v) {
@@ -3249,8 +3253,8 @@ __device__ inline void lc_publish(unsigned long long *st, unsigned long long v) 
 __global__ __launch_bounds__(LC_T) void k_live_compact(const Eng *__restrict__ E, unsigned long long *__restrict__ status,
                                                        uint32_t *__restrict__ ticket, uint32_t *__restrict__ total) {
     __shared__ uint32_t tile_s, excl_s;
-    __shared__ uint32_t woff[LC_R * 4];   // (round, wave) -> exclusive offset within the tile
-    __shared__ uint32_t stage[4][4 * 64];  // per-wave staging of one round's live tokens
+    __shared__ uint32_t woff[LC_R * LC_W];  // (round, wave) -> exclusive offset within the tile
+    __shared__ uint32_t stage[LC_W][4 * 64];  // per-wave staging of one round's live tokens
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) tile_s = atomicAdd(ticket, 1u);
     __syncthreads();
@@ -3266,7 +3270,7 @@ __global__ __launch_bounds__(LC_T) void k_live_compact(const Eng *__restrict__ E
         // c in 0..4: prefix and total from three ballots
         const unsigned long long b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
         pre[r] = (uint32_t)__popcll(b0 & lt) + 2u * (uint32_t)__popcll(b1 & lt) + 4u * (uint32_t)__popcll(b2 & lt);
-        if (lane == 0) woff[r * 4 + w] = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
+        if (lane == 0) woff[r * LC_W + w] = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
     }
     __syncthreads();
     if (w == 0) {
@@ -3320,7 +3324,7 @@ __global__ __launch_bounds__(LC_T) void k_live_compact(const Eng *__restrict__ E
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's staging stores landed
         __builtin_amdgcn_wave_barrier();
         const uint32_t cnt = __shfl(o, 63);  // lane 63's end = the wave's total this round
-        const uint32_t dst = base + woff[r * 4 + w];
+        const uint32_t dst = base + woff[r * LC_W + w];
         for (uint32_t k = lane; k < cnt; k += 64) out[dst + k] = sg[k];
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
