@@ -246,3 +246,31 @@ def test_reference_corpora_literal_inputs(fname):
     out = subprocess.run([os.path.join(root, "tools", "bpe_main"), path], capture_output=True, check=True,
                          timeout=120, env=env).stdout
     assert len(out) == fx["print_text_len"] and hashlib.md5(out).hexdigest() == fx["print_text_md5"]
+
+
+@pytest.mark.parametrize("kind", ["one_byte", "alternating", "mostly_space", "english_like"])
+def test_skewed_corpora_at_sort_group_sizes_vs_oracle(kind):
+    """Skewed corpora large enough that the init sort adapts (round 5): the
+    sampled first-byte share shrinks the pass-B groups (one byte: 1 tile per
+    group), and the LDS rank step folds each wave's largest bin groups.
+    Merges and ids == the oracle (RULE order: untracked at these sizes)."""
+    n = (4 << 20) if kind == "one_byte" else (24 << 20)
+    rng = np.random.default_rng(8)
+    if kind == "one_byte":
+        data = b"a" * n
+    elif kind == "alternating":
+        data = b"ab" * (n // 2)
+    elif kind == "mostly_space":
+        data = np.where(rng.random(n) < 0.97, 32, rng.integers(33, 127, n)).astype(np.uint8).tobytes()
+    else:
+        from llmtokenizer_amd.synth import english_like
+        data = english_like(n)
+    mm = 3 if kind == "one_byte" else 40
+    e = api.Engine(0)
+    e.load(data)
+    e.train(mm)
+    m, ids = e.merges(), e.ids()
+    e.close()
+    om, oids, _ = O.train(data, mm, O.RULE)
+    assert m.shape == om.shape and (m == om).all(), (kind, m[:4], om[:4])
+    assert ids.size == oids.size and (ids == oids).all(), kind
