@@ -72,7 +72,7 @@ constexpr uint32_t RU = BPE_RU;  // rewrite occurrences per thread per round
 // debug timeline of a batch (BPE_DEBUG_TS; E->dbgts rows indexed by batch)
 enum { BT_SCAN_IN = 0, BT_SCAN_CAND, BT_SCAN_OUT, BT_APPLY_IN, BT_APPLY_PRO, BT_APPLY_A, BT_APPLY_B, BT_SEL_IN,
        BT_SEL_RED, BT_SEL_LIST, BT_SEL_OUT, BT_SEL_FORMED, BT_SEL_CAND, BT_SEL_FOLD, BT_SEL_WB,
-       BT_F_TIE, BT_F_CM, BT_F_MEMB, BT_F_FOLD, BT_F_PRE, BT_F_CHK, BT_B_DEC, BT_B_UPD, BT_N };
+       BT_F_TIE, BT_F_CM, BT_F_MEMB, BT_F_FOLD, BT_F_PRE, BT_F_CHK, BT_B_DEC, BT_B_UPD, BT_R_LOAD, BT_R_SORT, BT_R_TREE, BT_N };
 static_assert(BT_N <= TS_N, "batch stamps fit a timeline row");
 __device__ inline uint32_t bat_idx(const Eng *E) {
     return E->dbgts ? (uint32_t)(E->bat->nbatch + E->bat->nretry) : 0u;
@@ -150,12 +150,20 @@ __device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bs
             const unsigned long long key = E->hkey[(uint64_t)(slot) * E->hks] - 1;
             if (c) x = KV{pack_val(c, (uint32_t)(key >> 32), (uint32_t)key, Bsz), key};
         }
+        if (E->dbgts && base == base0 && lane == 0) {  // (timeline: this wave's first keys loaded)
+            __builtin_amdgcn_s_waitcnt(0);
+            atomicMax(&E->dbgts[(uint64_t)(bat_idx(E) % TS_SLOTS) * TS_N + BT_R_LOAD], wall_clock64());
+        }
         x = wave_sort64(x);
+        if (E->dbgts && base == base0 && lane == 0)
+            atomicMax(&E->dbgts[(uint64_t)(bat_idx(E) % TS_SLOTS) * TS_N + BT_R_SORT], wall_clock64());
         run = base == base0 ? x : wave_top(run, x);  // (the first round: nothing to merge with)
     }
     part[w][lane] = run;
     __syncthreads();
     block_list_tree(part, nw);
+    if (E->dbgts && threadIdx.x == 0)
+        atomicMax(&E->dbgts[(uint64_t)(bat_idx(E) % TS_SLOTS) * TS_N + BT_R_TREE], wall_clock64());
     if (threadIdx.x < TOPK) out[threadIdx.x] = part[0][threadIdx.x];
     __syncthreads();
 }

@@ -1502,7 +1502,7 @@ void print_batch_timeline(bpe_gpu_ctx *c, uint64_t nb) {
     const double khz = ikhz > 0 ? ikhz : 100000.0;
     static const char *nm[BT_N] = {"scan in", "scan cands done", "scan out", "apply in", "apply prologue",
                                    "role A out", "role B out", "sel in", "reduce published", "list merged", "sel out",
-                                   "formed", "members staged", "folded", "written back", "f:tie", "f:cm", "f:memb", "f:fold", "f:pre", "f:chk", "b:decoded", "b:updated"};
+                                   "formed", "members staged", "folded", "written back", "f:tie", "f:cm", "f:memb", "f:fold", "f:pre", "f:chk", "b:decoded", "b:updated", "r:loaded", "r:sorted", "r:tree"};
     double sum[BT_N] = {}, gap = 0;
     uint32_t n = 0, ng = 0;
     for (uint64_t b = 1; b + 1 < nb && b < TS_SLOTS; b++) {

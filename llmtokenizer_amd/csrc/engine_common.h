@@ -46,7 +46,7 @@ constexpr uint32_t TS_SLOTS = 16384;     // merges kept by the debug block timel
 // atomicMax keeps the earliest): K1 = k_rescan_spec, K2 = k_fused
 enum { TS_K1_IN = 0, TS_K1_RESCAN, TS_K1_SCAN, TS_K2_IN, TS_K2_SELECT, TS_K2_APPLY_A, TS_K2_APPLY_B, TS_K1_LASTIN,
        TS_S_CAND, TS_S_LIST, TS_S_DELTA, TS_B_DVAL, TS_B_TABLE, TS_B_MARKS, TS_B_PROBE, TS_B_COUNT, TS_K1_CLEARED,
-       TS_SPARE0, TS_SPARE1, TS_SPARE2, TS_SPARE3, TS_SPARE4, TS_SPARE5, TS_N };  // (spares: the batch engine's timeline has more stamps)
+       TS_SPARE0, TS_SPARE1, TS_SPARE2, TS_SPARE3, TS_SPARE4, TS_SPARE5, TS_SPARE6, TS_SPARE7, TS_SPARE8, TS_N };  // (spares: the batch engine's timeline has more stamps)
 
 enum { V_DL = 0, V_DR = 1, V_IL = 2, V_IR = 3 };
 
