@@ -840,6 +840,12 @@ __device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat 
             stop_ = B->ra_top;
             ablk[k] = nA;
             am = BK;
+            // (BPE_RW_HOLD_US: a small rewrite waits so that the select's hot-set
+            // loads of this launch do not queue behind its random stores)
+            if (E->rw_hold && k && tot < E->rw_hold_max) {
+                const unsigned long long t0 = wall_clock64();
+                while (wall_clock64() - t0 < E->rw_hold) __builtin_amdgcn_s_sleep(2);
+            }
         }
     }
     __syncthreads();

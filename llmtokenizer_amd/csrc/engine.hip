@@ -494,6 +494,13 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.dbgts = nullptr;
     h.dbg_form = (uint32_t)getenv_int("BPE_DEBUG_FORM", 0);
     h.prefix_apply = (uint32_t)(getenv_int("BPE_PREFIX", 1) != 0);
+    {
+        int khz = 0;
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
+        const int us = getenv_int("BPE_RW_HOLD_US", 0);
+        h.rw_hold = (uint32_t)std::max(0, us) * (uint32_t)std::max(1, khz / 1000);
+        h.rw_hold_max = (uint32_t)getenv_int("BPE_RW_HOLD_MAX", 1 << 20);
+    }
     h.tie_verify = (uint32_t)getenv_int("BPE_TIE_VERIFY", 1);
     if (h.tie_verify && getenv_int("BPE_TIE_TEST", 0)) h.tie_verify = 2;  // (tests: every verification fails)
     if (getenv("BPE_DEBUG_TS") && !encode && (r = dalloc(c, &h.dbgts, (size_t)TS_SLOTS * TS_N))) return r;

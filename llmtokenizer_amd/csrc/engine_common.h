@@ -257,6 +257,8 @@ struct Eng {
     unsigned long long *dbgts;      // [TS_SLOTS][TS_N] per-merge block timeline (BPE_DEBUG_TS) or null
     uint32_t dbg_form;
     uint32_t prefix_apply;  // batches: apply a verified prefix that abuts no dropped member (BPE_PREFIX, default 1)
+    uint32_t rw_hold;       // k_bsel's rewrite blocks wait this many wall-clock ticks (BPE_RW_HOLD_US) before
+    uint32_t rw_hold_max;   // ... a rewrite of fewer occurrences than this, so the reduce's loads go first
     uint32_t *tlog;       // batches: undo log of a verified-tie batch's table updates (slot, delta)
     uint32_t tlog_cap;    // ... records
     uint32_t tie_verify;  // batches: admit members on the tie-order guess k_bapply verifies (BPE_TIE_VERIFY,
