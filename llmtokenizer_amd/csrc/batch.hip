@@ -55,6 +55,12 @@ static_assert(BK < 64, "member masks are 64-bit");
 #endif
 constexpr uint32_t AU = BPE_AU;  // k_bapply role B: table updates per thread in flight together
 constexpr uint32_t SU = BPE_SU;  // k_bscan candidates per thread per round (1: measured fastest, 85 vs 91 ms at 4)
+#ifndef BPE_RUN_THREAD_PAIRS
+#define BPE_RUN_THREAD_PAIRS 16
+#endif
+// a == b members: a thread walks a run's first RUN_THREAD_PAIRS pairs, then
+// hands the rest to a wave (RUN_Q handed-off runs per block; more walk on)
+constexpr uint32_t RUN_THREAD_PAIRS = BPE_RUN_THREAD_PAIRS, RUN_Q = 256;
 #ifndef BPE_FR
 #define BPE_FR 4
 #endif
@@ -1088,6 +1094,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     __shared__ uint32_t list[SCAN_T * SU * FR];  // the rounds' occurrences (position, tag), flushed every FR rounds
     __shared__ uint16_t ltag[SCAN_T * SU * FR];
     __shared__ uint32_t lcount, gbase, list_n, covc, sm, sk, sz0, bRs;
+    __shared__ uint32_t lr_n, lr_pos[RUN_Q];  // a == b: long runs handed from a thread to a wave (next pair's start)
     __shared__ unsigned long long badj;  // the members whose occurrences abut my member's (Bat::adj)
     __shared__ uint32_t gcnt[2];
     __shared__ uint32_t sa[BK], sb[BK], sla[BK];
@@ -1098,6 +1105,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     if (tid == 0) {
         sm = BK;
         covc = lcount = bRs = 0;
+        lr_n = 0;
         badj = 0;
         gcnt[0] = gcnt[1] = 0;
         sk = B->k;
@@ -1340,7 +1348,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         if (lane == 0 && wocc) atomicAdd(&bRs, wocc);  // (the block's occurrences: read after the barrier below)
 #endif
     } else {
-        // a == b (a batch of its own): the thread holding a run's first token
+        // a == b: the thread holding a run's first token
         // walks it, pairing tokens 0-1, 2-3, ... (greedy left-to-right); a run
         // that enters from the left shard continues its parity (H.hlr)
         for (uint32_t e0 = bid * SCAN_T; e0 < len; e0 += nblk * SCAN_T) {  // uniform trip count
@@ -1403,6 +1411,14 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     vadd_b(s, E, m, V_IR, rq, gcnt);
                 }
                 if (!knext || kq >= n) break;
+                // a long run: the rest goes to a wave (next pair at an even run index)
+                if (mi + 1 >= RUN_THREAD_PAIRS && nocc) {
+                    const uint32_t qs = atomicAdd(&lr_n, 1u);
+                    if (qs < RUN_Q) {
+                        lr_pos[qs] = (uint32_t)kq;
+                        break;
+                    }
+                }
                 pos = kq;
             }
             __syncthreads();
@@ -1419,6 +1435,60 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 tagz[gbase + q] = ltag[q];
             }
             __syncthreads();
+        }
+        // The long runs, 64 tokens per wave step (a run of millions of equal
+        // tokens took that many dependent steps of one thread): lane l holds
+        // the token at run index c + l (c even, so the pairs are the even
+        // lanes), the run goes on while every token is an in-shard a; per pair
+        // exactly the thread walk's occurrence, tag and deltas (its left
+        // neighbour is the previous pair's z; its right one from lanes l + 2,
+        // l + 3; tokens past my edge from the halo, as tok_at / v_right)
+        const uint32_t lane = tid & 63, nlr = min(lr_n, RUN_Q);
+        for (uint32_t qi = tid >> 6; qi < nlr; qi += SCAN_T / 64) {  // (wave-uniform)
+            int64_t cpos = lr_pos[qi];
+            for (;;) {
+                const int64_t L0 = (n - cpos + la - 1) / la;  // first lane at or past my right edge
+                auto posl = [&](int64_t l) -> int64_t { return l < L0 ? cpos + l * la : n + (l - L0); };
+                const int64_t P = posl(lane);
+                const uint32_t t = tok_at(P);
+                const bool in = P < n && t == a;
+                uint32_t tx = HOLE;  // lanes 0 / 1: the tokens at run indices c + 64 / c + 65
+                if (lane < 2) tx = tok_at(posl(64 + lane));
+                const uint32_t t64 = (uint32_t)__shfl((int)tx, 0), t65 = (uint32_t)__shfl((int)tx, 1);
+                const bool in64 = posl(64) < n && t64 == a;
+                const unsigned long long outm = __ballot(!in);
+                const uint32_t f = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;
+                const uint32_t d2 = (uint32_t)__shfl_down((int)t, 2), d3 = (uint32_t)__shfl_down((int)t, 3);
+                const uint32_t q = lane + 2 < 64 ? d2 : t64;
+                const uint32_t q3 = lane + 3 < 64 ? d3 : (lane + 3 == 64 ? t64 : t65);
+                const bool pair = (lane & 1) == 0 && lane + 1 < f;
+                const bool knext = q == a, nocc = knext && q3 == a;
+                // (the run's last pair: a right neighbour that starts another
+                // member's occurrence becomes its id, as in the thread walk)
+                const uint32_t st = (pair && !knext && q != HOLE)
+                                        ? starts_of<SH>(tok, rt, sb, sla, H, q, posl((int64_t)lane + 2), n)
+                                        : BK;
+                if (st < BK) tadj |= 1ull << st;
+                const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
+                const unsigned long long pm = __ballot(pair);
+                uint32_t g = 0;
+                if (lane == 0 && pm) {
+                    g = atomicAdd(Rm, (uint32_t)__popcll(pm));
+                    atomicAdd(&bRs, (uint32_t)__popcll(pm));
+                }
+                g = (uint32_t)__shfl((int)g, 0);
+                if (pair) {
+                    const uint32_t r = g + (uint32_t)__popcll(pm & ((1ull << lane) - 1ull));
+                    occz[r] = (uint32_t)P;
+                    tagz[r] = nb_tag(z, rq);
+                    if (q != HOLE) {
+                        vadd_b(s, E, m, V_DR, q, gcnt);
+                        vadd_b(s, E, m, V_IR, rq, gcnt);
+                    }
+                }
+                if (f < 64 || !in64) break;  // (the run ended in this step or at my edge)
+                cpos = posl(64);
+            }
         }
     }
     __syncthreads();
