@@ -111,6 +111,25 @@ def test_batches_match_oracle_text():
     assert st["batches"] > 0
 
 
+def test_long_runs_match_oracle():
+    """a == a runs longer than a thread's 16 pairs go to a wave (k_bscan, 64
+    tokens per step): run lengths around the hand-off and the step boundaries,
+    odd and even, ended by tokens that start other members' occurrences (the
+    run's last pair takes their id), runs of merged tokens (la > 1) once "aa"
+    exists, and one byte repeated (a single run of 4 Mi tokens)"""
+    rng = random.Random(11)
+    seps = [b"xy", b"yx", b"zxy", b"b", b"xyz", b"qb"]
+    parts = []
+    for _ in range(700):
+        L = rng.choice([31, 32, 33, 34, 35, 63, 64, 65, 66, 67, 97, 128, 129, 130, 131, 200, 257, 1000, 1001])
+        parts.append(bytes([rng.choice(b"aq")]) * L + rng.choice(seps))
+    data = b"".join(parts)
+    st = _check(data, 400)
+    assert st["batches"] > 0
+    _check(b"a" * (4 << 20), 4)
+    _check(b"b" + b"a" * ((1 << 20) + 3) + b"c", 3)
+
+
 def test_cap_inside_a_batch():
     """a merge cap that ends the run in the middle of a batch"""
     data = synth_bytes(504, 256 << 10)
