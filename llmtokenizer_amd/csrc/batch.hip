@@ -10,8 +10,8 @@
 //            block sorts its share with wave bitonic networks, the last block
 //            to finish merges the partial lists) -> the batch: the longest
 //            prefix of that order whose pairs commute (no id is the left id of
-//            one member and the right id of another; an a == b pair only
-//            alone), each member after the first strictly ahead of the next
+//            one member and the right id of another, so an a == b pair's id
+//            is in no other member), each member after the first strictly ahead of the next
 //            key in the order
 //   k_bscan  every member's occurrences in the PRE-batch tokens (commuting
 //            members never share a token, so these are exactly the
