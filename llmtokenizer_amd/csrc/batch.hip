@@ -61,6 +61,10 @@ constexpr uint32_t SU = BPE_SU;  // k_bscan candidates per thread per round (1: 
 // a == b members: a thread walks a run's first RUN_THREAD_PAIRS pairs, then
 // hands the rest to a wave (RUN_Q handed-off runs per block; more walk on)
 constexpr uint32_t RUN_THREAD_PAIRS = BPE_RUN_THREAD_PAIRS, RUN_Q = 256;
+#ifndef BPE_RUN_BLOCK_Q
+#define BPE_RUN_BLOCK_Q 2
+#endif
+constexpr uint32_t RUN_BLOCK_Q = BPE_RUN_BLOCK_Q;  // at most this many runs in a block: the whole block walks each
 #ifndef BPE_FR
 #define BPE_FR 4
 #endif
@@ -1094,7 +1098,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     __shared__ uint32_t list[SCAN_T * SU * FR];  // the rounds' occurrences (position, tag), flushed every FR rounds
     __shared__ uint16_t ltag[SCAN_T * SU * FR];
     __shared__ uint32_t lcount, gbase, list_n, covc, sm, sk, sz0, bRs;
-    __shared__ uint32_t lr_n, lr_pos[RUN_Q];  // a == b: long runs handed from a thread to a wave (next pair's start)
+    __shared__ uint32_t lr_n, lr_brk, lr_pos[RUN_Q];  // a == b: long runs handed from a thread to a wave (next pair's start)
     __shared__ unsigned long long badj;  // the members whose occurrences abut my member's (Bat::adj)
     __shared__ uint32_t gcnt[2];
     __shared__ uint32_t sa[BK], sb[BK], sla[BK];
@@ -1438,56 +1442,85 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         }
         // The long runs, 64 tokens per wave step (a run of millions of equal
         // tokens took that many dependent steps of one thread): lane l holds
-        // the token at run index c + l (c even, so the pairs are the even
-        // lanes), the run goes on while every token is an in-shard a; per pair
-        // exactly the thread walk's occurrence, tag and deltas (its left
+        // the token at run index c + o + l (c + o even, so the pairs are the
+        // even lanes), the run goes on while every token is an in-shard a; per
+        // pair exactly the thread walk's occurrence, tag and deltas (its left
         // neighbour is the previous pair's z; its right one from lanes l + 2,
-        // l + 3; tokens past my edge from the halo, as tok_at / v_right)
-        const uint32_t lane = tid & 63, nlr = min(lr_n, RUN_Q);
-        for (uint32_t qi = tid >> 6; qi < nlr; qi += SCAN_T / 64) {  // (wave-uniform)
-            int64_t cpos = lr_pos[qi];
-            for (;;) {
-                const int64_t L0 = (n - cpos + la - 1) / la;  // first lane at or past my right edge
-                auto posl = [&](int64_t l) -> int64_t { return l < L0 ? cpos + l * la : n + (l - L0); };
-                const int64_t P = posl(lane);
-                const uint32_t t = tok_at(P);
-                const bool in = P < n && t == a;
-                uint32_t tx = HOLE;  // lanes 0 / 1: the tokens at run indices c + 64 / c + 65
-                if (lane < 2) tx = tok_at(posl(64 + lane));
-                const uint32_t t64 = (uint32_t)__shfl((int)tx, 0), t65 = (uint32_t)__shfl((int)tx, 1);
-                const bool in64 = posl(64) < n && t64 == a;
-                const unsigned long long outm = __ballot(!in);
-                const uint32_t f = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;
-                const uint32_t d2 = (uint32_t)__shfl_down((int)t, 2), d3 = (uint32_t)__shfl_down((int)t, 3);
-                const uint32_t q = lane + 2 < 64 ? d2 : t64;
-                const uint32_t q3 = lane + 3 < 64 ? d3 : (lane + 3 == 64 ? t64 : t65);
-                const bool pair = (lane & 1) == 0 && lane + 1 < f;
-                const bool knext = q == a, nocc = knext && q3 == a;
-                // (the run's last pair: a right neighbour that starts another
-                // member's occurrence becomes its id, as in the thread walk)
-                const uint32_t st = (pair && !knext && q != HOLE)
-                                        ? starts_of<SH>(tok, rt, sb, sla, H, q, posl((int64_t)lane + 2), n)
-                                        : BK;
-                if (st < BK) tadj |= 1ull << st;
-                const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
-                const unsigned long long pm = __ballot(pair);
-                uint32_t g = 0;
-                if (lane == 0 && pm) {
-                    g = atomicAdd(Rm, (uint32_t)__popcll(pm));
-                    atomicAdd(&bRs, (uint32_t)__popcll(pm));
+        // l + 3; tokens past my edge from the halo, as tok_at / v_right).
+        // seg() walks one 64-token segment, emits its pairs if live(brk) says
+        // so, and returns brk (wave-uniform): the run ends in it or at my edge
+        const uint32_t lane = tid & 63, wv = tid >> 6, nlr = min(lr_n, RUN_Q);
+        auto seg = [&](int64_t c, uint32_t o, auto &&live) -> bool {
+            const int64_t L0 = (n - c + la - 1) / la;  // first run index at or past my right edge
+            auto posl = [&](int64_t l) -> int64_t { return l < L0 ? c + l * la : n + (l - L0); };
+            const int64_t P = posl((int64_t)o + lane);
+            const uint32_t t = tok_at(P);
+            const bool in = P < n && t == a;
+            uint32_t tx = HOLE;  // lanes 0 / 1: the tokens at run indices o + 64 / o + 65
+            if (lane < 2) tx = tok_at(posl((int64_t)o + 64 + lane));
+            const uint32_t t64 = (uint32_t)__shfl((int)tx, 0), t65 = (uint32_t)__shfl((int)tx, 1);
+            const bool in64 = posl((int64_t)o + 64) < n && t64 == a;
+            const unsigned long long outm = __ballot(!in);
+            const uint32_t f = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;
+            const bool brk = f < 64 || !in64;
+            const bool lv = live(brk);
+            const uint32_t d2 = (uint32_t)__shfl_down((int)t, 2), d3 = (uint32_t)__shfl_down((int)t, 3);
+            const uint32_t q = lane + 2 < 64 ? d2 : t64;
+            const uint32_t q3 = lane + 3 < 64 ? d3 : (lane + 3 == 64 ? t64 : t65);
+            const bool pair = lv && (lane & 1) == 0 && lane + 1 < f;
+            const bool knext = q == a, nocc = knext && q3 == a;
+            // (the run's last pair: a right neighbour that starts another
+            // member's occurrence becomes its id, as in the thread walk)
+            const uint32_t st = (pair && !knext && q != HOLE)
+                                    ? starts_of<SH>(tok, rt, sb, sla, H, q, posl((int64_t)o + lane + 2), n)
+                                    : BK;
+            if (st < BK) tadj |= 1ull << st;
+            const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
+            const unsigned long long pm = __ballot(pair);
+            uint32_t g = 0;
+            if (lane == 0 && pm) {
+                g = atomicAdd(Rm, (uint32_t)__popcll(pm));
+                atomicAdd(&bRs, (uint32_t)__popcll(pm));
+            }
+            g = (uint32_t)__shfl((int)g, 0);
+            if (pair) {
+                const uint32_t r = g + (uint32_t)__popcll(pm & ((1ull << lane) - 1ull));
+                occz[r] = (uint32_t)P;
+                tagz[r] = nb_tag(z, rq);
+                if (q != HOLE) {
+                    vadd_b(s, E, m, V_DR, q, gcnt);
+                    vadd_b(s, E, m, V_IR, rq, gcnt);
                 }
-                g = (uint32_t)__shfl((int)g, 0);
-                if (pair) {
-                    const uint32_t r = g + (uint32_t)__popcll(pm & ((1ull << lane) - 1ull));
-                    occz[r] = (uint32_t)P;
-                    tagz[r] = nb_tag(z, rq);
-                    if (q != HOLE) {
-                        vadd_b(s, E, m, V_DR, q, gcnt);
-                        vadd_b(s, E, m, V_IR, rq, gcnt);
-                    }
+            }
+            return brk;
+        };
+        if (nlr > RUN_BLOCK_Q) {
+            // many runs: one per wave, 64 tokens per step
+            for (uint32_t qi = wv; qi < nlr; qi += SCAN_T / 64) {  // (wave-uniform)
+                int64_t c = lr_pos[qi];
+                while (!seg(c, 0, [](bool) { return true; })) c += 64 * (int64_t)la;
+            }
+        } else {
+            // a few runs (one byte repeated: one run of the whole corpus): the
+            // whole block on each, 1024 tokens per step -- wave w takes
+            // segment w, and segments after the first one where the run ends
+            // emit nothing
+            constexpr uint32_t NW = SCAN_T / 64;
+            for (uint32_t qi = 0; qi < nlr; qi++) {  // (block-uniform)
+                int64_t c = lr_pos[qi];
+                for (;;) {
+                    if (tid == 0) lr_brk = NW;
+                    __syncthreads();
+                    seg(c, 64 * wv, [&](bool brk) {
+                        if (lane == 0 && brk) atomicMin(&lr_brk, wv);
+                        __syncthreads();
+                        return wv <= lr_brk;
+                    });
+                    const bool done = lr_brk < NW;
+                    __syncthreads();
+                    if (done) break;
+                    c += (int64_t)NW * 64 * la;
                 }
-                if (f < 64 || !in64) break;  // (the run ended in this step or at my edge)
-                cpos = posl(64);
             }
         }
     }
