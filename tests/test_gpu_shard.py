@@ -76,6 +76,29 @@ def test_group_small_random_vs_oracle_rule(seed):
         _assert_same(m, ids, om, oi, (seed, n, cuts))
 
 
+def test_group_long_runs_across_edges_vs_oracle_rule():
+    """a == a runs long enough for k_bscan's wave and block walks (> 16 pairs),
+    with shard cuts inside them at odd and even offsets (the run's parity
+    enters from the left shard, its last pair is the edge step's)"""
+    rng = random.Random(31)
+    for _ in range(6):
+        parts = []
+        for _ in range(rng.randint(2, 6)):
+            parts.append(b"a" * rng.randint(40, 5000) + rng.choice([b"b", b"xy", b"ab", b"ba"]))
+        data = b"".join(parts)
+        k = rng.randint(2, 6)
+        cuts = _split(len(data), k, rng)
+        mm = rng.choice([-1, 40])
+        m, ids, _ = _group_train(data, cuts, mm)
+        om, oi, _ = O.train(data, mm, O.RULE)
+        _assert_same(m, ids, om, oi, (len(data), cuts))
+    data = b"a" * 100001
+    for cuts in ([0, 33333, 66667, 100001], [0, 2, 50001, 100001]):
+        m, ids, _ = _group_train(data, cuts, 5)
+        om, oi, _ = O.train(data, 5, O.RULE)
+        _assert_same(m, ids, om, oi, cuts)
+
+
 @pytest.mark.parametrize("k", [2, 3, 8])
 def test_group_text_vs_oracle_rule(k):
     data = synth_bytes(960 + k, 200000)
