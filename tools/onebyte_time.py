@@ -1,7 +1,9 @@
+"""One byte repeated (a single a == a run): time the first merge and the first
+three (api.Engine.train), per size in MiB (argv; default 4 16 64)."""
 import sys, time
 sys.path.insert(0, '/root/repo')
 from llmtokenizer_amd import api
-for mib in (4, 16, 64):
+for mib in [int(x) for x in sys.argv[1:]] or (4, 16, 64):
     e = api.Engine(0)
     e.load(b'a' * (mib << 20))
     t = time.time(); e.train(1); t1 = time.time() - t
