@@ -65,6 +65,10 @@ constexpr uint32_t RUN_THREAD_PAIRS = BPE_RUN_THREAD_PAIRS, RUN_Q = 256;
 #define BPE_RUN_BLOCK_Q 2
 #endif
 constexpr uint32_t RUN_BLOCK_Q = BPE_RUN_BLOCK_Q;  // at most this many runs in a block: the whole block walks each
+#ifndef BPE_RUN_BU
+#define BPE_RUN_BU 2
+#endif
+constexpr uint32_t RUN_BU = BPE_RUN_BU;  // the block walk: 64-token segments per wave per step
 #ifndef BPE_FR
 #define BPE_FR 4
 #endif
@@ -1447,79 +1451,98 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         // pair exactly the thread walk's occurrence, tag and deltas (its left
         // neighbour is the previous pair's z; its right one from lanes l + 2,
         // l + 3; tokens past my edge from the halo, as tok_at / v_right).
-        // seg() walks one 64-token segment, emits its pairs if live(brk) says
-        // so, and returns brk (wave-uniform): the run ends in it or at my edge
+        // segs() walks U consecutive 64-token segments from run index o (their
+        // loads issued together), asks live(fb) -- fb: the first of them where
+        // the run ends, in it or at my edge (U: none) -- how many of them emit
+        // their pairs, and returns fb < U (wave-uniform)
         const uint32_t lane = tid & 63, wv = tid >> 6, nlr = min(lr_n, RUN_Q);
-        auto seg = [&](int64_t c, uint32_t o, auto &&live) -> bool {
+        auto segs = [&](int64_t c, uint32_t o, auto Uc, auto &&live) -> bool {
+            constexpr uint32_t U = decltype(Uc)::value;
             const int64_t L0 = (n - c + la - 1) / la;  // first run index at or past my right edge
             auto posl = [&](int64_t l) -> int64_t { return l < L0 ? c + l * la : n + (l - L0); };
-            const int64_t P = posl((int64_t)o + lane);
-            const uint32_t t = tok_at(P);
-            const bool in = P < n && t == a;
-            uint32_t tx = HOLE;  // lanes 0 / 1: the tokens at run indices o + 64 / o + 65
-            if (lane < 2) tx = tok_at(posl((int64_t)o + 64 + lane));
-            const uint32_t t64 = (uint32_t)__shfl((int)tx, 0), t65 = (uint32_t)__shfl((int)tx, 1);
-            const bool in64 = posl((int64_t)o + 64) < n && t64 == a;
-            const unsigned long long outm = __ballot(!in);
-            const uint32_t f = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;
-            const bool brk = f < 64 || !in64;
-            const bool lv = live(brk);
-            const uint32_t d2 = (uint32_t)__shfl_down((int)t, 2), d3 = (uint32_t)__shfl_down((int)t, 3);
-            const uint32_t q = lane + 2 < 64 ? d2 : t64;
-            const uint32_t q3 = lane + 3 < 64 ? d3 : (lane + 3 == 64 ? t64 : t65);
-            const bool pair = lv && (lane & 1) == 0 && lane + 1 < f;
-            const bool knext = q == a, nocc = knext && q3 == a;
-            // (the run's last pair: a right neighbour that starts another
-            // member's occurrence becomes its id, as in the thread walk)
-            const uint32_t st = (pair && !knext && q != HOLE)
-                                    ? starts_of<SH>(tok, rt, sb, sla, H, q, posl((int64_t)o + lane + 2), n)
-                                    : BK;
-            if (st < BK) tadj |= 1ull << st;
-            const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
-            const unsigned long long pm = __ballot(pair);
-            uint32_t g = 0;
-            if (lane == 0 && pm) {
-                g = atomicAdd(Rm, (uint32_t)__popcll(pm));
-                atomicAdd(&bRs, (uint32_t)__popcll(pm));
+            int64_t P[U];
+            uint32_t t[U], tx[U], f[U];
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const int64_t ou = (int64_t)o + 64 * u;
+                P[u] = posl(ou + lane);
+                t[u] = tok_at(P[u]);
+                tx[u] = lane < 2 ? tok_at(posl(ou + 64 + lane)) : HOLE;  // lanes 0 / 1: run indices ou + 64 / 65
             }
-            g = (uint32_t)__shfl((int)g, 0);
-            if (pair) {
-                const uint32_t r = g + (uint32_t)__popcll(pm & ((1ull << lane) - 1ull));
-                occz[r] = (uint32_t)P;
-                tagz[r] = nb_tag(z, rq);
-                if (q != HOLE) {
-                    vadd_b(s, E, m, V_DR, q, gcnt);
-                    vadd_b(s, E, m, V_IR, rq, gcnt);
+            uint32_t fb = U;
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const uint32_t t64 = (uint32_t)__shfl((int)tx[u], 0);
+                const bool in64 = posl((int64_t)o + 64 * u + 64) < n && t64 == a;
+                const unsigned long long outm = __ballot(!(P[u] < n && t[u] == a));
+                f[u] = outm ? (uint32_t)__builtin_ctzll(outm) : 64u;
+                if (fb == U && (f[u] < 64 || !in64)) fb = u;
+            }
+            const uint32_t nl = live(fb);
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                if (u < nl) {  // (uniform)
+                    const uint32_t t64 = (uint32_t)__shfl((int)tx[u], 0), t65 = (uint32_t)__shfl((int)tx[u], 1);
+                    const uint32_t d2 = (uint32_t)__shfl_down((int)t[u], 2), d3 = (uint32_t)__shfl_down((int)t[u], 3);
+                    const uint32_t q = lane + 2 < 64 ? d2 : t64;
+                    const uint32_t q3 = lane + 3 < 64 ? d3 : (lane + 3 == 64 ? t64 : t65);
+                    const bool pair = (lane & 1) == 0 && lane + 1 < f[u];
+                    const bool knext = q == a, nocc = knext && q3 == a;
+                    // (the run's last pair: a right neighbour that starts another
+                    // member's occurrence becomes its id, as in the thread walk)
+                    const uint32_t st = (pair && !knext && q != HOLE)
+                                            ? starts_of<SH>(tok, rt, sb, sla, H, q, posl((int64_t)o + 64 * u + lane + 2), n)
+                                            : BK;
+                    if (st < BK) tadj |= 1ull << st;
+                    const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
+                    const unsigned long long pm = __ballot(pair);
+                    uint32_t g = 0;
+                    if (lane == 0 && pm) {
+                        g = atomicAdd(Rm, (uint32_t)__popcll(pm));
+                        atomicAdd(&bRs, (uint32_t)__popcll(pm));
+                    }
+                    g = (uint32_t)__shfl((int)g, 0);
+                    if (pair) {
+                        const uint32_t r = g + (uint32_t)__popcll(pm & ((1ull << lane) - 1ull));
+                        occz[r] = (uint32_t)P[u];
+                        tagz[r] = nb_tag(z, rq);
+                        if (q != HOLE) {
+                            vadd_b(s, E, m, V_DR, q, gcnt);
+                            vadd_b(s, E, m, V_IR, rq, gcnt);
+                        }
+                    }
                 }
             }
-            return brk;
+            return fb < U;
         };
         if (nlr > RUN_BLOCK_Q) {
             // many runs: one per wave, 64 tokens per step
             for (uint32_t qi = wv; qi < nlr; qi += SCAN_T / 64) {  // (wave-uniform)
                 int64_t c = lr_pos[qi];
-                while (!seg(c, 0, [](bool) { return true; })) c += 64 * (int64_t)la;
+                while (!segs(c, 0, std::integral_constant<uint32_t, 1>{}, [](uint32_t) { return 1u; }))
+                    c += 64 * (int64_t)la;
             }
         } else {
             // a few runs (one byte repeated: one run of the whole corpus): the
-            // whole block on each, 1024 tokens per step -- wave w takes
-            // segment w, and segments after the first one where the run ends
-            // emit nothing
-            constexpr uint32_t NW = SCAN_T / 64;
+            // whole block on each, RUN_BU * 1024 tokens per step -- wave w
+            // takes segments [w * RUN_BU, (w + 1) * RUN_BU), and segments after
+            // the first one where the run ends emit nothing
+            constexpr uint32_t NS = SCAN_T / 64 * RUN_BU;
             for (uint32_t qi = 0; qi < nlr; qi++) {  // (block-uniform)
                 int64_t c = lr_pos[qi];
                 for (;;) {
-                    if (tid == 0) lr_brk = NW;
+                    if (tid == 0) lr_brk = NS;
                     __syncthreads();
-                    seg(c, 64 * wv, [&](bool brk) {
-                        if (lane == 0 && brk) atomicMin(&lr_brk, wv);
+                    segs(c, 64 * RUN_BU * wv, std::integral_constant<uint32_t, RUN_BU>{}, [&](uint32_t fb) {
+                        if (lane == 0 && fb < RUN_BU) atomicMin(&lr_brk, wv * RUN_BU + fb);
                         __syncthreads();
-                        return wv <= lr_brk;
+                        const uint32_t gb = lr_brk, w0 = wv * RUN_BU;
+                        return gb < w0 ? 0u : min(RUN_BU, gb - w0 + 1);
                     });
-                    const bool done = lr_brk < NW;
+                    const bool done = lr_brk < NS;
                     __syncthreads();
                     if (done) break;
-                    c += (int64_t)NW * 64 * la;
+                    c += (int64_t)NS * 64 * la;
                 }
             }
         }
