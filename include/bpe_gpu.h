@@ -109,6 +109,11 @@ typedef struct {
     uint64_t keys_skipped;    /* training, batches: listed keys the applied batches skipped (they do not
                                  commute with an earlier member; its merge lowers their count) */
     uint64_t skip_failed;     /* ... batches whose first failed member failed on a skipped key */
+    uint64_t stop_reason;     /* training: why the run ended -- 1 the reference's stop rule (no pair
+                                 left or max count <= 1, bpe.c:730-750), 2 the caller's merge cap,
+                                 3 the engine's own cap on an unbounded run (2^24 merges; 2^22 over
+                                 several devices in compress_multi) before that rule: reported on
+                                 stderr too, since the reference has no cap */
 } bpe_gpu_stats;
 
 /* Per-merge record (training): the structured per-iteration metrics the

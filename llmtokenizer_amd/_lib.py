@@ -53,7 +53,8 @@ class GpuStats(ctypes.Structure):
         [(n, ctypes.c_uint64) for n in ("end_list", "end_count", "end_unused", "end_dup", "end_tie", "end_conflict",
                                          "end_table", "end_staging")] + \
         [("ms_select_span", ctypes.c_double), ("select_launches", ctypes.c_uint64)] + \
-        [(n, ctypes.c_uint64) for n in ("tie_verified", "tie_failed", "keys_zeroed", "keys_skipped", "skip_failed")]
+        [(n, ctypes.c_uint64) for n in ("tie_verified", "tie_failed", "keys_zeroed", "keys_skipped", "skip_failed",
+                                         "stop_reason")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -288,6 +288,15 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         // the formation after the host's work -- a byte-pair list rebuild, a
         // hot-set rebuild or table growth leaves the counts as they were)
         const uint32_t retry = applied ? B->retry : B->rhold;
+        // (the formation's view of it: BPE_TEST_LOSE_RETRY drops the cut, so the
+        // failing batch is formed again -- what the watchdog below must end)
+        const uint32_t fretry = E->lose_retry ? 0u : retry;
+        // no-progress watchdog: a batch that applied nothing is re-formed with
+        // its verified prefix, whose first member always verifies; STALL_LIMIT
+        // such batches in a row mean the formation repeats itself (a lost retry
+        // cut, round 5): the run stops with an error instead of looping
+        const uint32_t nst = applied ? (jst ? 0u : Bg->nstall + 1u) : Bg->nstall;
+        const bool stalled = nst >= STALL_LIMIT;
         // (read before the lanes overwrite the member fields)
         const uint32_t olda = jst ? B->a[jst - 1] : 0, oldb = jst ? B->b[jst - 1] : 0, oldz0 = B->z0;
         const uint32_t oldsum = B->sumlen;
@@ -323,7 +332,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 ske--;
             }
         }
-        const bool skip_now = E->skip_on && (skg == 0 || retry != 0);
+        const bool skip_now = E->skip_on && (skg == 0 || fretry != 0);
         const uint32_t crate = Bg->crate;
         const uint32_t raerr = aload(&Bg->ra_err);  // a token too long for an end code (rewrite blocks)
         const bool sh = E->sharded != 0;
@@ -358,7 +367,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             relist_due = cs > os && cs - os >= E->relist_stale;
         }
         uint32_t stop = STOP_NONE;
-        if (C->err || raerr) stop = STOP_ERROR;
+        if (C->err || raerr || stalled) stop = STOP_ERROR;
         else if (!E->fast && n_live < TRACK_LIMIT) stop = STOP_MODE;
         else if (md >= E->mcap) stop = STOP_CAP;
         else if ((cnt0 < hotT && hotT > 2) || C->hot_n > HOT_LIMIT) stop = STOP_HOT;
@@ -547,9 +556,9 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                     }
                 }
                 if (pass == 0) ts_mark(E, bi, BT_F_MEMB, false);
-                if (retry && retry < kk + (uint32_t)__popcll(M)) {  // the last batch failed at member `retry` (nothing changed since)
+                if (fretry && fretry < kk + (uint32_t)__popcll(M)) {  // the last batch failed at member `retry` (nothing changed since)
                     unsigned long long xm = M;
-                    for (uint32_t q = kk; q < retry; q++) xm &= xm - 1;
+                    for (uint32_t q = kk; q < fretry; q++) xm &= xm - 1;
                     kend = (uint32_t)__builtin_ctzll(xm);
                     M &= (1ull << kend) - 1;
                     S &= (1ull << kend) - 1;
@@ -597,7 +606,7 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 npass = pass + 1;
                 // the first list used up (every entry a member or skipped): the second
                 more = pass == 0 && kend == 64 && endwhy == 8 && nl == TOPK && nl2 > 0 && kk < BK &&
-                       !(retry && retry <= kk);
+                       !(fretry && fretry <= kk);
             }
             k = kk;
             ts_mark(E, bi, BT_SEL_FORMED, false);
@@ -699,6 +708,8 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             }
             B->sc_in = B->sc_out = B->ap_in = B->ap_out = 0;
             B->rhold = stop != STOP_NONE ? retry : 0u;
+            Bg->nstall = nst;
+            if (stalled && !C->err) C->err = 10;
             B->skgate = (stop == STOP_NONE && !retry && skg ? skg - 1u : skg) | (ske << 16);
             if (applied) {
                 // the formation's guess of the keys a member zeroes: twice the

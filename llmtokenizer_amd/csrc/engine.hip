@@ -561,6 +561,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     // tied members admitted on a guess of the keys the members before them
     // create (D's upper side), checked by k_bapply like the lower side
     h.tie_up = (uint32_t)(getenv_int("BPE_TIE_UP", 0) != 0);
+    h.lose_retry = (uint32_t)(getenv_int("BPE_TEST_LOSE_RETRY", 0) != 0);
     h.xbat = nullptr;
     h.xsp_out = h.xsp_in = nullptr;
     h.xsp_cap = 0;
@@ -1307,9 +1308,27 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
     int last_graph = -1;             // graph replayed last (0 plain, 1 tracked)
     uint64_t iters_before = 0;
     bool need_scan = true;           // speculative graph: the committed merge is not scanned yet
+    // host-side no-progress guard: every pass of this loop that is not the
+    // last either replays graphs that commit merges or serves a host-side stop
+    // (a rebuild, growth, a resolver event) after which merges follow; this
+    // many passes in a row without a new merge mean a stop repeats itself
+    // (round 5: a retry cut lost across a byte-pair list rebuild) -- an error,
+    // not an endless loop.  (The device ends a loop inside the batch graph
+    // itself: Bat::nstall.)
+    constexpr uint32_t DRIVE_IDLE_LIMIT = 256;
+    uint64_t last_md = ~0ull;
+    uint32_t idle = 0;
     for (;;) {
         if ((r = pull_ctl(c))) return r;
         Ctl &C = *c->hC;
+        if (!encode) {
+            if (C.merges_done != last_md) {
+                last_md = C.merges_done;
+                idle = 0;
+            } else if (++idle > DRIVE_IDLE_LIMIT && C.stop != STOP_ERROR) {
+                return fail(BPE_GPU_EINTERNAL, "training made no progress (256 host-side passes in a row without a merge)");
+            }
+        }
         if (last_graph >= 0 && c->profile) {
             // iterations of the last replay that did real work (the rest early-exited)
             const uint64_t done = std::min<uint64_t>(C.counters[0] - iters_before, ITERS_PER_GRAPH);
@@ -1366,7 +1385,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             return 0;
         case STOP_ERROR:
             return fail(C.err == 5 ? BPE_GPU_ERANGE : BPE_GPU_EINTERNAL,
-                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than an end code holds (2^31 - 3 bytes)" : C.err == 7 ? "tracked iterations: the light pass waited for the track block in vain" : C.err == 9 ? "batch apply: the tie-verification barrier timed out" : "thread-stat table full");
+                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than an end code holds (2^31 - 3 bytes)" : C.err == 7 ? "tracked iterations: the light pass waited for the track block in vain" : C.err == 9 ? "batch apply: the tie-verification barrier timed out" : C.err == 10 ? "batch formation made no progress (64 batches in a row applied no merge)" : "thread-stat table full");
         case STOP_REDO:  // missed prediction: k_select committed the real merge
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;
@@ -1896,6 +1915,14 @@ int ctx_new(int device, hipStream_t shared, bpe_gpu_ctx **out) {
 
 // ------------------------------------------------ window encoder (encode_win.hip)
 
+// the engine's own merge cap on an unbounded run (2^24: the per-id arrays
+// are sized for it); BPE_ENGINE_MAX_MERGES lowers it (tests of the report)
+uint64_t engine_merge_cap() {
+    const char *t = getenv("BPE_ENGINE_MAX_MERGES");
+    const long long v = t ? atoll(t) : 0;
+    return v > 0 && v < (1ll << 24) ? (uint64_t)v : (1ull << 24);
+}
+
 int getenv_int(const char *k, int dflt) {
     const char *v = getenv(k);
     return v && *v ? atoi(v) : dflt;
@@ -2330,7 +2357,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->merges_done = 0;
     if (c->n0 < 2) return fail(BPE_GPU_EINVAL, "fewer than 2 tokens");
     uint64_t cap = c->n0 - 1;  // a run can never learn more merges than pairs
-    cap = std::min<uint64_t>(cap, 1ull << 24);
+    cap = std::min<uint64_t>(cap, engine_merge_cap());
     if (max_merges >= 0) cap = std::min<uint64_t>(cap, (uint64_t)max_merges);
     const double t0 = now_ms();
     int r;
@@ -2407,6 +2434,12 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
     c->stats.ms_init = t1 - t0;
     c->stats.ms_train = t2 - t1;
     c->stats.ms_total = t2 - t0;
+    c->stats.stop_reason = run_stop_reason(C.stop, cap, c->n0, max_merges);
+    if (c->stats.stop_reason == 3)
+        fprintf(stderr,
+                "bpe: training stopped at the engine's merge cap (%llu merges) before the reference's stop rule "
+                "(max count <= 1); pass a merge cap to choose the length\n",
+                (unsigned long long)cap);
     fill_profile(c);
     batch_profile(c);
     return 0;

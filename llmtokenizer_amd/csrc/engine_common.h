@@ -119,6 +119,8 @@ constexpr uint32_t BK = 63;     // members per batch (one list entry stays for t
 constexpr uint32_t BRB = 32;    // k_bsel reduce blocks (partial lists)
 constexpr uint32_t BREPL = 2;   // replicas of a member's dense delta accumulators
 constexpr uint32_t BSB = 256;   // k_bscan blocks (1024 threads, one per CU)
+constexpr uint32_t STALL_LIMIT = 64;  // consecutive batches without a merge before the run fails (never legit:
+                                      // a re-formed batch always verifies its first member)
 constexpr uint32_t P2P_MAXR_B = 16;  // shards of a sharded batch run (BPE_GPU_P2P_MAX_RANKS; the gathered lists)
 
 struct Bat {
@@ -165,7 +167,9 @@ struct Bat {
     uint32_t ra_z[BK], ra_la[BK], ra_lb[BK], ra_R[BK], ra_sbase[BK], ra_pre[BK + 1];
     uint32_t ra_xl, ra_xlb;           // sharded: my first token, retired (its b's length), or HOLE
     uint32_t ra_lo[BK];               // occurrences k_bapply's role-A blocks rewrote already (the first ones)
-    uint32_t ra_split, pad6;          // k_bapply's share of the rewrite, in 1/256 (BPE_RA_SPLIT)
+    uint32_t ra_split;                // k_bapply's share of the rewrite, in 1/256 (BPE_RA_SPLIT)
+    uint32_t nstall;                  // selections in a row that followed a batch which applied no merge (the
+                                      // no-progress watchdog: STALL_LIMIT of them end the run with an error)
     // k_bsel's device wall-clock span (first block entry, complemented; last
     // block exit), folded by the next k_bapply (outside the select's staged
     // head, which it writes back whole); launches folded
@@ -296,6 +300,8 @@ struct Eng {
     uint32_t skip_on;     // batches: skip non-commuting list entries instead of ending there (BPE_SKIP, default 1)
     uint32_t list2;       // batches: the selection lists the next TOPK keys too (BPE_LIST2, default 0)
     uint32_t tie_up;      // batches: the tie order's upper side on a guess of the keys created, verified (BPE_TIE_UP, default 0)
+    uint32_t lose_retry;  // tests (BPE_TEST_LOSE_RETRY=1): the select forgets a failed batch's retry cut, so the
+                          // failing batch is formed again and again -- the stall the no-progress watchdog ends
     uint32_t bvs;         // ids >= DENSE per (member, vector) in bvec / bvlist
     Bat *bat;
     uint16_t *btag;       // [n0] neighbour tags of the staged occurrences
@@ -493,6 +499,18 @@ __host__ __device__ inline uint32_t murmur_pair(uint32_t a, uint32_t b) {
 
 // slot hash for our own open-addressed tables (independent of murmur so the
 // tie-order bits do not correlate with probe clustering)
+// stats.stop_reason of a finished training run (bpe_gpu.h): the stop code,
+// the merge cap the run had and the caller's request (< 0: unbounded); the
+// engine's own cap (2^24 merges) on an unbounded run is reported on stderr
+// (the reference has no cap: it stops only at bpe.c:730-750's rules)
+inline uint64_t run_stop_reason(uint32_t stop, uint64_t cap, uint64_t ntok, long requested) {
+    if (stop == STOP_DONE) return 1;
+    if (stop != STOP_CAP) return 0;
+    if (cap >= ntok - 1) return 1;  // (n - 1 merges leave one token: no pair left, bpe.c:730)
+    if (requested >= 0 && (uint64_t)requested <= cap) return 2;
+    return 3;
+}
+
 __host__ __device__ inline uint64_t mix64(uint64_t x) {
     x ^= x >> 33;
     x *= 0xff51afd7ed558ccdull;

@@ -406,10 +406,21 @@ int drive_group(bpe_gpu_group *g) {
     const bool fused = !g->encoding && group_fused(g);
     bool need_scan = true;     // fused: the committed merge is not scanned yet
     bool ran_fused = false;    // fused: the last launch was the fused graph
+    // no-progress guard, as drive() (engine.hip): the same count on every rank
+    uint64_t last_md = ~0ull;
+    uint32_t idle = 0;
     for (;;) {
         for (bpe_gpu_ctx *c : g->cs)
             if ((r = pull_ctl(c))) return r;
         const Ctl &C0 = *g->cs[0]->hC;
+        if (!g->encoding) {
+            if (C0.merges_done != last_md) {
+                last_md = C0.merges_done;
+                idle = 0;
+            } else if (++idle > 256 && C0.stop != STOP_ERROR) {
+                return fail(BPE_GPU_EINTERNAL, "training made no progress (256 host-side passes in a row without a merge)");
+            }
+        }
         for (size_t q = 0; q < g->cs.size(); q++) {
             const Ctl &Cq = *g->cs[q]->hC;
             if (Cq.stop != C0.stop || Cq.merges_done != C0.merges_done || Cq.D != C0.D) {
@@ -467,6 +478,7 @@ int drive_group(bpe_gpu_group *g) {
             if (C0.err == 5) return fail(BPE_GPU_ERANGE, "a token longer than an end code holds (2^31 - 3 bytes)");
             return fail(BPE_GPU_EINTERNAL, (C0.err & P2P_ERR_BIT) ? "p2p exchange timed out (a peer rank stopped or diverged)"
                                            : C0.err == 1 ? "engine invariant violated (count decrement of an absent pair)"
+                                           : C0.err == 10 ? "batch formation made no progress (64 batches in a row applied no merge)"
                                                          : "pair table full");
         case STOP_HOT: {  // batch runs: the hot set's rebuild, the same on every shard
             if (!g->cs[0]->h.batch) return fail(BPE_GPU_EINTERNAL, "unexpected stop state in sharded training");
@@ -561,7 +573,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     if ((r = group_total(g, &ntot))) return r;
     g->stats.n_in = ntot;
     if (ntot < 2) return fail(BPE_GPU_EINVAL, "fewer than 2 tokens");
-    uint64_t cap = std::min<uint64_t>(ntot - 1, 1ull << 24);
+    uint64_t cap = std::min<uint64_t>(ntot - 1, engine_merge_cap());
     if (max_merges >= 0) cap = std::min<uint64_t>(cap, (uint64_t)max_merges);
     for (uint32_t k = 0; k < K; k++) {
         bpe_gpu_ctx *c = g->cs[k];
@@ -702,6 +714,12 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     *n_merges = C.merges_done;
     g->stats.n_out = nout;
     g->stats.merges = C.merges_done;
+    g->stats.stop_reason = run_stop_reason(C.stop, cap, ntot, max_merges);
+    if (g->stats.stop_reason == 3 && g->shard0 == 0)
+        fprintf(stderr,
+                "bpe: training stopped at the engine's merge cap (%llu merges) before the reference's stop rule "
+                "(max count <= 1); pass a merge cap to choose the length\n",
+                (unsigned long long)cap);
     g->stats.iterations = C.counters[0] + 1;
     g->stats.distinct_pairs = C.D;
     g->stats.merged_buckets = C.B;

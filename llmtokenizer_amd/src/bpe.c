@@ -473,6 +473,15 @@ dyn_arr_t *bpe_train_bytes_devices(const uint8_t *bytes, size_t n, long max_merg
     arr = pairs_to_arr(pairs, k);
     if (arr) {
         bpe_gpu_group_get_stats(gs[0], &g_last_stats);
+        /* an unbounded request that ended at this path's own cap is not the
+         * reference's stop rule (bpe.c:745-750): say so (stats and stderr) */
+        if (max_merges < 0 && g_last_stats.stop_reason == 2 && (long)k == cap) {
+            g_last_stats.stop_reason = 3;
+            fprintf(stderr,
+                    "bpe: training stopped at the multi-device merge cap (%ld merges) before the reference's stop "
+                    "rule (max count <= 1); pass a merge cap to choose the length\n",
+                    cap);
+        }
         *encoding = ids;
         *len = total;
         ids = NULL;

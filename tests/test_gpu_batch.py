@@ -83,6 +83,25 @@ def test_dropped_members_match_oracle():
     assert dropped > 0
 
 
+def test_lost_retry_cut_is_an_error_not_a_hang(monkeypatch):
+    """The no-progress watchdog (Bat::nstall, DESIGN 1.0).  BPE_TEST_LOSE_RETRY
+    makes the select forget a failed batch's retry cut -- round 5's bug, where
+    the failing batch was formed again forever (a hang; a SIGSEGV under the
+    profiler).  With members forced to fail (BPE_BATCH_DROP_TEST) and no
+    verified-prefix apply (BPE_PREFIX=0) every batch then fails alike: the run
+    must stop with an error after STALL_LIMIT batches, and a fresh context on
+    the same device must train correctly afterwards."""
+    monkeypatch.setenv("BPE_TEST_LOSE_RETRY", "1")
+    monkeypatch.setenv("BPE_BATCH_DROP_TEST", "3")
+    monkeypatch.setenv("BPE_PREFIX", "0")
+    data = synth_bytes(505, 200000)
+    with pytest.raises(api.BpeError, match="no progress"):
+        _train(data, 600)
+    monkeypatch.delenv("BPE_TEST_LOSE_RETRY")
+    st = _check(data, 600)  # (the drop test alone: re-formed batches, exact merges)
+    assert st["merges"] == 600
+
+
 def test_staging_cut_matches_oracle(monkeypatch):
     """BPE_BATCH_STAGE: a small occurrence staging area ends batch formation
     where the members' candidate lists stop fitting (never before the first)"""

@@ -274,3 +274,47 @@ def test_skewed_corpora_at_sort_group_sizes_vs_oracle(kind):
     om, oids, _ = O.train(data, mm, O.RULE)
     assert m.shape == om.shape and (m == om).all(), (kind, m[:4], om[:4])
     assert ids.size == oids.size and (ids == oids).all(), kind
+
+
+STOP_WORKER = r"""
+import sys
+from llmtokenizer_amd import api
+from llmtokenizer_amd.synth import synth_bytes
+e = api.Engine(0)
+e.load(synth_bytes(61, 1 << 16))
+e.train(int(sys.argv[1]))
+st = e.stats()
+print("RESULT", st["merges"], st["stop_reason"])
+"""
+
+
+def test_stop_reason_reports_the_engine_cap():
+    """stats.stop_reason: 1 the reference's rule (bpe.c:730-750), 2 the
+    caller's cap, 3 the engine's own cap on an unbounded run -- which the
+    reference does not have, so it is reported on stderr
+    (BPE_ENGINE_MAX_MERGES lowers the 2^24 cap for this test)"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(mm, cap=None):
+        env = dict(os.environ, PYTHONPATH=root)
+        if cap is not None:
+            env["BPE_ENGINE_MAX_MERGES"] = str(cap)
+        p = subprocess.run([sys.executable, "-c", STOP_WORKER, str(mm)], env=env, capture_output=True, text=True,
+                           timeout=120)
+        assert p.returncode == 0, p.stderr[-2000:]
+        line = [x for x in p.stdout.splitlines() if x.startswith("RESULT")][-1].split()
+        return int(line[1]), int(line[2]), p.stderr
+
+    m, why, err = run(-1, cap=50)
+    assert (m, why) == (50, 3) and "engine's merge cap (50 merges)" in err, (m, why, err[-500:])
+    m, why, err = run(40, cap=50)
+    assert (m, why) == (40, 2) and "merge cap" not in err
+    m, why, err = run(60, cap=50)  # (asked above the engine's cap: still the engine's)
+    assert (m, why) == (50, 3) and "engine's merge cap" in err
+    e = api.Engine(0)
+    e.load(b"the cat sat on the mat with the hat " * 3)
+    e.train(-1)
+    assert e.stats()["stop_reason"] == 1  # converged: max count <= 1
+    e.close()
