@@ -40,7 +40,6 @@ namespace bpeamd {
 
 static_assert(TOPK == 64, "a wave holds a list, one entry per lane");
 static_assert(BRB == 2 * (1024 / 64), "the select's 16 waves merge two partial lists each");
-static_assert(BK < 64, "member masks are 64-bit");
 #ifndef BPE_SU
 #define BPE_SU 1
 #endif
@@ -70,7 +69,7 @@ constexpr uint32_t RUN_BLOCK_Q = BPE_RUN_BLOCK_Q;  // at most this many runs in 
 #endif
 constexpr uint32_t RUN_BU = BPE_RUN_BU;  // the block walk: 64-token segments per wave per step
 #ifndef BPE_FR
-#define BPE_FR 4
+#define BPE_FR (BPE_BK > 63 ? 3 : 4)  // (3: the LDS holds the 128-member role tables)
 #endif
 // k_bscan rounds staged in LDS per flush (one block barrier pair per flush;
 // 1 GiB x 8192: 1 -> 75.6 ms, 2 -> 72.5, 4 -> 71.8)
@@ -96,14 +95,14 @@ __device__ inline uint32_t bat_idx(const Eng *E) {
 struct KV {
     unsigned long long v, k;  // packed value (count << 32 | ~bucket), key (a << 32 | b)
 };
-__device__ inline KV kv_empty() { return KV{0ull, ~0ull}; }
-__device__ inline bool kv_ahead(const KV &x, const KV &y) { return x.v > y.v || (x.v == y.v && x.k < y.k); }
-__device__ inline KV kv_shfl(const KV &x, int src) { return KV{__shfl(x.v, src), __shfl(x.k, src)}; }
-__device__ inline KV kv_xor(const KV &x, int m) { return KV{__shfl_xor(x.v, m), __shfl_xor(x.k, m)}; }
+__device__ __attribute__((always_inline)) inline KV kv_empty() { return KV{0ull, ~0ull}; }
+__device__ __attribute__((always_inline)) inline bool kv_ahead(const KV &x, const KV &y) { return x.v > y.v || (x.v == y.v && x.k < y.k); }
+__device__ __attribute__((always_inline)) inline KV kv_shfl(const KV &x, int src) { return KV{__shfl(x.v, src), __shfl(x.k, src)}; }
+__device__ __attribute__((always_inline)) inline KV kv_xor(const KV &x, int m) { return KV{__shfl_xor(x.v, m), __shfl_xor(x.k, m)}; }
 
 // bitonic sort of the wave's 64 entries (one per lane): lane 0 holds the first
 // in argmax order
-__device__ inline KV wave_sort64(KV x) {
+__device__ __attribute__((always_inline)) inline KV wave_sort64(KV x) {
     const uint32_t lane = lane_id();
 #pragma unroll
     for (uint32_t k = 2; k <= 64; k <<= 1) {
@@ -118,7 +117,7 @@ __device__ inline KV wave_sort64(KV x) {
 }
 
 // a bitonic sequence over the 64 lanes, sorted (lane 0 first in argmax order)
-__device__ inline KV wave_merge64(KV x) {
+__device__ __attribute__((always_inline)) inline KV wave_merge64(KV x) {
     const uint32_t lane = lane_id();
 #pragma unroll
     for (uint32_t j = 32; j > 0; j >>= 1) {
@@ -130,13 +129,13 @@ __device__ inline KV wave_merge64(KV x) {
 
 // the top 64 of two sorted lists a, b (one entry per lane): the better of
 // a[i] and b[63 - i] is the top 64 of the union as a bitonic sequence
-__device__ inline KV wave_top(const KV &a, const KV &b) {
+__device__ __attribute__((always_inline)) inline KV wave_top(const KV &a, const KV &b) {
     const KV br = kv_shfl(b, (int)(63 - lane_id()));
     return wave_merge64(kv_ahead(br, a) ? br : a);
 }
 
 // tree of the block's wave lists in part[w] (sorted, TOPK each): part[0] = top TOPK
-__device__ inline void block_list_tree(KV (*part)[TOPK], uint32_t nw) {
+__device__ __attribute__((always_inline)) inline void block_list_tree(KV (*part)[TOPK], uint32_t nw) {
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     for (uint32_t s = 1; s < nw; s <<= 1) {
         if (w % (2 * s) == 0 && w + s < nw) part[w][lane] = wave_top(part[w][lane], part[w + s][lane]);
@@ -148,7 +147,7 @@ __device__ inline void block_list_tree(KV (*part)[TOPK], uint32_t nw) {
 // this block's share of the hot set (counts after the batch applied last,
 // buckets under B_final of its D) as a sorted top-TOPK list in out (LDS)
 // slot0: hot_slot of this thread's first entry, loaded by the caller ahead
-__device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bsz, KV *out, uint32_t slot0) {
+__device__ __attribute__((always_inline)) inline void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bsz, KV *out, uint32_t slot0) {
     __shared__ KV part[16][TOPK];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     KV run = kv_empty();
@@ -185,7 +184,7 @@ __device__ void bat_block_top(const Eng *__restrict__ E, uint32_t n, uint64_t Bs
 constexpr uint32_t BAT_HEAD_WORDS = offsetof(Bat, pv) / 4;
 
 // every level B = B_sz 2^e in [lo, hi] has its bit (e + 5) in mask
-__device__ inline bool tie_levels_ok(uint64_t lo, uint64_t hi, uint64_t Bsz, uint32_t mask) {
+__device__ __attribute__((always_inline)) inline bool tie_levels_ok(uint64_t lo, uint64_t hi, uint64_t Bsz, uint32_t mask) {
     const int zsz = __builtin_ctzll(Bsz);
     for (uint64_t Bx = lo; Bx <= hi; Bx <<= 1) {
         const int lv = __builtin_ctzll(Bx) - zsz + 5;
@@ -202,7 +201,147 @@ struct alignas(16) BatHead {  // the words of Bat up to the partial lists
     uint32_t w[BAT_HEAD_WORDS];
 };
 
-__device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, Bat *__restrict__ Bg, uint32_t nhot,
+// member masks over the batch (bit q = member q; NBK words)
+struct MK {
+    unsigned long long w[NBK];
+};
+__device__ __attribute__((always_inline)) inline MK mk_zero() {
+    MK m;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) m.w[b] = 0;
+    return m;
+}
+// (the word is chosen with selects, never a dynamic register index: scratch)
+__device__ __attribute__((always_inline)) inline void mk_set(MK &m, uint32_t q) {
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) m.w[b] |= (q >> 6) == b ? 1ull << (q & 63) : 0ull;
+}
+__device__ __attribute__((always_inline)) inline bool mk_test(const MK &m, uint32_t q) {
+    bool r = false;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) r |= (q >> 6) == b && ((m.w[b] >> (q & 63)) & 1ull);
+    return r;
+}
+__device__ __attribute__((always_inline)) inline bool mk_any(const MK &m) {
+    unsigned long long x = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) x |= m.w[b];
+    return x != 0;
+}
+__device__ __attribute__((always_inline)) inline MK mk_or(const MK &x, const MK &y) {
+    MK m;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) m.w[b] = x.w[b] | y.w[b];
+    return m;
+}
+// bits [0, q)
+__device__ __attribute__((always_inline)) inline MK mk_below(uint32_t q) {
+    MK m;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) m.w[b] = q >= 64 * (b + 1) ? ~0ull : q <= 64 * b ? 0ull : (1ull << (q - 64 * b)) - 1ull;
+    return m;
+}
+__device__ __attribute__((always_inline)) inline bool mk_meets(const MK &x, const MK &y) {
+    unsigned long long r = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) r |= x.w[b] & y.w[b];
+    return r != 0;
+}
+// lowest set bit, or 64 NBK
+__device__ __attribute__((always_inline)) inline uint32_t mk_first(const MK &m) {
+    uint32_t r = 64 * NBK;
+#pragma unroll
+    for (int b = (int)NBK - 1; b >= 0; b--)
+        if (m.w[b]) r = 64 * (uint32_t)b + (uint32_t)__builtin_ctzll(m.w[b]);
+    return r;
+}
+// a wave ballot per bank: bit q of the result = pred of member q (lane q % 64, bank q / 64)
+template <typename F>
+__device__ __attribute__((always_inline)) inline MK mk_ballot(F &&pred) {
+    MK m;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) m.w[b] = __ballot(pred(b));
+    return m;
+}
+// value v of member q, held by lane q % 64 in bank q / 64 (q wave-uniform)
+template <typename T>
+__device__ __attribute__((always_inline)) inline T bank_shfl(const T (&v)[NBK], uint32_t q) {
+    T r = v[0];
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) {
+        const T x = __shfl(v[b], (int)(q & 63));
+        r = (q >> 6) == b ? x : r;
+    }
+    return r;
+}
+// inclusive prefix sum over the members (bank by bank, lane order)
+template <typename T>
+__device__ __attribute__((always_inline)) inline void bank_scan(T (&v)[NBK]) {
+    const uint32_t lane = lane_id();
+    T carry = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) {
+        T p = v[b];
+        for (int o = 1; o < 64; o <<= 1) {
+            const T y = __shfl_up(p, o);
+            if ((int)lane >= o) p += y;
+        }
+        v[b] = p + carry;
+        carry = __shfl(v[b], 63);
+    }
+}
+// a wave-uniform value, kept in a scalar register (the select's wave 0 holds
+// many: as vector registers they pushed it into scratch)
+__device__ __attribute__((always_inline)) inline uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __attribute__((always_inline)) inline unsigned long long uni(unsigned long long x) {
+    return ((unsigned long long)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
+}
+template <typename T>
+__device__ __attribute__((always_inline)) inline T wave_sum(T x) {
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+// inclusive prefix maximum over the members
+template <typename T>
+__device__ __attribute__((always_inline)) inline void bank_scan_max(T (&v)[NBK]) {
+    const uint32_t lane = lane_id();
+    T carry = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) {
+        T p = v[b];
+        for (int o = 1; o < 64; o <<= 1) {
+            const T y = __shfl_up(p, o);
+            if ((int)lane >= o) p = max(p, y);
+        }
+        v[b] = max(p, carry);
+        carry = __shfl(v[b], 63);
+    }
+}
+// the inclusive prefix v at the member before mine (bank b; member 0: its own)
+template <typename T>
+__device__ __attribute__((always_inline)) inline T bank_prev(const T (&v)[NBK], uint32_t b) {
+    const uint32_t lane = lane_id();
+    T r = __shfl_up(v[b], 1);  // (lane 0: its own)
+#pragma unroll
+    for (uint32_t bb = 0; bb + 1 < NBK; bb++) {
+        const T t = __shfl(v[bb], 63);
+        if (lane == 0 && b == bb + 1) r = t;
+    }
+    return r;
+}
+// value v of member idx (per lane)
+template <typename T>
+__device__ __attribute__((always_inline)) inline T bank_gather(const T (&v)[NBK], uint32_t idx) {
+    T r = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) {
+        const T x = __shfl(v[b], (int)(idx & 63));
+        r = (idx >> 6) == b ? x : r;
+    }
+    return r;
+}
+
+__device__ __attribute__((always_inline)) inline void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, Bat *__restrict__ Bg, uint32_t nhot,
                               uint32_t bi) {
     __shared__ Ctl sc;
     __shared__ BatHead sbh;
@@ -210,9 +349,15 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
     __shared__ uint32_t srank[256];
     __shared__ uint32_t clear_k, nmem, xclr_k, xclr_w;
     __shared__ uint32_t ctl[BK];
+    // the members formed so far, by member index (wave 0 writes and reads them)
+    __shared__ uint32_t fm_u[BK + 1], fm_v[BK + 1], fm_c[BK + 1], fm_tm[BK + 1], fm_nsk[BK + 1];
+    __shared__ unsigned long long fm_span[BK + 1];
+    __shared__ KV hzs[16];  // per wave the horizon of its partial lists
+    __shared__ KV lists[NLIST][TOPK];  // the lists the formation may walk, in order
     constexpr uint32_t CW = sizeof(Ctl) / 4;
-    static_assert(CW <= 1024 && BAT_HEAD_WORDS <= 1024, "staged one word per thread");
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr uint32_t HW = (BAT_HEAD_WORDS + 1023) / 1024;  // head words staged per thread
+    static_assert(CW <= 1024 && HW <= 2, "staged words per thread");
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
     uint32_t *scw = reinterpret_cast<uint32_t *>(&sc);
     uint32_t *sbw = sbh.w;
     const uint32_t *cgw = reinterpret_cast<const uint32_t *>(Cg);
@@ -224,97 +369,115 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
     y.v = aload64(&Bg->pv[(2 * w + 1) * TOPK + lane]);
     y.k = aload64(&Bg->pk[(2 * w + 1) * TOPK + lane]);
     const uint32_t cv = tid < CW ? aload(cgw + tid) : 0u;
-    const uint32_t bv = tid < BAT_HEAD_WORDS ? aload(bgw + tid) : 0u;
+    uint32_t bv[HW];
+#pragma unroll
+    for (uint32_t h = 0; h < HW; h++) bv[h] = tid + 1024 * h < BAT_HEAD_WORDS ? aload(bgw + tid + 1024 * h) : 0u;
     const uint32_t rk = tid < 256 ? E->rank[tid] : 0u;
     part[w][lane] = wave_top(x, y);
     if (tid < CW) scw[tid] = cv;
-    if (tid < BAT_HEAD_WORDS) sbw[tid] = bv;
+#pragma unroll
+    for (uint32_t h = 0; h < HW; h++)
+        if (tid + 1024 * h < BAT_HEAD_WORDS) sbw[tid + 1024 * h] = bv[h];
     if (tid < 256) srank[tid] = rk;
     if (tid == 0) clear_k = nmem = xclr_k = 0;
-    __syncthreads();
-    block_list_tree(part, blockDim.x >> 6);
-    // The list's next TOPK keys (E->list2): the same tree over the partial
-    // lists with the entries the first list took removed (a partial list's
-    // entries in it are a prefix: both are in argmax order).  A FULL partial
-    // list may hold further keys behind its last entry, so the second list is
-    // exact only down to the most advanced such last entry (the horizon) --
-    // with ~500 keys per partial list and ~4 of them in the first 128, it
-    // hardly ever binds.
-    KV e1 = kv_empty(), e2 = kv_empty();
-    uint32_t nl2 = 0;
-    bool trunc2 = false;
-    const KV l1last = part[0][TOPK - 1];
-    if (tid < 64) e1 = part[0][lane];
-    if (E->list2 && l1last.v != 0) {  // (block-uniform)
-        __shared__ KV hzs[16];
-        __syncthreads();  // (every wave has read the first list)
-        auto shift = [&](const KV &z) {
-            const uint32_t n1 = (uint32_t)__popcll(__ballot(z.v != 0 && !kv_ahead(l1last, z)));
-            const uint32_t src = lane + n1;
-            const KV r = kv_shfl(z, (int)(src < 64 ? src : 63));
-            return src < 64 ? r : kv_empty();
-        };
+    {
+        // the horizon: a FULL partial list may hold further keys behind its
+        // last entry, so the lists after the first are exact only down to the
+        // most advanced such last entry (with ~500 keys per partial list and a
+        // few of them in each list, it hardly ever binds)
         const KV xl = kv_shfl(x, 63), yl = kv_shfl(y, 63);
         KV hz = kv_empty();
         if (xl.v != 0) hz = xl;
         if (yl.v != 0 && (hz.v == 0 || kv_ahead(yl, hz))) hz = yl;
-        part[w][lane] = wave_top(shift(x), shift(y));
         if (lane == 0) hzs[w] = hz;
-        __syncthreads();
-        block_list_tree(part, blockDim.x >> 6);
-        if (tid < 64) {
-            e2 = part[0][lane];
-            KV H = kv_empty();
-            for (uint32_t q = 0; q < (blockDim.x >> 6); q++)
-                if (hzs[q].v != 0 && (H.v == 0 || kv_ahead(hzs[q], H))) H = hzs[q];
-            const bool ok = e2.v != 0 && (H.v == 0 || !kv_ahead(H, e2));  // (ahead of or at the horizon)
-            nl2 = (uint32_t)__popcll(__ballot(ok));
-            trunc2 = nl2 == TOPK || nl2 < (uint32_t)__popcll(__ballot(e2.v != 0));
-            if (!ok) e2 = kv_empty();
+    }
+    __syncthreads();
+    block_list_tree(part, nw);
+    // The next lists (E->nlists), when the first one is full: the same tree
+    // over the partial lists with the entries not behind the last list's end
+    // removed (a partial list's entries in the earlier lists are a prefix of
+    // it, both being in argmax order).  Made before the formation, which
+    // walks list p + 1 only once list p is used up.
+    if (tid < 64) lists[0][lane] = part[0][lane];
+    uint32_t nlc = 1;  // lists made
+    if (NLIST > 1 && E->nlists > 1) {
+        for (uint32_t p = 1; p < E->nlists && p < NLIST; p++) {  // (block-uniform)
+            __syncthreads();  // (lists[p - 1] written, part read)
+            const KV prev = lists[p - 1][TOPK - 1];
+            if (prev.v == 0) break;  // (list p - 1 not full: no keys behind it)
+            auto shift = [&](const KV &z) {
+                const uint32_t n1 = (uint32_t)__popcll(__ballot(z.v != 0 && !kv_ahead(prev, z)));
+                const uint32_t src = lane + n1;
+                const KV r = kv_shfl(z, (int)(src < 64 ? src : 63));
+                return src < 64 ? r : kv_empty();
+            };
+            part[w][lane] = wave_top(shift(x), shift(y));
+            __syncthreads();
+            block_list_tree(part, nw);
+            if (tid < 64) lists[p][lane] = part[0][lane];
+            nlc = p + 1;
         }
     }
     ts_mark(E, bi, BT_SEL_LIST, false);
     Bat *B = reinterpret_cast<Bat *>(&sbh);  // (head fields only)
-    // Wave 0 decides, one list entry per lane; every lane reads the staged
-    // words itself (no lane waits on another's LDS store); lane 0 writes the
-    // scalar results, lane q member q's
+    Ctl *C = &sc;
+    // ---- wave 0: the batch applied last, folded; the reference's stop rules
+    // on the argmax.  Every lane reads the staged words itself (no lane waits
+    // on another's LDS store); lane 0 writes the scalar results, lane q member q's
+    bool applied = false;
+    uint32_t jst = 0, kpr = 0, retry = 0, fretry = 0, olda = 0, oldb = 0, oldz0 = 0, oldsum = 0, rescan = 0, ocand = 0,
+             oocc = 0, oldnsk = 0, skg = 0, ske = 0, crate = 0, raerr = 0, nst = 0, md = 0, cnt0 = 0, ties = 0, edge = 0,
+             hotT = 0, stop = STOP_NONE, nl0 = 0;
+    bool stalled = false, skip_now = false, sh = E->sharded != 0;
+    unsigned long long rs = 0, rg = 0, D = 0, n_live = 0, v0 = 0;
+    uint64_t Bsz = 0;
+    const KV e0 = tid < 64 ? lists[0][lane] : kv_empty();  // the first list, one entry per lane
     if (tid < 64) {
-        Ctl *C = &sc;
-        // ---- the batch applied last, folded
-        const bool applied = B->applied != 0;
-        const uint32_t jst = applied ? B->jstar : 0, kpr = applied ? B->k : 0;
+        applied = B->applied != 0;
+        jst = applied ? B->jstar : 0;
+        kpr = applied ? B->k : 0;
         // the last batch failed at member `retry` (or did before a host-side
         // stop: a selection that stops folds the batch but holds its retry for
         // the formation after the host's work -- a byte-pair list rebuild, a
         // hot-set rebuild or table growth leaves the counts as they were)
-        const uint32_t retry = applied ? B->retry : B->rhold;
+        retry = applied ? B->retry : B->rhold;
         // (the formation's view of it: BPE_TEST_LOSE_RETRY drops the cut, so the
         // failing batch is formed again -- what the watchdog below must end)
-        const uint32_t fretry = E->lose_retry ? 0u : retry;
+        fretry = E->lose_retry ? 0u : retry;
         // no-progress watchdog: a batch that applied nothing is re-formed with
         // its verified prefix, whose first member always verifies; STALL_LIMIT
         // such batches in a row mean the formation repeats itself (a lost retry
         // cut, round 5): the run stops with an error instead of looping
-        const uint32_t nst = applied ? (jst ? 0u : Bg->nstall + 1u) : Bg->nstall;
-        const bool stalled = nst >= STALL_LIMIT;
+        nst = applied ? (jst ? 0u : Bg->nstall + 1u) : Bg->nstall;
+        stalled = nst >= STALL_LIMIT;
         // (read before the lanes overwrite the member fields)
-        const uint32_t olda = jst ? B->a[jst - 1] : 0, oldb = jst ? B->b[jst - 1] : 0, oldz0 = B->z0;
-        const uint32_t oldsum = B->sumlen;
-        // candidates scanned for nothing (a re-formed batch's, a dropped
-        // member's): they scan again, so they do not count as stale list entries
-        uint32_t rescan = applied && !retry && lane >= jst && lane < kpr ? B->len[lane] : 0u;
-        // and the applied members' candidates and occurrences from occurrence
-        // lists: a byte-pair list rebuild leaves those lists as they are, so
-        // only byte-pair lists' stale entries count towards one
-        const bool occm = lane < jst && B->mode[lane] != 0;
-        uint32_t ocand = occm ? B->len[lane] : 0u, oocc = occm ? B->R[lane] : 0u;
-        for (int o = 32; o > 0; o >>= 1) {
-            rescan += __shfl_xor(rescan, o);
-            ocand += __shfl_xor(ocand, o);
-            oocc += __shfl_xor(oocc, o);
+        olda = jst ? B->a[jst - 1] : 0;
+        oldb = jst ? B->b[jst - 1] : 0;
+        oldz0 = B->z0;
+        oldsum = B->sumlen;
+        unsigned long long rsl = 0, rgl = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            // candidates scanned for nothing (a re-formed batch's, a dropped
+            // member's): they scan again, so they do not count as stale list entries
+            rescan += applied && !retry && q >= jst && q < kpr ? B->len[q] : 0u;
+            // and the applied members' candidates and occurrences from occurrence
+            // lists: a byte-pair list rebuild leaves those lists as they are, so
+            // only byte-pair lists' stale entries count towards one
+            const bool occm = q < jst && B->mode[q] != 0;
+            ocand += occm ? B->len[q] : 0u;
+            oocc += occm ? B->R[q] : 0u;
+            rsl += q < jst ? B->R[q] : 0ull;                       // this shard's occurrences
+            rgl += q < jst ? (sh ? B->Rg[q] : B->R[q]) : 0ull;     // all shards'
         }
+        rescan = wave_sum(rescan);
+        ocand = wave_sum(ocand);
+        oocc = wave_sum(oocc);
+        rs = wave_sum(rsl);
+        rg = wave_sum(rgl);
         if (applied && retry) rescan = oldsum;
-        const uint32_t oldnsk = Bg->nsk;  // (outside the staged head; the formation below rewrites it)
+        oldnsk = Bg->nsk;  // (outside the staged head; the formation below rewrites it)
         // skipped keys back off where batches holding them keep failing
         // (skewed text: the members past a skipped key rarely verify, and
         // every failure costs a batch): each failure of a batch with skipped
@@ -323,7 +486,8 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         // nothing (4 ... 128).  Isolated failures (uniform corpora) never
         // gate.  A re-formation keeps them (its verified prefix may hold
         // skipped keys).
-        uint32_t skg = B->skgate & 0xFFFFu, ske = B->skgate >> 16;
+        skg = B->skgate & 0xFFFFu;
+        ske = B->skgate >> 16;
         if (applied && oldnsk) {
             if (retry || jst < kpr) {
                 ske = min(ske + 1u, 7u);
@@ -332,33 +496,21 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
                 ske--;
             }
         }
-        const bool skip_now = E->skip_on && (skg == 0 || fretry != 0);
-        const uint32_t crate = Bg->crate;
-        const uint32_t raerr = aload(&Bg->ra_err);  // a token too long for an end code (rewrite blocks)
-        const bool sh = E->sharded != 0;
-        unsigned long long rs = lane < jst ? B->R[lane] : 0ull;   // this shard's occurrences
-        unsigned long long rg = lane < jst ? (sh ? B->Rg[lane] : B->R[lane]) : 0ull;  // all shards'
-        for (int o = 32; o > 0; o >>= 1) {
-            rs += __shfl_xor(rs, o);
-            rg += __shfl_xor(rg, o);
-        }
+        skip_now = E->skip_on && (skg == 0 || fretry != 0);
+        crate = Bg->crate;
+        raerr = aload(&Bg->ra_err);  // a token too long for an end code (rewrite blocks)
         ts_mark(E, bi, BT_F_FOLD, false);
-        const unsigned long long D = C->D + (applied ? B->dD : 0ull);
-        const uint32_t md = C->merges_done + jst;
-        const unsigned long long n_live = C->n_live - rg;
-        // ---- the list, one entry per lane
-        const KV e = e1;  // (part[0] may hold the second list now)
-        const unsigned long long kprev = __shfl(e.k, (int)(lane ? lane - 1 : 0));
-        const uint32_t nl = (uint32_t)__popcll(__ballot(lane < TOPK && e.v != 0));  // non-empty (sorted first)
-        const bool truncated = nl == TOPK;  // more keys may follow the list
-        const unsigned long long v0 = __shfl(e.v, 0), k0 = __shfl(e.k, 0);
-        const uint32_t cnt0 = (uint32_t)(v0 >> 32);
-        const uint32_t ties =
-            (uint32_t)__popcll(__ballot(lane < nl && e.v == v0 && (lane == 0 || e.k != kprev)));
-        uint32_t edge;
+        D = C->D + (applied ? B->dD : 0ull);
+        md = C->merges_done + jst;
+        n_live = C->n_live - rg;
+        const unsigned long long kprev = __shfl(e0.k, (int)(lane ? lane - 1 : 0));
+        nl0 = (uint32_t)__popcll(__ballot(e0.v != 0));  // non-empty (sorted first)
+        v0 = __shfl(e0.v, 0);
+        cnt0 = (uint32_t)(v0 >> 32);
+        ties = (uint32_t)__popcll(__ballot(lane < nl0 && e0.v == v0 && (lane == 0 || e0.k != kprev)));
         const uint64_t Bn = bfinal_nominal(D, &edge);
-        const uint64_t Bsz = edge ? 2 * Bn : Bn;
-        const uint32_t hotT = C->hot_T;
+        Bsz = edge ? 2 * Bn : Bn;
+        hotT = C->hot_T;
         // byte-pair lists gone stale (opt-in, BPE_RELIST): the host rebuilds them
         bool relist_due = false;
         if (E->relist_stale) {
@@ -366,7 +518,6 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
             const uint32_t os = (uint32_t)(C->counters[5] + rs - oocc) - C->relist_o0;
             relist_due = cs > os && cs - os >= E->relist_stale;
         }
-        uint32_t stop = STOP_NONE;
         if (C->err || raerr || stalled) stop = STOP_ERROR;
         else if (!E->fast && n_live < TRACK_LIMIT) stop = STOP_MODE;
         else if (md >= E->mcap) stop = STOP_CAP;
@@ -374,393 +525,453 @@ __device__ void bselect_block(const Eng *__restrict__ E, Ctl *__restrict__ Cg, B
         else if (relist_due) stop = STOP_RELIST;
         else if (v0 == 0 || cnt0 <= 1) stop = STOP_DONE;
         else if (C->nkeys + 4ull * (256ull + md + 2) >= E->hcap / 2) stop = STOP_GROW;
-        // ---- the batch: members from the list in order, skipping the entries
-        // that do not commute with an earlier member, up to the first entry
-        // that qualifies as neither; over the second list too when the first
-        // one is used up (two passes of the same rules)
-        uint32_t k = 0;
-        ts_mark(E, bi, BT_F_PRE, false);
-        if (stop == STOP_NONE) {
-            const int zsz = __builtin_ctzll(Bsz);
-            uint32_t kk = 0, nskt = 0, tpend = BK, endwhy = 8, kend = 64;
-            unsigned long long spanbase = 0;
-            // the members so far, lane q = member q (list order)
-            uint32_t mu = 0, mv = 0, mc = 0, mtmask = 0, mnskb = 0;
-            unsigned long long mspan = 0;
-            bool more = true;
-            uint32_t npass = 0;
+        jst = uni(jst);
+        kpr = uni(kpr);
+        retry = uni(retry);
+        fretry = uni(fretry);
+        olda = uni(olda);
+        oldb = uni(oldb);
+        oldz0 = uni(oldz0);
+        oldsum = uni(oldsum);
+        rescan = uni(rescan);
+        ocand = uni(ocand);
+        oocc = uni(oocc);
+        oldnsk = uni(oldnsk);
+        skg = uni(skg);
+        ske = uni(ske);
+        crate = uni(crate);
+        raerr = uni(raerr);
+        nst = uni(nst);
+        md = uni(md);
+        cnt0 = uni(cnt0);
+        ties = uni(ties);
+        edge = uni(edge);
+        hotT = uni(hotT);
+        stop = uni(stop);
+        nl0 = uni(nl0);
+        rs = uni(rs);
+        rg = uni(rg);
+        D = uni(D);
+        n_live = uni(n_live);
+        v0 = uni(v0);
+        Bsz = uni((unsigned long long)Bsz);
+    }
+    // ---- the batch: members from the lists in order, skipping the entries
+    // that do not commute with an earlier member, up to the first entry that
+    // qualifies as neither; each list after the first once the one before it
+    // is used up (the same rules over the next TOPK keys: the partial lists
+    // with the entries not behind the last list's end removed -- a partial
+    // list's entries in the earlier lists are a prefix of it, both being in
+    // argmax order)
+    uint32_t kk = 0, nskt = 0, tpend = BK, endwhy = 8, kend = 64, npass = 0;
+    unsigned long long spanbase = 0;
+    ts_mark(E, bi, BT_F_PRE, false);
+    if (tid < 64 && stop == STOP_NONE) {
+    KV prev = kv_empty();  // the entry before the list's first (the last list's last)
 #pragma unroll
-            for (uint32_t pass = 0; pass < 2; pass++) {  // (uniform)
-                if (!more) break;
-                more = false;
-                const KV ep = pass ? e2 : e;
-                const uint32_t nlp = pass ? nl2 : nl;
-                const bool trunc = pass ? trunc2 : truncated;
-                const uint32_t u = (uint32_t)(ep.k >> 32), v = (uint32_t)ep.k, c = (uint32_t)(ep.v >> 32);
-                // the entry before me (the first list's last one for the second's first)
-                const unsigned long long vprev0 = __shfl(ep.v, (int)(lane ? lane - 1 : 0));
-                const unsigned long long kprevp = lane ? __shfl(ep.k, (int)(lane - 1)) : (pass ? l1last.k : ep.k);
-                const uint32_t cprev = (uint32_t)((lane ? vprev0 : (pass ? l1last.v : 0ull)) >> 32);
-                const bool first = pass == 0 && lane == 0;  // the argmax itself
-                // ties with the next key keep their pre-batch order when the members
-                // before it cannot move B_final: a member adds or zeroes at most
-                // 2 min(ids, count) + 1 keys (its neighbours' pairs and its own),
-                // where the ids a neighbour can be are the A byte values present and
-                // the merged ids up to this batch's last (not all 256 byte values:
-                // text has ~95, which early in a run is most of the bound)
-                unsigned long long span =
-                    !first && lane < nlp ? min(2ull * ((unsigned long long)E->A + md + BK), 2ull * cprev) + 1 : 0ull;
-                for (int o = 1; o < 64; o <<= 1) {
-                    const unsigned long long y = __shfl_up(span, o);
-                    if ((int)lane >= o) span += y;
-                }
-                span += spanbase;
-                const uint64_t Blo = summary_B(D > span ? D - span : 0), Bhi = summary_B(D + span);
-                const bool stable = Blo == Bsz && Bhi == Bsz;
-                // D only falls by the keys the members zero (their own and a few
-                // neighbour pairs): with a guess of those from the batches so far,
-                // the lower end of the reachable B is usually B_sz; k_bapply counts
-                // the keys really zeroed and checks that guess (verified members)
-                const unsigned long long zg = 16ull + (unsigned long long)B->zrate * (kk + lane);
-                const uint64_t Blo_o = summary_B(D > zg ? D - zg : 0);
-                // and D only rises by the keys they create, fewer than the span
-                // bound allows: a guess from the run's creations so far, checked
-                // by k_bapply against the keys really created (round 5)
-                const unsigned long long cg = E->tie_up ? min(span, 16ull + (unsigned long long)crate * (kk + lane)) : span;
-                const uint64_t Bhi_o = summary_B(D + cg);
-                const uint32_t cnext = __shfl(c, (int)(lane < 63 ? lane + 1 : 63));
-                // otherwise keys of one count keep my order against them under every
-                // B the members before me can reach (bucket = murmur & (B - 1), then
-                // the key): checked against the listed keys of my count after me, as
-                // a mask of the levels B = B_sz 2^e (bit e + 5) where it holds
-                const uint32_t hsh = murmur_pair(u, v);
-                const uint32_t clast = __shfl(c, (int)(nlp ? nlp - 1 : 0));
-                uint32_t tmask = 0xFFu;
-                const bool tie_next = lane < nlp && !(c > (lane + 1 < nlp ? cnext : 0u));
-                const bool check = __ballot(!stable && !first && tie_next) != 0;  // (wave-uniform)
-                if (pass == 0) ts_mark(E, bi, BT_F_CHK, false);
-                if (check) {
-                    // per level B = B_sz 2^(e - 5) (e in [0, 8), where my range
-                    // [Blo, Bhi] reaches it): the smallest (bucket, key) among the
-                    // listed keys of my count after me must be above mine -- a
-                    // segmented suffix minimum over the lanes (equal counts are
-                    // contiguous in the list), ~20 shuffles per level instead of a
-                    // 63-step readlane loop (9 of the formation's ~25 us)
-                    const uint32_t khi = (uint32_t)(ep.k >> 32), klo = (uint32_t)ep.k;
-                    const bool inl = lane < nlp;
-                    const bool has = lane + 1 < nlp && cnext == c;  // a key of my count after me
-#pragma unroll 1
-                    for (uint32_t ee = 0; ee < 8; ee++) {  // (uniform)
-                        const uint64_t Bx = ee >= 5 ? (Bsz << (ee - 5)) : (Bsz >> (5 - ee));
-                        if (Bx == 0 || (Bx << (ee >= 5 ? 0 : 5 - ee)) != (ee >= 5 ? Bx : Bsz)) continue;  // (B_sz < 2^(5 - e))
-                        const bool need = inl && has && Bx >= Blo && Bx <= Bhi;
-                        if (!__ballot(need)) continue;
-                        const uint32_t bk = hsh & (uint32_t)(Bx - 1);
-                        uint32_t m0 = inl ? bk : ~0u, m1 = inl ? khi : ~0u, m2 = inl ? klo : ~0u;
-                        for (uint32_t d = 1; d < 64; d <<= 1) {  // inclusive suffix minimum within my count
-                            const uint32_t o0 = __shfl_down(m0, d), o1 = __shfl_down(m1, d), o2 = __shfl_down(m2, d);
-                            const uint32_t cd = __shfl_down(c, d);
-                            if (lane + d < nlp && cd == c && (o0 < m0 || (o0 == m0 && (o1 < m1 || (o1 == m1 && o2 < m2))))) {
-                                m0 = o0;
-                                m1 = o1;
-                                m2 = o2;
-                            }
-                        }
-                        const uint32_t x0 = __shfl_down(m0, 1), x1 = __shfl_down(m1, 1), x2 = __shfl_down(m2, 1);
-                        const bool ahead = bk < x0 || (bk == x0 && (khi < x1 || (khi == x1 && klo < x2)));
-                        if (need && !ahead) tmask &= ~(1u << ee);
-                    }
-                }
-                if (pass == 0) ts_mark(E, bi, BT_F_TIE, false);
-                // (keys past this list -- the second list's, or unknown -- keep
-                // their order under B_sz only)
-                const bool past = trunc || (pass == 0 && E->list2);
-                if (past && c == clast) tmask &= 1u << 5;
-                const bool tie_rel = !stable && ((past && c == clast) || tie_next);
-                const bool cons_ok = tie_levels_ok(Blo, Bhi, Bsz, tmask);
-                const bool opt_ok = tie_levels_ok(Blo_o, Bhi_o, Bsz, tmask);
-                const uint32_t mi = kk + lane;  // (at least my member index)
-                uint32_t why = 0;               // 0: qualifies
-                if (lane >= nlp) why = 8;       // past the list (reported as "list")
-                else if (!first) {
-                    if (ep.k == kprevp) why = 3;  // the same key listed twice (the one-merge engine's undo): end here
-                    else if (md + mi >= E->mcap || c <= 1 || (hotT > 2 && c < hotT)) why = 1;
-                    else if (tie_rel && !cons_ok && !(opt_ok && E->tie_verify))
-                        why = 4;  // (a tie whose order the batch could change, or one running past the list)
-                    else if (C->nkeys + 4ull * (256ull + md + mi + 2) * (mi + 1) >= E->hcap / 2) why = 6;
-                }
-                // the earlier entries of this list that do not commute with me
-                // (one uses my left id on its right or my right id on its left),
-                // and the earlier passes' members that do not (by member index)
-                unsigned long long cm = 0, cmk = 0;
-#pragma unroll
-                for (uint32_t p = 0; p < BK; p++) {
-                    const uint32_t up = __builtin_amdgcn_readlane((int)u, (int)p), vp = __builtin_amdgcn_readlane((int)v, (int)p);
-                    if (p < lane && (u == vp || v == up)) cm |= 1ull << p;
-                }
-                for (uint32_t q = 0; q < kk; q++) {  // (uniform)
-                    const uint32_t uq = __builtin_amdgcn_readlane((int)mu, (int)q), vq = __builtin_amdgcn_readlane((int)mv, (int)q);
-                    if (u == vq || v == uq) cmk |= 1ull << q;
-                }
-                // Members, entry by entry.  An entry that commutes with every earlier
-                // MEMBER joins (its occurrences are the pre-batch ones).  One that
-                // does not is SKIPPED: the sequential passes lower its count when
-                // those members merge (their occurrences consume its tokens), so
-                // it is not the argmax at its turn provided its lowered count falls
-                // below the next member's -- k_bscan counts the decrements, k_bapply
-                // checks every member against the skipped keys before it.  It
-                // merges in a later batch.  (Ids below DENSE: the scan's LDS
-                // vectors hold the decrements; a tie order of its own is moot.)
-                if (pass == 0) ts_mark(E, bi, BT_F_CM, false);
-                const bool skok = skip_now && u < DENSE && v < DENSE && (why == 0 || why == 4);
-                unsigned long long M = 0, S = 0;
-                kend = 64;
-                {
-                    // The rules above applied entry by entry in list order, computed
-                    // lane-parallel: which entries are members is a greedy
-                    // independent set of the conflict graph in list order (an entry
-                    // joins iff none of the earlier entries it conflicts with did),
-                    // settled in rounds -- an entry is decided once every earlier
-                    // entry it conflicts with is (a few rounds; the 64-step readlane
-                    // loop took 6 us).  The batch then ends at the first entry whose
-                    // end condition holds given the members and skips before it.
-                    const bool myck = cmk != 0;
-                    unsigned long long X = 0;  // entries that conflict with an earlier member
-                    for (;;) {  // (uniform; <= 64 rounds: the first undecided entry is always ready)
-                        const unsigned long long dec = M | X;
-                        if (dec == ~0ull) break;
-                        const bool ready = !((dec >> lane) & 1ull) && (cm & ~dec) == 0;
-                        const bool isx = ready && (myck || (cm & M) != 0);
-                        const unsigned long long nm = __ballot(ready && !isx), nx = __ballot(isx);
-                        M |= nm;
-                        X |= nx;
-                    }
-                    const unsigned long long skm = __ballot(skok), below_l = (1ull << lane) - 1ull;
-                    const unsigned long long Sc = X & skm;  // skipped, unless the skip cap ends the batch first
-                    uint32_t ew = 0;
-                    if ((X >> lane) & 1ull) {
-                        if (!skok || nskt + (uint32_t)__popcll(Sc & below_l) >= BK) ew = 5;
-                    } else if (why) {
-                        ew = why;
-                    } else if (kk + (uint32_t)__popcll(M & below_l) >= BK) {  // (the member cap: reported as "list")
-                        ew = 8;
-                    }
-                    const unsigned long long ends = __ballot(ew != 0);
-                    if (ends) {
-                        kend = (uint32_t)__builtin_ctzll(ends);
-                        endwhy = (uint32_t)__builtin_amdgcn_readlane((int)ew, (int)kend);
-                        M &= (1ull << kend) - 1ull;
-                        S = Sc & ((1ull << kend) - 1ull);
-                    } else {
-                        S = Sc;
-                    }
-                }
-                if (pass == 0) ts_mark(E, bi, BT_F_MEMB, false);
-                if (fretry && fretry < kk + (uint32_t)__popcll(M)) {  // the last batch failed at member `retry` (nothing changed since)
-                    unsigned long long xm = M;
-                    for (uint32_t q = kk; q < fretry; q++) xm &= xm - 1;
-                    kend = (uint32_t)__builtin_ctzll(xm);
-                    M &= (1ull << kend) - 1;
-                    S &= (1ull << kend) - 1;
-                    endwhy = 8;
-                }
-                const uint32_t km = (uint32_t)__popcll(M);
-                const unsigned long long below = (1ull << lane) - 1;
-                const bool isM = (M >> lane) & 1;
-                // skipped keys, in list order: key, count, the members (by index)
-                // that lower it
-                if ((S >> lane) & 1) {
-                    const uint32_t si = nskt + (uint32_t)__popcll(S & below);
-                    unsigned long long cmm = cmk;
-                    for (unsigned long long xq = cm & M; xq; xq &= xq - 1)
-                        cmm |= 1ull << (kk + __popcll(M & ((1ull << __builtin_ctzll(xq)) - 1)));
-                    Bg->sk_a[si] = u;
-                    Bg->sk_b[si] = v;
-                    Bg->sk_c[si] = c;
-                    Bg->sk_cm[si] = cmm;
-                    Bg->sdec[si] = 0;
-                }
-                const bool pend = isM && !first && tie_rel && !cons_ok;  // admitted on the guess: k_bapply verifies
-                const unsigned long long pmk = __ballot(pend);
-                if (tpend == BK && pmk) tpend = kk + (uint32_t)__popcll(M & ((1ull << __builtin_ctzll(pmk)) - 1));
-                // this pass's members into lanes kk..kk+km-1 (forward permute:
-                // a full permutation, the rest into the other lanes in order)
-                const uint32_t j = (uint32_t)__popcll(~M & below);
-                const uint32_t dst = isM ? kk + (uint32_t)__popcll(M & below) : (j < kk ? j : j + km);
-                auto fwd = [&](uint32_t xv) { return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst * 4), (int)xv); };
-                const uint32_t nskb = nskt + (uint32_t)__popcll(S & below);
-                const uint32_t pu = fwd(u), pv = fwd(v), pc = fwd(c), ptm = fwd(tmask), pnb = fwd(nskb);
-                const unsigned long long psp =
-                    ((unsigned long long)fwd((uint32_t)(span >> 32)) << 32) | (unsigned long long)fwd((uint32_t)span);
-                if (lane >= kk && lane < kk + km) {
-                    mu = pu;
-                    mv = pv;
-                    mc = pc;
-                    mtmask = ptm;
-                    mnskb = pnb;
-                    mspan = psp;
-                }
-                spanbase = __shfl(span, 63);
-                kk += km;
-                nskt += (uint32_t)__popcll(S);
-                npass = pass + 1;
-                // the first list used up (every entry a member or skipped): the second
-                more = pass == 0 && kend == 64 && endwhy == 8 && nl == TOPK && nl2 > 0 && kk < BK &&
-                       !(fretry && fretry <= kk);
+    for (uint32_t pass = 0; pass < NLIST; pass++) {  // (wave-uniform)
+        if (pass >= nlc) break;
+        KV ep = lists[pass][lane];
+        uint32_t nlp = nl0;
+        bool trunc = nl0 == TOPK;  // more keys may follow the list
+        if (pass > 0) {
+            KV H = kv_empty();
+            for (uint32_t q = 0; q < nw; q++)
+                if (hzs[q].v != 0 && (H.v == 0 || kv_ahead(hzs[q], H))) H = hzs[q];
+            const bool ok = ep.v != 0 && (H.v == 0 || !kv_ahead(H, ep));  // (ahead of or at the horizon)
+            nlp = (uint32_t)__popcll(__ballot(ok));
+            trunc = nlp == TOPK || nlp < (uint32_t)__popcll(__ballot(ep.v != 0));
+            if (!ok) ep = kv_empty();
+        }
+        {
+            const uint32_t u = (uint32_t)(ep.k >> 32), v = (uint32_t)ep.k, c = (uint32_t)(ep.v >> 32);
+            // the entry before me (the last list's last one for this list's first)
+            const unsigned long long vprev0 = __shfl(ep.v, (int)(lane ? lane - 1 : 0));
+            const unsigned long long kprevp = lane ? __shfl(ep.k, (int)(lane - 1)) : (pass ? prev.k : ep.k);
+            const uint32_t cprev = (uint32_t)((lane ? vprev0 : (pass ? prev.v : 0ull)) >> 32);
+            const bool first = pass == 0 && lane == 0;  // the argmax itself
+            // ties with the next key keep their pre-batch order when the members
+            // before it cannot move B_final: a member adds or zeroes at most
+            // 2 min(ids, count) + 1 keys (its neighbours' pairs and its own),
+            // where the ids a neighbour can be are the A byte values present and
+            // the merged ids up to this batch's last (not all 256 byte values:
+            // text has ~95, which early in a run is most of the bound)
+            unsigned long long span =
+                !first && lane < nlp ? min(2ull * ((unsigned long long)E->A + md + BK), 2ull * cprev) + 1 : 0ull;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned long long yy = __shfl_up(span, o);
+                if ((int)lane >= o) span += yy;
             }
-            k = kk;
-            ts_mark(E, bi, BT_SEL_FORMED, false);
+            span += spanbase;
+            const uint64_t Blo = summary_B(D > span ? D - span : 0), Bhi = summary_B(D + span);
+            const bool stable = Blo == Bsz && Bhi == Bsz;
+            // D only falls by the keys the members zero (their own and a few
+            // neighbour pairs): with a guess of those from the batches so far,
+            // the lower end of the reachable B is usually B_sz; k_bapply counts
+            // the keys really zeroed and checks that guess (verified members)
+            const unsigned long long zg = 16ull + (unsigned long long)B->zrate * (kk + lane);
+            const uint64_t Blo_o = summary_B(D > zg ? D - zg : 0);
+            // and D only rises by the keys they create, fewer than the span
+            // bound allows: a guess from the run's creations so far, checked
+            // by k_bapply against the keys really created (round 5)
+            const unsigned long long cg = E->tie_up ? min(span, 16ull + (unsigned long long)crate * (kk + lane)) : span;
+            const uint64_t Bhi_o = summary_B(D + cg);
+            const uint32_t cnext = __shfl(c, (int)(lane < 63 ? lane + 1 : 63));
+            // otherwise keys of one count keep my order against them under every
+            // B the members before me can reach (bucket = murmur & (B - 1), then
+            // the key): checked against the listed keys of my count after me, as
+            // a mask of the levels B = B_sz 2^e (bit e + 5) where it holds
+            const uint32_t hsh = murmur_pair(u, v);
+            const uint32_t clast = __shfl(c, (int)(nlp ? nlp - 1 : 0));
+            uint32_t tmask = 0xFFu;
+            const bool tie_next = lane < nlp && !(c > (lane + 1 < nlp ? cnext : 0u));
+            const bool check = __ballot(!stable && !first && tie_next) != 0;  // (wave-uniform)
+            if (pass == 0) ts_mark(E, bi, BT_F_CHK, false);
+            if (check) {
+                // per level B = B_sz 2^(e - 5) (e in [0, 8), where my range
+                // [Blo, Bhi] reaches it): the smallest (bucket, key) among the
+                // listed keys of my count after me must be above mine -- a
+                // segmented suffix minimum over the lanes (equal counts are
+                // contiguous in the list), ~20 shuffles per level instead of a
+                // 63-step readlane loop
+                const uint32_t khi = (uint32_t)(ep.k >> 32), klo = (uint32_t)ep.k;
+                const bool inl = lane < nlp;
+                const bool has = lane + 1 < nlp && cnext == c;  // a key of my count after me
+#pragma unroll 1
+                for (uint32_t ee = 0; ee < 8; ee++) {  // (uniform)
+                    const uint64_t Bx = ee >= 5 ? (Bsz << (ee - 5)) : (Bsz >> (5 - ee));
+                    if (Bx == 0 || (Bx << (ee >= 5 ? 0 : 5 - ee)) != (ee >= 5 ? Bx : Bsz)) continue;  // (B_sz < 2^(5 - e))
+                    const bool need = inl && has && Bx >= Blo && Bx <= Bhi;
+                    if (!__ballot(need)) continue;
+                    const uint32_t bk = hsh & (uint32_t)(Bx - 1);
+                    uint32_t m0 = inl ? bk : ~0u, m1 = inl ? khi : ~0u, m2 = inl ? klo : ~0u;
+                    for (uint32_t d = 1; d < 64; d <<= 1) {  // inclusive suffix minimum within my count
+                        const uint32_t o0 = __shfl_down(m0, d), o1 = __shfl_down(m1, d), o2 = __shfl_down(m2, d);
+                        const uint32_t cd = __shfl_down(c, d);
+                        if (lane + d < nlp && cd == c && (o0 < m0 || (o0 == m0 && (o1 < m1 || (o1 == m1 && o2 < m2))))) {
+                            m0 = o0;
+                            m1 = o1;
+                            m2 = o2;
+                        }
+                    }
+                    const uint32_t x0 = __shfl_down(m0, 1), x1 = __shfl_down(m1, 1), x2 = __shfl_down(m2, 1);
+                    const bool ahead = bk < x0 || (bk == x0 && (khi < x1 || (khi == x1 && klo < x2)));
+                    if (need && !ahead) tmask &= ~(1u << ee);
+                }
+            }
+            if (pass == 0) ts_mark(E, bi, BT_F_TIE, false);
+            // (keys past this list -- the next list's, or unknown -- keep
+            // their order under B_sz only)
+            if (trunc && c == clast) tmask &= 1u << 5;
+            const bool tie_rel = !stable && ((trunc && c == clast) || tie_next);
+            const bool cons_ok = tie_levels_ok(Blo, Bhi, Bsz, tmask);
+            const bool opt_ok = tie_levels_ok(Blo_o, Bhi_o, Bsz, tmask);
+            const uint32_t mi = kk + lane;  // (at least my member index)
+            uint32_t why = 0;               // 0: qualifies
+            if (lane >= nlp) why = 8;       // past the list (reported as "list")
+            else if (!first) {
+                if (ep.k == kprevp) why = 3;  // the same key listed twice (the one-merge engine's undo): end here
+                else if (md + mi >= E->mcap || c <= 1 || (hotT > 2 && c < hotT)) why = 1;
+                else if (tie_rel && !cons_ok && !(opt_ok && E->tie_verify))
+                    why = 4;  // (a tie whose order the batch could change, or one running past the list)
+                else if (C->nkeys + 4ull * (256ull + md + mi + 2) * (mi + 1) >= E->hcap / 2) why = 6;
+            }
+            // the earlier entries of this list that do not commute with me
+            // (one uses my left id on its right or my right id on its left),
+            // and the earlier lists' members that do not (by member index)
+            unsigned long long cm = 0;
+#pragma unroll 8
+            for (uint32_t p = 0; p < TOPK - 1; p++) {
+                const uint32_t up = __builtin_amdgcn_readlane((int)u, (int)p), vp = __builtin_amdgcn_readlane((int)v, (int)p);
+                if (p < lane && (u == vp || v == up)) cm |= 1ull << p;
+            }
+            MK cmk = mk_zero();
+#pragma unroll 1
+            for (uint32_t q = 0; q < kk; q++) {  // (uniform; LDS broadcast reads)
+                const uint32_t uq = fm_u[q], vq = fm_v[q];
+                if (u == vq || v == uq) mk_set(cmk, q);
+            }
+            // Members, entry by entry.  An entry that commutes with every earlier
+            // MEMBER joins (its occurrences are the pre-batch ones).  One that
+            // does not is SKIPPED: the sequential passes lower its count when
+            // those members merge (their occurrences consume its tokens), so
+            // it is not the argmax at its turn provided its lowered count falls
+            // below the next member's -- k_bscan counts the decrements, k_bapply
+            // checks every member against the skipped keys before it.  It
+            // merges in a later batch.  (Ids below DENSE: the scan's LDS
+            // vectors hold the decrements; a tie order of its own is moot.)
+            if (pass == 0) ts_mark(E, bi, BT_F_CM, false);
+            const bool skok = skip_now && u < DENSE && v < DENSE && (why == 0 || why == 4);
+            unsigned long long M = 0, S = 0;
+            kend = 64;
+            {
+                // The rules above applied entry by entry in list order, computed
+                // lane-parallel: which entries are members is a greedy
+                // independent set of the conflict graph in list order (an entry
+                // joins iff none of the earlier entries it conflicts with did),
+                // settled in rounds -- an entry is decided once every earlier
+                // entry it conflicts with is.  The batch then ends at the first
+                // entry whose end condition holds given the members and skips
+                // before it.
+                const bool myck = mk_any(cmk);
+                unsigned long long X = 0;  // entries that conflict with an earlier member
+                for (;;) {  // (uniform; <= 64 rounds: the first undecided entry is always ready)
+                    const unsigned long long dec = M | X;
+                    if (dec == ~0ull) break;
+                    const bool ready = !((dec >> lane) & 1ull) && (cm & ~dec) == 0;
+                    const bool isx = ready && (myck || (cm & M) != 0);
+                    const unsigned long long nm = __ballot(ready && !isx), nx = __ballot(isx);
+                    M |= nm;
+                    X |= nx;
+                }
+                const unsigned long long skm = __ballot(skok), below_l = (1ull << lane) - 1ull;
+                const unsigned long long Sc = X & skm;  // skipped, unless the skip cap ends the batch first
+                uint32_t ew = 0;
+                if ((X >> lane) & 1ull) {
+                    if (!skok || nskt + (uint32_t)__popcll(Sc & below_l) >= SKMAX) ew = 5;
+                } else if (why) {
+                    ew = why;
+                } else if (kk + (uint32_t)__popcll(M & below_l) >= BK) {  // (the member cap: reported as "list")
+                    ew = 8;
+                }
+                const unsigned long long ends = __ballot(ew != 0);
+                if (ends) {
+                    kend = (uint32_t)__builtin_ctzll(ends);
+                    endwhy = (uint32_t)__builtin_amdgcn_readlane((int)ew, (int)kend);
+                    M &= (1ull << kend) - 1ull;
+                    S = Sc & ((1ull << kend) - 1ull);
+                } else {
+                    S = Sc;
+                }
+            }
+            if (pass == 0) ts_mark(E, bi, BT_F_MEMB, false);
+            if (fretry && fretry < kk + (uint32_t)__popcll(M)) {  // the last batch failed at member `retry` (nothing changed since)
+                unsigned long long xm = M;
+                for (uint32_t q = kk; q < fretry; q++) xm &= xm - 1;
+                kend = (uint32_t)__builtin_ctzll(xm);
+                M &= (1ull << kend) - 1;
+                S &= (1ull << kend) - 1;
+                endwhy = 8;
+            }
+            const uint32_t km = (uint32_t)__popcll(M);
+            const unsigned long long below = (1ull << lane) - 1;
+            const bool isM = (M >> lane) & 1;
+            // skipped keys, in list order: key, count, the members (by index)
+            // that lower it
+            if ((S >> lane) & 1) {
+                const uint32_t si = nskt + (uint32_t)__popcll(S & below);
+                MK cmm = cmk;
+                for (unsigned long long xq = cm & M; xq; xq &= xq - 1)
+                    mk_set(cmm, kk + (uint32_t)__popcll(M & ((1ull << __builtin_ctzll(xq)) - 1)));
+                Bg->sk_a[si] = u;
+                Bg->sk_b[si] = v;
+                Bg->sk_c[si] = c;
+#pragma unroll
+                for (uint32_t b = 0; b < NBK; b++) Bg->sk_cm[si][b] = cmm.w[b];
+                Bg->sdec[si] = 0;
+            }
+            const bool pend = isM && !first && tie_rel && !cons_ok;  // admitted on the guess: k_bapply verifies
+            const unsigned long long pmk = __ballot(pend);
+            if (tpend == BK && pmk) tpend = kk + (uint32_t)__popcll(M & ((1ull << __builtin_ctzll(pmk)) - 1));
+            // this list's members after the earlier ones (member index order)
+            if (isM) {
+                const uint32_t dst = kk + (uint32_t)__popcll(M & below);
+                fm_u[dst] = u;
+                fm_v[dst] = v;
+                fm_c[dst] = c;
+                fm_tm[dst] = tmask;
+                fm_nsk[dst] = nskt + (uint32_t)__popcll(S & below);
+                fm_span[dst] = span;
+            }
+            spanbase = uni((unsigned long long)__shfl(span, 63));
+            kk = uni(kk + km);
+            nskt = uni(nskt + (uint32_t)__popcll(S));
+            tpend = uni(tpend);
+            kend = uni(kend);
+            endwhy = uni(endwhy);
+            npass = pass + 1;
+            // the list used up (every entry a member or skipped): the next
+            const bool more = pass + 1 < nlc && kend == 64 && endwhy == 8 && nlp == TOPK && kk < BK &&
+                              !(fretry && fretry <= kk);
+            prev = kv_shfl(ep, 63);  // (nlp == TOPK when it matters)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the member rows before the next pass reads them)
+            __builtin_amdgcn_wave_barrier();
+            if (!more) break;
+        }
+    }
+    }
+    uint32_t k = kk;
+    if (tid < 64 && stop == STOP_NONE) {
+        ts_mark(E, bi, BT_SEL_FORMED, false);
 #if BPE_FORM_PRINT  // (a build option: the printf costs k_bsel 180 B of scratch per lane)
-            if (E->dbg_form && md + 1 >= E->dbg_form && lane == 0)  // (diagnostics: where the formation ended; from merge BPE_DEBUG_FORM - 1)
-                printf("form shard %u md %u passes %u k %u end %u why %u skipped %u D %llu B %llu pend %u zrate %u\n", E->shard,
-                       md, npass, kk, kend, endwhy, nskt, D, (unsigned long long)Bsz, tpend, B->zrate);
+        if (E->dbg_form && md + 1 >= E->dbg_form && lane == 0)  // (diagnostics: where the formation ended; from merge BPE_DEBUG_FORM - 1)
+            printf("form shard %u md %u passes %u k %u end %u why %u skipped %u D %llu B %llu pend %u zrate %u\n", E->shard,
+                   md, npass, kk, kend, endwhy, nskt, D, (unsigned long long)Bsz, tpend, B->zrate);
 #endif
-            // candidate lists and token lengths, one lane per member
-            uint32_t mode = 1, off = 0, len = 0, tl = 0;
-            if (lane < k) {
-                cand_of(E, mu, mv, true, srank, E->poff, &mode, &off, &len);
+        // candidate lists and token lengths, lane q % 64 of bank q / 64 = member q
+        uint32_t mode[NBK], off[NBK], len[NBK], tl[NBK], slot[NBK], slot_k[NBK], nb[NBK], bpre[NBK];
+        unsigned long long pre[NBK];
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            mode[b] = 1;
+            off[b] = len[b] = tl[b] = 0;
+            if (q < k) {
+                const uint32_t mu = fm_u[q], mv = fm_v[q];
+                cand_of(E, mu, mv, true, srank, E->poff, &mode[b], &off[b], &len[b]);
                 const uint32_t tlu = E->tlen[mu], tlv = E->tlen[mv];
-                tl = tlu + tlv;
-                Bg->mla[lane] = tlu;
-                Bg->mlb[lane] = tlv;
-                Bg->nskb[lane] = (uint8_t)mnskb;
-                Bg->cnew[lane] = 0;
-                Bg->adj[lane] = 0;
+                tl[b] = tlu + tlv;
+                Bg->mla[q] = tlu;
+                Bg->mlb[q] = tlv;
+                Bg->nskb[q] = (uint8_t)fm_nsk[q];
+                Bg->cnew[q] = 0;
+#pragma unroll
+                for (uint32_t bb = 0; bb < NBK; bb++) Bg->adj[q][bb] = 0;
             }
             // the members' candidates fit the occurrence staging (ids_out, n0
             // positions; sharded: + one slot per member for the occurrence
             // across my right edge, which no candidate list holds)
-            const uint32_t slot = len + (sh && lane < k ? 1u : 0u);
-            unsigned long long pre = slot;  // inclusive prefix
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned long long y = __shfl_up(pre, o);
-                if ((int)lane >= o) pre += y;
-            }
-            const unsigned long long over = __ballot(lane > 0 && lane < k && pre > B->stage_cap);
-            uint32_t why_end = endwhy == 8 ? 0 : endwhy;
-            // sharded: every shard must form the same batch, so a shard whose
-            // staging overflows scans nothing from that member on and flags it
-            // in the exchange; the verification then drops the batch there
-            const uint32_t ovm = over ? (uint32_t)__ffsll(over) - 1 : BK;
-            if (over && !sh) {
-                k = ovm;
-                why_end = 7;
-            }
-            uint32_t slot_k = slot;
-            if (sh && lane >= ovm) len = slot_k = 0;
-            if (sh && ovm < k) {  // (members from ovm on scan nothing here)
-                const unsigned long long pcut = __shfl(pre, (int)ovm - 1);
-                if (lane >= ovm) pre = pcut;
-            }
-            const unsigned long long stage_end = __shfl(pre, (int)(k - 1));
-            unsigned long long sumlen = lane < k ? len : 0u;  // candidates
-            for (int o = 32; o > 0; o >>= 1) sumlen += __shfl_xor(sumlen, o);
-            // scan blocks in proportion to the candidate lists (>= 1 each), the
-            // rest to the largest member
-            const uint32_t nb = lane < k ? 1 + (uint32_t)(sumlen ? (uint64_t)(BSB - k) * len / sumlen : 0) : 0;
-            uint32_t bpre = nb;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(bpre, o);
-                if ((int)lane >= o) bpre += y;
-            }
-            const uint32_t used = __shfl(bpre, (int)(k - 1));
-            unsigned long long big = lane < k ? ((unsigned long long)len << 8) | (255u - lane) : 0ull;
-            for (int o = 32; o > 0; o >>= 1) big = max(big, (unsigned long long)__shfl_xor(big, o));
-            const uint32_t bigm = 255u - (uint32_t)(big & 255u);
-            const uint32_t extra = BSB - used;
-            if (lane < k) {
-                B->a[lane] = mu;
-                B->b[lane] = mv;
-                B->cnt[lane] = mc;
-                B->mode[lane] = mode;
-                B->off[lane] = off;
-                B->len[lane] = len;
-                B->sbase[lane] = (uint32_t)(pre - slot_k);
-                B->R[lane] = 0;
-                B->bound[lane] = 0;
-                B->blk0[lane] = bpre - nb + (lane > bigm ? extra : 0);
-                B->tmask[lane] = (uint8_t)mtmask;
-                B->tspan[lane] = (uint32_t)min(mspan, 0xFFFFFFFFull);
-                ctl[lane] = tl;
-            }
-            // the skipped keys a member must beat: those before the last member
-            const uint32_t nsk = k ? (uint32_t)__builtin_amdgcn_readlane((int)mnskb, (int)(k - 1)) : 0u;
-            if (lane == 0) {
-                B->sbase[k] = (uint32_t)stage_end;
-                B->blk0[k] = BSB;
-                B->sumlen = (uint32_t)sumlen;
-                B->over = ovm < k ? ovm : BK;
-                B->tpend = tpend < k ? tpend : BK;
-                Bg->nsk = nsk;
-                B->ztot = 0;
-                B->tbar = 0;
-                B->tlog_n = 0;
-                B->why[why_end]++;
-                if (ties > 1) C->counters[2]++;
-            }
-            ts_mark(E, bi, BT_SEL_CAND, false);
+            slot[b] = len[b] + (sh && q < k ? 1u : 0u);
+            pre[b] = slot[b];
         }
+        bank_scan(pre);  // inclusive prefix
+        const MK over = mk_ballot([&](uint32_t b) {
+            const uint32_t q = 64 * b + lane;
+            return q > 0 && q < k && pre[b] > B->stage_cap;
+        });
+        uint32_t why_end = endwhy == 8 ? 0 : endwhy;
+        // sharded: every shard must form the same batch, so a shard whose
+        // staging overflows scans nothing from that member on and flags it
+        // in the exchange; the verification then drops the batch there
+        const uint32_t of = mk_first(over), ovm = of < k ? of : BK;
+        if (ovm < BK && !sh) {
+            k = ovm;
+            why_end = 7;
+        }
+        const unsigned long long pcut = sh && ovm < k ? bank_shfl(pre, ovm - 1) : 0ull;
+        unsigned long long sumlen = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            slot_k[b] = slot[b];
+            if (sh && q >= ovm) len[b] = slot_k[b] = 0;
+            if (sh && ovm < k && q >= ovm) pre[b] = pcut;  // (members from ovm on scan nothing here)
+            sumlen += q < k ? len[b] : 0u;  // candidates
+        }
+        const unsigned long long stage_end = bank_shfl(pre, k - 1);
+        sumlen = wave_sum(sumlen);
+        // scan blocks in proportion to the candidate lists (>= 1 each), the
+        // rest to the largest member
+        unsigned long long big = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            nb[b] = q < k ? 1 + (uint32_t)(sumlen ? (uint64_t)(BSB - k) * len[b] / sumlen : 0) : 0;
+            bpre[b] = nb[b];
+            if (q < k) big = max(big, ((unsigned long long)len[b] << 8) | (255u - q));
+        }
+        bank_scan(bpre);
+        for (int o = 32; o > 0; o >>= 1) big = max(big, (unsigned long long)__shfl_xor(big, o));
+        const uint32_t used = bank_shfl(bpre, k - 1);
+        const uint32_t bigm = 255u - (uint32_t)(big & 255u);
+        const uint32_t extra = BSB - used;
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            if (q < k) {
+                B->a[q] = fm_u[q];
+                B->b[q] = fm_v[q];
+                B->cnt[q] = fm_c[q];
+                B->mode[q] = mode[b];
+                B->off[q] = off[b];
+                B->len[q] = len[b];
+                B->sbase[q] = (uint32_t)(pre[b] - slot_k[b]);
+                B->R[q] = 0;
+                B->bound[q] = 0;
+                B->blk0[q] = bpre[b] - nb[b] + (q > bigm ? extra : 0);
+                B->tmask[q] = (uint8_t)fm_tm[q];
+                B->tspan[q] = (uint32_t)min(fm_span[q], 0xFFFFFFFFull);
+                ctl[q] = tl[b];
+            }
+        }
+        // the skipped keys a member must beat: those before the last member
+        const uint32_t nsk = k ? fm_nsk[k - 1] : 0u;
         if (lane == 0) {
-            if (B->sc_out && B->ap_out) {  // spans of the batch just scanned and applied
-                B->sc_ticks += B->sc_out - ~B->sc_in;
-                B->ap_ticks += B->ap_out - ~B->ap_in;
-                B->nspan++;
-            }
-            B->sc_in = B->sc_out = B->ap_in = B->ap_out = 0;
-            B->rhold = stop != STOP_NONE ? retry : 0u;
-            Bg->nstall = nst;
-            if (stalled && !C->err) C->err = 10;
-            B->skgate = (stop == STOP_NONE && !retry && skg ? skg - 1u : skg) | (ske << 16);
-            if (applied) {
-                // the formation's guess of the keys a member zeroes: twice the
-                // run's average so far, + 2
-                B->zrate = (uint32_t)min(2ull * B->nzero / (md ? md : 1u) + 2ull, 1ull << 20);
-                Bg->crate = (uint32_t)min(2ull * Bg->ncre / (md ? md : 1u) + 16ull, 1ull << 20);
-                C->merges_done = md;
-                C->occ_top += (uint32_t)rs;
-                C->n_live = n_live;
-                C->D = D;
-                C->counters[0] += jst;
-                C->counters[4] += oldsum;
-                C->relist_c0 += rescan + ocand;
-                C->relist_o0 += oocc;
-                C->counters[5] += rs;
-                if (jst) {
-                    C->a = olda;
-                    C->b = oldb;
-                    C->z = oldz0 + jst - 1;
-                }
-                if (retry) {
-                    B->nretry++;
-                    B->ndrop += kpr - retry;
-                } else {
-                    B->nbatch++;
-                    B->ndrop += kpr - jst;  // (a verified prefix applied alone)
-                    Bg->nskip += oldnsk;
-                }
-                B->retry = 0;
-                B->applied = 0;
-                B->dD = 0;
-            }
-            clear_k = kpr;
-            xclr_k = sh && applied ? kpr : 0u;
-            xclr_w = oldz0 + kpr;
-            C->hot_scanned += nhot;
-            C->stop_z = C->z;
-            C->B = Bsz;
-            C->full = 0;
-            C->W = v0;
-            C->edge = edge;
-            C->ties = ties;
-            C->stop = stop;
-            if (raerr && !C->err) C->err = raerr;
-            B->ticket = 0;
-            B->k = k;
-            B->z0 = 256 + md;
-            nmem = k;
+            B->sbase[k] = (uint32_t)stage_end;
+            B->blk0[k] = BSB;
+            B->sumlen = (uint32_t)sumlen;
+            B->over = ovm < k ? ovm : BK;
+            B->tpend = tpend < k ? tpend : BK;
+            Bg->nsk = nsk;
+            B->ztot = 0;
+            B->tbar = 0;
+            B->tlog_n = 0;
+            B->why[why_end]++;
+            if (ties > 1) C->counters[2]++;
         }
-        ts_mark(E, bi, BT_SEL_FOLD, false);
+        ts_mark(E, bi, BT_SEL_CAND, false);
     }
+    if (tid < 64 && stop != STOP_NONE) k = 0;
+    if (tid == 0) {
+        if (B->sc_out && B->ap_out) {  // spans of the batch just scanned and applied
+            B->sc_ticks += B->sc_out - ~B->sc_in;
+            B->ap_ticks += B->ap_out - ~B->ap_in;
+            B->nspan++;
+        }
+        B->sc_in = B->sc_out = B->ap_in = B->ap_out = 0;
+        B->rhold = stop != STOP_NONE ? retry : 0u;
+        Bg->nstall = nst;
+        if (stalled && !C->err) C->err = 10;
+        B->skgate = (stop == STOP_NONE && !retry && skg ? skg - 1u : skg) | (ske << 16);
+        if (applied) {
+            // the formation's guess of the keys a member zeroes: twice the
+            // run's average so far, + 2
+            B->zrate = (uint32_t)min(2ull * B->nzero / (md ? md : 1u) + 2ull, 1ull << 20);
+            Bg->crate = (uint32_t)min(2ull * Bg->ncre / (md ? md : 1u) + 16ull, 1ull << 20);
+            C->merges_done = md;
+            C->occ_top += (uint32_t)rs;
+            C->n_live = n_live;
+            C->D = D;
+            C->counters[0] += jst;
+            C->counters[4] += oldsum;
+            C->relist_c0 += rescan + ocand;
+            C->relist_o0 += oocc;
+            C->counters[5] += rs;
+            if (jst) {
+                C->a = olda;
+                C->b = oldb;
+                C->z = oldz0 + jst - 1;
+            }
+            if (retry) {
+                B->nretry++;
+                B->ndrop += kpr - retry;
+            } else {
+                B->nbatch++;
+                B->ndrop += kpr - jst;  // (a verified prefix applied alone)
+                Bg->nskip += oldnsk;
+            }
+            B->retry = 0;
+            B->applied = 0;
+            B->dD = 0;
+        }
+        clear_k = kpr;
+        xclr_k = sh && applied ? kpr : 0u;
+        xclr_w = oldz0 + kpr;
+        C->hot_scanned += nhot;
+        C->stop_z = C->z;
+        C->B = Bsz;
+        C->full = 0;
+        C->W = v0;
+        C->edge = edge;
+        C->ties = ties;
+        C->stop = stop;
+        if (raerr && !C->err) C->err = raerr;
+        B->ticket = 0;
+        B->k = k;
+        B->z0 = 256 + md;
+        nmem = k;
+    }
+    ts_mark(E, bi, BT_SEL_FOLD, false);
     __syncthreads();
     if (tid < nmem) E->tlen[256 + sc.merges_done + tid] = ctl[tid];
     // the select's words of the control block; of the tail (which sharded
@@ -831,34 +1042,45 @@ __device__ inline void rewrite_occ(const Eng *__restrict__ E, Ctl *__restrict__ 
     }
 }
 
-__device__ void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat *__restrict__ B) {
+__device__ __attribute__((always_inline)) inline void bat_rewrite(const Eng *__restrict__ E, Ctl *__restrict__ C, Bat *__restrict__ B) {
     __shared__ uint32_t sz[BK], sla[BK], slb[BK], sR[BK], slo[BK], ssb[BK], spre[BK + 1], ablk[BK + 1];
     __shared__ uint32_t sk, stop_, am, last;
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t nA = gridDim.x - BRB, bid = blockIdx.x - BRB;
-    if (tid < 64) {
+    if (tid < 64) {  // lane q % 64 of bank q / 64: member q
         const uint32_t k = aload(&B->ra_k);
-        const bool in = lane < k;
-        const uint32_t R = in ? B->ra_R[lane] : 0u;
-        const uint32_t lo = in ? B->ra_lo[lane] : 0u;  // (k_bapply rewrote [0, lo))
-        unsigned long long tot = R - lo;
-        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
-        // blocks in proportion to the occurrences left (>= 1 per member)
-        const uint32_t nb = in ? 1 + (uint32_t)(tot ? (uint64_t)(nA - k) * (R - lo) / tot : 0) : 0;
-        uint32_t nbp = nb;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(nbp, o);
-            if ((int)lane >= o) nbp += y;
+        uint32_t R[NBK], lo[NBK], nb[NBK], nbp[NBK];
+        unsigned long long tot = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            const bool in = q < k;
+            R[b] = in ? B->ra_R[q] : 0u;
+            lo[b] = in ? B->ra_lo[q] : 0u;  // (k_bapply rewrote [0, lo))
+            tot += R[b] - lo[b];
         }
-        if (in) {
-            sz[lane] = B->ra_z[lane];
-            sla[lane] = B->ra_la[lane];
-            slb[lane] = B->ra_lb[lane];
-            sR[lane] = R;
-            slo[lane] = lo;
-            ssb[lane] = B->ra_sbase[lane];
-            spre[lane] = B->ra_pre[lane];
-            ablk[lane] = nbp - nb;
+        tot = wave_sum(tot);
+        // blocks in proportion to the occurrences left (>= 1 per member)
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            nb[b] = q < k ? 1 + (uint32_t)(tot ? (uint64_t)(nA - k) * (R[b] - lo[b]) / tot : 0) : 0;
+            nbp[b] = nb[b];
+        }
+        bank_scan(nbp);
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            if (q < k) {
+                sz[q] = B->ra_z[q];
+                sla[q] = B->ra_la[q];
+                slb[q] = B->ra_lb[q];
+                sR[q] = R[b];
+                slo[q] = lo[b];
+                ssb[q] = B->ra_sbase[q];
+                spre[q] = B->ra_pre[q];
+                ablk[q] = nbp[b] - nb[b];
+            }
         }
         if (lane == 0) {
             sk = k;
@@ -973,30 +1195,58 @@ __global__ __launch_bounds__(1024) void k_bsel(const Eng *__restrict__ E, Ctl *_
 }
 
 // ----------------------------------------------------------------- k_bscan
-constexpr uint32_t RH = 256;  // LDS role table: member ids -> (left-member mask, right-member mask)
-__device__ inline uint32_t rh_hash(uint32_t id) { return (id * 2654435761u) >> 24; }
+constexpr uint32_t RH = 512;  // LDS id table: the members' ids (at most 2 BK)
+constexpr uint32_t RP = 256;  // LDS pair table: the members' keys (BK)
+__device__ inline uint32_t rh_hash(uint32_t id) { return (id * 2654435761u) >> 23; }
+__device__ inline uint32_t rp_hash(uint32_t a, uint32_t b) { return (a * 2654435761u ^ b * 0x85ebca6bu) >> 24; }
+static_assert(RH == 512 && RP == 256, "hash widths");
 
+// The members' roles for the scan's neighbour tests: per id, its token length
+// when it is some member's a and a flag when it is some member's b (most
+// neighbours are neither: one LDS probe settles them); per member key (a, b),
+// the member.  Keys never repeat within a batch, so a pair names at most one
+// member (the masks of round 5 held 64 members at most).
 struct RoleTab {
     uint32_t id[RH];
-    unsigned long long lm[RH], rm[RH];
-    __device__ inline void put(uint32_t x, bool right, uint32_t m) {
+    uint32_t fl[RH];            // token length of the id if it is an a (every such member: the same) | 1 << 31 if a b
+    unsigned long long pk[RP];  // (a << 32 | b) + 1, 0 = empty
+    uint8_t pm[RP];             // its member
+    __device__ inline void put_id(uint32_t x, uint32_t f) {
         uint32_t s = rh_hash(x);
         for (;;) {
             const uint32_t prev = atomicCAS(&id[s], HOLE, x);
             if (prev == HOLE || prev == x) {
-                atomicOr(right ? &rm[s] : &lm[s], 1ull << m);
+                atomicOr(&fl[s], f);
                 return;
             }
             s = (s + 1) & (RH - 1);
         }
     }
-    __device__ inline void get(uint32_t x, unsigned long long *l, unsigned long long *r) const {
+    __device__ inline void put(uint32_t a, uint32_t b, uint32_t la, uint32_t m) {
+        put_id(a, la);
+        put_id(b, 1u << 31);
+        const unsigned long long key = (((unsigned long long)a << 32) | b) + 1ull;
+        uint32_t s = rp_hash(a, b);
+        while (atomicCAS(&pk[s], 0ull, key) != 0ull) s = (s + 1) & (RP - 1);
+        pm[s] = (uint8_t)m;
+    }
+    __device__ inline uint32_t get(uint32_t x) const {
         uint32_t s = rh_hash(x);
-        for (;;) {  // at most 2 BK < RH / 2 ids
+        for (;;) {  // (at most 2 BK < RH / 2 ids)
             const uint32_t v = id[s];
-            if (v == x) { *l = lm[s]; *r = rm[s]; return; }
-            if (v == HOLE) { *l = *r = 0; return; }
+            if (v == x) return fl[s];
+            if (v == HOLE) return 0;
             s = (s + 1) & (RH - 1);
+        }
+    }
+    __device__ inline uint32_t member(uint32_t a, uint32_t b) const {  // the member (a, b), or BK
+        const unsigned long long key = (((unsigned long long)a << 32) | b) + 1ull;
+        uint32_t s = rp_hash(a, b);
+        for (;;) {
+            const unsigned long long v = pk[s];
+            if (v == key) return pm[s];
+            if (v == 0ull) return BK;
+            s = (s + 1) & (RP - 1);
         }
     }
 };
@@ -1052,47 +1302,35 @@ __device__ inline uint32_t tok_at_b(const uint32_t *__restrict__ tok, const BHal
 // (bpe.c:760-772) makes p the second token of a pair iff the run is even
 // (sharded: the run may continue into the shards on my left, H.hlr).
 template <bool SH>
-__device__ inline uint32_t cover_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const uint32_t *sa,
-                                    const uint32_t *sb, const BHalo &H, uint32_t p, int64_t ps, int64_t n) {
-    unsigned long long lmk, rmk;
-    rt.get(p, &lmk, &rmk);
-    if (!rmk) return BK;
+__device__ inline uint32_t cover_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const BHalo &H, uint32_t p,
+                                    int64_t ps, int64_t n) {
+    if (!(rt.get(p) >> 31)) return BK;
     const int64_t pps = v_left<SH>(tok, ps);
     const uint32_t pp = tok_at_b<SH>(tok, H, pps, n);
-    for (unsigned long long q = rmk; q; q &= q - 1) {
-        const uint32_t mm = __ffsll(q) - 1;
-        if (sa[mm] != pp) continue;
-        if (sa[mm] != sb[mm]) return mm;
-        uint32_t L;  // run of p ending at ps
-        if (SH && ps < 0) {
-            L = H.hlr[mm];
-        } else {
-            L = 1;
-            int64_t x = v_left<SH>(tok, ps);
-            for (; x >= 0 && tok[x] == p; x = v_left<SH>(tok, x)) L++;
-            if (SH && x < 0) L += H.hlr[mm];  // the run reaches my first token and goes on leftwards
-        }
-        return (L & 1) ? BK : mm;
+    const uint32_t mm = rt.member(pp, p);
+    if (mm >= BK || pp != p) return mm;
+    uint32_t L;  // run of p ending at ps
+    if (SH && ps < 0) {
+        L = H.hlr[mm];
+    } else {
+        L = 1;
+        int64_t x = v_left<SH>(tok, ps);
+        for (; x >= 0 && tok[x] == p; x = v_left<SH>(tok, x)) L++;
+        if (SH && x < 0) L += H.hlr[mm];  // the run reaches my first token and goes on leftwards
     }
-    return BK;
+    return (L & 1) ? BK : mm;
 }
 
 // The member whose occurrence starts at the token q at kq (q is its a and the
 // token after it its b: for a != b always an occurrence; for a == b q starts
 // a run -- the token before it is an occurrence's b -- so it pairs), or BK.
 template <bool SH>
-__device__ inline uint32_t starts_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const uint32_t *sb,
-                                     const uint32_t *sla, const BHalo &H, uint32_t q, int64_t kq, int64_t n) {
-    unsigned long long lmk, rmk;
-    rt.get(q, &lmk, &rmk);
-    if (!lmk) return BK;
-    const int64_t kn = v_right(kq, sla[__ffsll(lmk) - 1], n);
-    const uint32_t qq = tok_at_b<SH>(tok, H, kn, n);
-    for (unsigned long long t = lmk; t; t &= t - 1) {
-        const uint32_t mm = __ffsll(t) - 1;
-        if (sb[mm] == qq) return mm;
-    }
-    return BK;
+__device__ inline uint32_t starts_of(const uint32_t *__restrict__ tok, const RoleTab &rt, const BHalo &H, uint32_t q,
+                                     int64_t kq, int64_t n) {
+    const uint32_t lq = rt.get(q) & 0x7FFFFFFFu;
+    if (!lq) return BK;
+    const int64_t kn = v_right(kq, lq, n);
+    return rt.member(q, tok_at_b<SH>(tok, H, kn, n));
 }
 
 // Every member's occurrences in the pre-batch tokens and the batch's count
@@ -1114,9 +1352,9 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     __shared__ uint16_t ltag[SCAN_T * SU * FR];
     __shared__ uint32_t lcount, gbase, list_n, covc, sm, sk, sz0, bRs;
     __shared__ uint32_t lr_n, lr_brk, lr_pos[RUN_Q];  // a == b: long runs handed from a thread to a wave (next pair's start)
-    __shared__ unsigned long long badj;  // the members whose occurrences abut my member's (Bat::adj)
+    __shared__ unsigned long long badj[NBK];  // the members whose occurrences abut my member's (Bat::adj)
     __shared__ uint32_t gcnt[2];
-    __shared__ uint32_t sa[BK], sb[BK], sla[BK];
+    __shared__ uint32_t sa[BK], sb[BK];
     __shared__ RoleTab rt;
     __shared__ BHalo H;
     __shared__ uint32_t wmx[2][16];
@@ -1125,21 +1363,24 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         sm = BK;
         covc = lcount = bRs = 0;
         lr_n = 0;
-        badj = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) badj[b] = 0;
         gcnt[0] = gcnt[1] = 0;
         sk = B->k;
         sz0 = B->z0;
     }
     for (uint32_t q = tid; q < RH; q += SCAN_T) {
         rt.id[q] = HOLE;
-        rt.lm[q] = rt.rm[q] = 0;
+        rt.fl[q] = 0;
     }
+    for (uint32_t q = tid; q < RP; q += SCAN_T) rt.pk[q] = 0;
+    uint32_t mla = 0;  // (tid < k: member tid's a's token length)
     if (tid < BK) {
         const uint32_t lo = B->blk0[tid], hi = B->blk0[tid + 1];
         const uint32_t ma = B->a[tid];
         sa[tid] = ma;
         sb[tid] = B->b[tid];
-        sla[tid] = E->tlen[ma];
+        mla = E->tlen[ma];
         if (blockIdx.x >= lo && blockIdx.x < hi && tid < B->k) sm = tid;
     }
     __syncthreads();
@@ -1148,10 +1389,9 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         if (tid == 0) atomicMax(&B->sc_out, wall_clock64());
         return;
     }
-    unsigned long long tadj = 0;  // members whose occurrences abut the ones this thread found
+    MK tadj = mk_zero();  // members whose occurrences abut the ones this thread found
     if (tid < k) {
-        rt.put(sa[tid], false, tid);
-        rt.put(sb[tid], true, tid);
+        rt.put(sa[tid], sb[tid], mla, tid);
         if (SH) {
             Halo h;
             shard_halo(E->erec, E->nshards, E->shard, sa[tid], &h);
@@ -1164,8 +1404,8 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 }
         }
     }
-    const uint32_t a = sa[m], b = sb[m], z = z0 + m, la = sla[m];
-    const uint32_t lb = E->tlen[b];
+    const uint32_t a = sa[m], b = sb[m], z = z0 + m;
+    const uint32_t la = E->tlen[a], lb = E->tlen[b];
     const uint32_t mode = B->mode[m], off = B->off[m], len = B->len[m];
     const uint32_t bid = blockIdx.x - B->blk0[m], nblk = B->blk0[m + 1] - B->blk0[m];
     const uint32_t sbase = B->sbase[m];
@@ -1285,10 +1525,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     const uint32_t p = pv[u];
                     lfin = p;
                     if (p != HOLE) {
-                        const uint32_t cv = cover_of<SH>(tok, rt, sa, sb, H, p, ps[u], n);
+                        const uint32_t cv = cover_of<SH>(tok, rt, H, p, ps[u], n);
                         if (cv < BK) {
                             lfin = z0 + cv;
-                            tadj |= 1ull << cv;
+                            mk_set(tadj, cv);
                             atomicAdd(&covc, 1u);
                         } else {
                             vadd_b(s, E, m, V_DL, p, gcnt);
@@ -1300,10 +1540,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     const uint32_t q = kq < n ? tr[u] : tok_at(kq);
                     rfin = q;
                     if (q != HOLE) {
-                        const uint32_t st = starts_of<SH>(tok, rt, sb, sla, H, q, kq, n);
+                        const uint32_t st = starts_of<SH>(tok, rt, H, q, kq, n);
                         if (st < BK) {
                             rfin = z0 + st;
-                            tadj |= 1ull << st;
+                            mk_set(tadj, st);
                         }
                         vadd_b(s, E, m, V_DR, q, gcnt);
                         vadd_b(s, E, m, V_IR, rfin, gcnt);
@@ -1389,10 +1629,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
             const int64_t ps = ok ? v_left<SH>(tok, i) : -1;
             const uint32_t p = ok ? tok_at(ps) : HOLE;
             // the run's left neighbour, unless another member's occurrence covers it
-            const uint32_t cv = (ok && p != HOLE && p != a) ? cover_of<SH>(tok, rt, sa, sb, H, p, ps, n) : BK;
+            const uint32_t cv = (ok && p != HOLE && p != a) ? cover_of<SH>(tok, rt, H, p, ps, n) : BK;
             if (cv < BK) {
                 atomicAdd(&covc, 1u);
-                tadj |= 1ull << cv;
+                mk_set(tadj, cv);
             }
             const bool left = p != HOLE && p != a && cv == BK;
             // my first token continues a run of the left shard: pairs with its
@@ -1407,9 +1647,9 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 const bool knext = q == a;
                 const bool nocc = knext && tok_at(v_right(kq, la, n)) == a;
                 // a right neighbour that starts another member's occurrence becomes its id
-                const uint32_t st = (!knext && q != HOLE) ? starts_of<SH>(tok, rt, sb, sla, H, q, kq, n) : BK;
+                const uint32_t st = (!knext && q != HOLE) ? starts_of<SH>(tok, rt, H, q, kq, n) : BK;
                 const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
-                if (st < BK) tadj |= 1ull << st;
+                if (st < BK) mk_set(tadj, st);
                 const uint32_t pfin = (mi > 0 || cont) ? z : (left ? p : cv < BK ? z0 + cv : HOLE);
                 const uint32_t slot = atomicAdd(&lcount, 1u);
                 if (slot < SCAN_T * SU) {
@@ -1502,9 +1742,9 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     // (the run's last pair: a right neighbour that starts another
                     // member's occurrence becomes its id, as in the thread walk)
                     const uint32_t st = (pair && !knext && q != HOLE)
-                                            ? starts_of<SH>(tok, rt, sb, sla, H, q, posl((int64_t)o + 64 * u + lane + 2), n)
+                                            ? starts_of<SH>(tok, rt, H, q, posl((int64_t)o + 64 * u + lane + 2), n)
                                             : BK;
-                    if (st < BK) tadj |= 1ull << st;
+                    if (st < BK) mk_set(tadj, st);
                     const uint32_t rq = nocc ? z : st < BK ? z0 + st : q;
                     const unsigned long long pm = __ballot(pair);
                     uint32_t g = 0;
@@ -1565,7 +1805,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     // left neighbours x) -- from this block's LDS vectors.  Pairs a covered
     // left neighbour or the edge step accounts elsewhere are left out: the
     // sum is a lower bound on the decrements, so k_bapply's check errs safe
-    if (tid < BK && tid < B->nsk && ((B->sk_cm[tid] >> m) & 1ull)) {
+    if (tid < SKMAX && tid < B->nsk && ((B->sk_cm[tid][m >> 6] >> (m & 63)) & 1ull)) {
         const uint32_t xs = B->sk_a[tid], ys = B->sk_b[tid];
         uint32_t d = 0;
         if (xs == b && ys < lim) d += s[V_DR][ys];
@@ -1597,7 +1837,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 const uint32_t p = tok_at(ps);
                 uint32_t lfin = p, bnd = 1;
                 if (p != HOLE) {
-                    const uint32_t cv = cover_of<SH>(tok, rt, sa, sb, H, p, ps, n);
+                    const uint32_t cv = cover_of<SH>(tok, rt, H, p, ps, n);
                     if (cv < BK) {
                         lfin = z0 + cv;
                         bnd = 2;
@@ -1609,7 +1849,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 const uint32_t q = H.HR[1];
                 uint32_t rfin = q;
                 if (q != HOLE) {
-                    const uint32_t st = starts_of<SH>(tok, rt, sb, sla, H, q, n + 1, n);
+                    const uint32_t st = starts_of<SH>(tok, rt, H, q, n + 1, n);
                     if (st < BK) rfin = z0 + st;
                     xadd(E, xo, Wx, mm, V_DR, q);
                     xadd(E, xo, Wx, mm, V_IR, rfin);
@@ -1629,10 +1869,14 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     // which members' occurrences abut my member's: k_bapply may apply a
     // verified prefix only when none of them abuts a dropped member
     if (k > 1) {
-        for (int o = 32; o > 0; o >>= 1) tadj |= __shfl_xor(tadj, o);
-        if ((tid & 63) == 0 && tadj) atomicOr(&badj, tadj);
+#pragma unroll
+        for (uint32_t bb = 0; bb < NBK; bb++) {
+            unsigned long long t = tadj.w[bb];
+            for (int o = 32; o > 0; o >>= 1) t |= __shfl_xor(t, o);
+            if ((tid & 63) == 0 && t) atomicOr(&badj[bb], t);
+        }
         __syncthreads();
-        if (tid == 0 && badj) atomicOr(&B->adj[m], badj);
+        if (tid < NBK && badj[tid]) atomicOr(&B->adj[m][tid], badj[tid]);
     }
     // deltas into replica (block % BREPL) of the member's accumulators (SH:
     // the exchange buffer), and the member's new-key bound: per block max over
@@ -1677,9 +1921,11 @@ template __global__ void k_bscan<false>(const Eng *, const Ctl *);
 template __global__ void k_bscan<true>(const Eng *, const Ctl *);
 
 // ----------------------------------------------------------------- k_bpack
+constexpr uint32_t XSP_SHIFT = 23;  // (member * 4 + vector) above the id (batch runs: ids < 2^18)
+static_assert(4 * BK < (1u << (32 - XSP_SHIFT)), "member-vector index fits above the id");
 // Sharded batches with ids >= DENSE (after k_bscan, before the exchange): my
 // members' (id, delta) lists of those ids, which the scan kept in bvec /
-// bvlist, packed into xsp_out in member order as (member * 4 + vector) << 24 |
+// bvlist, packed into xsp_out in member order as (member * 4 + vector) << XSP_SHIFT |
 // id, delta; bvec cleared as read (k_bsel clears bvnl).  Entries beyond
 // xsp_cap: the first member whose lists do not fit is flagged in xbat[] like a
 // staging overflow (summed over the shards), so every shard fails the batch
@@ -1690,11 +1936,12 @@ __global__ __launch_bounds__(256) void k_bpack(const Eng *__restrict__ E, const 
     __shared__ uint32_t pre[BK * 4 + 1];
     __shared__ uint32_t written;
     const uint32_t k = B->k, tid = threadIdx.x, nmv = 4 * k;
-    if (tid < 64) {  // exclusive prefix of the list lengths, 4 (member, vector) lists per lane
-        uint32_t c[4], sum = 0;
+    if (tid < 64) {  // exclusive prefix of the list lengths, LP (member, vector) lists per lane
+        constexpr uint32_t LP = 4 * NBK;
+        uint32_t c[LP], sum = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < 4; j++) {
-            c[j] = 4 * tid + j < nmv ? E->bvnl[4 * tid + j] : 0u;
+        for (uint32_t j = 0; j < LP; j++) {
+            c[j] = LP * tid + j < nmv ? E->bvnl[LP * tid + j] : 0u;
             sum += c[j];
         }
         uint32_t incl = sum;
@@ -1704,8 +1951,8 @@ __global__ __launch_bounds__(256) void k_bpack(const Eng *__restrict__ E, const 
         }
         uint32_t r = incl - sum;
 #pragma unroll
-        for (uint32_t j = 0; j < 4; j++) {
-            if (4 * tid + j <= nmv) pre[4 * tid + j] = r;
+        for (uint32_t j = 0; j < LP; j++) {
+            if (LP * tid + j <= nmv) pre[LP * tid + j] = r;
             r += c[j];
         }
     }
@@ -1734,7 +1981,7 @@ __global__ __launch_bounds__(256) void k_bpack(const Eng *__restrict__ E, const 
         const uint32_t val = E->bvec[base + (x - DENSE)];
         E->bvec[base + (x - DENSE)] = 0;
         if (q < w) {
-            E->xsp_out[2 + 2 * (uint64_t)q] = (lo << 24) | x;
+            E->xsp_out[2 + 2 * (uint64_t)q] = (lo << XSP_SHIFT) | x;
             E->xsp_out[3 + 2 * (uint64_t)q] = val;
         }
     }
@@ -1778,33 +2025,49 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         B->sl_in = B->sl_out = 0;
     }
     // wave 0 issues every word its prologue reads together with the stop
-    // flag, lane q member q's (one round trip instead of four dependent ones:
-    // stop, k, the members' words, their token lengths)
+    // flag, lane q % 64 of bank q / 64 member q's and skipped key q's (one
+    // round trip instead of four dependent ones: stop, k, the members' words,
+    // their token lengths)
     const uint32_t tid = threadIdx.x, lane = tid & 63;
-    uint32_t pf_k = 0, pf_z0 = 0, pf_dt = 0, pf_a = 0, pf_b = 0, pf_R = 0, pf_cnt = 0, pf_bnd = 0, pf_sb = 0, pf_la = 0,
-             pf_lb = 0, pf_nsk = 0, pf_skc = 0, pf_sdec = 0, pf_nskb = 0, pf_nl[4] = {0, 0, 0, 0};
-    unsigned long long pf_live = 0, pf_adj = 0;
+    uint32_t pf_k = 0, pf_z0 = 0, pf_dt = 0, pf_nsk = 0;
+    uint32_t pf_a[NBK], pf_b[NBK], pf_R[NBK], pf_cnt[NBK], pf_bnd[NBK], pf_sb[NBK], pf_la[NBK], pf_lb[NBK], pf_skc[NBK],
+        pf_sdec[NBK], pf_nskb[NBK], pf_nl[NBK][4];
+    MK pf_adj[NBK];
+    unsigned long long pf_live = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < NBK; b++) {
+        pf_a[b] = pf_b[b] = pf_R[b] = pf_cnt[b] = pf_bnd[b] = pf_sb[b] = pf_la[b] = pf_lb[b] = 0;
+        pf_skc[b] = pf_sdec[b] = pf_nskb[b] = 0;
+#pragma unroll
+        for (uint32_t v = 0; v < 4; v++) pf_nl[b][v] = 0;
+        pf_adj[b] = mk_zero();
+    }
     if (tid < 64) {
         pf_k = B->k;
         pf_z0 = B->z0;
         pf_dt = B->drop_test;
         pf_live = C->n_live;
         pf_nsk = B->nsk;
-        if (lane < BK) {
-            pf_a = B->a[lane];
-            pf_b = B->b[lane];
-            pf_R = B->R[lane];
-            pf_cnt = B->cnt[lane];
-            pf_bnd = B->bound[lane];
-            pf_sb = B->sbase[lane];
-            pf_la = B->mla[lane];
-            pf_lb = B->mlb[lane];
-            pf_adj = B->adj[lane];
-            pf_skc = B->sk_c[lane];
-            pf_sdec = B->sdec[lane];
-            pf_nskb = B->nskb[lane];
 #pragma unroll
-            for (uint32_t v = 0; v < 4; v++) pf_nl[v] = E->bvnl[4 * lane + v];
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            if (q < BK) {
+                pf_a[b] = B->a[q];
+                pf_b[b] = B->b[q];
+                pf_R[b] = B->R[q];
+                pf_cnt[b] = B->cnt[q];
+                pf_bnd[b] = B->bound[q];
+                pf_sb[b] = B->sbase[q];
+                pf_la[b] = B->mla[q];
+                pf_lb[b] = B->mlb[q];
+#pragma unroll
+                for (uint32_t bb = 0; bb < NBK; bb++) pf_adj[b].w[bb] = B->adj[q][bb];
+                pf_skc[b] = B->sk_c[q];
+                pf_sdec[b] = B->sdec[q];
+                pf_nskb[b] = B->nskb[q];
+#pragma unroll
+                for (uint32_t v = 0; v < 4; v++) pf_nl[b][v] = E->bvnl[4 * q + v];
+            }
         }
     }
     if (C->stop) return;
@@ -1817,15 +2080,12 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
     __shared__ uint32_t sk, sj, sz0;
     __shared__ uint32_t ssp[P2P_MAXR_B + 1];  // SH: prefix of the shards' list lengths
     if (tid >= 64 && tid < 64 + BK) s_cnew[tid - 64] = 0;  // (ordered by the prologue's barrier)
-    // prologue, wave 0, lane q = member q: the verified prefix, prefix sums of
-    // the occurrences and of the listed-id counts, role A's blocks per member
+    // prologue, wave 0, lane q % 64 of bank q / 64 = member q: the verified
+    // prefix, prefix sums of the occurrences and of the listed-id counts, role
+    // A's blocks per member
     if (tid < 64) {
         const uint32_t k = pf_k, z0 = pf_z0, dt = pf_dt;
         const unsigned long long live0 = pf_live;
-        const bool in = lane < k;
-        const uint32_t ma = in ? pf_a : 0, mb = in ? pf_b : 0;
-        const uint32_t R = in ? pf_R : 0, cnt = in ? pf_cnt : 0;
-        uint32_t bnd = in && !SH ? pf_bnd : 0;
         if (SH && lane == 0) {  // every shard's list of ids >= DENSE (gathered): prefix of their lengths
             uint32_t acc = 0;
             ssp[0] = 0;
@@ -1835,85 +2095,88 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             }
             if (!E->xsp_in) ssp[1] = 0;
         }
-        unsigned long long ovm = 0;  // SH: members some shard could not stage
-        uint32_t Rg = R;             // occurrences over all shards (the live-token count is global)
-        if (SH) {
-            uint32_t *xm = E->xbat + XBH + (uint64_t)lane * xbat_member_words(z0 + k);
-            // (every block's prologue reads these words: the next select clears them)
-            if (in) {
-                const uint32_t rg = xm[0];
-                Rg = rg;
-                bnd = xm[1];
-                if (blockIdx.x == 0) B->Rg[lane] = rg;
-                sRg[lane] = rg;
-            }
-            const uint32_t ov = lane < BK ? E->xbat[lane] : 0;
-            ovm = __ballot(lane < k && ov != 0);
-        }
-        const uint32_t sbase = in ? pf_sb : 0;
-        uint32_t nlv[4], nls = 0;  // my member's listed-id counts (ids >= DENSE) per vector
+        uint32_t R[NBK], cnt[NBK], bnd[NBK], Rg[NBK], nls[NBK], lpre[NBK], bpre[NBK], ov[NBK];
+        unsigned long long rpre[NBK], gpre[NBK];
 #pragma unroll
-        for (uint32_t v = 0; v < 4; v++) {
-            nlv[v] = in ? pf_nl[v] : 0u;
-            nls += nlv[v];
-        }
-        const uint32_t tla = in ? pf_la : 0, tlb = in ? pf_lb : 0;
-        // exclusive prefix sum of R and max of bound over the members before me
-        unsigned long long rpre = R;
-        uint32_t bpre = bnd, lpre = nls;
-        for (int o = 1; o < 64; o <<= 1) {
-            const unsigned long long y = __shfl_up(rpre, o);
-            const uint32_t yb = __shfl_up(bpre, o), yl = __shfl_up(lpre, o);
-            if ((int)lane >= o) {
-                rpre += y;
-                bpre = max(bpre, yb);
-                lpre += yl;
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            const bool in = q < k;
+            R[b] = in ? pf_R[b] : 0;
+            cnt[b] = in ? pf_cnt[b] : 0;
+            bnd[b] = in && !SH ? pf_bnd[b] : 0;
+            Rg[b] = R[b];  // occurrences over all shards (the live-token count is global)
+            ov[b] = 0;
+            if (SH) {
+                uint32_t *xm = E->xbat + XBH + (uint64_t)q * xbat_member_words(z0 + k);
+                // (every block's prologue reads these words: the next select clears them)
+                if (in) {
+                    const uint32_t rg = xm[0];
+                    Rg[b] = rg;
+                    bnd[b] = xm[1];
+                    if (blockIdx.x == 0) B->Rg[q] = rg;
+                    sRg[q] = rg;
+                }
+                ov[b] = q < BK ? E->xbat[q] : 0;
             }
+            nls[b] = 0;  // my member's listed-id counts (ids >= DENSE)
+#pragma unroll
+            for (uint32_t v = 0; v < 4; v++) nls[b] += in ? pf_nl[b][v] : 0u;
+            rpre[b] = R[b];
+            gpre[b] = Rg[b];
+            bpre[b] = bnd[b];
+            lpre[b] = nls[b];
         }
-        const unsigned long long rex = rpre - R;                            // occurrences of the members before me
-        // the same over all shards: C->n_live counts every shard's tokens
-        unsigned long long rexg = rex;
-        if (SH) {
-            unsigned long long g = Rg;
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned long long y = __shfl_up(g, o);
-                if ((int)lane >= o) g += y;
-            }
-            rexg = g - Rg;
-        }
-        const uint32_t pm = __shfl_up(bpre, 1);                              // max bound of the members before me
-        // the keys the formation skipped (lane s = skipped key s): their count
-        // after the decrements of the members that conflict with them (summed
-        // over the shards), as a running max in list order; member q must be
-        // strictly ahead of every skipped key listed before it
+        // SH: members some shard could not stage
+        const MK ovm = mk_ballot([&](uint32_t b) { return 64 * b + lane < k && ov[b] != 0; });
+        // prefix sums of R (this shard's and all shards') and of the listed ids,
+        // and the prefix max of bound
+        bank_scan(rpre);
+        bank_scan(gpre);
+        bank_scan(lpre);
+        bank_scan_max(bpre);
+        // the keys the formation skipped (lane s % 64 of bank s / 64 = skipped
+        // key s): their count after the decrements of the members that conflict
+        // with them (summed over the shards), as a running max in list order;
+        // member q must be strictly ahead of every skipped key listed before it
         const uint32_t nsk = pf_nsk;
-        uint32_t skub = 0;
-        if (lane < nsk) {
-            // (BPE_SKIP_TEST: tests pretend no member lowered it, so every member
-            // after a skipped key fails and the batch is re-formed before it)
-            const uint32_t dec = E->skip_on > 1 ? 0u : SH ? E->xbat[BK + lane] : pf_sdec, cs = pf_skc;
-            skub = cs > dec ? cs - dec : 0u;
+        uint32_t skub[NBK];
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t s = 64 * b + lane;
+            skub[b] = 0;
+            if (s < nsk) {
+                // (BPE_SKIP_TEST: tests pretend no member lowered it, so every member
+                // after a skipped key fails and the batch is re-formed before it)
+                const uint32_t dec = E->skip_on > 1 ? 0u : SH ? E->xbat[BK + s] : pf_sdec[b], cs = pf_skc[b];
+                skub[b] = cs > dec ? cs - dec : 0u;
+            }
         }
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(skub, o);
-            if ((int)lane >= o) skub = max(skub, y);
+        bank_scan_max(skub);
+        bool fail[NBK], skf[NBK];
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            const bool in = q < k;
+            const uint32_t pm = bank_prev(bpre, b);  // max bound of the members before me
+            const uint32_t nsb = in && nsk ? pf_nskb[b] : 0u;
+            const uint32_t skmax = bank_gather(skub, nsb ? nsb - 1 : 0);
+            skf[b] = nsb && !(skmax < cnt[b]);
+            const unsigned long long rexg = gpre[b] - Rg[b];  // occurrences of the members before me, all shards
+            // member q is the argmax after the members before it: its count beats
+            // every key they can create and every key they lowered past it, and
+            // the run is still untracked then
+            fail[b] = in && q > 0 &&
+                      (!(pm < cnt[b]) || skf[b] || (dt && (z0 + q) % dt == 0) ||
+                       (!E->fast && live0 - rexg < TRACK_LIMIT) || mk_meets(ovm, mk_below(q + 1)));
         }
-        const uint32_t nsb = in && nsk ? pf_nskb : 0u;
-        const uint32_t skmax = __shfl(skub, (int)(nsb ? nsb - 1 : 0));
-        const bool skfail = nsb && !(skmax < cnt);
-        // member q is the argmax after the members before it: its count beats
-        // every key they can create and every key they lowered past it, and
-        // the run is still untracked then
-        const bool fail = in && lane > 0 &&
-                          (!(pm < cnt) || skfail || (dt && (z0 + lane) % dt == 0) ||
-                           (!E->fast && live0 - rexg < TRACK_LIMIT) || (ovm & ((2ull << lane) - 1ull)) != 0);
-        const unsigned long long fm = __ballot(fail);
-        uint32_t js = fm ? (uint32_t)__ffsll(fm) - 1 : k;
-        if (fm && blockIdx.x == 0 && __ballot(skfail) & fm & (0ull - fm)) {  // (the first failure was a skipped key's)
-            if (lane == 0) atomicAdd(&B->nskfail, 1ull);
+        const MK fm = mk_ballot([&](uint32_t b) { return fail[b]; });
+        const uint32_t f0 = mk_first(fm);
+        uint32_t js = f0 < k ? f0 : k;
+        if (js < k && blockIdx.x == 0 && mk_test(mk_ballot([&](uint32_t b) { return skf[b]; }), js)) {
+            if (lane == 0) atomicAdd(&B->nskfail, 1ull);  // (the first failure was a skipped key's)
         }
         if (E->dbg_form && C->merges_done + 1 >= E->dbg_form && blockIdx.x == 0 && lane == 0)
-            printf("verify shard %u z0 %u k %u js %u ovm %llx R0 %u Rg0 %u\n", E->shard, z0, k, js, ovm, R, Rg);
+            printf("verify shard %u z0 %u k %u js %u ovm %llx R0 %u Rg0 %u\n", E->shard, z0, k, js, ovm.w[0], R[0], Rg[0]);
         // A member failed: the verified prefix is applied as it stands when no
         // occurrence of its members abuts one of a dropped member (the pair
         // between two abutting occurrences is counted once, by the left one,
@@ -1922,51 +2185,71 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
         // prefix (nothing changed in between, so the selection repeats).
         // (Sharded runs re-form always: the adjacency is per shard.)
         if (js < k) {
-            const unsigned long long am = in ? pf_adj : 0ull, pre = (1ull << js) - 1ull;
-            const bool abut = lane < js ? (am & ~pre) != 0 : (am & pre) != 0;
-            if (SH || E->prefix_apply == 0 || __ballot(in && abut)) {
+            const MK pre = mk_below(js);
+            const MK ab = mk_ballot([&](uint32_t b) {
+                const uint32_t q = 64 * b + lane;
+                if (q >= k) return false;
+                bool hi = false, lo = false;  // abuts a member at or past js / before js
+#pragma unroll
+                for (uint32_t bb = 0; bb < NBK; bb++) {
+                    hi |= (pf_adj[b].w[bb] & ~pre.w[bb]) != 0;
+                    lo |= (pf_adj[b].w[bb] & pre.w[bb]) != 0;
+                }
+                return q < js ? hi : lo;
+            });
+            if (SH || E->prefix_apply == 0 || mk_any(ab)) {
                 if (lane == 0) B->retry = js;
                 js = 0;
             }
         }
-        const uint32_t rall = (uint32_t)__shfl(rpre, (int)(k ? k - 1 : 0));
+        const uint32_t rall = k ? (uint32_t)bank_shfl(rpre, k - 1) : 0u;
         // the first part of each verified member's rewrite runs here, in
         // blocks in proportion to it (>= 1 per member)
         const uint32_t nA1 = gridDim.x - roleB_blocks;
-        const uint32_t cut = (in && lane < js && nA1 && !(B->tpend < js)) ? (uint32_t)((uint64_t)R * B->ra_split / 256) : 0u;
-        unsigned long long ctot = cut;
-        for (int o = 32; o > 0; o >>= 1) ctot += __shfl_xor(ctot, o);
-        const uint32_t nb1 = lane < js ? 1 + (uint32_t)(ctot ? (uint64_t)(nA1 > js ? nA1 - js : 0) * cut / ctot : 0) : 0;
-        uint32_t nbp1 = nb1;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(nbp1, o);
-            if ((int)lane >= o) nbp1 += y;
-        }
-        if (lane < js) {
-            scut[lane] = cut;
-            ablk[lane] = nbp1 - nb1;
-        }
-        if (lane == 0) ablk[js] = nA1;
-        if (in) {
-            sa[lane] = ma;
-            sb[lane] = mb;
-            sla[lane] = tla;
-            slb[lane] = tlb;
-            sR[lane] = R;
-            ssb[lane] = sbase;
-            spre[lane] = (uint32_t)rex;
-        }
-        if (in) {
-            uint32_t q = lpre - nls;
+        const uint32_t tpend = B->tpend;
+        uint32_t cut[NBK], nb1[NBK], nbp1[NBK];
+        unsigned long long ctot = 0;
 #pragma unroll
-            for (uint32_t v = 0; v < 4; v++) {
-                q += nlv[v];
-                snl[4 * lane + v + 1] = q;
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            cut[b] = (q < k && q < js && nA1 && !(tpend < js)) ? (uint32_t)((uint64_t)R[b] * B->ra_split / 256) : 0u;
+            ctot += cut[b];
+        }
+        ctot = wave_sum(ctot);
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            nb1[b] = q < js ? 1 + (uint32_t)(ctot ? (uint64_t)(nA1 > js ? nA1 - js : 0) * cut[b] / ctot : 0) : 0;
+            nbp1[b] = nb1[b];
+        }
+        bank_scan(nbp1);
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            if (q < js) {
+                scut[q] = cut[b];
+                ablk[q] = nbp1[b] - nb1[b];
+            }
+            if (q < k) {
+                sa[q] = pf_a[b];
+                sb[q] = pf_b[b];
+                sla[q] = pf_la[b];
+                slb[q] = pf_lb[b];
+                sR[q] = R[b];
+                ssb[q] = pf_sb[b];
+                spre[q] = (uint32_t)(rpre[b] - R[b]);  // occurrences of the members before me
+                uint32_t s = lpre[b] - nls[b];
+#pragma unroll
+                for (uint32_t v = 0; v < 4; v++) {
+                    s += pf_nl[b][v];
+                    snl[4 * q + v + 1] = s;
+                }
             }
         }
         if (lane == 0) {
+            ablk[js] = nA1;
             snl[0] = 0;
-            spre[k] = k ? rall : 0u;
+            spre[k] = rall;
             sk = k;
             sj = js;
             sz0 = z0;
@@ -2049,15 +2332,15 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                 }
             }
         } else if (SH && t < total) {
-            // the shards' lists of ids >= DENSE: (member-vector << 24 | id, delta)
+            // the shards' lists of ids >= DENSE: (member-vector << XSP_SHIFT | id, delta)
             const uint32_t q = t - dense_total;
             uint32_t sh = 0;
             while (q >= ssp[sh + 1]) sh++;
             const uint32_t *en = E->xsp_in + (uint64_t)sh * E->xsp_stride + 2 + 2 * (uint64_t)(q - ssp[sh]);
-            const uint32_t mv = en[0] >> 24;
+            const uint32_t mv = en[0] >> XSP_SHIFT;
             m = mv / 4;
             cat = mv % 4;
-            x = en[0] & 0xFFFFFFu;
+            x = en[0] & ((1u << XSP_SHIFT) - 1u);
             val = en[1];
         } else if (t < total) {
             const uint32_t q = t - dense_total;
@@ -2198,7 +2481,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             jf = BK;  // (not mine to decide: no bookkeeping here)
         } else {
             keep = true;
-            if (tid < 64) {  // lane = member: its tie order under every B its turn can see
+            if (tid < 64) {  // lane q % 64 of bank q / 64 = member q: its tie order under every B its turn can see
                 // (BPE_TIE_TEST: tests pretend every key was zeroed, so the check fails and the revert runs)
                 const uint32_t Z = E->tie_verify > 1 ? 0xFFFFFFFFu
                                                      : __hip_atomic_load(&B->ztot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
@@ -2208,18 +2491,25 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                 // at most D0 + the keys the members before it created (new
                 // keys only rise); members before tpend were admitted on the
                 // conservative bounds: not re-checked
-                uint32_t cb = lane < jsB ? __hip_atomic_load(&B->cnew[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-                for (int o = 1; o < 64; o <<= 1) {
-                    const uint32_t y = __shfl_up(cb, o);
-                    if ((int)lane >= o) cb += y;
+                uint32_t cb[NBK];
+#pragma unroll
+                for (uint32_t b = 0; b < NBK; b++) {
+                    const uint32_t q = 64 * b + lane;
+                    cb[b] = q < jsB ? __hip_atomic_load(&B->cnew[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
                 }
-                cb = __shfl_up(cb, 1);
-                if (lane == 0) cb = 0;
-                const unsigned long long hiD = D0 + min((unsigned long long)cb, (unsigned long long)B->tspan[lane < BK ? lane : 0]);
-                const bool f = lane >= 1 && lane >= B->tpend && lane < jsB &&
-                               !tie_levels_ok(lo, summary_B(hiD), Bsz, B->tmask[lane]);
-                const unsigned long long fm = __ballot(f);
-                if (lane == 0) sjf = fm ? (uint32_t)__ffsll(fm) - 1 : jsB;
+                bank_scan(cb);
+                const uint32_t tp = B->tpend;
+                bool f[NBK];
+#pragma unroll
+                for (uint32_t b = 0; b < NBK; b++) {
+                    const uint32_t q = 64 * b + lane;
+                    const uint32_t cbx = q ? bank_prev(cb, b) : 0u;  // created by the members before me
+                    const unsigned long long hiD =
+                        D0 + min((unsigned long long)cbx, (unsigned long long)B->tspan[q < BK ? q : 0]);
+                    f[b] = q >= 1 && q >= tp && q < jsB && !tie_levels_ok(lo, summary_B(hiD), Bsz, B->tmask[q]);
+                }
+                const MK fm = mk_ballot([&](uint32_t b) { return f[b]; });
+                if (lane == 0) sjf = mk_any(fm) ? mk_first(fm) : jsB;
             }
             __syncthreads();
             if (sjf < jsB) {  // revert every logged update (this block alone: rare)

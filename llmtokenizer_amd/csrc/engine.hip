@@ -555,9 +555,14 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     // (BPE_SKIP=0: the formation ends there, as before round 5)
     h.skip_on = (uint32_t)(getenv_int("BPE_SKIP", 1) != 0);
     if (h.skip_on && getenv_int("BPE_SKIP_TEST", 0)) h.skip_on = 2;  // (tests: every skipped key's check fails)
-    // and take members from the next TOPK keys once the first list is used up
-    // (BPE_LIST2=0: one list)
-    h.list2 = (uint32_t)(getenv_int("BPE_LIST2", 0) != 0);
+    // and take members from the next TOPK keys once a list is used up, up to
+    // nlists lists (BPE_NLIST; BPE_LIST2=1 is two lists, the round-5 knob)
+    {
+        int nl = BK > 63 ? (int)NLIST : 1;
+        if (getenv_int("BPE_LIST2", 0)) nl = std::max(nl, 2);
+        nl = getenv_int("BPE_NLIST", nl);
+        h.nlists = (uint32_t)std::max(1, std::min(nl, (int)NLIST));
+    }
     // tied members admitted on a guess of the keys the members before them
     // create (D's upper side), checked by k_bapply like the lower side
     h.tie_up = (uint32_t)(getenv_int("BPE_TIE_UP", 0) != 0);

@@ -114,8 +114,18 @@ struct EncBatch {
 // occurrences in the pre-batch tokens; k_bapply applies the prefix of members
 // that are provably the argmax in turn (count above every key the earlier
 // members can create) and drops the rest, which the next selection sees again.
-constexpr uint32_t TOPK = 64;   // sorted list length (partials and the merged list): one entry per lane
-constexpr uint32_t BK = 63;     // members per batch (one list entry stays for the strictness test)
+constexpr uint32_t TOPK = 64;   // sorted list length (partials and the merged lists): one entry per lane
+#ifndef BPE_BK
+#define BPE_BK 127
+#endif
+constexpr uint32_t BK = BPE_BK;  // members per batch: 64 NBK - 1 (member q in bank q / 64, lane q % 64)
+constexpr uint32_t NBK = (BK + 1) / 64;
+static_assert(BK + 1 == 64 * NBK && NBK >= 1 && NBK <= 2, "BK is 63 or 127");
+constexpr uint32_t SKMAX = BK;  // keys a batch may skip (Bat::sk_*)
+#ifndef BPE_NLIST
+#define BPE_NLIST 4
+#endif
+constexpr uint32_t NLIST = BPE_NLIST;  // lists of TOPK keys one formation may walk (Eng::nlists of them)
 constexpr uint32_t BRB = 32;    // k_bsel reduce blocks (partial lists)
 constexpr uint32_t BREPL = 2;   // replicas of a member's dense delta accumulators
 constexpr uint32_t BSB = 256;   // k_bscan blocks (1024 threads, one per CU)
@@ -156,7 +166,7 @@ struct Bat {
     uint32_t tbar, zrate;             // k_bapply's blocks finished (the last one checks); the formation's
                                       // zeroed-keys-per-member guess
     unsigned long long ntie, ntfail, nzero;  // batches verified that way, of them re-formed; keys zeroed (all batches)
-    uint8_t tmask[64];                // per member: B_final levels (bit e + 5: B = B_sz 2^e, e in [-5, 2])
+    uint8_t tmask[BK + 1];            // per member: B_final levels (bit e + 5: B = B_sz 2^e, e in [-5, 2])
                                       // under which its tie order holds
     uint32_t tspan[BK];               // per member: the formation's bound on D's rise before its turn
     uint32_t tlog_n;                  // k_bapply's undo log: (slot, delta) records written
@@ -174,7 +184,7 @@ struct Bat {
     // block exit), folded by the next k_bapply (outside the select's staged
     // head, which it writes back whole); launches folded
     unsigned long long sl_in, sl_out, sl_ticks, nsl;
-    unsigned long long adj[BK];       // per member: the members whose occurrences abut its own (k_bscan; cleared by
+    unsigned long long adj[BK][NBK];  // per member: the members whose occurrences abut its own (k_bscan; cleared by
                                       // the select that forms the batch)
     uint32_t mla[BK], mlb[BK];        // per member: the token lengths of its a and b (the select; k_bapply's prologue)
     // keys the formation skipped (batch.hip): a listed key that shares an id,
@@ -183,10 +193,10 @@ struct Bat {
     // member after it must beat its lowered count (k_bapply).  Written by the
     // selection directly (outside its staged head).
     uint32_t nsk, skpad;
-    uint32_t sk_a[BK], sk_b[BK], sk_c[BK];
-    uint32_t sdec[BK];                  // one GPU: the decrements its conflicting members made (k_bscan, atomic)
-    unsigned long long sk_cm[BK];       // those members (bit = member index)
-    uint8_t nskb[64];                   // per member: keys skipped before it in the list
+    uint32_t sk_a[SKMAX], sk_b[SKMAX], sk_c[SKMAX];
+    uint32_t sdec[SKMAX];               // one GPU: the decrements its conflicting members made (k_bscan, atomic)
+    unsigned long long sk_cm[SKMAX][NBK];  // those members (bit = member index)
+    uint8_t nskb[BK + 1];               // per member: keys skipped before it in the list
     unsigned long long nskip, nskfail;  // keys skipped in applied batches; batches re-formed by that check
     // verified tie order, upper side (round 5): the keys each member of a
     // logged batch created (role B, in member order), the run's creations so
@@ -205,7 +215,7 @@ struct Bat {
 // delta) lists (xsp_*, k_bpack)
 __host__ __device__ inline uint32_t xbat_vw(uint32_t W) { return W < DENSE ? W : DENSE; }
 __host__ __device__ inline uint32_t xbat_member_words(uint32_t W) { return 2 + 4 * xbat_vw(W); }
-constexpr uint32_t XBH = 2 * BK;  // head words of the exchange: overflow flags, skipped keys' decrements
+constexpr uint32_t XBH = BK + SKMAX;  // head words of the exchange: overflow flags [BK], skipped keys' decrements [SKMAX]
 __host__ __device__ inline uint32_t xbat_words(uint32_t k, uint32_t W) { return XBH + k * xbat_member_words(W); }
 
 // Device-resident descriptor: every kernel takes a pointer to it, so tables can
@@ -298,7 +308,8 @@ struct Eng {
     // batched training (batch.hip; occurrence positions staged in ids_out)
     uint32_t batch;       // 1: the batch kernels drive the run
     uint32_t skip_on;     // batches: skip non-commuting list entries instead of ending there (BPE_SKIP, default 1)
-    uint32_t list2;       // batches: the selection lists the next TOPK keys too (BPE_LIST2, default 0)
+    uint32_t nlists;      // batches: lists of TOPK keys a formation may walk, each once the one before is used up
+                          // (BPE_NLIST, 1..NLIST; BPE_LIST2=1 is 2)
     uint32_t tie_up;      // batches: the tie order's upper side on a guess of the keys created, verified (BPE_TIE_UP, default 0)
     uint32_t lose_retry;  // tests (BPE_TEST_LOSE_RETRY=1): the select forgets a failed batch's retry cut, so the
                           // failing batch is formed again and again -- the stall the no-progress watchdog ends
