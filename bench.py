@@ -622,7 +622,7 @@ def main():
                                           "batch_dropped", "batch_retries", "table_updates", "spec_hits",
                                           "spec_misses", "select_launches", "keys_skipped", "skip_failed",
                                           "tie_verified", "tie_failed")},
-        "batch_end": {k2[4:]: st[k2] for k2 in st if k2.startswith("end_") and k2 != "end_unused"},
+        "batch_end": {k2[4:]: st[k2] for k2 in st if k2.startswith("end_")},
     })
     out.update(extra)
     cp = committed_profile(name, sharded)

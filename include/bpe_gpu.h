@@ -95,8 +95,9 @@ typedef struct {
     uint64_t track_light;     /* tracked iterations: on-device exact counts of only the
                                  threads whose bound reached a growth threshold   */
     uint64_t batch_end[8];    /* training, batches: what ended each batch's formation --
-                                 [0] the list (64 keys, 63 members) [1] merge cap / count <= 1 /
-                                 hot threshold [2] unused [3] a key listed twice [4] a tie whose
+                                 [0] the lists used up or 127 members [1] merge cap / count <= 1 /
+                                 hot threshold [2] a member predicted to lose to a skipped key
+                                 [3] a key listed twice [4] a tie whose
                                  order the batch could change [5] a member that does not commute
                                  with an earlier one [6] pair-table margin [7] occurrence staging */
     double ms_select_span;    /* training, batches: average k_bsel span (the selection beside the

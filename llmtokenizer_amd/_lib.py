@@ -50,7 +50,7 @@ class GpuStats(ctypes.Structure):
                                                      "batch_dropped", "batch_retries", "table_updates")] + \
         [(n, ctypes.c_double) for n in ("ms_scan_span", "ms_apply_span")] + \
         [(n, ctypes.c_uint64) for n in ("track_exact", "track_skipped", "track_violations", "track_light")] + \
-        [(n, ctypes.c_uint64) for n in ("end_list", "end_count", "end_unused", "end_dup", "end_tie", "end_conflict",
+        [(n, ctypes.c_uint64) for n in ("end_list", "end_count", "end_skipgate", "end_dup", "end_tie", "end_conflict",
                                          "end_table", "end_staging")] + \
         [("ms_select_span", ctypes.c_double), ("select_launches", ctypes.c_uint64)] + \
         [(n, ctypes.c_uint64) for n in ("tie_verified", "tie_failed", "keys_zeroed", "keys_skipped", "skip_failed",

@@ -426,7 +426,7 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
     // on another's LDS store); lane 0 writes the scalar results, lane q member q's
     bool applied = false;
     uint32_t jst = 0, kpr = 0, retry = 0, fretry = 0, olda = 0, oldb = 0, oldz0 = 0, oldsum = 0, rescan = 0, ocand = 0,
-             oocc = 0, oldnsk = 0, skg = 0, ske = 0, crate = 0, raerr = 0, nst = 0, md = 0, cnt0 = 0, ties = 0, edge = 0,
+             oocc = 0, oldnsk = 0, skg = 0, ske = 0, crate = 0, skr = 0, raerr = 0, nst = 0, md = 0, cnt0 = 0, ties = 0, edge = 0,
              hotT = 0, stop = STOP_NONE, nl0 = 0;
     bool stalled = false, skip_now = false, sh = E->sharded != 0;
     unsigned long long rs = 0, rg = 0, D = 0, n_live = 0, v0 = 0;
@@ -498,6 +498,7 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
         }
         skip_now = E->skip_on && (skg == 0 || fretry != 0);
         crate = Bg->crate;
+        skr = E->skip_on == 1 ? Bg->skr : 0u;
         raerr = aload(&Bg->ra_err);  // a token too long for an end code (rewrite blocks)
         ts_mark(E, bi, BT_F_FOLD, false);
         D = C->D + (applied ? B->dD : 0ull);
@@ -540,6 +541,7 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
         skg = uni(skg);
         ske = uni(ske);
         crate = uni(crate);
+        skr = uni(skr);
         raerr = uni(raerr);
         nst = uni(nst);
         md = uni(md);
@@ -564,6 +566,7 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
     // list's entries in the earlier lists are a prefix of it, both being in
     // argmax order)
     uint32_t kk = 0, nskt = 0, tpend = BK, endwhy = 8, kend = 64, npass = 0;
+    uint32_t pbm = 0;  // the largest predicted lowered count of the keys skipped so far (Bat::skr)
     unsigned long long spanbase = 0;
     ts_mark(E, bi, BT_F_PRE, false);
     if (tid < 64 && stop == STOP_NONE) {
@@ -726,6 +729,19 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
                 }
                 const unsigned long long skm = __ballot(skok), below_l = (1ull << lane) - 1ull;
                 const unsigned long long Sc = X & skm;  // skipped, unless the skip cap ends the batch first
+                // A member must beat every key skipped before it at that key's
+                // count after the earlier members' decrements (k_bapply checks
+                // the exact bound).  With the run's estimate of those
+                // decrements (skr: a share of the count) a member predicted to
+                // fail ends the batch before it instead of failing it (a failed
+                // member costs the batch's scan again)
+                const uint32_t pbl = ((Sc >> lane) & 1ull) && skr ? c - (uint32_t)(((uint64_t)c * skr) >> 16) : 0u;
+                uint32_t pbx = pbl;  // inclusive prefix max, then exclusive
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t yy = __shfl_up(pbx, o);
+                    if ((int)lane >= o) pbx = max(pbx, yy);
+                }
+                pbx = max(lane ? (uint32_t)__shfl_up(pbx, 1) : 0u, pbm);
                 uint32_t ew = 0;
                 if ((X >> lane) & 1ull) {
                     if (!skok || nskt + (uint32_t)__popcll(Sc & below_l) >= SKMAX) ew = 5;
@@ -733,6 +749,8 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
                     ew = why;
                 } else if (kk + (uint32_t)__popcll(M & below_l) >= BK) {  // (the member cap: reported as "list")
                     ew = 8;
+                } else if (skr && pbx && !(c > pbx)) {  // (predicted to fail on a skipped key)
+                    ew = 2;
                 }
                 const unsigned long long ends = __ballot(ew != 0);
                 if (ends) {
@@ -756,6 +774,11 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
             const uint32_t km = (uint32_t)__popcll(M);
             const unsigned long long below = (1ull << lane) - 1;
             const bool isM = (M >> lane) & 1;
+            {
+                uint32_t pq = ((S >> lane) & 1ull) && skr ? c - (uint32_t)(((uint64_t)c * skr) >> 16) : 0u;
+                for (int o = 32; o > 0; o >>= 1) pq = max(pq, (uint32_t)__shfl_xor(pq, o));
+                pbm = uni(max(pbm, pq));
+            }
             // skipped keys, in list order: key, count, the members (by index)
             // that lower it
             if ((S >> lane) & 1) {
@@ -2149,6 +2172,24 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                 // after a skipped key fails and the batch is re-formed before it)
                 const uint32_t dec = E->skip_on > 1 ? 0u : SH ? E->xbat[BK + s] : pf_sdec[b], cs = pf_skc[b];
                 skub[b] = cs > dec ? cs - dec : 0u;
+            }
+        }
+        // the run's estimate of the skipped keys' decrements (Bat::skr): a
+        // running mean of each batch's smallest share (dec / count, 2^-16)
+        if (nsk && blockIdx.x == 0 && E->skip_on == 1) {
+            uint32_t rmin = 0xFFFFu;
+#pragma unroll
+            for (uint32_t b = 0; b < NBK; b++) {
+                const uint32_t s = 64 * b + lane;
+                if (s < nsk) {
+                    const uint32_t dec = SH ? E->xbat[BK + s] : pf_sdec[b], cs = pf_skc[b];
+                    rmin = min(rmin, cs ? (uint32_t)min((uint64_t)dec * 65536ull / cs, 0xFFFFull) : 0xFFFFu);
+                }
+            }
+            for (int o = 32; o > 0; o >>= 1) rmin = min(rmin, (uint32_t)__shfl_xor(rmin, o));
+            if (lane == 0) {
+                const uint32_t old = B->skr;
+                B->skr = old ? (3u * old + rmin) / 4u : max(rmin, 1u);
             }
         }
         bank_scan_max(skub);

@@ -558,7 +558,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     // and take members from the next TOPK keys once a list is used up, up to
     // nlists lists (BPE_NLIST; BPE_LIST2=1 is two lists, the round-5 knob)
     {
-        int nl = BK > 63 ? (int)NLIST : 1;
+        int nl = BK > 63 ? 2 : 1;  // (configs[2]: 1 list 69.1 ms loop / 156 batches, 2 lists 65.4 / 102, 3 66.4 / 102)
         if (getenv_int("BPE_LIST2", 0)) nl = std::max(nl, 2);
         nl = getenv_int("BPE_NLIST", nl);
         h.nlists = (uint32_t)std::max(1, std::min(nl, (int)NLIST));

@@ -202,7 +202,10 @@ struct Bat {
     // logged batch created (role B, in member order), the run's creations so
     // far (the formation's guess per member), and the guess itself
     uint32_t cnew[BK];
-    uint32_t crate, pad7;
+    uint32_t crate;
+    uint32_t skr;                       // the skipped keys' decrement as a share of their count (2^-16), the run's
+                                        // running estimate from the batches' minima (k_bapply); 0: none yet.  The
+                                        // formation ends a batch before a member it predicts to fail against them
     unsigned long long ncre;
 };
 

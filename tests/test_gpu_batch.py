@@ -208,17 +208,18 @@ def test_table_layouts_agree_on_batches(monkeypatch):
     assert out[0][2] > 0
 
 
-@pytest.mark.parametrize("skip,list2,test", [("0", "0", "0"), ("1", "0", "0"), ("1", "1", "0"), ("1", "1", "1")])
-def test_formation_variants_match_oracle(skip, list2, test, monkeypatch):
+@pytest.mark.parametrize("skip,nlist,test", [("0", "1", "0"), ("1", "1", "0"), ("1", "2", "0"), ("1", "4", "0"),
+                                             ("1", "4", "1")])
+def test_formation_variants_match_oracle(skip, nlist, test, monkeypatch):
     """Skipped keys (BPE_SKIP: a listed key that does not commute with an
     earlier member is passed over, and every later member must beat its count
-    after that member's decrements) and the second list (BPE_LIST2: members
-    from the next 64 keys once the first 64 are used up) change only how many
-    merges a batch holds: merges and ids == the oracle's RULE order.
-    BPE_SKIP_TEST: every such check fails, so the batches are re-formed
-    before the first member after a skipped key (the retry path)."""
+    after that member's decrements) and the later lists (BPE_NLIST: members
+    from the next 64 keys once a list is used up, up to 127 members) change
+    only how many merges a batch holds: merges and ids == the oracle's RULE
+    order.  BPE_SKIP_TEST: every such check fails, so the batches are
+    re-formed before the first member after a skipped key (the retry path)."""
     monkeypatch.setenv("BPE_SKIP", skip)
-    monkeypatch.setenv("BPE_LIST2", list2)
+    monkeypatch.setenv("BPE_NLIST", nlist)
     monkeypatch.setenv("BPE_SKIP_TEST", test)
     skipped = failed = retries = 0
     for data, mm in _small_cases()[::2] + [(synth_bytes(508, 1 << 20), 800), (synth_bytes(509, 3 << 20), 1200)]:
@@ -226,7 +227,7 @@ def test_formation_variants_match_oracle(skip, list2, test, monkeypatch):
         skipped += st["keys_skipped"]
         failed += st["skip_failed"]
         retries += st["batch_retries"]
-    print("skip", skip, "list2", list2, "test", test, {"skipped": skipped, "skip_failed": failed, "retries": retries})
+    print("skip", skip, "nlist", nlist, "test", test, {"skipped": skipped, "skip_failed": failed, "retries": retries})
     if skip == "1" and test == "0":
         assert skipped > 0
     if test == "1":  # (re-formed, or a verified prefix applied alone)

@@ -34,4 +34,4 @@ print(json.dumps({"batch": os.environ.get("BPE_BATCH", "1"), "merges": int(st["m
                   "retries": int(st["batch_retries"]), "tie_verified": int(st["tie_verified"]),
                   "tie_failed": int(st["tie_failed"]), "keys_zeroed": int(st["keys_zeroed"]),
                   "keys_skipped": int(st["keys_skipped"]), "skip_failed": int(st["skip_failed"]),
-                  "end": {k[4:]: int(st[k]) for k in st if k.startswith("end_") and k != "end_unused"}}))
+                  "end": {k[4:]: int(st[k]) for k in st if k.startswith("end_")}}))
