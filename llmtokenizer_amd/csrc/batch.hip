@@ -926,6 +926,13 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
             B->over = ovm < k ? ovm : BK;
             B->tpend = tpend < k ? tpend : BK;
             Bg->nsk = nsk;
+            Bg->gr_n = 0;
+#pragma unroll
+            for (uint32_t g = 0; g < GRUN; g++) {
+                Bg->gr_tk[g] = 0;
+                Bg->gr_endc[g] = 0xFFFFFFFFu;
+                Bg->gr_ready[g] = 0;
+            }
             B->ztot = 0;
             B->tbar = 0;
             B->tlog_n = 0;
@@ -1289,6 +1296,22 @@ __device__ inline void vadd_b(uint32_t (*s)[DENSE], const Eng *E, uint32_t m, in
     if (v == V_DL || v == V_DR) atomicAdd(&gcnt[v], 1u);
 }
 
+// one add of cnt to member m's vector v at id x straight into its global
+// accumulators (replica 0 below DENSE, else the list): the chunked long runs,
+// walked by blocks of any member
+__device__ inline void vadd_g(const Eng *E, uint32_t m, int v, uint32_t x, uint32_t cnt) {
+    if (!cnt) return;
+    if (x < DENSE) {
+        atomicAdd(&E->bvecd[((uint64_t)m * BREPL * 4 + v) * DENSE + x], cnt);
+        return;
+    }
+    const uint64_t base = ((uint64_t)m * 4 + v) * E->bvs;
+    if (atomicAdd(&E->bvec[base + (x - DENSE)], cnt) == 0) {
+        const uint32_t p = atomicAdd(&E->bvnl[m * 4 + v], 1u);
+        E->bvlist[base + p] = x;
+    }
+}
+
 // sharded: one add of member m, vector v, id x into the exchange (dense
 // below Wx, else my list of ids >= DENSE, which k_bpack packs)
 __device__ inline void xadd(const Eng *E, uint32_t *xo, uint32_t Wx, uint32_t m, int v, uint32_t x) {
@@ -1356,6 +1379,201 @@ __device__ inline uint32_t starts_of(const uint32_t *__restrict__ tok, const Rol
     return rt.member(q, tok_at_b<SH>(tok, H, kn, n));
 }
 
+// The chunked long runs (one-shard runs).  A thread walking an a == a run
+// that still goes on GR_PROBE tokens past its hand-off registers the rest of
+// it (Bat::gr_*: from an even run index, so pairs start at even chunk
+// offsets); every wave of the launch, once its block is done with its own
+// work, takes chunks of GR_CH tokens by ticket -- no block barrier anywhere.
+// A chunk reads its tokens (where the run ends inside it, if it does) and
+// publishes that (LOCAL: goes on / ends here), then finds whether the run
+// reaches it by a decoupled look-back over its predecessors' flags (the first
+// INCLUSIVE one decides; a LOCAL "goes on" passes the look-back further left,
+// a LOCAL "ends here" means not reached), publishes its INCLUSIVE flag and --
+// when reached -- emits its pairs exactly as the block walk would:
+// occurrence, tag nb_tag(z, right), deltas DR[right] / IR[right's new id] of
+// the run's member (straight into its global accumulators; interior pairs
+// aggregated: their right neighbour is a, its new id z), its bound raised by
+// the pairs.  A look-back only waits for a LOCAL flag, which its chunk
+// publishes without waiting on anything (the chunk was claimed earlier, so
+// it runs already); every wait is bounded (B->ra_err = 11).
+enum : uint32_t { GRF_LGO = 1, GRF_LEND = 2, GRF_IGO = 3, GRF_IEND = 4 };  // chunk flag states (low 3 bits)
+__device__ void bscan_long_runs(const Eng *__restrict__ E, Bat *__restrict__ B, const uint32_t *__restrict__ tok,
+                                const RoleTab &rt, const BHalo &H, int64_t n, uint32_t z0, uint32_t sgen) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t ng = uni(min(aload(&B->gr_n), GRUN));
+    const uint64_t stride = gr_stride(E->n0), maxch = stride - 1;
+    auto flag_of = [&](uint32_t st) { return (sgen << 3) | st; };
+    for (uint32_t gi = 0; gi < ng; gi++) {  // (wave-uniform)
+        uint32_t ok = 1;
+        if (lane == 0) {
+            const unsigned long long t0 = wall_clock64();
+            while (__hip_atomic_load(&B->gr_ready[gi], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != sgen) {
+                if (wall_clock64() - t0 > E->gr_wait) {
+                    ok = 0;
+                    B->ra_err = 11;
+                    atomicAdd(&B->gr_tready, 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (!uni((uint32_t)__shfl((int)ok, 0))) return;
+        const uint32_t mg = uni(aload(&B->gr_m[gi])), ag = uni(B->a[mg]), zg = z0 + mg;
+        const int64_t c0 = uni(aload(&B->gr_c[gi])), lag = uni(E->tlen[ag]);
+        uint32_t *occg = E->ids_out + B->sbase[mg];
+        uint16_t *tagg = E->btag + B->sbase[mg];
+        const uint32_t slice = B->sbase[mg + 1] - B->sbase[mg];  // (the member's staging capacity)
+        uint32_t *flags = E->grflag + (uint64_t)gi * stride;
+        auto pos = [&](int64_t l) -> int64_t { return c0 + l * lag; };
+        auto tk = [&](int64_t l) -> uint32_t {
+            const int64_t p = pos(l);
+            return p < n ? tok[p] : HOLE;
+        };
+        for (;;) {  // (wave-uniform) chunks by ticket
+            uint32_t chl = 0, endl = 0;
+            if (lane == 0) {
+                chl = atomicAdd(&B->gr_tk[gi], 1u);
+                endl = aload(&B->gr_endc[gi]);
+            }
+            const uint32_t ch = uni((uint32_t)__shfl((int)chl, 0)), endc = uni((uint32_t)__shfl((int)endl, 0));
+            if (ch >= maxch) break;  // (chunks from maxch on start past the corpus: never a flag there)
+            if (ch > endc) {  // (past the run's end; a later ticket may not see the end yet: it finds this one ended)
+                if (lane == 0) __hip_atomic_store(&flags[ch], flag_of(GRF_IEND), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            const int64_t cb = (int64_t)ch * GR_CH;  // the chunk's first run index (from c0)
+            // where the run ends inside the chunk: the first offset whose token
+            // is not a (GR_CH: none); 4 segments' loads in flight per step
+            uint32_t fe = GR_CH;
+            for (uint32_t o = 0; o < GR_CH && fe == GR_CH; o += 4 * 64) {  // (wave-uniform)
+                uint32_t t[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) t[u] = tk(cb + o + 64 * u + lane);
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) {
+                    const unsigned long long nm = __ballot(t[u] != ag);
+                    if (nm && fe == GR_CH) fe = o + 64 * u + (uint32_t)__builtin_ctzll(nm);
+                }
+            }
+            fe = uni(fe);
+            // publish LOCAL, look back for the INCLUSIVE status (64 predecessors
+            // per round trip, one per lane: the nearest one that is not a
+            // LOCAL "goes on" decides -- INCLUSIVE "goes on" or the run start:
+            // reached; an end: not reached; not published yet: wait), publish
+            // INCLUSIVE.  (Relaxed: the flags publish no data; tok[] is
+            // read-only during the scan.)
+            if (lane == 0)
+                __hip_atomic_store(&flags[ch], flag_of(fe == GR_CH ? GRF_LGO : GRF_LEND), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t reached = 1;
+            {
+                const unsigned long long t0 = wall_clock64();
+                for (int64_t base = (int64_t)ch - 1; base >= 0;) {  // (wave-uniform)
+                    const int64_t jj = base - (int64_t)lane;
+                    uint32_t st = GRF_IGO;  // (before chunk 0: the run's start)
+                    if (jj >= 0) {
+                        const uint32_t f = __hip_atomic_load(&flags[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        st = (f >> 3) == sgen ? (f & 7u) : 0u;
+                    }
+                    const unsigned long long nm = __ballot(st != GRF_LGO);
+                    if (!nm) {
+                        base -= 64;
+                        continue;
+                    }
+                    const uint32_t stk = (uint32_t)__shfl((int)st, (int)__builtin_ctzll(nm));
+                    if (stk == 0) {  // (not published yet: its chunk runs and publishes LOCAL without waiting)
+                        if (wall_clock64() - t0 > E->gr_wait) {
+                            if (lane == 0) {
+                                B->ra_err = 11;
+                                atomicAdd(&B->gr_tchunk, 1u);
+                            }
+                            reached = 0;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    reached = stk == GRF_IGO;
+                    break;
+                }
+            }
+            reached = uni(reached);
+            if (lane == 0) {
+                const bool goes_on = reached && fe == GR_CH;
+                __hip_atomic_store(&flags[ch], flag_of(goes_on ? GRF_IGO : GRF_IEND), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                if (!goes_on) atomicMin(&B->gr_endc[gi], ch);
+            }
+            if (!reached) continue;
+            // the pairs: even offsets e with e + 1 < fe
+            uint32_t nint_dr = 0, nint_ir = 0, npairs = 0;
+            MK tadj = mk_zero();
+            for (uint32_t o4 = 0; o4 < fe; o4 += 4 * 64) {  // (wave-uniform; 4 segments' loads in flight)
+              uint32_t t4[4], tx4[4];
+#pragma unroll
+              for (uint32_t u = 0; u < 4; u++) {
+                  t4[u] = o4 + 64 * u < fe ? tk(cb + o4 + 64 * u + lane) : HOLE;
+                  tx4[u] = o4 + 64 * u < fe && lane < 2 ? tk(cb + o4 + 64 * u + 64 + lane) : HOLE;
+              }
+#pragma unroll
+              for (uint32_t u = 0; u < 4; u++) {
+                const uint32_t o = o4 + 64 * u;
+                if (o >= fe) break;
+                const int64_t l = cb + o + lane;
+                const uint32_t t = t4[u];
+                const uint32_t tx = tx4[u];
+                const uint32_t t64 = (uint32_t)__shfl((int)tx, 0), t65 = (uint32_t)__shfl((int)tx, 1);
+                const uint32_t d2 = (uint32_t)__shfl_down((int)t, 2), d3 = (uint32_t)__shfl_down((int)t, 3);
+                const uint32_t q = lane + 2 < 64 ? d2 : t64;
+                const uint32_t q3 = lane + 3 < 64 ? d3 : (lane + 3 == 64 ? t64 : t65);
+                const uint32_t f = min(fe - o, 64u);
+                const bool pair = (lane & 1) == 0 && lane + 1 < f;
+                const bool knext = q == ag, nocc = knext && q3 == ag;
+                const uint32_t sm_ = (pair && !knext && q != HOLE) ? starts_of<false>(tok, rt, H, q, pos(l + 2), n) : BK;
+                if (sm_ < BK) mk_set(tadj, sm_);
+                const uint32_t rq = nocc ? zg : sm_ < BK ? z0 + sm_ : q;
+                const unsigned long long pm = __ballot(pair);
+                uint32_t g = 0;
+                if (lane == 0 && pm) g = atomicAdd(&B->R[mg], (uint32_t)__popcll(pm));
+                g = (uint32_t)__shfl((int)g, 0);
+                if (pair) {
+                    const uint32_t r = g + (uint32_t)__popcll(pm & ((1ull << lane) - 1ull));
+                    if (r < slice) {
+                        occg[r] = (uint32_t)pos(l);
+                        tagg[r] = nb_tag(zg, rq);
+                    } else {
+                        B->ra_err = 12;  // (never: a run's pairs are candidates of its member)
+                    }
+                    npairs++;
+                    if (q != HOLE) {
+                        if (q == ag) nint_dr++;
+                        else vadd_g(E, mg, V_DR, q, 1u);
+                        if (rq == zg) nint_ir++;
+                        else vadd_g(E, mg, V_IR, rq, 1u);
+                    }
+                }
+              }
+            }
+            nint_dr = wave_sum(nint_dr);
+            nint_ir = wave_sum(nint_ir);
+            npairs = wave_sum(npairs);
+            if (lane == 0) {
+                vadd_g(E, mg, V_DR, ag, nint_dr);
+                vadd_g(E, mg, V_IR, zg, nint_ir);
+                // (the bound: no key the run makes counts more than its pairs)
+                if (npairs) atomicAdd(&B->bound[mg], npairs);
+                atomicAdd(&B->nchunks, 1ull);
+            }
+#pragma unroll
+            for (uint32_t bb = 0; bb < NBK; bb++) {
+                unsigned long long tm = tadj.w[bb];
+                for (int o = 32; o > 0; o >>= 1) tm |= __shfl_xor(tm, o);
+                if (lane == 0 && tm) atomicOr(&B->adj[mg][bb], tm);
+            }
+        }
+    }
+}
+
 // Every member's occurrences in the pre-batch tokens and the batch's count
 // deltas.  SH (sharded corpus): neighbours beyond my edges come from the
 // halo; an occurrence whose a is my last token and whose b starts the next
@@ -1382,6 +1600,8 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     __shared__ BHalo H;
     __shared__ uint32_t wmx[2][16];
     const uint32_t tid = threadIdx.x;
+    // this scan's generation (the chunk flags of the long runs carry it)
+    const uint32_t sgen = ((uint32_t)(B->nbatch + B->nretry) & 0x0FFFFFFFu) + 1u;
     if (tid == 0) {
         sm = BK;
         covc = lcount = bRs = 0;
@@ -1434,6 +1654,11 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     const uint32_t sbase = B->sbase[m];
     uint32_t *occz = E->ids_out + sbase;
     uint16_t *tagz = E->btag + sbase;
+    // every staging store stays inside the member's slice (its candidates:
+    // an occurrence is one); one that would not is an error (B->ra_err = 12:
+    // k_bapply applies nothing, the select stops the run), never a stray store
+    const uint32_t sslice = B->sbase[m + 1] - sbase;
+#define STG(IDX, WHERE) if ((IDX) >= sslice) { B->ra_err = 12; } else
     uint32_t *Rm = &B->R[m];
     const int64_t n = (int64_t)E->n0;
     const uint32_t *__restrict__ tok = E->tok;
@@ -1599,8 +1824,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 if (lane == 0 && wcnt) g = atomicAdd(Rm, wcnt);
                 g = __shfl(g, 0);
                 for (uint32_t q = lane; q < wcnt; q += 64) {
+                    STG(g + q, "wflush") {
                     occz[g + q] = list[wbase + q];
                     tagz[g + q] = ltag[wbase + q];
+                    }
                 }
                 wocc += wcnt;
                 wcnt = 0;
@@ -1619,8 +1846,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 }
                 __syncthreads();
                 for (uint32_t q = tid; q < list_n; q += SCAN_T) {
+                    STG(gbase + q, "bflush") {
                     occz[gbase + q] = list[q];
                     tagz[gbase + q] = ltag[q];
+                    }
                 }
                 __syncthreads();
             }
@@ -1681,8 +1910,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                 } else {  // (a long run overflows the round's list: straight out)
                     const uint32_t g = atomicAdd(Rm, 1u);
                     atomicAdd(&bRs, 1u);
+                    STG(g, "tstraight") {
                     occz[g] = (uint32_t)pos;
                     tagz[g] = nb_tag(pfin, rq);
+                    }
                 }
                 if (mi == 0 && left) {
                     vadd_b(s, E, m, V_DL, p, gcnt);
@@ -1693,8 +1924,20 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     vadd_b(s, E, m, V_IR, rq, gcnt);
                 }
                 if (!knext || kq >= n) break;
-                // a long run: the rest goes to a wave (next pair at an even run index)
+                // a long run: the rest goes to a wave (next pair at an even run
+                // index), or -- when it still goes on GR_PROBE tokens ahead (one
+                // byte repeated) -- into chunks any block of the launch takes
                 if (mi + 1 >= RUN_THREAD_PAIRS && nocc) {
+                    if (!SH && E->grflag && kq + (int64_t)GR_PROBE * la < n && tok[kq + (int64_t)GR_PROBE * la] == a) {
+                        const uint32_t gi = atomicAdd(&B->gr_n, 1u);
+                        if (gi < GRUN) {
+                            B->gr_c[gi] = (uint32_t)kq;
+                            B->gr_m[gi] = m;
+                            atomicAdd(&B->gr_nreg, 1u);
+                            __hip_atomic_store(&B->gr_ready[gi], sgen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                    }
                     const uint32_t qs = atomicAdd(&lr_n, 1u);
                     if (qs < RUN_Q) {
                         lr_pos[qs] = (uint32_t)kq;
@@ -1713,8 +1956,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
             }
             __syncthreads();
             for (uint32_t q = tid; q < list_n; q += SCAN_T) {
+                STG(gbase + q, "tflush") {
                 occz[gbase + q] = list[q];
                 tagz[gbase + q] = ltag[q];
+                }
             }
             __syncthreads();
         }
@@ -1778,8 +2023,10 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     g = (uint32_t)__shfl((int)g, 0);
                     if (pair) {
                         const uint32_t r = g + (uint32_t)__popcll(pm & ((1ull << lane) - 1ull));
+                        STG(r, "segs") {
                         occz[r] = (uint32_t)P[u];
                         tagz[r] = nb_tag(z, rq);
+                        }
                         if (q != HOLE) {
                             vadd_b(s, E, m, V_DR, q, gcnt);
                             vadd_b(s, E, m, V_IR, rq, gcnt);
@@ -1822,6 +2069,7 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
         }
     }
     __syncthreads();
+    if (!SH && E->grflag) bscan_long_runs(E, B, tok, rt, H, n, z0, sgen);
     ts_mark(E, bi, BT_SCAN_CAND, false, true);
     // the skipped keys my member lowers (Bat::sk_*): a key (x, y) loses the
     // pairs whose x is my b (my right neighbours y) and whose y is my a (my
@@ -2093,7 +2341,9 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
             }
         }
     }
-    if (C->stop) return;
+    // (a scan error -- a long run's chunk wait or staging: B->ra_err -- applies
+    // nothing; the next select stops the run with it)
+    if (C->stop || aload(&B->ra_err)) return;
     const uint32_t bi = bat_idx(E);
     ts_mark(E, bi, BT_APPLY_IN, true);
     if (threadIdx.x == 0) atomicMax(&B->ap_in, ~wall_clock64());

@@ -575,6 +575,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.btag = nullptr;
     h.bvecd = h.bvec = h.bvlist = h.bvnl = nullptr;
     h.tlog = nullptr;
+    h.grflag = nullptr;
     h.tlog_cap = 0;
     h.bvs = h.vcap > DENSE ? h.vcap - DENSE : 1;
     if (h.batch) {
@@ -584,6 +585,13 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         if ((r = dalloc(c, &h.bvec, (size_t)BK * 4 * h.bvs))) return r;
         if ((r = dalloc(c, &h.bvlist, (size_t)BK * 4 * h.bvs, false))) return r;
         if ((r = dalloc(c, &h.bvnl, (size_t)BK * 4))) return r;
+        // long a == a runs walked in chunks by any scan block (cleared: no stale generation matches)
+        if (!c->sharded && getenv_int("BPE_GR", 1) && (r = dalloc(c, &h.grflag, (size_t)GRUN * gr_stride(n0)))) return r;
+        {
+            int khz = 0;
+            (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->dev);
+            h.gr_wait = (unsigned long long)std::max(1, getenv_int("BPE_GR_WAIT_MS", 20000)) * (unsigned long long)std::max(1, khz);
+        }
         // verified tie order: the undo log (records of 2 words)
         h.tlog_cap = 1u << 22;
         if ((r = dalloc(c, &h.tlog, 2ull * h.tlog_cap, false))) return r;
@@ -1390,7 +1398,7 @@ int drive(bpe_gpu_ctx *c, bool encode, uint32_t n_enc) {
             return 0;
         case STOP_ERROR:
             return fail(C.err == 5 ? BPE_GPU_ERANGE : BPE_GPU_EINTERNAL,
-                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than an end code holds (2^31 - 3 bytes)" : C.err == 7 ? "tracked iterations: the light pass waited for the track block in vain" : C.err == 9 ? "batch apply: the tie-verification barrier timed out" : C.err == 10 ? "batch formation made no progress (64 batches in a row applied no merge)" : "thread-stat table full");
+                    C.err == 1 ? "engine invariant violated (count decrement of an absent pair)" : C.err == 2 ? "pair table full" : C.err == 3 ? "thread-stat lookup failed" : C.err == 5 ? "a token longer than an end code holds (2^31 - 3 bytes)" : C.err == 7 ? "tracked iterations: the light pass waited for the track block in vain" : C.err == 9 ? "batch apply: the tie-verification barrier timed out" : C.err == 10 ? "batch formation made no progress (64 batches in a row applied no merge)" : C.err == 11 ? "batch scan: a chunk of a long run waited for its predecessor in vain" : C.err == 12 ? "batch scan: a long run's pairs overflowed its member's staging" : "thread-stat table full");
         case STOP_REDO:  // missed prediction: k_select committed the real merge
             C.stop = STOP_NONE;
             if ((r = push_ctl(c))) return r;
@@ -1595,6 +1603,14 @@ int batch_stats(bpe_gpu_ctx *c) {
         }
     }
     if (c->h.dbgts) print_batch_timeline(c, hb.nbatch + hb.nretry);
+    if (getenv("BPE_DEBUG") && c->h.grflag) {
+        uint32_t g[4] = {0, 0, 0, 0};
+        unsigned long long nch = 0;
+        HIPCHK(hipMemcpy(g, &c->h.bat->gr_tready, 16, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&nch, &c->h.bat->nchunks, 8, hipMemcpyDeviceToHost));
+        fprintf(stderr, "long runs: %u registered, %llu chunks walked, wait timeouts %u (registration) %u (chunk)\n", g[2],
+                nch, g[0], g[1]);
+    }
     if (getenv("BPE_DEBUG"))
         fprintf(stderr, "batches %llu, dropped %llu, re-formed %llu; formation ended by: list %llu, cap/count/hot_T %llu, a==b %llu, "
                 "duplicate %llu, tie %llu, conflict %llu, table margin %llu, staging %llu; tie-verified %llu (re-formed %llu); "

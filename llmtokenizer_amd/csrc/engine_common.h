@@ -131,6 +131,13 @@ constexpr uint32_t BREPL = 2;   // replicas of a member's dense delta accumulato
 constexpr uint32_t BSB = 256;   // k_bscan blocks (1024 threads, one per CU)
 constexpr uint32_t STALL_LIMIT = 64;  // consecutive batches without a merge before the run fails (never legit:
                                       // a re-formed batch always verifies its first member)
+// a == a runs longer than a block walks quickly (one byte repeated: one run
+// of the whole corpus) are split into chunks of GR_CH tokens that any k_bscan
+// wave may take (Bat::gr_*): up to GRUN such runs per batch, one-shard runs
+constexpr uint32_t GRUN = 4;
+constexpr uint32_t GR_CH = 16384;     // run tokens per chunk (even; one wave walks a chunk)
+constexpr uint32_t GR_PROBE = 4096;   // a run whose token this many past the hand-off is still its id goes global
+__host__ __device__ inline uint64_t gr_stride(uint64_t n0) { return n0 / GR_CH + 2; }  // chunk flags per run
 constexpr uint32_t P2P_MAXR_B = 16;  // shards of a sharded batch run (BPE_GPU_P2P_MAX_RANKS; the gathered lists)
 
 struct Bat {
@@ -203,6 +210,14 @@ struct Bat {
     // far (the formation's guess per member), and the guess itself
     uint32_t cnew[BK];
     uint32_t crate;
+    // chunked long runs (k_bscan): registered runs, their continuation (an
+    // even run index), member, chunk ticket, first chunk where the run ended,
+    // registration published (the scan's generation)
+    uint32_t gr_n, gr_pad;
+    uint32_t gr_c[GRUN], gr_m[GRUN], gr_tk[GRUN], gr_endc[GRUN], gr_ready[GRUN];
+    unsigned long long nchunks;         // chunks of long runs walked (stats)
+    uint32_t gr_tready, gr_tchunk;      // waits for a registration / a chunk's predecessor that timed out
+    uint32_t gr_nreg, gr_pad2;          // runs registered (all batches)
     uint32_t skr;                       // the skipped keys' decrement as a share of their count (2^-16), the run's
                                         // running estimate from the batches' minima (k_bapply); 0: none yet.  The
                                         // formation ends a batch before a member it predicts to fail against them
@@ -324,6 +339,8 @@ struct Eng {
     uint32_t *bvlist;     // [BK][4][bvs]
     uint32_t *bvnl;       // [BK][4] list lengths
     uint32_t *xbat;       // sharded batches: the exchange buffer (xbat_words), zero between batches
+    uint32_t *grflag;     // [GRUN][gr_stride(n0)] chunk states of the long runs, (scan generation << 2) | state
+    unsigned long long gr_wait;  // wall-clock ticks a chunk waits for its predecessor (BPE_GR_WAIT_MS; ~21 s)
     // sharded batches with ids >= DENSE: my (member-vector << 24 | id, delta)
     // list of them ([0] entries, [1] unused, then pairs; xsp_cap entries at
     // most), and every shard's list gathered ([nshards][xsp_stride] words)

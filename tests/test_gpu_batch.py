@@ -149,6 +149,24 @@ def test_long_runs_match_oracle():
     _check(b"b" + b"a" * ((1 << 20) + 3) + b"c", 3)
 
 
+def test_chunked_long_runs_match_oracle():
+    """a == a runs that still go on GR_PROBE tokens past the thread walk's
+    hand-off are walked in chunks of GR_CH tokens by any block (k_bscan,
+    bscan_long_runs): run ends around chunk edges (the chunks start 32 run
+    indices after the run's first token), more long runs in one batch than
+    the GRUN chunked slots (the rest walk in their blocks), runs of merged
+    tokens (la = 2: "xy" repeated, then (z, z)), a run ending at the corpus
+    end, and runs whose last pair's right neighbour starts another member's
+    occurrence"""
+    CH = 16384
+    parts = [b"a" * (32 + 2 * CH + d) + b"b" for d in (-3, -2, -1, 0, 1, 2, 3)]
+    _check(b"".join(parts), 3)
+    _check(b"".join(b"q" * (6000 + 977 * k) + b"r" for k in range(7)), 4)  # (7 long runs)
+    _check(b"xy" * 120000, 3)
+    _check(b"c" + b"a" * (3 * CH + 5), 2)
+    _check((b"a" * (CH + 4097) + b"bc") * 3, 6)
+
+
 def test_cap_inside_a_batch():
     """a merge cap that ends the run in the middle of a batch"""
     data = synth_bytes(504, 256 << 10)
