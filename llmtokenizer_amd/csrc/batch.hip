@@ -1505,7 +1505,12 @@ __device__ void bscan_long_runs(const Eng *__restrict__ E, Bat *__restrict__ B, 
                 if (!goes_on) atomicMin(&B->gr_endc[gi], ch);
             }
             if (!reached) continue;
-            // the pairs: even offsets e with e + 1 < fe
+            // the pairs: even offsets e with e + 1 < fe, fe / 2 of them, staged in
+            // order from one reservation per chunk (a reservation per segment
+            // put every wave of the launch on one counter: 200 ms for 1 GiB)
+            uint32_t rb = 0;
+            if (lane == 0 && fe >= 2) rb = atomicAdd(&B->R[mg], fe / 2);
+            rb = (uint32_t)__shfl((int)rb, 0);
             uint32_t nint_dr = 0, nint_ir = 0, npairs = 0;
             MK tadj = mk_zero();
             for (uint32_t o4 = 0; o4 < fe; o4 += 4 * 64) {  // (wave-uniform; 4 segments' loads in flight)
@@ -1532,12 +1537,8 @@ __device__ void bscan_long_runs(const Eng *__restrict__ E, Bat *__restrict__ B, 
                 const uint32_t sm_ = (pair && !knext && q != HOLE) ? starts_of<false>(tok, rt, H, q, pos(l + 2), n) : BK;
                 if (sm_ < BK) mk_set(tadj, sm_);
                 const uint32_t rq = nocc ? zg : sm_ < BK ? z0 + sm_ : q;
-                const unsigned long long pm = __ballot(pair);
-                uint32_t g = 0;
-                if (lane == 0 && pm) g = atomicAdd(&B->R[mg], (uint32_t)__popcll(pm));
-                g = (uint32_t)__shfl((int)g, 0);
                 if (pair) {
-                    const uint32_t r = g + (uint32_t)__popcll(pm & ((1ull << lane) - 1ull));
+                    const uint32_t r = rb + (o + lane) / 2;
                     if (r < slice) {
                         occg[r] = (uint32_t)pos(l);
                         tagg[r] = nb_tag(zg, rq);
