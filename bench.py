@@ -27,7 +27,7 @@ The line also carries
                   algorithmic bytes per launch (8 B/candidate + 20 B/occurrence)
                   and its average span from the device wall clock, both over
                   the LAST timed job; the committed rocprofv3 summary and PMC
-                  traffic of this same command (profiles/r5_*) beside them;
+                  traffic of this same command (profiles/<PROFILE_TAG>_*) beside them;
   roofline_apply  the batch apply k_bapply (table updates, 16 B each), same way;
   roofline_count_pass  the corpus-wide pair-count pass (1 B/token read; the
                   initial u32 ids are written by the counting sort's first
@@ -56,7 +56,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 GIB = 1 << 30
-PROFILE_TAG = "r5"     # profiles/<tag>_train_kernel_stats.csv, <tag>_pmc_traffic.json (tools/gpu_profile.sh)
+PROFILE_TAG = "r6"     # profiles/<tag>_train_kernel_stats.csv, <tag>_pmc_traffic.json (tools/gpu_profile.sh)
 
 
 def count_pass_kernel(form):
