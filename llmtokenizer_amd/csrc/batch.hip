@@ -491,7 +491,7 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
         if (applied && oldnsk) {
             if (retry || jst < kpr) {
                 ske = min(ske + 1u, 7u);
-                if (ske >= 2) skg = 1u << ske;
+                if (ske >= E->skg_exp) skg = 1u << ske;
             } else if (ske) {
                 ske--;
             }

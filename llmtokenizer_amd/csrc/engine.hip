@@ -555,6 +555,9 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     // (BPE_SKIP=0: the formation ends there, as before round 5)
     h.skip_on = (uint32_t)(getenv_int("BPE_SKIP", 1) != 0);
     if (h.skip_on && getenv_int("BPE_SKIP_TEST", 0)) h.skip_on = 2;  // (tests: every skipped key's check fails)
+    // skipping backs off after 2 consecutive failures of batches with
+    // skipped keys (BPE_SKGATE: that count; 8 never backs off)
+    h.skg_exp = (uint32_t)getenv_int("BPE_SKGATE", 2);
     // and take members from the next TOPK keys once a list is used up, up to
     // nlists lists (BPE_NLIST; BPE_LIST2=1 is two lists, the round-5 knob)
     {
