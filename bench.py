@@ -669,6 +669,13 @@ def main():
                                   "rocprof_summary": sp.get("rocprof_summary"),
                                   "note": "hot-set reduce (16 B/key) + the previous batch's rewrite (12 B per "
                                           "occurrence, one dirtied sector each); device wall clock per launch"}
+        # its own random-access rate: the rewrite's paired token stores (the
+        # new id at the occurrence, the end code at its end slot) per span
+        lr = line_rate(st["occurrences"] / st["select_launches"] / (st["ms_select_span"] * 1e-3), "store_pair", 16,
+                       "occurrences rewritten per k_bsel launch / its span (the select's own latency chain "
+                       "runs beside the rewrite blocks in the same span)")
+        if lr:
+            out["roofline_select"]["line_rate"] = lr
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.seed, args.cpu_size, args.cpu_merges)
     if enc is not None:

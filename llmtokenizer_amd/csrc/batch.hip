@@ -81,6 +81,29 @@ constexpr uint32_t FR = BPE_FR;
 #define BPE_SCAN_PF 1
 #endif
 constexpr uint32_t RU = BPE_RU;  // rewrite occurrences per thread per round
+#ifndef BPE_SCAN_PD
+#define BPE_SCAN_PD 1
+#endif
+constexpr uint32_t SCAN_PD = BPE_SCAN_PD;  // k_bscan: list segments per wave loaded ahead (1 or 2)
+
+// the position of the r-th set bit (from 0) of M, r < popcount(M): a
+// six-step binary search on the halves' popcounts
+__device__ __attribute__((always_inline)) inline uint32_t kth_bit(unsigned long long M, uint32_t r) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t w = 32; w; w >>= 1) {
+        const unsigned long long lo = M & ((1ull << w) - 1ull);
+        const uint32_t c = (uint32_t)__popcll(lo);
+        if (r >= c) {
+            r -= c;
+            M >>= w;
+            pos += w;
+        } else {
+            M = lo;
+        }
+    }
+    return pos;
+}
 
 // debug timeline of a batch (BPE_DEBUG_TS; E->dbgts rows indexed by batch)
 enum { BT_SCAN_IN = 0, BT_SCAN_CAND, BT_SCAN_OUT, BT_APPLY_IN, BT_APPLY_PRO, BT_APPLY_A, BT_APPLY_B, BT_SEL_IN,
@@ -883,15 +906,27 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
         }
         const unsigned long long stage_end = bank_shfl(pre, k - 1);
         sumlen = wave_sum(sumlen);
-        // scan blocks in proportion to the candidate lists (>= 1 each), the
-        // rest to the largest member
-        unsigned long long big = 0;
+        // scan blocks in proportion to the members' work (>= 1 each), the
+        // rest to the largest member.  A byte pair's list entry costs a window
+        // gather; an occurrence list's entry costs a streamed (position, tag)
+        // read unless its tag passes, and about as many pass as the member's
+        // count (text: merged ids' lists are long and mostly filtered, so
+        // weighting by entries starves the byte pairs; E->scan_occd)
+        uint32_t wk[NBK];
+        unsigned long long sumw = 0, big = 0;
 #pragma unroll
         for (uint32_t b = 0; b < NBK; b++) {
             const uint32_t q = 64 * b + lane;
-            nb[b] = q < k ? 1 + (uint32_t)(sumlen ? (uint64_t)(BSB - k) * len[b] / sumlen : 0) : 0;
+            wk[b] = q < k && mode[b] != 0 && E->scan_occd ? min(len[b], fm_c[q] + len[b] / E->scan_occd) : len[b];
+            sumw += q < k ? wk[b] : 0u;
+        }
+        sumw = wave_sum(sumw);
+#pragma unroll
+        for (uint32_t b = 0; b < NBK; b++) {
+            const uint32_t q = 64 * b + lane;
+            nb[b] = q < k ? 1 + (uint32_t)(sumw ? (uint64_t)(BSB - k) * wk[b] / sumw : 0) : 0;
             bpre[b] = nb[b];
-            if (q < k) big = max(big, ((unsigned long long)len[b] << 8) | (255u - q));
+            if (q < k) big = max(big, ((unsigned long long)wk[b] << 8) | (255u - q));
         }
         bank_scan(bpre);
         for (int o = 32; o > 0; o >>= 1) big = max(big, (unsigned long long)__shfl_xor(big, o));
@@ -1672,44 +1707,95 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
     auto tok_at = [&](int64_t p) -> uint32_t { return tok_at_b<SH>(tok, H, p, n); };
 
     if (a != b) {
-        // SU candidates per thread per round, in stages, so that their chains of
-        // dependent gathers overlap; the round's occurrences are staged in LDS
-        // and leave with one global atomic per block
-        // the next round's list entries are loaded while this round runs
-        const uint32_t stride = nblk * SCAN_T * SU;
+        // Rounds of 64 list entries per wave (one per lane), each wave on its
+        // own segments (block stride); the round's occurrences are staged in
+        // the wave's LDS slice and leave with one global atomic per wave.  The
+        // next segment's entries load while a round runs.  An occurrence
+        // list's entries (mode 1 / 2) are mostly other neighbours' (text: ~6
+        // entries per occurrence), so there the entries whose tag passes are
+        // packed into whole rounds first (E->scan_compact): a round's chain
+        // of dependent gathers then serves 64 occurrences, not ~10.
+        static_assert(SU == 1 && BPE_WFLUSH, "the wave-driven candidate loop: one entry per lane per round");
+        const uint32_t stride = nblk * SCAN_T;
+        const uint32_t lane = tid & 63, wbase = (tid >> 6) * 64 * FR;
+        uint32_t wcnt = 0, wocc = 0;  // (wave-uniform)
         uint32_t nent[SU];
         uint16_t ntg[SU];
-        auto fetch = [&](uint32_t f0) {
-#pragma unroll
-            for (uint32_t u = 0; u < SU; u++) {
-                const uint32_t e = f0 + u * SCAN_T + tid;
-                nent[u] = 0;
-                ntg[u] = 0xFFFFu;
-                if (e < len) {
-                    nent[u] = mode == 0 ? E->plist[off + e] : E->occ[off + e];
-                    if (mode) ntg[u] = E->occnb[off + e];
-                }
+        uint32_t eS = bid * SCAN_T + (tid & ~63u);  // my wave's next segment (wave-uniform)
+        // my lane's entry of the segment at s0 (BPE_SCAN_PD segments ahead in flight)
+        auto load1 = [&](uint32_t s0, uint32_t &en, uint16_t &tg) {
+            const uint32_t e = s0 + lane;
+            en = 0;
+            tg = 0xFFFFu;
+            if (e < len) {
+                en = mode == 0 ? E->plist[off + e] : E->occ[off + e];
+                if (mode) tg = E->occnb[off + e];
             }
         };
-        fetch(bid * SCAN_T * SU);
-        uint32_t round = 0;
-#if BPE_WFLUSH
-        const uint32_t lane = tid & 63, wbase = (tid >> 6) * 64 * SU * FR;
-        uint32_t wcnt = 0, wocc = 0;  // (wave-uniform)
-        (void)round;
-#endif
-        for (uint32_t e0 = bid * SCAN_T * SU; e0 < len; e0 += stride) {  // uniform trip count
+        uint32_t pent = 0;
+        uint16_t ptg = 0xFFFFu;
+        auto advance = [&]() {  // eS to my wave's next segment, its entry into nent / ntg
+            eS += stride;
+            if (SCAN_PD > 1) {
+                nent[0] = pent;
+                ntg[0] = ptg;
+                if (eS + stride < len) load1(eS + stride, pent, ptg);
+            } else if (eS < len) {
+                load1(eS, nent[0], ntg[0]);
+            }
+        };
+        auto flush = [&]() {  // (wave-uniform)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the slice's LDS stores before the reads)
+            __builtin_amdgcn_wave_barrier();
+            uint32_t g = 0;
+            if (lane == 0 && wcnt) g = atomicAdd(Rm, wcnt);
+            g = __shfl(g, 0);
+            for (uint32_t q = lane; q < wcnt; q += 64) {
+                STG(g + q, "wflush") {
+                occz[g + q] = list[wbase + q];
+                tagz[g + q] = ltag[wbase + q];
+                }
+            }
+            wocc += wcnt;
+            wcnt = 0;
+            __builtin_amdgcn_wave_barrier();
+        };
+        const bool cmp = mode != 0 && E->scan_compact != 0;  // (block-uniform)
+        const uint32_t tsh = mode == 2 ? 8u : 0u;            // the tag byte of the neighbour `want` names
+        uint32_t qpos = 0, qn = 0;                           // packed entries: lanes [0, qn) (wave-uniform count)
+        load1(eS, nent[0], ntg[0]);
+        if (SCAN_PD > 1) load1(eS + stride, pent, ptg);
+        for (;;) {  // (wave-uniform)
             uint32_t ent[SU];
             uint16_t etg[SU];
             bool val[SU];
-            if (!BPE_SCAN_PF) fetch(e0);
-#pragma unroll
-            for (uint32_t u = 0; u < SU; u++) {
-                val[u] = e0 + u * SCAN_T + tid < len;
-                ent[u] = nent[u];
-                etg[u] = ntg[u];
+            if (!cmp) {
+                if (eS >= len) break;
+                val[0] = eS + lane < len;
+                ent[0] = nent[0];
+                etg[0] = ntg[0];
+                advance();
+            } else {
+                // pack segments while they fit (a segment that does not waits
+                // for the next round; qn == 0 always takes one)
+                while (eS < len) {
+                    const bool pass = eS + lane < len && tag_ok(((uint32_t)ntg[0] >> tsh) & 0xFFu, want);
+                    const unsigned long long M = __ballot(pass);
+                    const uint32_t np = (uint32_t)__popcll(M);
+                    if (qn + np > 64) break;
+                    const uint32_t r = lane - qn;
+                    const bool mine = lane >= qn && r < np;
+                    const uint32_t pv = (uint32_t)__shfl((int)nent[0], (int)(mine ? kth_bit(M, r) : lane));
+                    if (mine) qpos = pv;
+                    qn += np;
+                    advance();
+                }
+                if (qn == 0) break;
+                val[0] = lane < qn;
+                ent[0] = qpos;
+                etg[0] = 0xFFFFu;  // (checked)
+                qn = 0;
             }
-            if (BPE_SCAN_PF && e0 + stride < len) fetch(e0 + stride);
             int64_t ii[SU], jj[SU];
             TokWin W[SU];
 #pragma unroll
@@ -1798,7 +1884,6 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                         vadd_b(s, E, m, V_IR, rfin, gcnt);
                     }
                 }
-#if BPE_WFLUSH
                 // the wave's own slice of the staging list (no block barrier)
                 const unsigned long long om = __ballot(ok[u]);
                 if (ok[u]) {
@@ -1807,58 +1892,12 @@ __global__ __launch_bounds__(SCAN_T) void k_bscan(const Eng *__restrict__ E, con
                     ltag[slot] = nb_tag(lfin, rfin);
                 }
                 wcnt += (uint32_t)__popcll(om);
-#else
-                const uint32_t slot = wave_append(ok[u], &lcount);
-                if (ok[u]) {
-                    list[slot] = (uint32_t)i;
-                    ltag[slot] = nb_tag(lfin, rfin);
-                }
-#endif
             }
-#if BPE_WFLUSH
-            // flush the wave's slice once another round may not fit, and at the
-            // end: one global atomic per wave, no block barrier
-            if (wcnt + 64 * SU > 64 * SU * FR || e0 + stride >= len) {  // (wave-uniform)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the slice's LDS stores before the reads)
-                __builtin_amdgcn_wave_barrier();
-                uint32_t g = 0;
-                if (lane == 0 && wcnt) g = atomicAdd(Rm, wcnt);
-                g = __shfl(g, 0);
-                for (uint32_t q = lane; q < wcnt; q += 64) {
-                    STG(g + q, "wflush") {
-                    occz[g + q] = list[wbase + q];
-                    tagz[g + q] = ltag[wbase + q];
-                    }
-                }
-                wocc += wcnt;
-                wcnt = 0;
-                __builtin_amdgcn_wave_barrier();
-            }
-#else
-            // flush the staged rounds' list: one global atomic per block
-            if (++round % FR == 0 || e0 + stride >= len) {  // (uniform)
-                __syncthreads();
-                if (tid == 0) {
-                    const uint32_t c = lcount;
-                    gbase = c ? atomicAdd(Rm, c) : 0u;
-                    bRs += c;
-                    lcount = 0;
-                    list_n = c;
-                }
-                __syncthreads();
-                for (uint32_t q = tid; q < list_n; q += SCAN_T) {
-                    STG(gbase + q, "bflush") {
-                    occz[gbase + q] = list[q];
-                    tagz[gbase + q] = ltag[q];
-                    }
-                }
-                __syncthreads();
-            }
-#endif
+            // flush the wave's slice once another round may not fit
+            if (wcnt + 64 > 64 * FR) flush();
         }
-#if BPE_WFLUSH
+        if (wcnt) flush();
         if (lane == 0 && wocc) atomicAdd(&bRs, wocc);  // (the block's occurrences: read after the barrier below)
-#endif
     } else {
         // a == b: the thread holding a run's first token
         // walks it, pairing tokens 0-1, 2-3, ... (greedy left-to-right); a run

@@ -558,6 +558,13 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     // skipping backs off after 2 consecutive failures of batches with
     // skipped keys (BPE_SKGATE: that count; 8 never backs off)
     h.skg_exp = (uint32_t)getenv_int("BPE_SKGATE", 2);
+    // scan blocks per member: by entries of its candidate list, an occurrence
+    // list's by count + entries / BPE_SCAN_OCCD (0: by entries)
+    h.scan_occd = (uint32_t)std::max(0, getenv_int("BPE_SCAN_OCCD", 3));
+    // and pack an occurrence list's entries whose neighbour tag passes into
+    // whole rounds before their gathers (BPE_SCAN_COMPACT=0: one entry per
+    // lane per round, as before round 6)
+    h.scan_compact = (uint32_t)(getenv_int("BPE_SCAN_COMPACT", 1) != 0);
     // and take members from the next TOPK keys once a list is used up, up to
     // nlists lists (BPE_NLIST; BPE_LIST2=1 is two lists, the round-5 knob)
     {

@@ -326,6 +326,8 @@ struct Eng {
     // batched training (batch.hip; occurrence positions staged in ids_out)
     uint32_t batch;       // 1: the batch kernels drive the run
     uint32_t skip_on;     // batches: skip non-commuting list entries instead of ending there (BPE_SKIP, default 1)
+    uint32_t scan_compact;  // batches: k_bscan packs an occurrence list's tag-passing entries into whole rounds (BPE_SCAN_COMPACT)
+    uint32_t scan_occd;   // batches: scan blocks weigh an occurrence list by count + entries / this (0: entries; BPE_SCAN_OCCD)
     uint32_t skg_exp;     // batches: the failure exponent from which skipping backs off (BPE_SKGATE, default 2; 8 never)
     uint32_t nlists;      // batches: lists of TOPK keys a formation may walk, each once the one before is used up
                           // (BPE_NLIST, 1..NLIST; BPE_LIST2=1 is 2)

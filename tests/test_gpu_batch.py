@@ -10,6 +10,7 @@ runs that must stay alone), text-shaped and uniform corpora (long batches),
 and caps that end a run inside a batch.  The tests also require that batches
 of more than one merge actually ran and that the verification dropped members
 somewhere (new pairs overtaking later members)."""
+import json
 import os
 import random
 import subprocess
@@ -303,3 +304,54 @@ def test_hot_set_past_the_reduce_blocks(monkeypatch):
     data = synth_bytes(510, 3 << 20)
     st = _check(data, 1500)
     assert st["batches"] > 0
+
+
+ENGLISH_RECOUNT_WORKER = r"""
+import hashlib, json, sys
+import numpy as np
+sys.path.insert(0, %r)
+from llmtokenizer_amd import api
+from llmtokenizer_amd.synth import english_like
+n, mm = int(sys.argv[1]), int(sys.argv[2])
+e = api.Engine(0)
+e.load(english_like(n))
+e.train(mm)
+m1, ids = e.merges().copy(), e.ids().astype(np.uint64)
+out = {"md5": hashlib.md5(m1.tobytes()).hexdigest(), "checksum": "%%016x" %% e.ids_checksum(),
+       "batches": int(e.stats()["batches"])}
+e.set_merge_log(True)
+e.train(mm + 1)
+m2, log = e.merges(), e.merge_log()
+out["prefix_equal"] = bool(np.array_equal(m2[:mm], m1))
+# checkpoint recount (the reference's count pass, bpe.c:684-685: every
+# adjacent position of the token sequence after mm merges)
+keys, cnt = np.unique((ids[:-1] << np.uint64(32)) | ids[1:], return_counts=True)
+nxt = (int(m2[mm][0]) << 32) | int(m2[mm][1])
+at = np.searchsorted(keys, np.uint64(nxt))
+out["next_recount"] = int(cnt[at]) if at < len(keys) and int(keys[at]) == nxt else 0
+out["next_logged"] = int(log["count"][mm])
+out["max_recount"] = int(cnt.max())
+print(json.dumps(out))
+""" % ROOT
+
+
+def test_english_like_64mib_matches_one_merge_engine_and_recount():
+    """64 MiB of english-like text x 1024 merges (skewed counts: most batches
+    end at a non-commuting entry or a failed skip): the batch engine's merges
+    and ids equal the one-merge engine's, and at the checkpoint the next
+    merge is a maximal pair of a numpy recount of the ids there, at the
+    count the engine logged (bpe.c:698-743's argmax)."""
+    outs = {}
+    for flag in ("1", "0"):
+        env = dict(os.environ, BPE_BATCH=flag)
+        p = subprocess.run([sys.executable, "-c", ENGLISH_RECOUNT_WORKER, str(64 << 20), "1024"], env=env,
+                           capture_output=True, text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-2000:]
+        outs[flag] = json.loads(p.stdout.strip().splitlines()[-1])
+    print(outs)
+    b, o = outs["1"], outs["0"]
+    assert (b["md5"], b["checksum"]) == (o["md5"], o["checksum"]), outs
+    assert b["batches"] > 0 and o["batches"] == 0, outs
+    for r in (b, o):
+        assert r["prefix_equal"], outs
+        assert r["next_recount"] == r["next_logged"] == r["max_recount"], outs

@@ -24,7 +24,8 @@ for mib, mm in [(int(a), int(b)) for a, b in (x.split('x') for x in os.environ.g
                       "batches": int(st["batches"]), "retries": int(st["batch_retries"]),
                       "dropped": int(st["batch_dropped"]), "skipped": int(st["keys_skipped"]),
                       "skip_failed": int(st["skip_failed"]), "tie_verified": int(st["tie_verified"]),
-                      "tie_failed": int(st["tie_failed"]), "candidates": int(st["candidates"]),
+                      "tie_failed": int(st["tie_failed"]), "candidates": int(st["candidates"]), "relists": int(st["relists"]),
+                      "n_out": int(st["n_out"]),
                       "occurrences": int(st["occurrences"]), "scan_span_ms": round(st["ms_scan_span"], 4),
                       "apply_span_ms": round(st["ms_apply_span"], 4), "select_span_ms": round(st["ms_select_span"], 4),
                       "end": {k[4:]: int(st[k]) for k in st if k.startswith("end_")}}), flush=True)
