@@ -560,7 +560,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.skg_exp = (uint32_t)getenv_int("BPE_SKGATE", 2);
     // scan blocks per member: by entries of its candidate list, an occurrence
     // list's by count + entries / BPE_SCAN_OCCD (0: by entries)
-    h.scan_occd = (uint32_t)std::max(0, getenv_int("BPE_SCAN_OCCD", 3));
+    h.scan_occd = (uint32_t)std::max(0, getenv_int("BPE_SCAN_OCCD", 6));
     // and pack an occurrence list's entries whose neighbour tag passes into
     // whole rounds before their gathers (BPE_SCAN_COMPACT=0: one entry per
     // lane per round, as before round 6)
