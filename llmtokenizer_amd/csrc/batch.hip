@@ -992,7 +992,7 @@ __device__ __attribute__((always_inline)) inline void bselect_block(const Eng *_
             // the formation's guess of the keys a member zeroes: twice the
             // run's average so far, + 2
             B->zrate = (uint32_t)min(2ull * B->nzero / (md ? md : 1u) + 2ull, 1ull << 20);
-            Bg->crate = (uint32_t)min(2ull * Bg->ncre / (md ? md : 1u) + 16ull, 1ull << 20);
+            Bg->crate = (uint32_t)min((unsigned long long)E->crate_pct * Bg->ncre / (100ull * (md ? md : 1u)) + 16ull, 1ull << 20);
             C->merges_done = md;
             C->occ_top += (uint32_t)rs;
             C->n_live = n_live;
@@ -2779,16 +2779,17 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                 const uint32_t hp = wave_append(hot_in, &C->hot_n);
                 if (hot_in && hp < HOT_CAP) E->hot_slot[hp] = (uint32_t)slot[q];
             }
-            if (tie) {  // (uniform) the undo log: (slot, delta)
+            if (tie) {  // (uniform) the undo log: (slot, delta, member)
                 const uint32_t lp = wave_append(logged, &B->tlog_n);
                 if (logged) {
-                    E->tlog[2 * (uint64_t)lp] = (uint32_t)slot[q];
-                    E->tlog[2 * (uint64_t)lp + 1] = d;
+                    E->tlog[3 * (uint64_t)lp] = (uint32_t)slot[q];
+                    E->tlog[3 * (uint64_t)lp + 1] = d;
+                    E->tlog[3 * (uint64_t)lp + 2] = m[q];
                 }
             }
         }
     }
-    __shared__ uint32_t sjf, slast, szb[16];
+    __shared__ uint32_t sjf, slast, szb[16], spart;
     uint32_t jf = jsB;  // the applied prefix
     bool keep = !tie && blockIdx.x == 0;  // this block writes the bookkeeping
     if (tie) {
@@ -2840,19 +2841,48 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                     f[b] = q >= 1 && q >= tp && q < jsB && !tie_levels_ok(lo, summary_B(hiD), Bsz, B->tmask[q]);
                 }
                 const MK fm = mk_ballot([&](uint32_t b) { return f[b]; });
-                if (lane == 0) sjf = mk_any(fm) ? mk_first(fm) : jsB;
+                const uint32_t jx = mk_any(fm) ? mk_first(fm) : jsB;
+                // the members before the failing one stand as a batch of their own
+                // when none of their occurrences abuts one of a member at or past
+                // it (the abutting pair's deltas assume both merge, as for the
+                // verified prefix of k_bapply's prologue); otherwise every update
+                // is reverted and the batch re-formed cut there
+                bool part = false;
+                if (jx < jsB && jx > 0 && !SH && E->prefix_apply) {
+                    const MK pre = mk_below(jx);
+                    const MK ab = mk_ballot([&](uint32_t b) {
+                        const uint32_t q = 64 * b + lane;
+                        if (q >= jsB) return false;
+                        bool hi = false, lo = false;  // abuts a member at or past jx / before jx
+#pragma unroll
+                        for (uint32_t bb = 0; bb < NBK; bb++) {
+                            const unsigned long long w = __hip_atomic_load(&B->adj[q][bb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            hi |= (w & ~pre.w[bb]) != 0;
+                            lo |= (w & pre.w[bb]) != 0;
+                        }
+                        return q < jx ? hi : lo;
+                    });
+                    part = !mk_any(ab);
+                }
+                if (lane == 0) {
+                    sjf = jx;
+                    spart = part ? 1u : 0u;
+                }
             }
             __syncthreads();
-            if (sjf < jsB) {  // revert every logged update (this block alone: rare)
+            if (sjf < jsB) {  // revert the logged updates (this block alone: rare)
                 const uint32_t nl = __hip_atomic_load(&B->tlog_n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t from = spart ? sjf : 0u;  // (members from here on)
                 long long rd = 0;
                 for (uint32_t q = tid; q < nl; q += blockDim.x) {
-                    const uint32_t slot = E->tlog[2 * (uint64_t)q], d = E->tlog[2 * (uint64_t)q + 1];
+                    const uint32_t slot = E->tlog[3 * (uint64_t)q], d = E->tlog[3 * (uint64_t)q + 1],
+                                   mq = E->tlog[3 * (uint64_t)q + 2];
+                    if (mq < from) continue;
                     const uint32_t old = atomicAdd(&E->hcnt[(uint64_t)slot * E->hcs], 0u - d);
                     rd += (long long)(old - d != 0) - (long long)(old != 0);
                 }
                 dD += rd;  // (this block's sum below carries the whole revert's D change)
-                jf = 0;
+                jf = from;
             } else if (tid == 0) {
                 // the batch stands: its zeroed keys count towards the zrate
                 // guess (every block's share is in ztot; reverted batches add none)
@@ -2901,7 +2931,7 @@ __global__ __launch_bounds__(1024) void k_bapply(const Eng *__restrict__ E, Ctl 
                 B->ntie++;
                 if (jf < jsB) {
                     B->ntfail++;
-                    B->retry = sjf;
+                    if (!spart) B->retry = sjf;  // (else the prefix stands: the next formation starts fresh)
                 }
             }
             if (lfull) B->retry = B->tpend;

@@ -576,6 +576,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     // tied members admitted on a guess of the keys the members before them
     // create (D's upper side), checked by k_bapply like the lower side
     h.tie_up = (uint32_t)(getenv_int("BPE_TIE_UP", 0) != 0);
+    h.crate_pct = (uint32_t)std::max(100, getenv_int("BPE_CRATE_PCT", 200));
     h.lose_retry = (uint32_t)(getenv_int("BPE_TEST_LOSE_RETRY", 0) != 0);
     h.xbat = nullptr;
     h.xsp_out = h.xsp_in = nullptr;
@@ -604,7 +605,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         }
         // verified tie order: the undo log (records of 2 words)
         h.tlog_cap = 1u << 22;
-        if ((r = dalloc(c, &h.tlog, 2ull * h.tlog_cap, false))) return r;
+        if ((r = dalloc(c, &h.tlog, 3ull * h.tlog_cap, false))) return r;  // (slot, delta, member)
         // sharded: the batch exchange (zero between batches; a multiple of 4 words)
         if (c->sharded && (r = dalloc(c, &h.xbat, (xbat_words(BK, h.vcap) + 3) / 4 * 4))) return r;
         if (c->sharded && h.vcap > DENSE) {

@@ -291,7 +291,7 @@ struct Eng {
     uint32_t prefix_apply;  // batches: apply a verified prefix that abuts no dropped member (BPE_PREFIX, default 1)
     uint32_t rw_hold;       // k_bsel's rewrite blocks wait this many wall-clock ticks (BPE_RW_HOLD_US) before
     uint32_t rw_hold_max;   // ... a rewrite of fewer occurrences than this, so the reduce's loads go first
-    uint32_t *tlog;       // batches: undo log of a verified-tie batch's table updates (slot, delta)
+    uint32_t *tlog;       // batches: undo log of a verified-tie batch's table updates (slot, delta, member)
     uint32_t tlog_cap;    // ... records
     uint32_t tie_verify;  // batches: admit members on the tie-order guess k_bapply verifies (BPE_TIE_VERIFY,
                           // default 1; 2 = BPE_TIE_TEST: every such check fails, the revert runs)              // BPE_DEBUG_FORM=1: k_bsel prints why each batch's formation ended
@@ -332,6 +332,7 @@ struct Eng {
     uint32_t nlists;      // batches: lists of TOPK keys a formation may walk, each once the one before is used up
                           // (BPE_NLIST, 1..NLIST; BPE_LIST2=1 is 2)
     uint32_t tie_up;      // batches: the tie order's upper side on a guess of the keys created, verified (BPE_TIE_UP, default 0)
+    uint32_t crate_pct;   // batches, BPE_TIE_UP: the guess of the keys a member creates, % of the run's average (BPE_CRATE_PCT, 200)
     uint32_t lose_retry;  // tests (BPE_TEST_LOSE_RETRY=1): the select forgets a failed batch's retry cut, so the
                           // failing batch is formed again and again -- the stall the no-progress watchdog ends
     uint32_t bvs;         // ids >= DENSE per (member, vector) in bvec / bvlist

@@ -219,16 +219,21 @@ C3_MERGES_MD5 = "b58e334e1360ca73030996c9cdfe044a"  # 1 GiB x 1024 (train_1024),
 C3_IDS_CHECKSUM = 0x9EB1D5D726D3C952
 
 
-@pytest.mark.parametrize("mode", ["verify", "forced_fail", "off"])
+@pytest.mark.parametrize("mode", ["verify", "forced_fail", "forced_fail_full", "off"])
 def test_verified_tie_order_1g_1024(mode, monkeypatch):
     """Members admitted on a tie order that holds only if the earlier members
     zero few keys (k_bapply: decrements, count of zeroed keys, check, then
     increments or revert): the same merges and ids as without them (off), with
-    the check passing (verify) and with every check failing (forced_fail:
-    decrements reverted, batch re-formed before the member)."""
+    the check passing (verify) and with every check failing (forced_fail: the
+    members from the failing one on reverted, the ones before it standing as a
+    batch when none abuts a reverted one, else everything reverted and the
+    batch re-formed before the member; forced_fail_full: BPE_PREFIX=0, always
+    the latter)."""
     monkeypatch.setenv("BPE_TIE_VERIFY", "0" if mode == "off" else "1")
-    if mode == "forced_fail":
+    if mode.startswith("forced_fail"):
         monkeypatch.setenv("BPE_TIE_TEST", "1")
+    if mode == "forced_fail_full":
+        monkeypatch.setenv("BPE_PREFIX", "0")
     e = api.Engine(0)
     try:
         e.synth(2, GIB)
@@ -242,6 +247,8 @@ def test_verified_tie_order_1g_1024(mode, monkeypatch):
     if mode == "verify":
         assert st["tie_verified"] > 0 and st["tie_failed"] == 0
     elif mode == "forced_fail":
+        assert st["tie_failed"] > 0 and st["tie_failed"] == st["tie_verified"] and st["batch_dropped"] > 0
+    elif mode == "forced_fail_full":
         assert st["tie_failed"] > 0 and st["tie_failed"] == st["tie_verified"] and st["batch_retries"] >= st["tie_failed"]
     else:
         assert st["tie_verified"] == 0
