@@ -292,6 +292,10 @@ struct bpe_gpu_ctx {
     size_t merges_done = 0;
     std::vector<std::pair<void *, size_t>> train_allocs;  // live buffers of the current run
     std::vector<std::pair<void *, size_t>> pool;          // released buffers, reused by size
+    // setup_run's zero fills, collected while zdefer is set and issued as one
+    // kernel (flush_zero) instead of ~40 hipMemsetAsync launches
+    bool zdefer = false;
+    std::vector<std::pair<void *, size_t>> zpend;
     uint32_t *d_tileoff = nullptr;
     uint32_t *d_enc_pairs = nullptr;
     hipGraphExec_t g_plain = nullptr, g_tracked = nullptr, g_encode = nullptr, g_batch = nullptr;
@@ -308,6 +312,10 @@ struct bpe_gpu_ctx {
     uint64_t scan_n = 0, event_n = 0;
     std::string prof_name;
     double prof_ms = 0, prof_bytes = 0;
+    // the count pass's events: read once the run is done (settle_count_pass),
+    // not with a host wait between the count pass and the sort
+    hipEvent_t cp_ev[2] = {};
+    bool cp_pending = false;
     uint64_t prof_launches = 0;
     // grow-only device scratch of decode (ids, pairs, elen, offsets, scan
     // temporaries, output, error words; slots 0-6), of the window encoder
@@ -325,7 +333,58 @@ struct bpe_gpu_ctx {
     bool pres_valid = false;     // d_pres describes the bytes loaded now
 };
 
+namespace bpeamd {
+
+// Zero fills of many buffers in one launch: the ranges' 16-byte words laid end
+// to end (every size a multiple of 256 B: dalloc rounds), a grid-stride loop of
+// uint4 stores; each thread finds its range by a short scan of the prefix.
+constexpr uint32_t ZMANY = 48;
+struct ZeroSet {
+    uint4 *p[ZMANY];
+    unsigned long long end[ZMANY];  // inclusive prefix of the ranges' 16-byte words
+    uint32_t n;
+};
+
+__global__ __launch_bounds__(256) void k_zero_many(const ZeroSet z) {
+    const unsigned long long tot = z.end[z.n - 1];
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    uint32_t r = 0;
+    const uint4 zero = make_uint4(0, 0, 0, 0);
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
+        while (i >= z.end[r]) r++;  // (i only grows: the range index too)
+        const unsigned long long b = r ? z.end[r - 1] : 0ull;
+        z.p[r][i - b] = zero;
+    }
+}
+
+// the batch state's run parameters (by value: no staging buffer, no sync)
+__global__ void k_bat_params(Bat *B, uint32_t drop_test, uint32_t ra_split, unsigned long long stage_cap) {
+    B->drop_test = drop_test;
+    B->ra_split = ra_split;
+    B->stage_cap = stage_cap;
+}
+
+}  // namespace bpeamd
+
 namespace {
+
+int flush_zero(bpe_gpu_ctx *c) {
+    size_t k = 0;
+    while (k < c->zpend.size()) {
+        ZeroSet z{};
+        unsigned long long acc = 0;
+        for (; k < c->zpend.size() && z.n < ZMANY; k++) {
+            z.p[z.n] = reinterpret_cast<uint4 *>(c->zpend[k].first);
+            acc += c->zpend[k].second / 16;
+            z.end[z.n++] = acc;
+        }
+        const unsigned long long blocks = std::min<unsigned long long>((acc + 255) / 256, 8192);
+        k_zero_many<<<(uint32_t)std::max<unsigned long long>(blocks, 1), 256, 0, c->st>>>(z);
+        HIPCHK(hipGetLastError());
+    }
+    c->zpend.clear();
+    return 0;
+}
 
 // Device buffers are pooled per context: a second train()/encode() on the
 // same context reuses the previous run's allocations of equal size instead of
@@ -368,7 +427,9 @@ int dalloc(bpe_gpu_ctx *c, T **p, size_t count, bool zero = true) {
         }
     }
     c->train_allocs.push_back({(void *)*p, bytes});
-    if (zero) {
+    if (zero && c->zdefer) {
+        c->zpend.push_back({(void *)*p, bytes});  // (bytes: a multiple of 256)
+    } else if (zero) {
         hipError_t e = hipMemsetAsync(*p, 0, bytes, c->st);
         if (e != hipSuccess) return fail(BPE_GPU_EHIP, "hipMemsetAsync", e);
     }
@@ -432,7 +493,21 @@ void xsp_layout(uint64_t vcap, uint32_t *cap, uint32_t *stride) {
 }
 
 // allocate the per-run structures (sizes depend on the merge cap)
+int setup_run_body(bpe_gpu_ctx *c, uint32_t mcap, bool encode);
+
 int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
+    c->zdefer = getenv_int("BPE_ZMANY", 1) != 0;
+    c->zpend.clear();
+    const int r = setup_run_body(c, mcap, encode);
+    c->zdefer = false;
+    if (r) {
+        c->zpend.clear();
+        return r;
+    }
+    return 0;
+}
+
+int setup_run_body(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     free_train(c);
     Eng &h = c->h;
     h.n0 = c->n0;
@@ -589,6 +664,7 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     h.grflag = nullptr;
     h.tlog_cap = 0;
     h.bvs = h.vcap > DENSE ? h.vcap - DENSE : 1;
+    uint32_t bat_dt = 0, bat_split = 0;
     if (h.batch) {
         if ((r = dalloc(c, &h.bat, 1))) return r;
         if ((r = dalloc(c, &h.btag, n0, false))) return r;
@@ -616,17 +692,14 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
         }
         // BPE_BATCH_DROP_TEST=d: the verification drops members j >= 1 of id
         // z = 0 mod d (tests drive the drop path with it)
-        const uint32_t dt = (uint32_t)getenv_int("BPE_BATCH_DROP_TEST", 0);
-        if (dt) HIPCHK(hipMemcpyAsync(&h.bat->drop_test, &dt, 4, hipMemcpyHostToDevice, c->st));
+        bat_dt = (uint32_t)getenv_int("BPE_BATCH_DROP_TEST", 0);
         // k_bapply's share of the rewrite (1/256; BPE_RA_SPLIT: tuning)
-        const uint32_t split = BAPPLY_RA ? (uint32_t)std::min(256, std::max(0, getenv_int("BPE_RA_SPLIT", 96))) : 0u;
-        HIPCHK(hipMemcpyAsync(&h.bat->ra_split, &split, 4, hipMemcpyHostToDevice, c->st));
+        bat_split = BAPPLY_RA ? (uint32_t)std::min(256, std::max(0, getenv_int("BPE_RA_SPLIT", 96))) : 0u;
         // BPE_BATCH_STAGE=p: only p staging positions (tests drive the overflow
         // cut -- sharded: the flag in the exchange and the re-formed batch)
         c->stage_cap = n0;
         if (const char *t = getenv("BPE_BATCH_STAGE")) c->stage_cap = std::min<uint64_t>(n0, std::max(1ll, atoll(t)));
-        HIPCHK(hipMemcpyAsync(&h.bat->stage_cap, &c->stage_cap, 8, hipMemcpyHostToDevice, c->st));
-        HIPCHK(hipStreamSynchronize(c->st));  // (dt, split are on the stack)
+        // (written by k_bat_params below, after the zero fill of Bat)
     }
     h.ntiles = (n0 + CTILE - 1) / CTILE;
     if ((r = dalloc(c, &h.tilecnt, h.ntiles))) return r;
@@ -712,6 +785,12 @@ int setup_run(bpe_gpu_ctx *c, uint32_t mcap, bool encode) {
     C.L1new = HOLE;
     C.xleft = HOLE;
     C.erec_ready = 1;  // (the set-up gathers the records before the first scan)
+    // the deferred zero fills, then what must land on zeroed memory
+    if ((r = flush_zero(c))) return r;
+    if (h.batch) {
+        k_bat_params<<<1, 1, 0, c->st>>>(h.bat, bat_dt, bat_split, (unsigned long long)c->stage_cap);
+        HIPCHK(hipGetLastError());
+    }
     if ((r = push_ctl(c))) return r;
     return push_desc(c);
 }
@@ -1787,6 +1866,7 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
     const uint32_t AA = h.A * h.A;
     if ((r = dalloc(c, &h.poff, AA + 1))) return r;
     if ((r = push_desc(c))) return r;
+    c->cp_pending = false;  // (a previous run's time was read when it ended)
     // counting sort of pair positions by rank key
     const uint64_t npairs = c->n0 - 1;
     uint64_t tile = std::max<uint64_t>(1 << 16, (npairs + 1023) / 1024);
@@ -1805,22 +1885,18 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
                       !(getenv("BPE_HIST_SPAN") && !atoi(getenv("BPE_HIST_SPAN")));
     if (npairs > 0) {
         // the one full pass over the corpus: time it with events on our stream
-        hipEvent_t e0, e1;
-        HIPCHK(hipEventCreate(&e0));
-        HIPCHK(hipEventCreate(&e1));
-        HIPCHK(hipEventRecord(e0, c->st));
+        // (read by settle_count_pass after the run: no host wait here)
+        for (hipEvent_t &e : c->cp_ev)
+            if (!e) HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipEventRecord(c->cp_ev[0], c->st));
         if (span) c->stats.count_pass_span = launch_count_pass(c, ntl, d_hist, tile, lo, S);
         else k_pair_hist<<<ntl * parts, 1024, 0, c->st>>>(c->dE, d_hist, tile, parts);
-        HIPCHK(hipEventRecord(e1, c->st));
-        HIPCHK(hipEventSynchronize(e1));
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-        hipEventDestroy(e0);
-        hipEventDestroy(e1);
+        HIPCHK(hipEventRecord(c->cp_ev[1], c->st));
+        c->cp_pending = true;
         c->prof_name = span ? "k_pair_hist_span" : "k_pair_hist";
-        c->stats.ms_count_pass = ms;
+        c->stats.ms_count_pass = 0;
         if (!span) c->stats.count_pass_span = 0;
-        c->prof_ms = ms;
+        c->prof_ms = -1.0;  // (the count pass's time, unless a later profile replaces it)
         // 1 B/token read (V = 256: re-read once per bin part); tok[] was
         // written by init_presence's streaming pass
         c->prof_bytes = (double)c->n0 * (span ? 1 : parts);
@@ -1859,6 +1935,18 @@ int init_sort(bpe_gpu_ctx *c, const std::vector<uint32_t> &bh, std::vector<uint3
     }
     *unrank_out = unrank;
     *d_tot_out = d_tot;
+    return 0;
+}
+
+// the count pass's time from its events (after the run, or before the next)
+int settle_count_pass(bpe_gpu_ctx *c) {
+    if (!c->cp_pending) return 0;
+    c->cp_pending = false;
+    HIPCHK(hipEventSynchronize(c->cp_ev[1]));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, c->cp_ev[0], c->cp_ev[1]));
+    c->stats.ms_count_pass = ms;
+    if (c->prof_ms < 0) c->prof_ms = ms;
     return 0;
 }
 
@@ -2309,6 +2397,8 @@ void bpe_gpu_destroy(bpe_gpu_ctx *c) {
         for (auto &b : a)
             for (auto &e : b)
                 if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->cp_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->st && c->own_stream) (void)hipStreamDestroy(c->st);
     delete c;
 }
@@ -2463,6 +2553,7 @@ int bpe_gpu_train_ex(bpe_gpu_ctx *c, long max_merges, unsigned flags, size_t *n_
         fprintf(stderr, "select phases (ticks/iter): reduce %.1f merge %.1f tail %.1f\n",
                 (double)C.counters[9] / C.counters[0], (double)C.counters[10] / C.counters[0],
                 (double)C.counters[11] / C.counters[0]);
+    if ((r = settle_count_pass(c))) return r;
     c->stats.ms_init = t1 - t0;
     c->stats.ms_train = t2 - t1;
     c->stats.ms_total = t2 - t0;
@@ -2901,6 +2992,8 @@ int bpe_gpu_ids_checksum(bpe_gpu_ctx *c, uint64_t base, uint64_t *sum) {
 
 int bpe_gpu_get_stats(bpe_gpu_ctx *c, bpe_gpu_stats *st) {
     if (!c || !st) return BPE_GPU_EINVAL;
+    int r;
+    if (c->cp_pending && (r = settle_count_pass(c))) return r;
     *st = c->stats;
     return 0;
 }
@@ -2975,6 +3068,8 @@ int bpe_gpu_device_tokens(bpe_gpu_ctx *c, const void **dev_tok, size_t *n) {
 int bpe_gpu_kernel_profile(bpe_gpu_ctx *c, const char **name, double *avg_ms, double *bytes_per_launch,
                            uint64_t *launches) {
     if (!c) return BPE_GPU_EINVAL;
+    int r;
+    if ((r = settle_count_pass(c))) return r;
     if (name) *name = c->prof_name.c_str();
     if (avg_ms) *avg_ms = c->prof_ms;
     if (bytes_per_launch) *bytes_per_launch = c->prof_bytes;

@@ -569,8 +569,15 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     g->merges_done = 0;
     *n_merges = 0;
     const double t0 = now_ms();
+    static const bool dbg_init = getenv_int("BPE_DEBUG_INIT", 0) != 0;
+    auto phase = [&](const char *what) {  // (BPE_DEBUG_INIT: host-side phase times of the init)
+        if (!dbg_init) return;
+        (void)hipStreamSynchronize(g->st);
+        fprintf(stderr, "group init %s %.3f ms\n", what, now_ms() - t0);
+    };
     uint64_t ntot;
     if ((r = group_total(g, &ntot))) return r;
+    phase("total");
     g->stats.n_in = ntot;
     if (ntot < 2) return fail(BPE_GPU_EINVAL, "fewer than 2 tokens");
     uint64_t cap = std::min<uint64_t>(ntot - 1, engine_merge_cap());
@@ -605,6 +612,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         c->hC->n_live = ntot;  // global token count (the tracking thresholds are global)
         if ((r = push_ctl(c))) return r;
     }
+    phase("setup");
     // pointer tables for the one-device exchange
     if (local_mode(g)) {
         if (!g->d_ptrs) {
@@ -629,11 +637,13 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     std::vector<uint32_t> pres(256);
     HIPCHK(hipMemcpyAsync(pres.data(), bh[0], 1024, hipMemcpyDeviceToHost, g->st));
     HIPCHK(hipStreamSynchronize(g->st));
+    phase("alphabet");
     // 2. local counting sorts under the global ranks
     std::vector<uint32_t> unrank;
     std::vector<uint32_t *> tot(K), d_unrank(K);
     for (uint32_t k = 0; k < K; k++)
         if ((r = init_sort(g->cs[k], pres, &unrank, &tot[k]))) return r;
+    phase("sort");
     // 3. edge records, the byte pairs across edges, global byte-pair counts
     for (bpe_gpu_ctx *c : g->cs) k_edges<<<1, 256, 0, g->st>>>(c->dE, c->dC, 1);
     if ((r = ex_records(g, g->d_ptrs))) return r;
@@ -641,13 +651,18 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     const uint32_t A = g->cs[0]->h.A, AA = A * A;
     if (local_mode(g) && (r = upload_table(g, g->d_ptrs_tmp, tot))) return r;
     if (AA && (r = ex_allreduce(g, g->d_ptrs_tmp, tot, AA))) return r;
+    // (the slots of the byte-pair keys: the first hot set is built from them,
+    // as on one GPU, not from a pass over the whole, freshly cleared table)
+    std::vector<uint32_t *> islots(K, nullptr);
     for (uint32_t k = 0; k < K; k++) {
         bpe_gpu_ctx *c = g->cs[k];
         if ((r = dalloc(c, &d_unrank[k], unrank.size()))) return r;
         if (!unrank.empty())
             HIPCHK(hipMemcpyAsync(d_unrank[k], unrank.data(), unrank.size() * 4, hipMemcpyHostToDevice, g->st));
-        if (AA) k_init_counts<<<(AA + 255) / 256, 256, 0, g->st>>>(c->dE, c->dC, tot[k], d_unrank[k], nullptr);
+        if (AA && (r = dalloc(c, &islots[k], AA, false))) return r;
+        if (AA) k_init_counts<<<(AA + 255) / 256, 256, 0, g->st>>>(c->dE, c->dC, tot[k], d_unrank[k], islots[k]);
     }
+    phase("pair counts");
     // warm the per-merge collective once outside any graph (lazy connection setup)
     {
         std::vector<uint32_t *> xb;
@@ -655,11 +670,12 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
         if ((r = ex_allreduce(g, g->d_ptrs, xb, 4ull * g->cs[0]->h.vcap + 2))) return r;
         for (auto *c : g->cs) HIPCHK(hipMemsetAsync(c->h.xbuf, 0, 2ull * c->h.xstride * 4, g->st));
     }
+    phase("warm exchange");
     if (g->cs[0]->h.batch) {
         // the hot set and the first batch (the records of the initial tokens
         // are current: gathered above)
-        for (bpe_gpu_ctx *c : g->cs)
-            if ((r = hot_rebuild(c))) return r;
+        for (uint32_t k = 0; k < K; k++)
+            if ((r = hot_rebuild(g->cs[k], islots[k], AA))) return r;
         if ((r = group_after_rebuild(g))) return r;
     } else {
         for (bpe_gpu_ctx *c : g->cs) {
@@ -669,6 +685,7 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(g->st));
+    phase("hot set + first select");
     if ((r = p2p_check(g))) return r;
     const double t1 = now_ms();
     if ((r = drive_group(g))) return r;
@@ -738,6 +755,8 @@ int group_train(bpe_gpu_group *g, long max_merges, size_t *n_merges) {
     g->stats.ms_init = t1 - t0;
     g->stats.ms_train = t2 - t1;
     g->stats.ms_total = t2 - t0;
+    for (bpe_gpu_ctx *c : g->cs)
+        if ((r = settle_count_pass(c))) return r;
     g->stats.ms_count_pass = g->cs[0]->stats.ms_count_pass;
     g->stats.count_pass_span = g->cs[0]->stats.count_pass_span;
     return 0;
